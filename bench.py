@@ -1,0 +1,182 @@
+#!/usr/bin/env python3
+"""Throughput benchmark -- BASELINE.json headline: ResNet-50 bf16 DDP training,
+samples/sec for the whole node, one process per GPU over RCCL.
+
+    python bench.py --gpus N --steps K --warmup W          (N=1)
+    torchrun --nproc-per-node N bench.py --gpus N ...      (N>1)
+
+Per step (all inside the timed region): forward, fused cross-entropy,
+backward with bucketed RCCL all-reduce overlapped on a side stream, fused SGD
+(momentum 0.9, wd 5e-5) update of fp32 masters + bf16 shadows.  Synthetic,
+device-resident ImageNet-shaped batches (3x224x224, generated directly in the
+model's NHWC-bf16 input format, several distinct batches cycled), random-init
+weights.  Weak scaling: --batch-size images per GPU.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "samples/sec (whole node) + DDP scaling eff., ResNet-50 bf16 at 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "gpt2", "simplenet"])
+    ap.add_argument("--batch-size", type=int, default=None, help="per-GPU batch (resnet50: 256, gpt2: 8 seqs)")
+    ap.add_argument("--seq-len", type=int, default=1024)
+    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--first-bucket-mb", type=float, default=1.0)
+    ap.add_argument("--grad-accum", type=int, default=1)
+    ap.add_argument("--optimizer", default=None)
+    ap.add_argument("--lr", type=float, default=None)
+    ap.add_argument("--graph", type=int, default=0, help="capture the step in a hipGraph (1) or run eagerly (0)")
+    ap.add_argument("--bucket-timing", action="store_true")
+    ap.add_argument("--nbatches", type=int, default=4, help="distinct synthetic batches cycled")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    from distributed_pytorch_example_amd.utils.env import ensure_single_process_env
+    from distributed_pytorch_example_amd.parallel import dist as pdist
+    from distributed_pytorch_example_amd.parallel import DDP
+    from distributed_pytorch_example_amd.models import get_model
+    from distributed_pytorch_example_amd.optim import build_optimizer
+    from distributed_pytorch_example_amd.ops import functional as Fx
+
+    ensure_single_process_env()
+    rank, world, local_rank = pdist.init_process_group("auto")
+    if world != args.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    torch.manual_seed(1234 + rank)
+
+    if args.model == "resnet50":
+        bs = args.batch_size or 256
+        model = get_model("resnet50").to(dev)
+        opt_name, lr = args.optimizer or "sgd", args.lr or 0.1
+        wd = 5e-5
+        g = torch.Generator(device=dev)
+        g.manual_seed(99 + rank)
+        if dev.type == "cuda":
+            xs = [torch.randn(bs, 224, 224, 8, device=dev, generator=g).to(torch.bfloat16) for _ in range(args.nbatches)]
+            for x in xs:
+                x[..., 3:] = 0
+        else:
+            xs = [torch.randn(bs, 3, 224, 224, generator=g, device=dev) for _ in range(args.nbatches)]
+        ys = [torch.randint(0, 1000, (bs,), device=dev, generator=g) for _ in range(args.nbatches)]
+        samples_per_step = bs * args.grad_accum
+        unit_mult = 1
+        cfg = {"model": "resnet50-v1.5", "global_batch": bs * world * args.grad_accum, "seq_len": None,
+               "image": [3, 224, 224], "per_gpu_batch": bs, "grad_accum": args.grad_accum,
+               "bucket_mb": args.bucket_mb, "parallelism": f"dp{world}", "optimizer": "sgd-momentum0.9"}
+        metric, unit = METRIC, "samples/s"
+        num_classes = 1000
+    elif args.model == "gpt2":
+        bs = args.batch_size or 8
+        model = get_model("gpt2").to(dev)
+        opt_name, lr = args.optimizer or "adamw", args.lr or 6e-4
+        wd = 0.1
+        g = torch.Generator(device=dev)
+        g.manual_seed(99 + rank)
+        V = 50257
+        toks = [torch.randint(0, V, (bs, args.seq_len + 1), device=dev, generator=g) for _ in range(args.nbatches)]
+        xs = [t[:, :-1].contiguous() for t in toks]
+        ys = [t[:, 1:].contiguous() for t in toks]
+        samples_per_step = bs * args.seq_len * args.grad_accum
+        cfg = {"model": "gpt2-small-124M", "global_batch": bs * world * args.grad_accum, "seq_len": args.seq_len,
+               "parallelism": f"dp{world}", "optimizer": "adamw"}
+        metric, unit = "tokens/sec (whole node), GPT-2-small bf16", "tokens/s"
+        num_classes = V
+    else:
+        bs = args.batch_size or 64
+        model = get_model("simplenet").to(dev)
+        opt_name, lr = args.optimizer or "adam", args.lr or 1e-3
+        wd = 0.0
+        xs = [torch.randn(bs, 784, device=dev) for _ in range(args.nbatches)]
+        ys = [torch.randint(0, 10, (bs,), device=dev) for _ in range(args.nbatches)]
+        samples_per_step = bs * args.grad_accum
+        cfg = {"model": "simplenet-mlp", "global_batch": bs * world, "seq_len": None, "parallelism": f"dp{world}"}
+        metric, unit = "samples/sec (whole node), SimpleNet MLP", "samples/s"
+        num_classes = 10
+
+    ddp = DDP(model, bucket_cap_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb)
+    opt = build_optimizer(opt_name, model.parameters(), lr=lr, weight_decay=wd)
+
+    def step(i):
+        for a in range(args.grad_accum):
+            x, y = xs[(i * args.grad_accum + a) % len(xs)], ys[(i * args.grad_accum + a) % len(ys)]
+            last = a == args.grad_accum - 1
+            ctx = ddp.no_sync() if not last else _null()
+            with ctx:
+                out = ddp(x)
+                loss = Fx.cross_entropy(out, y, num_classes)
+                if args.grad_accum > 1:
+                    loss = loss / args.grad_accum
+                loss.backward()
+        opt.step()
+        for p in model.parameters():
+            p.grad = None  # buckets re-zeroed at next forward
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    _sync(dev)
+    pdist.barrier()
+    _sync(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(args.warmup + i)
+    _sync(dev)
+    pdist.barrier()
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = t.item()
+    ms = 1000.0 * dt / args.steps
+    value = samples_per_step * world * args.steps / dt
+    extra = {}
+    if args.bucket_timing and hasattr(ddp, "bucket_timings"):
+        extra["buckets"] = ddp.num_buckets()
+    if rank == 0:
+        line = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "bf16", "data": "synthetic (device-resident, random)",
+                "config": cfg, "loss": float(loss.item())}
+        line.update(extra)
+        print(json.dumps(line), flush=True)
+    pdist.destroy_process_group()
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,599 @@
+// pybind11 bindings for the gfx950 kernels.  Every entry point validates
+// device / dtype / layout and fails loudly (no silent fallback), picks the
+// launch configuration (tile shape, split-K) and enqueues on torch's current
+// HIP stream, so the ops compose with the caching allocator and hipGraph
+// capture (no host sync, no hipMalloc inside).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include "../kernels/igemm.h"
+
+using at::Tensor;
+
+extern "C" {
+int dpe_bn_stats_nblocks(int64_t M, int C);
+int dpe_bn_stats(const uint16_t* x, int64_t M, int C, int nb, float* part, hipStream_t st);
+int dpe_bn_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* beta, float* rmean,
+                    float* rvar, float momentum, float eps, float* coef, hipStream_t st);
+int dpe_bn_eval_coeff(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
+                      float* coef, hipStream_t st);
+int dpe_bn_apply(const uint16_t* x, const uint16_t* res, uint16_t* y, int64_t M, int C, const float* coef, int relu,
+                 hipStream_t st);
+int dpe_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* coef, int64_t M, int C, int nb,
+                      float* part, hipStream_t st);
+int dpe_bn_bwd_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* coef, float* dgamma,
+                        float* dbeta, float* bcoef, hipStream_t st);
+int dpe_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* bcoef, uint16_t* dx,
+                     uint16_t* dz_out, int64_t M, int C, hipStream_t st);
+int dpe_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int k, int s,
+                    int p, hipStream_t st);
+int dpe_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int OH, int OW, int k,
+                    int s, int p, hipStream_t st);
+int dpe_gavgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st);
+int dpe_gavgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st);
+int dpe_cross_entropy(const void* logits, int in_bf16, const int64_t* labels, int B, int V, int64_t ld, float grad_scale,
+                      void* dlogits, int out_bf16, float* loss_rows, float* loss_sum, float* correct, int ignore_index,
+                      hipStream_t st);
+int dpe_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st);
+int dpe_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
+int dpe_act(const void* a, const void* b, void* out, int64_t n, int op, int bf16, hipStream_t st);
+int dpe_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset, int bf16, hipStream_t st);
+int dpe_add(const void* a, const void* b, void* out, int64_t n, float alpha, int bf16, hipStream_t st);
+int dpe_colsum(const void* dy, int64_t M, int N, int64_t ld, float* db, int accumulate, int bf16, hipStream_t st);
+int dpe_nchw_to_nhwc(const float* x, uint16_t* y, int N, int C, int HW, int Cp, hipStream_t st);
+int dpe_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* wpe, float* out, int64_t rows, int T, int D,
+                      hipStream_t st);
+int dpe_embedding_bwd(const int64_t* idx, const float* dout, float* dwte, float* dwpe, int64_t rows, int T, int D,
+                      hipStream_t st);
+int dpe_optim_chunk_size();
+int dpe_optim_desc_bytes();
+int dpe_optim_step(int kind, const void* desc, const void* chunks, int nchunks, const float* hp, const float* steps,
+                   hipStream_t st);
+int dpe_layernorm_fwd(const void* x, int x_bf16, const float* w, const float* b, uint16_t* y, float* mean, float* rstd,
+                      int64_t rows, int D, float eps, hipStream_t st);
+int dpe_layernorm_bwd(const uint16_t* dy, const void* x, int x_bf16, const float* w, const float* mean, const float* rstd,
+                      void* dx, int dx_accumulate_f32, float* dw, float* db, float* part, int64_t rows, int D,
+                      hipStream_t st);
+int dpe_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int T, int H, int D, float scale, int causal,
+                 hipStream_t st);
+int dpe_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
+                 float* dq_acc, uint16_t* dqkv, int B, int T, int H, int D, float scale, int causal, hipStream_t st);
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_GPU(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+#define CHECK_RC(rc, what)                                                                          \
+  do {                                                                                              \
+    const int rc_ = (rc);                                                                           \
+    const hipError_t e_ = hipGetLastError();                                                        \
+    TORCH_CHECK(rc_ == 0 && e_ == hipSuccess, "dpe kernel launch failed: " what " rc=", rc_, " hip=", \
+                hipGetErrorString(e_));                                                             \
+  } while (0)
+
+inline const uint16_t* bp(const Tensor& t) { return (const uint16_t*)t.data_ptr(); }
+inline uint16_t* bpm(const Tensor& t) { return (uint16_t*)t.data_ptr(); }
+inline float* fp(const Tensor& t) { return (float*)t.data_ptr(); }
+inline const float* fpo(const c10::optional<Tensor>& t) { return t.has_value() && t->defined() ? (const float*)t->data_ptr() : nullptr; }
+inline float* fpom(const c10::optional<Tensor>& t) { return t.has_value() && t->defined() ? (float*)t->data_ptr() : nullptr; }
+
+// --------------------------------------------------------------- GEMM tiling
+struct Cfg { int bm, bn, splits, k_split; };
+
+Cfg pick_cfg(int64_t M, int64_t N, int64_t K, bool allow_split) {
+  Cfg c{128, N <= 64 ? 64 : 128, 1, (int)((K + 31) / 32 * 32)};
+  auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  const int64_t target = 512;  // >= 2 workgroups per CU on 256 CUs
+  if (tiles(c.bm, c.bn) < target && M <= 64) c.bm = 64;
+  if (tiles(c.bm, c.bn) < target && c.bn == 128 && c.bm == 128 && tiles(128, 64) <= tiles(64, 128)) c.bn = 64;
+  if (tiles(c.bm, c.bn) < target && c.bm == 128) c.bm = 64;
+  if (tiles(c.bm, c.bn) < target && c.bn == 128) c.bn = 64;
+  if (allow_split) {
+    const int64_t t = tiles(c.bm, c.bn);
+    int64_t splits = (1024 + t - 1) / t;
+    const int64_t ksteps = (K + 31) / 32;
+    const int64_t max_splits = std::max<int64_t>(1, ksteps / 4);  // >= 4 K-steps per split
+    splits = std::min(splits, max_splits);
+    if (splits < 1) splits = 1;
+    const int64_t kps = (ksteps + splits - 1) / splits;
+    c.k_split = (int)(kps * 32);
+    c.splits = (int)((ksteps + kps - 1) / kps);
+  }
+  return c;
+}
+
+void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_split) {
+  Cfg c = pick_cfg(a.M, a.N, a.K, allow_split && epi == dpe::EPI_ATOMIC_F32);
+  a.k_split = c.k_split;
+  const int rc = dpe_igemm_launch(&a, c.bm, c.bn, aload, bload, epi, c.splits, cur_stream());
+  const hipError_t e = hipGetLastError();
+  TORCH_CHECK(e == hipSuccess, "igemm launch failed: ", hipGetErrorString(e));
+  TORCH_CHECK(rc == 0, "igemm: unsupported configuration (aload=", aload, " bload=", bload, " epi=", epi, ") rc=", rc);
+}
+
+dpe::IgemmArgs base_args() {
+  dpe::IgemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.alpha = 1.f;
+  return a;
+}
+
+// -------------------------------------------------------------- dense GEMMs
+// y[M,N] = act(x[M,K] @ w[N,K]^T + bias) (+ residual)
+Tensor linear_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, int64_t act, bool out_f32,
+                  const c10::optional<Tensor>& residual, const c10::optional<Tensor>& out) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(w);
+  TORCH_CHECK(x.stride(-1) == 1, "x must have unit inner stride");
+  const int64_t K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "linear: weight shape mismatch");
+  TORCH_CHECK(K % 8 == 0, "linear: in_features must be a multiple of 8");
+  Tensor x2 = x.reshape({-1, K});
+  TORCH_CHECK(x2.stride(0) % 8 == 0, "x row stride must be a multiple of 8");
+  const int64_t M = x2.size(0);
+  auto sizes = x.sizes().vec();
+  sizes.back() = N;
+  Tensor y;
+  if (out.has_value() && out->defined()) {
+    y = *out;
+    TORCH_CHECK(y.numel() == M * N && y.is_contiguous(), "linear: bad out tensor");
+  } else {
+    y = at::empty(sizes, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  }
+  auto a = base_args();
+  a.A = bp(x2); a.B = bp(w); a.C = y.data_ptr();
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  a.lda = x2.stride(0); a.ldb = K; a.ldc = N;
+  a.bias = fpo(bias);
+  a.act = (int)act;
+  if (residual.has_value() && residual->defined()) {
+    TORCH_CHECK(!out_f32, "residual add only for bf16 outputs");
+    CHECK_BF16((*residual)); CHECK_CONTIG((*residual));
+    a.residual = bp(*residual);
+  }
+  run_igemm(a, dpe::A_DENSE_K, dpe::B_DENSE_K, out_f32 ? dpe::EPI_F32 : dpe::EPI_BF16, false);
+  return y;
+}
+
+// dx[M,K] = dy[M,N] @ w[N,K]
+Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const c10::optional<Tensor>& residual) {
+  CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(dy);
+  const int64_t N = w.size(0), K = w.size(1);
+  TORCH_CHECK(dy.size(-1) == N, "linear_dgrad: shape mismatch");
+  TORCH_CHECK(N % 8 == 0 && K % 8 == 0, "linear_dgrad: features must be multiples of 8");
+  const int64_t M = dy.numel() / N;
+  auto sizes = dy.sizes().vec();
+  sizes.back() = K;
+  Tensor dx = at::empty(sizes, dy.options());
+  auto a = base_args();
+  a.A = bp(dy); a.B = bp(w); a.C = dx.data_ptr();
+  a.M = (int)M; a.N = (int)K; a.K = (int)N;
+  a.lda = N; a.ldb = K; a.ldc = K;
+  if (residual.has_value() && residual->defined()) { CHECK_BF16((*residual)); CHECK_CONTIG((*residual)); a.residual = bp(*residual); }
+  run_igemm(a, dpe::A_DENSE_K, dpe::B_DENSE_N, dpe::EPI_BF16, false);
+  return dx;
+}
+
+// dw[N,K] (+)= dy[M,N]^T @ x[M,K]   (fp32, atomic split-K; dw must be zeroed or hold an accumulation)
+void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha) {
+  CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(x); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
+  const int64_t N = dw.size(0), K = dw.size(1);
+  TORCH_CHECK(dy.size(-1) == N && x.size(-1) == K && dy.numel() / N == x.numel() / K, "linear_wgrad: shape mismatch");
+  TORCH_CHECK(N % 8 == 0 && K % 8 == 0, "linear_wgrad: features must be multiples of 8");
+  const int64_t M = dy.numel() / N;
+  auto a = base_args();
+  a.A = bp(dy); a.B = bp(x); a.C = dw.data_ptr();
+  a.M = (int)N; a.N = (int)K; a.K = (int)M;
+  a.lda = N; a.ldb = K; a.ldc = K;
+  a.alpha = (float)alpha;
+  run_igemm(a, dpe::A_DENSE_M, dpe::B_DENSE_N, dpe::EPI_ATOMIC_F32, true);
+}
+
+// ------------------------------------------------------------------- conv
+dpe::ConvGeom geom(const Tensor& x, const Tensor& w, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
+                   int64_t OH, int64_t OW) {
+  dpe::ConvGeom g;
+  g.N = (int)x.size(0); g.H = (int)x.size(1); g.W = (int)x.size(2); g.C = (int)x.size(3);
+  g.K = (int)w.size(0); g.R = (int)w.size(1); g.S = (int)w.size(2);
+  g.sh = (int)sh; g.sw = (int)sw; g.ph = (int)ph; g.pw = (int)pw; g.dh = (int)dh; g.dw = (int)dw;
+  g.OH = (int)OH; g.OW = (int)OW;
+  return g;
+}
+
+bool is_pointwise(const dpe::ConvGeom& g) {
+  return g.R == 1 && g.S == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0;
+}
+
+// x NHWC bf16 [N,H,W,C], w [K,R,S,C] bf16 -> y NHWC [N,OH,OW,K]
+Tensor conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64_t> stride, std::vector<int64_t> pad,
+                std::vector<int64_t> dil, const c10::optional<Tensor>& col_stats, const c10::optional<Tensor>& bias) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && x.size(3) == w.size(3), "conv: NHWC x / KRSC w shape mismatch");
+  TORCH_CHECK(x.size(3) % 8 == 0 && w.size(0) % 8 == 0, "conv: channels must be multiples of 8");
+  const int64_t H = x.size(1), W = x.size(2), R = w.size(1), S = w.size(2);
+  const int64_t OH = (H + 2 * pad[0] - dil[0] * (R - 1) - 1) / stride[0] + 1;
+  const int64_t OW = (W + 2 * pad[1] - dil[1] * (S - 1) - 1) / stride[1] + 1;
+  Tensor y = at::empty({x.size(0), OH, OW, w.size(0)}, x.options());
+  auto g = geom(x, w, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], OH, OW);
+  auto a = base_args();
+  a.g = g;
+  a.A = bp(x); a.B = bp(w); a.C = y.data_ptr();
+  a.M = (int)(x.size(0) * OH * OW); a.N = g.K; a.K = (int)(R * S * g.C);
+  a.lda = g.C; a.ldb = a.K; a.ldc = g.K;
+  a.bias = fpo(bias);
+  if (col_stats.has_value() && col_stats->defined()) {
+    CHECK_F32((*col_stats));
+    TORCH_CHECK(col_stats->numel() >= 2 * g.K, "col_stats must hold 2*K floats");
+    a.col_stats = fp(*col_stats);
+  }
+  run_igemm(a, is_pointwise(g) ? dpe::A_DENSE_K : dpe::A_CONV_FWD, dpe::B_DENSE_K, dpe::EPI_BF16, false);
+  return y;
+}
+
+// dx NHWC [N,H,W,C] = conv_transpose(dy, w); optional residual added into dx
+Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape, std::vector<int64_t> stride,
+                  std::vector<int64_t> pad, std::vector<int64_t> dil, const c10::optional<Tensor>& residual) {
+  CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(w); CHECK_CONTIG(dy); CHECK_CONTIG(w);
+  Tensor dx = at::empty(xshape, dy.options());
+  auto g = geom(dx, w, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], dy.size(1), dy.size(2));
+  TORCH_CHECK(dy.size(3) == g.K && dy.size(0) == g.N, "conv_dgrad: dy shape mismatch");
+  auto a = base_args();
+  a.g = g;
+  a.A = bp(dy); a.B = bp(w); a.C = dx.data_ptr();
+  a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.K;
+  a.lda = g.K; a.ldb = g.C; a.ldc = g.C;
+  if (residual.has_value() && residual->defined()) { CHECK_BF16((*residual)); CHECK_CONTIG((*residual)); a.residual = bp(*residual); }
+  if (is_pointwise(g)) run_igemm(a, dpe::A_DENSE_K, dpe::B_DENSE_N, dpe::EPI_BF16, false);
+  else run_igemm(a, dpe::A_CONV_DGRAD, dpe::B_CONV_DGRAD, dpe::EPI_BF16, false);
+  return dx;
+}
+
+// dw [K,R,S,C] fp32 (+)= alpha * dy^T (x) im2col(x)
+void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64_t> stride, std::vector<int64_t> pad,
+                std::vector<int64_t> dil, double alpha) {
+  CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(x); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
+  auto g = geom(x, dw, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], dy.size(1), dy.size(2));
+  TORCH_CHECK(dy.size(3) == g.K && dy.size(0) == g.N, "conv_wgrad: dy shape mismatch");
+  auto a = base_args();
+  a.g = g;
+  a.A = bp(dy); a.B = bp(x); a.C = dw.data_ptr();
+  a.M = g.K; a.N = g.R * g.S * g.C; a.K = g.N * g.OH * g.OW;
+  a.lda = g.K; a.ldb = g.C; a.ldc = a.N;
+  a.alpha = (float)alpha;
+  run_igemm(a, dpe::A_DENSE_M, is_pointwise(g) ? dpe::B_DENSE_N : dpe::B_CONV_WGRAD, dpe::EPI_ATOMIC_F32, true);
+}
+
+// --------------------------------------------------------------- BatchNorm
+int64_t rows_of(const Tensor& x) { return x.numel() / x.size(-1); }
+
+// returns (y, coef[4][C]); stats: optional precomputed [2][C] column sums (from conv epilogue)
+std::vector<Tensor> bn_fwd_train(const Tensor& x, const c10::optional<Tensor>& gamma, const c10::optional<Tensor>& beta,
+                                 const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar, double momentum,
+                                 double eps, bool relu, const c10::optional<Tensor>& residual,
+                                 const c10::optional<Tensor>& stats) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  const int64_t C = x.size(-1), M = rows_of(x);
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn: C must be a multiple of 8 and <= 2048");
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor coef = at::empty({4, C}, fo);
+  hipStream_t st = cur_stream();
+  if (stats.has_value() && stats->defined()) {
+    CHECK_RC(dpe_bn_finalize(fp(*stats), 1, (int)C, M, fpo(gamma), fpo(beta), fpom(rmean), fpom(rvar), (float)momentum,
+                             (float)eps, fp(coef), st), "bn_finalize");
+  } else {
+    const int nb = dpe_bn_stats_nblocks(M, (int)C);
+    Tensor part = at::empty({nb, 2, C}, fo);
+    CHECK_RC(dpe_bn_stats(bp(x), M, (int)C, nb, fp(part), st), "bn_stats");
+    CHECK_RC(dpe_bn_finalize(fp(part), nb, (int)C, M, fpo(gamma), fpo(beta), fpom(rmean), fpom(rvar), (float)momentum,
+                             (float)eps, fp(coef), st), "bn_finalize");
+  }
+  Tensor y = at::empty_like(x);
+  const uint16_t* res = nullptr;
+  if (residual.has_value() && residual->defined()) { CHECK_BF16((*residual)); CHECK_CONTIG((*residual)); res = bp(*residual); }
+  CHECK_RC(dpe_bn_apply(bp(x), res, bpm(y), M, (int)C, fp(coef), relu ? 1 : 0, st), "bn_apply");
+  return {y, coef};
+}
+
+Tensor bn_fwd_eval(const Tensor& x, const c10::optional<Tensor>& gamma, const c10::optional<Tensor>& beta,
+                   const Tensor& rmean, const Tensor& rvar, double eps, bool relu, const c10::optional<Tensor>& residual) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  const int64_t C = x.size(-1), M = rows_of(x);
+  Tensor coef = at::empty({4, C}, x.options().dtype(at::kFloat));
+  hipStream_t st = cur_stream();
+  CHECK_RC(dpe_bn_eval_coeff((int)C, fpo(gamma), fpo(beta), fp(rmean), fp(rvar), (float)eps, fp(coef), st), "bn_eval");
+  Tensor y = at::empty_like(x);
+  const uint16_t* res = nullptr;
+  if (residual.has_value() && residual->defined()) res = bp(*residual);
+  CHECK_RC(dpe_bn_apply(bp(x), res, bpm(y), M, (int)C, fp(coef), relu ? 1 : 0, st), "bn_apply");
+  return y;
+}
+
+// returns (dx, dz or empty); dgamma/dbeta accumulated (+=) if given
+std::vector<Tensor> bn_bwd(const Tensor& dy, const c10::optional<Tensor>& y, const Tensor& x,
+                           const c10::optional<Tensor>& gamma, const Tensor& coef, const c10::optional<Tensor>& dgamma,
+                           const c10::optional<Tensor>& dbeta, bool want_dz) {
+  CHECK_GPU(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x);
+  const int64_t C = x.size(-1), M = rows_of(x);
+  const uint16_t* yp = (y.has_value() && y->defined()) ? bp(*y) : nullptr;
+  hipStream_t st = cur_stream();
+  auto fo = x.options().dtype(at::kFloat);
+  const int nb = dpe_bn_stats_nblocks(M, (int)C);
+  Tensor part = at::empty({nb, 2, C}, fo);
+  CHECK_RC(dpe_bn_bwd_reduce(bp(dy), yp, bp(x), fp(coef), M, (int)C, nb, fp(part), st), "bn_bwd_reduce");
+  Tensor bcoef = at::empty({3, C}, fo);
+  CHECK_RC(dpe_bn_bwd_finalize(fp(part), nb, (int)C, M, fpo(gamma), fp(coef), fpom(dgamma), fpom(dbeta), fp(bcoef), st),
+           "bn_bwd_finalize");
+  Tensor dx = at::empty_like(x);
+  Tensor dz;
+  if (want_dz) dz = at::empty_like(x);
+  CHECK_RC(dpe_bn_bwd_apply(bp(dy), yp, bp(x), fp(bcoef), bpm(dx), want_dz ? bpm(dz) : nullptr, M, (int)C, st),
+           "bn_bwd_apply");
+  return {dx, dz};
+}
+
+// ----------------------------------------------------------------- pooling
+std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int64_t OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
+  Tensor y = at::empty({N, OH, OW, C}, x.options());
+  Tensor idx = at::empty({N, OH, OW, C}, x.options().dtype(at::kByte));
+  CHECK_RC(dpe_maxpool_fwd(bp(x), bpm(y), (uint8_t*)idx.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k,
+                           (int)s, (int)p, cur_stream()), "maxpool_fwd");
+  return {y, idx};
+}
+
+Tensor maxpool_bwd(const Tensor& dy, const Tensor& idx, std::vector<int64_t> xshape, int64_t k, int64_t s, int64_t p) {
+  CHECK_GPU(dy); CHECK_BF16(dy); CHECK_CONTIG(dy);
+  Tensor dx = at::empty(xshape, dy.options());
+  CHECK_RC(dpe_maxpool_bwd(bp(dy), (const uint8_t*)idx.data_ptr(), bpm(dx), (int)xshape[0], (int)xshape[1], (int)xshape[2],
+                           (int)xshape[3], (int)dy.size(1), (int)dy.size(2), (int)k, (int)s, (int)p, cur_stream()),
+           "maxpool_bwd");
+  return dx;
+}
+
+Tensor gavgpool_fwd(const Tensor& x) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  const int64_t N = x.size(0), C = x.size(-1), HW = x.numel() / (N * C);
+  Tensor y = at::empty({N, C}, x.options());
+  CHECK_RC(dpe_gavgpool_fwd(bp(x), bpm(y), (int)N, (int)HW, (int)C, cur_stream()), "gavgpool_fwd");
+  return y;
+}
+
+Tensor gavgpool_bwd(const Tensor& dy, std::vector<int64_t> xshape) {
+  CHECK_GPU(dy); CHECK_BF16(dy); CHECK_CONTIG(dy);
+  Tensor dx = at::empty(xshape, dy.options());
+  const int64_t N = xshape[0], C = xshape.back(), HW = dx.numel() / (N * C);
+  CHECK_RC(dpe_gavgpool_bwd(bp(dy), bpm(dx), (int)N, (int)HW, (int)C, cur_stream()), "gavgpool_bwd");
+  return dx;
+}
+
+// ------------------------------------------------------------------- loss
+// returns (loss_rows [B] f32, loss_sum [1], correct [1], dlogits or empty)
+std::vector<Tensor> cross_entropy(const Tensor& logits, const Tensor& labels, int64_t V, double grad_scale, bool want_grad,
+                                  bool grad_bf16, int64_t ignore_index) {
+  CHECK_GPU(logits); CHECK_CONTIG(logits); CHECK_CONTIG(labels);
+  TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
+  const bool in_bf16 = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(in_bf16 || logits.scalar_type() == at::kFloat, "logits must be f32 or bf16");
+  const int64_t ld = logits.size(-1), B = logits.numel() / ld;
+  TORCH_CHECK(labels.numel() == B, "labels size mismatch");
+  auto fo = logits.options().dtype(at::kFloat);
+  Tensor rows = at::empty({B}, fo);
+  Tensor sums = at::zeros({2}, fo);
+  Tensor d;
+  if (want_grad) d = at::empty(logits.sizes(), logits.options().dtype(grad_bf16 ? at::kBFloat16 : at::kFloat));
+  CHECK_RC(dpe_cross_entropy(logits.data_ptr(), in_bf16, (const int64_t*)labels.data_ptr(), (int)B, (int)V, ld,
+                             (float)grad_scale, want_grad ? d.data_ptr() : nullptr, grad_bf16, fp(rows), fp(sums),
+                             fp(sums) + 1, (int)ignore_index, cur_stream()), "cross_entropy");
+  return {rows, sums.slice(0, 0, 1), sums.slice(0, 1, 2), d};
+}
+
+// ---------------------------------------------------------------- eltwise
+Tensor cast_bf16(const Tensor& x, const c10::optional<Tensor>& out) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  Tensor y = (out.has_value() && out->defined()) ? *out : at::empty(x.sizes(), x.options().dtype(at::kBFloat16));
+  TORCH_CHECK(y.numel() == x.numel() && y.is_contiguous() && y.scalar_type() == at::kBFloat16, "cast_bf16: bad out");
+  CHECK_RC(dpe_cast_f32_bf16(fp(x), bpm(y), x.numel(), cur_stream()), "cast");
+  return y;
+}
+
+Tensor cast_f32(const Tensor& x) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  Tensor y = at::empty(x.sizes(), x.options().dtype(at::kFloat));
+  CHECK_RC(dpe_cast_bf16_f32(bp(x), fp(y), x.numel(), cur_stream()), "cast");
+  return y;
+}
+
+// op: 0 relu, 1 relu_bwd(dy, y), 2 gelu, 3 gelu_bwd(dy, x)
+Tensor act(const Tensor& a, const c10::optional<Tensor>& b, int64_t op) {
+  CHECK_GPU(a); CHECK_CONTIG(a);
+  const bool bf = a.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || a.scalar_type() == at::kFloat, "act: f32/bf16 only");
+  Tensor out = at::empty_like(a);
+  const void* bpv = (b.has_value() && b->defined()) ? b->data_ptr() : nullptr;
+  if (op == 1 || op == 3) TORCH_CHECK(bpv && b->is_contiguous() && b->scalar_type() == a.scalar_type(), "act: second operand");
+  CHECK_RC(dpe_act(a.data_ptr(), bpv, out.data_ptr(), a.numel(), (int)op, bf, cur_stream()), "act");
+  return out;
+}
+
+Tensor dropout(const Tensor& x, double p, int64_t seed, int64_t offset) {
+  CHECK_GPU(x); CHECK_CONTIG(x);
+  const bool bf = x.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || x.scalar_type() == at::kFloat, "dropout: f32/bf16 only");
+  Tensor y = at::empty_like(x);
+  CHECK_RC(dpe_dropout(x.data_ptr(), y.data_ptr(), x.numel(), (float)p, (uint64_t)seed, (uint64_t)offset, bf, cur_stream()),
+           "dropout");
+  return y;
+}
+
+Tensor add(const Tensor& a, const Tensor& b, double alpha) {
+  CHECK_GPU(a); CHECK_CONTIG(a); CHECK_CONTIG(b);
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() && a.numel() == b.numel(), "add: mismatch");
+  const bool bf = a.scalar_type() == at::kBFloat16;
+  Tensor out = at::empty_like(a);
+  CHECK_RC(dpe_add(a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), (float)alpha, bf, cur_stream()), "add");
+  return out;
+}
+
+void colsum(const Tensor& dy, Tensor& db, bool accumulate) {
+  CHECK_GPU(dy); CHECK_CONTIG(dy); CHECK_F32(db);
+  const int64_t N = dy.size(-1), M = dy.numel() / N;
+  const bool bf = dy.scalar_type() == at::kBFloat16;
+  CHECK_RC(dpe_colsum(dy.data_ptr(), M, (int)N, N, fp(db), accumulate ? 1 : 0, bf, cur_stream()), "colsum");
+}
+
+Tensor nchw_to_nhwc(const Tensor& x, int64_t cpad) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Cp = std::max<int64_t>(C, cpad);
+  Tensor y = at::empty({N, H, W, Cp}, x.options().dtype(at::kBFloat16));
+  CHECK_RC(dpe_nchw_to_nhwc(fp(x), bpm(y), (int)N, (int)C, (int)(H * W), (int)Cp, cur_stream()), "nchw_to_nhwc");
+  return y;
+}
+
+Tensor embedding_fwd(const Tensor& idx, const Tensor& wte, const c10::optional<Tensor>& wpe) {
+  CHECK_GPU(idx); CHECK_CONTIG(idx); CHECK_BF16(wte); CHECK_CONTIG(wte);
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.dim() == 2, "embedding: idx must be int64 [B,T]");
+  const int64_t B = idx.size(0), T = idx.size(1), D = wte.size(1);
+  Tensor out = at::empty({B, T, D}, wte.options().dtype(at::kFloat));
+  const uint16_t* pe = (wpe.has_value() && wpe->defined()) ? bp(*wpe) : nullptr;
+  CHECK_RC(dpe_embedding_fwd((const int64_t*)idx.data_ptr(), bp(wte), pe, fp(out), B * T, (int)T, (int)D, cur_stream()),
+           "embedding_fwd");
+  return out;
+}
+
+void embedding_bwd(const Tensor& idx, const Tensor& dout, Tensor& dwte, const c10::optional<Tensor>& dwpe) {
+  CHECK_GPU(dout); CHECK_F32(dout); CHECK_CONTIG(dout); CHECK_F32(dwte);
+  const int64_t B = idx.size(0), T = idx.size(1), D = dwte.size(1);
+  CHECK_RC(dpe_embedding_bwd((const int64_t*)idx.data_ptr(), fp(dout), fp(dwte), fpom(dwpe), B * T, (int)T, (int)D,
+                             cur_stream()), "embedding_bwd");
+}
+
+// --------------------------------------------------------------- optimizer
+void optim_step(int64_t kind, const Tensor& desc, const Tensor& chunks, const Tensor& hp, const Tensor& steps) {
+  CHECK_GPU(desc); CHECK_GPU(chunks); CHECK_GPU(hp); CHECK_GPU(steps); CHECK_F32(hp); CHECK_F32(steps);
+  TORCH_CHECK(chunks.scalar_type() == at::kInt && chunks.dim() == 2 && chunks.size(1) == 2, "chunks must be int32 [n,2]");
+  CHECK_RC(dpe_optim_step((int)kind, desc.data_ptr(), chunks.data_ptr(), (int)chunks.size(0), fp(hp), fp(steps), cur_stream()),
+           "optim_step");
+}
+
+// -------------------------------------------------------------- LayerNorm
+// x [rows, D] (f32 or bf16) -> y bf16, mean/rstd f32 [rows]
+std::vector<Tensor> layernorm_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& b, double eps) {
+  CHECK_GPU(x); CHECK_CONTIG(x); CHECK_F32(w);
+  const bool xb = x.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(xb || x.scalar_type() == at::kFloat, "layernorm: f32/bf16 input");
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && D <= 8192, "layernorm: D must be a multiple of 8 and <= 8192");
+  Tensor y = at::empty(x.sizes(), x.options().dtype(at::kBFloat16));
+  Tensor mean = at::empty({rows}, x.options().dtype(at::kFloat));
+  Tensor rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  CHECK_RC(dpe_layernorm_fwd(x.data_ptr(), xb, fp(w), fpo(b), bpm(y), fp(mean), fp(rstd), rows, (int)D, (float)eps,
+                             cur_stream()), "layernorm_fwd");
+  return {y, mean, rstd};
+}
+
+// dx: if dx_out (f32) given, dx is ACCUMULATED into it (residual stream); else a new tensor of x's dtype
+Tensor layernorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const Tensor& mean, const Tensor& rstd, Tensor& dw,
+                     const c10::optional<Tensor>& db, const c10::optional<Tensor>& dx_out) {
+  CHECK_GPU(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw);
+  const bool xb = x.scalar_type() == at::kBFloat16;
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  Tensor dx;
+  bool acc = false;
+  if (dx_out.has_value() && dx_out->defined()) {
+    dx = *dx_out;
+    CHECK_F32(dx); CHECK_CONTIG(dx);
+    acc = true;
+  } else {
+    dx = at::empty_like(x);
+  }
+  const int nb = (int)std::min<int64_t>(512, (rows + 31) / 32);
+  Tensor part = at::empty({nb, 2, D}, x.options().dtype(at::kFloat));
+  CHECK_RC(dpe_layernorm_bwd(bp(dy), x.data_ptr(), xb, fp(w), fp(mean), fp(rstd), dx.data_ptr(), acc ? 1 : 0, fp(dw),
+                             fpom(db), fp(part), rows, (int)D, cur_stream()), "layernorm_bwd");
+  return dx;
+}
+
+// ---------------------------------------------------------------- attention
+// qkv: [B, T, 3, H, D] bf16 -> out [B, T, H, D] bf16, lse [B, H, T] f32
+std::vector<Tensor> attn_fwd(const Tensor& qkv, int64_t H, double scale, bool causal) {
+  CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_CONTIG(qkv);
+  const int64_t B = qkv.size(0), T = qkv.size(1), D = qkv.size(-1);
+  TORCH_CHECK(qkv.numel() == B * T * 3 * H * D, "attn: qkv must be [B,T,3,H,D]");
+  TORCH_CHECK(D == 64, "attn: head dim 64 supported");
+  Tensor out = at::empty({B, T, H, D}, qkv.options());
+  Tensor lse = at::empty({B, H, T}, qkv.options().dtype(at::kFloat));
+  CHECK_RC(dpe_attn_fwd(bp(qkv), bpm(out), fp(lse), (int)B, (int)T, (int)H, (int)D, (float)scale, causal, cur_stream()),
+           "attn_fwd");
+  return {out, lse};
+}
+
+Tensor attn_bwd(const Tensor& qkv, const Tensor& out, const Tensor& dout, const Tensor& lse, int64_t H, double scale,
+                bool causal) {
+  CHECK_GPU(qkv); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_CONTIG(out);
+  const int64_t B = qkv.size(0), T = qkv.size(1), D = qkv.size(-1);
+  Tensor dqkv = at::empty_like(qkv);
+  Tensor delta = at::empty({B, H, T}, qkv.options().dtype(at::kFloat));
+  Tensor dq = at::zeros({B, T, H, D}, qkv.options().dtype(at::kFloat));
+  CHECK_RC(dpe_attn_bwd(bp(qkv), bp(out), bp(dout), fp(lse), fp(delta), fp(dq), bpm(dqkv), (int)B, (int)T, (int)H, (int)D,
+                        (float)scale, causal, cur_stream()), "attn_bwd");
+  return dqkv;
+}
+
+}  // namespace
+
+void register_ops(pybind11::module& m) {
+  namespace py = pybind11;
+  using c10::optional;
+  m.def("linear_fwd", &linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("act") = 0,
+        py::arg("out_f32") = false, py::arg("residual") = py::none(), py::arg("out") = py::none());
+  m.def("linear_dgrad", &linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("residual") = py::none());
+  m.def("linear_wgrad", &linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("alpha") = 1.0);
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
+        py::arg("col_stats") = py::none(), py::arg("bias") = py::none());
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"), py::arg("pad"),
+        py::arg("dil"), py::arg("residual") = py::none());
+  m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
+        py::arg("dil"), py::arg("alpha") = 1.0);
+  m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),
+        py::arg("momentum"), py::arg("eps"), py::arg("relu"), py::arg("residual") = py::none(), py::arg("stats") = py::none());
+  m.def("bn_fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),
+        py::arg("eps"), py::arg("relu"), py::arg("residual") = py::none());
+  m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("coef"), py::arg("dgamma"),
+        py::arg("dbeta"), py::arg("want_dz") = false);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("gavgpool_fwd", &gavgpool_fwd);
+  m.def("gavgpool_bwd", &gavgpool_bwd);
+  m.def("cross_entropy", &cross_entropy, py::arg("logits"), py::arg("labels"), py::arg("V"), py::arg("grad_scale"),
+        py::arg("want_grad"), py::arg("grad_bf16"), py::arg("ignore_index") = -100);
+  m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("out") = py::none());
+  m.def("cast_f32", &cast_f32);
+  m.def("act", &act, py::arg("a"), py::arg("b") = py::none(), py::arg("op") = 0);
+  m.def("dropout", &dropout);
+  m.def("add", &add, py::arg("a"), py::arg("b"), py::arg("alpha") = 1.0);
+  m.def("colsum", &colsum, py::arg("dy"), py::arg("db"), py::arg("accumulate") = false);
+  m.def("nchw_to_nhwc", &nchw_to_nhwc, py::arg("x"), py::arg("cpad") = 8);
+  m.def("embedding_fwd", &embedding_fwd, py::arg("idx"), py::arg("wte"), py::arg("wpe") = py::none());
+  m.def("embedding_bwd", &embedding_bwd, py::arg("idx"), py::arg("dout"), py::arg("dwte"), py::arg("dwpe") = py::none());
+  m.def("optim_step", &optim_step);
+  m.def("optim_chunk_size", []() { return dpe_optim_chunk_size(); });
+  m.def("optim_desc_bytes", []() { return dpe_optim_desc_bytes(); });
+  m.def("layernorm_fwd", &layernorm_fwd, py::arg("x"), py::arg("w"), py::arg("b") = py::none(), py::arg("eps") = 1e-5);
+  m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
+        py::arg("dw"), py::arg("db") = py::none(), py::arg("dx_out") = py::none());
+  m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("H"), py::arg("scale"), py::arg("causal") = true);
+  m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("H"),
+        py::arg("scale"), py::arg("causal") = true);
+  m.def("pick_gemm_cfg", [](int64_t M, int64_t N, int64_t K, bool split) {
+    auto c = pick_cfg(M, N, K, split);
+    return std::make_tuple(c.bm, c.bn, c.splits, c.k_split);
+  });
+}

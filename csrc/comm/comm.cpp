@@ -1,0 +1,299 @@
+// RCCL communicator and bucketed DDP reducer.  See comm.h.
+//
+// Reference parity: C3 (init broadcast) -> Communicator::broadcast;
+// C4 (per-backward bucket all-reduce, 25 MiB buckets, 1 MiB first) ->
+// Reducer; C6/C8 barriers -> Communicator::barrier; C7 metric all-reduce ->
+// Communicator::all_reduce.  Unlike gloo (host-staged TCP ring) the data
+// never leaves HBM: RCCL moves it over xGMI from a side stream.
+#include "comm.h"
+
+#include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <stdexcept>
+
+namespace dpe {
+
+#define NCCL_CHECK(cmd)                                                                       \
+  do {                                                                                        \
+    ncclResult_t r_ = (cmd);                                                                  \
+    if (r_ != ncclSuccess && r_ != ncclInProgress)                                            \
+      throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(r_) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));                    \
+  } while (0)
+
+#define HIP_CHECK(cmd)                                                                              \
+  do {                                                                                              \
+    hipError_t e_ = (cmd);                                                                          \
+    if (e_ != hipSuccess)                                                                           \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " + __FILE__ + \
+                               ":" + std::to_string(__LINE__));                                     \
+  } while (0)
+
+ncclDataType_t to_nccl(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return ncclFloat32;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kHalf: return ncclFloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    case at::kByte: return ncclUint8;
+    case at::kChar: return ncclInt8;
+    default: throw std::runtime_error("unsupported dtype for RCCL");
+  }
+}
+
+ncclRedOp_t to_nccl_op(const std::string& op) {
+  if (op == "sum") return ncclSum;
+  if (op == "avg") return ncclAvg;
+  if (op == "max") return ncclMax;
+  if (op == "min") return ncclMin;
+  if (op == "prod") return ncclProd;
+  throw std::runtime_error("unknown reduce op " + op);
+}
+
+std::string Communicator::unique_id() {
+  ncclUniqueId id;
+  NCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(id.internal, sizeof(id.internal));
+}
+
+Communicator::Communicator(const std::string& uid, int rank, int world, int device)
+    : rank_(rank), world_(world), device_(device), stream_(c10::hip::getStreamFromPool(true, device)) {
+  if (uid.size() != sizeof(ncclUniqueId::internal)) throw std::runtime_error("bad RCCL unique id size");
+  c10::hip::HIPGuard g(device);
+  ncclUniqueId id;
+  memcpy(id.internal, uid.data(), sizeof(id.internal));
+  NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
+  barrier_buf_ = at::zeros({1}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device));
+}
+
+Communicator::~Communicator() {
+  if (comm_ && !aborted_) ncclCommDestroy(comm_);
+  if (ev_in_) (void)hipEventDestroy(ev_in_);
+  if (ev_out_) (void)hipEventDestroy(ev_out_);
+}
+
+void Communicator::pre(const at::Tensor& t) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "collective tensors must be contiguous GPU tensors");
+  auto cur = c10::hip::getCurrentHIPStream(device_);
+  HIP_CHECK(hipEventRecord(ev_in_, cur.stream()));
+  HIP_CHECK(hipStreamWaitEvent(stream_.stream(), ev_in_, 0));
+  c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_);
+}
+
+void Communicator::post(const at::Tensor&) {
+  auto cur = c10::hip::getCurrentHIPStream(device_);
+  HIP_CHECK(hipEventRecord(ev_out_, stream_.stream()));
+  HIP_CHECK(hipStreamWaitEvent(cur.stream(), ev_out_, 0));
+}
+
+void Communicator::all_reduce(at::Tensor& t, const std::string& op) {
+  pre(t);
+  NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_nccl_op(op), comm_,
+                           stream_.stream()));
+  post(t);
+}
+
+void Communicator::all_reduce_raw(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
+  NCCL_CHECK(ncclAllReduce(buf, buf, count, dt, op, comm_, s));
+}
+
+void Communicator::broadcast(at::Tensor& t, int root) {
+  pre(t);
+  NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root, comm_, stream_.stream()));
+  post(t);
+}
+
+void Communicator::all_gather(const at::Tensor& in, at::Tensor& out) {
+  TORCH_CHECK(out.numel() == in.numel() * world_, "all_gather: out must hold world*in elements");
+  pre(in);
+  c10::hip::HIPCachingAllocator::recordStream(out.storage().data_ptr(), stream_);
+  NCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), to_nccl(in.scalar_type()), comm_, stream_.stream()));
+  post(out);
+}
+
+void Communicator::reduce_scatter(const at::Tensor& in, at::Tensor& out, const std::string& op) {
+  TORCH_CHECK(in.numel() == out.numel() * world_, "reduce_scatter: in must hold world*out elements");
+  pre(in);
+  c10::hip::HIPCachingAllocator::recordStream(out.storage().data_ptr(), stream_);
+  NCCL_CHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), to_nccl(in.scalar_type()), to_nccl_op(op), comm_,
+                               stream_.stream()));
+  post(out);
+}
+
+void Communicator::all_to_all(const at::Tensor& in, at::Tensor& out) {
+  TORCH_CHECK(in.numel() == out.numel() && in.numel() % world_ == 0, "all_to_all: equal sizes divisible by world");
+  pre(in);
+  c10::hip::HIPCachingAllocator::recordStream(out.storage().data_ptr(), stream_);
+  const size_t chunk = in.numel() / world_;
+  const size_t esz = in.element_size();
+  NCCL_CHECK(ncclGroupStart());
+  for (int r = 0; r < world_; ++r) {
+    NCCL_CHECK(ncclSend((char*)in.data_ptr() + r * chunk * esz, chunk, to_nccl(in.scalar_type()), r, comm_, stream_.stream()));
+    NCCL_CHECK(ncclRecv((char*)out.data_ptr() + r * chunk * esz, chunk, to_nccl(in.scalar_type()), r, comm_, stream_.stream()));
+  }
+  NCCL_CHECK(ncclGroupEnd());
+  post(out);
+}
+
+void Communicator::barrier() {
+  all_reduce(barrier_buf_, "sum");
+  HIP_CHECK(hipStreamSynchronize(c10::hip::getCurrentHIPStream(device_).stream()));
+}
+
+std::string Communicator::async_error() {
+  ncclResult_t st = ncclSuccess;
+  ncclResult_t r = ncclCommGetAsyncError(comm_, &st);
+  if (r != ncclSuccess) return ncclGetErrorString(r);
+  if (st != ncclSuccess && st != ncclInProgress) return ncclGetErrorString(st);
+  return "";
+}
+
+void Communicator::abort() {
+  if (comm_ && !aborted_) {
+    ncclCommAbort(comm_);
+    aborted_ = true;
+  }
+}
+
+// ------------------------------------------------------------------ Reducer
+Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params, int64_t nparams,
+                 std::shared_ptr<Communicator> comm, bool timing)
+    : buckets_(std::move(buckets)), bparams_(std::move(bucket_params)), comm_(std::move(comm)), timing_(timing) {
+  TORCH_CHECK(buckets_.size() == bparams_.size(), "bucket/param list size mismatch");
+  param_bucket_.assign(nparams, -1);
+  expected_.resize(buckets_.size());
+  for (size_t b = 0; b < bparams_.size(); ++b) {
+    TORCH_CHECK(buckets_[b].is_cuda() && buckets_[b].is_contiguous(), "bucket buffers must be contiguous GPU tensors");
+    for (int64_t p : bparams_[b]) {
+      TORCH_CHECK(p >= 0 && p < nparams && param_bucket_[p] == -1, "parameter in several buckets or out of range");
+      param_bucket_[p] = (int64_t)b;
+    }
+    expected_[b] = (int)bparams_[b].size();
+  }
+  pending_ = expected_;
+  ready_.assign(buckets_.size(), 0);
+  seen_.assign(nparams, 0);
+  const unsigned flags = timing_ ? hipEventDefault : hipEventDisableTiming;
+  ev_ready_.resize(buckets_.size());
+  ev_start_.resize(buckets_.size());
+  ev_end_.resize(buckets_.size());
+  for (size_t b = 0; b < buckets_.size(); ++b) {
+    HIP_CHECK(hipEventCreateWithFlags(&ev_ready_[b], hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_start_[b], flags));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_end_[b], flags));
+    if (comm_) c10::hip::HIPCachingAllocator::recordStream(buckets_[b].storage().data_ptr(), comm_->comm_stream());
+  }
+  HIP_CHECK(hipEventCreateWithFlags(&ev_bwd_end_, flags));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_step_begin_, flags));
+}
+
+Reducer::~Reducer() {
+  for (auto* v : {&ev_ready_, &ev_start_, &ev_end_})
+    for (auto e : *v) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(ev_bwd_end_);
+  (void)hipEventDestroy(ev_done_);
+  (void)hipEventDestroy(ev_step_begin_);
+}
+
+void Reducer::prepare() {
+  pending_ = expected_;
+  std::fill(ready_.begin(), ready_.end(), 0);
+  std::fill(seen_.begin(), seen_.end(), 0);
+  next_ = 0;
+  step_open_ = true;
+  if (timing_) HIP_CHECK(hipEventRecord(ev_step_begin_, c10::hip::getCurrentHIPStream().stream()));
+}
+
+void Reducer::launch(int64_t b) {
+  hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
+  if (!comm_ || comm_->world() == 1) return;
+  hipStream_t cs = comm_->comm_stream().stream();
+  HIP_CHECK(hipEventRecord(ev_ready_[b], cur));
+  HIP_CHECK(hipStreamWaitEvent(cs, ev_ready_[b], 0));
+  if (timing_) HIP_CHECK(hipEventRecord(ev_start_[b], cs));
+  auto& t = buckets_[b];
+  comm_->all_reduce_raw(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), ncclAvg, cs);
+  if (timing_) HIP_CHECK(hipEventRecord(ev_end_[b], cs));
+}
+
+void Reducer::mark_ready(int64_t p) {
+  TORCH_CHECK(p >= 0 && p < (int64_t)param_bucket_.size(), "mark_ready: bad parameter index");
+  if (!step_open_) prepare();
+  if (seen_[p]) return;  // a parameter used twice in one graph fires once (re-entrancy guard)
+  seen_[p] = 1;
+  const int64_t b = param_bucket_[p];
+  if (b < 0) return;
+  if (--pending_[b] == 0) ready_[b] = 1;
+  while (next_ < (int64_t)buckets_.size() && ready_[next_]) launch(next_++);
+}
+
+void Reducer::finalize() {
+  if (!step_open_) return;
+  hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
+  if (timing_) HIP_CHECK(hipEventRecord(ev_bwd_end_, cur));
+  // Unused parameters: their (zero / stale-accumulated) slices are reduced
+  // anyway so every rank issues the same collective sequence.
+  while (next_ < (int64_t)buckets_.size()) launch(next_++);
+  if (comm_ && comm_->world() > 1) {
+    HIP_CHECK(hipEventRecord(ev_done_, comm_->comm_stream().stream()));
+    HIP_CHECK(hipStreamWaitEvent(cur, ev_done_, 0));
+  }
+  step_open_ = false;
+}
+
+std::vector<std::tuple<int64_t, double, double>> Reducer::last_timings() {
+  std::vector<std::tuple<int64_t, double, double>> out;
+  if (!timing_ || !comm_ || comm_->world() == 1) return out;
+  HIP_CHECK(hipEventSynchronize(ev_done_));
+  for (size_t b = 0; b < buckets_.size(); ++b) {
+    float ms = 0.f, rel = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev_start_[b], ev_end_[b]));
+    // start of this bucket's all-reduce relative to the end of backward (negative = overlapped)
+    HIP_CHECK(hipEventElapsedTime(&rel, ev_bwd_end_, ev_start_[b]));
+    out.emplace_back((int64_t)b, (double)ms, (double)rel);
+  }
+  return out;
+}
+
+void register_comm(pybind11::module& m) {
+  namespace py = pybind11;
+  m.def("rccl_unique_id", []() { return py::bytes(Communicator::unique_id()); });
+  m.def("rccl_version", []() {
+    int v = 0;
+    ncclGetVersion(&v);
+    return v;
+  });
+  py::class_<Communicator, std::shared_ptr<Communicator>>(m, "Communicator")
+      .def(py::init([](py::bytes uid, int rank, int world, int device) {
+             return std::make_shared<Communicator>(std::string(uid), rank, world, device);
+           }),
+           py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"))
+      .def_property_readonly("rank", &Communicator::rank)
+      .def_property_readonly("world", &Communicator::world)
+      .def("all_reduce", &Communicator::all_reduce, py::arg("tensor"), py::arg("op") = "sum")
+      .def("broadcast", &Communicator::broadcast, py::arg("tensor"), py::arg("root") = 0)
+      .def("all_gather", &Communicator::all_gather)
+      .def("reduce_scatter", &Communicator::reduce_scatter, py::arg("input"), py::arg("output"), py::arg("op") = "sum")
+      .def("all_to_all", &Communicator::all_to_all)
+      .def("barrier", &Communicator::barrier)
+      .def("async_error", &Communicator::async_error)
+      .def("abort", &Communicator::abort)
+      .def("comm_stream_ptr", [](Communicator& c) { return (uint64_t)(uintptr_t)c.comm_stream().stream(); });
+  py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
+      .def(py::init<std::vector<at::Tensor>, std::vector<std::vector<int64_t>>, int64_t, std::shared_ptr<Communicator>, bool>(),
+           py::arg("buckets"), py::arg("bucket_params"), py::arg("nparams"), py::arg("comm"), py::arg("timing") = false)
+      .def("prepare", &Reducer::prepare)
+      .def("mark_ready", &Reducer::mark_ready)
+      .def("finalize", &Reducer::finalize)
+      .def("last_timings", &Reducer::last_timings)
+      .def_property_readonly("num_buckets", &Reducer::num_buckets)
+      .def_property_readonly("buckets_launched", &Reducer::buckets_launched);
+}
+
+}  // namespace dpe

@@ -1,0 +1,101 @@
+// RCCL communicator + DDP gradient reducer (native replacement for the
+// reference's ProcessGroupGloo + c10d::Reducer).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace dpe {
+
+// One RCCL communicator over all ranks of the job, bootstrapped from a
+// unique id the Python side distributes through the c10d TCPStore.  All
+// collectives run on a dedicated high-priority HIP stream (torch stream-pool
+// stream, so the caching allocator can track cross-stream tensor use) and
+// are ordered against the caller's current stream with events.
+class Communicator {
+ public:
+  static std::string unique_id();
+  Communicator(const std::string& uid, int rank, int world, int device);
+  ~Communicator();
+
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  c10::hip::HIPStream comm_stream() const { return stream_; }
+  ncclComm_t handle() const { return comm_; }
+
+  // Tensor collectives, enqueued after all prior work on the current stream;
+  // the current stream waits for their completion (async w.r.t. the host).
+  void all_reduce(at::Tensor& t, const std::string& op);
+  void broadcast(at::Tensor& t, int root);
+  void all_gather(const at::Tensor& in, at::Tensor& out);
+  void reduce_scatter(const at::Tensor& in, at::Tensor& out, const std::string& op);
+  void all_to_all(const at::Tensor& in, at::Tensor& out);
+  void barrier();
+
+  // Raw enqueue on the comm stream (no stream ordering): used by the reducer.
+  void all_reduce_raw(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s);
+
+  // Non-blocking health check (ncclCommGetAsyncError); returns error string or "".
+  std::string async_error();
+  void abort();
+
+ private:
+  void pre(const at::Tensor& t);
+  void post(const at::Tensor& t);
+  ncclComm_t comm_ = nullptr;
+  int rank_ = 0, world_ = 1, device_ = 0;
+  c10::hip::HIPStream stream_;
+  hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
+  at::Tensor barrier_buf_;
+  bool aborted_ = false;
+};
+
+ncclDataType_t to_nccl(at::ScalarType t);
+ncclRedOp_t to_nccl_op(const std::string& op);
+
+// Bucketed gradient reducer.  Buckets are flat buffers whose slices are the
+// parameters' .grad views (gradient-as-bucket-view), so no copy into or out
+// of the buckets is ever made.  mark_ready(i) is called once per parameter
+// per backward, after the kernel producing grad i was enqueued on the
+// current stream; when every parameter of bucket b is ready the all-reduce
+// (ncclAvg) is issued on the comm stream behind an event -- buckets are
+// issued strictly in index order so all ranks enqueue identical sequences.
+// finalize() issues any remaining buckets and makes the current stream wait
+// for the last one (optimizer ordering).
+class Reducer {
+ public:
+  Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params, int64_t nparams,
+          std::shared_ptr<Communicator> comm, bool timing);
+  ~Reducer();
+  void prepare();
+  void mark_ready(int64_t param);
+  void finalize();
+  // (bucket, comm_ms, issued_before_backward_end) for the last finalized step
+  std::vector<std::tuple<int64_t, double, double>> last_timings();
+  int64_t num_buckets() const { return (int64_t)buckets_.size(); }
+  int64_t buckets_launched() const { return next_; }
+
+ private:
+  void launch(int64_t b);
+  std::vector<at::Tensor> buckets_;
+  std::vector<std::vector<int64_t>> bparams_;
+  std::vector<int64_t> param_bucket_;
+  std::vector<int> pending_, expected_;
+  std::vector<char> ready_, seen_;
+  int64_t next_ = 0;
+  std::shared_ptr<Communicator> comm_;
+  bool timing_;
+  std::vector<hipEvent_t> ev_ready_, ev_start_, ev_end_;
+  hipEvent_t ev_bwd_end_ = nullptr, ev_done_ = nullptr, ev_step_begin_ = nullptr;
+  bool step_open_ = false;
+};
+
+void register_comm(pybind11::module& m);
+
+}  // namespace dpe

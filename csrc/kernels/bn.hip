@@ -1,0 +1,278 @@
+// BatchNorm2d training/eval kernels for NHWC bf16 activations (x viewed as
+// [M = N*H*W][C], C % 8 == 0).  Memory-bound: every pass moves 16 B per lane.
+//
+//  stats_partial : per-block partial (sum, sumsq) over a row range  -> [nb][2][C]
+//  finalize      : reduce partials in fp64, update running stats, emit
+//                  per-channel (scale, shift, mean, invstd)          -> [4][C]
+//  apply         : y = act(x*scale + shift [+ residual])
+//  bwd_reduce    : partial (sum dz, sum dz*(x-mean)), dz = dy * relu'(y)
+//  bwd_finalize  : dgamma/dbeta + the affine dx = a*dz + b*x + c coefficients
+//  bwd_apply     : dx = a*dz + b*x + c   [+ write dz for a residual branch]
+//
+// When a GEMM epilogue already accumulated the column (sum, sumsq) for this
+// BN (igemm col_stats), `finalize` is called with nb = 1 on that buffer and
+// the stats pass is skipped entirely.
+#include "common.h"
+
+namespace dpe {
+
+constexpr int BN_T = 256;
+
+// Thread layout for a [rows][C] pass: chunk c = tid % CPR (8 channels), row phase tid / CPR.
+__global__ __launch_bounds__(BN_T) void bn_stats_partial_kernel(const uint16_t* __restrict__ x, int64_t M, int C,
+                                                                int64_t rows_per_block, float* __restrict__ part) {
+  const int CPR = C >> 3;
+  const int tid = threadIdx.x;
+  const int RPI = BN_T / CPR;  // rows per iteration (CPR <= 256)
+  const int c = tid % CPR, r = tid / CPR;
+  const int64_t rb = blockIdx.x * rows_per_block;
+  const int64_t re = min(M, rb + rows_per_block);
+  float s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s[e] = 0.f; q[e] = 0.f; }
+  if (r < RPI) {
+    for (int64_t row = rb + r; row < re; row += RPI) {
+      float f[8];
+      unpack8(*(const u32x4*)(x + row * C + c * 8), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s[e] += f[e]; q[e] += f[e] * f[e]; }
+    }
+  }
+  __shared__ float red[2][BN_T][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][tid][e] = s[e]; red[1][tid][e] = q[e]; }
+  __syncthreads();
+  // each of the first C threads sums its channel over RPI row-phases
+  for (int ch = tid; ch < C; ch += BN_T) {
+    const int cc = ch >> 3, e = ch & 7;
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < RPI; ++rr) { a += red[0][rr * CPR + cc][e]; b += red[1][rr * CPR + cc][e]; }
+    part[(int64_t)blockIdx.x * 2 * C + ch] = a;
+    part[(int64_t)blockIdx.x * 2 * C + C + ch] = b;
+  }
+}
+
+// out: [4][C] = scale, shift, mean, invstd
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
+                                   float momentum, float eps, float* __restrict__ out) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < nb; ++b) {
+    s += part[(int64_t)b * 2 * C + ch];
+    q += part[(int64_t)b * 2 * C + C + ch];
+  }
+  const double mean = s / (double)M;
+  double var = q / (double)M - mean * mean;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[ch] : 1.f, bt = beta ? beta[ch] : 0.f;
+  const float sc = g * invstd;
+  out[ch] = sc;
+  out[C + ch] = bt - (float)mean * sc;
+  out[2 * C + ch] = (float)mean;
+  out[3 * C + ch] = invstd;
+  if (rmean) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    rmean[ch] = (1.f - momentum) * rmean[ch] + momentum * (float)mean;
+    rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * (float)unbiased;
+  }
+}
+
+// eval-mode coefficients from running stats
+__global__ void bn_eval_coeff_kernel(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                                     float eps, float* out) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= C) return;
+  const float invstd = rsqrtf(rvar[ch] + eps);
+  const float sc = (gamma ? gamma[ch] : 1.f) * invstd;
+  out[ch] = sc;
+  out[C + ch] = (beta ? beta[ch] : 0.f) - rmean[ch] * sc;
+  out[2 * C + ch] = rmean[ch];
+  out[3 * C + ch] = invstd;
+}
+
+// y = act(x*scale + shift [+ res]); grid-stride over 16-B chunks.
+__global__ __launch_bounds__(BN_T) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+                                                        uint16_t* __restrict__ y, int64_t nchunks, int C,
+                                                        const float* __restrict__ coef, int relu) {
+  const int CPR = C >> 3;
+  for (int64_t i = blockIdx.x * (int64_t)BN_T + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * BN_T) {
+    const int c8 = (int)(i % CPR) * 8;
+    float f[8];
+    unpack8(*(const u32x4*)(x + i * 8), f);
+    float g[8];
+    if (res) unpack8(*(const u32x4*)(res + i * 8), g);
+    const f32x4 sc0 = *(const f32x4*)(coef + c8), sc1 = *(const f32x4*)(coef + c8 + 4);
+    const f32x4 sh0 = *(const f32x4*)(coef + C + c8), sh1 = *(const f32x4*)(coef + C + c8 + 4);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float sc = e < 4 ? sc0[e] : sc1[e - 4];
+      const float sh = e < 4 ? sh0[e] : sh1[e - 4];
+      float v = f[e] * sc + sh;
+      if (res) v += g[e];
+      if (relu) v = fmaxf(v, 0.f);
+      f[e] = v;
+    }
+    *(u32x4*)(y + i * 8) = pack8(f);
+  }
+}
+
+// partial sums of dz and dz*(x-mean), dz = dy * (y > 0 if relu)
+__global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+                                                             const uint16_t* __restrict__ x, const float* __restrict__ coef,
+                                                             int64_t M, int C, int64_t rows_per_block, float* __restrict__ part) {
+  const int CPR = C >> 3;
+  const int tid = threadIdx.x;
+  const int RPI = BN_T / CPR;
+  const int c = tid % CPR, r = tid / CPR;
+  const int64_t rb = blockIdx.x * rows_per_block;
+  const int64_t re = min(M, rb + rows_per_block);
+  float s[8], q[8], mean[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s[e] = 0.f; q[e] = 0.f; mean[e] = coef[2 * C + c * 8 + e]; }
+  if (r < RPI) {
+    for (int64_t row = rb + r; row < re; row += RPI) {
+      const int64_t off = row * C + c * 8;
+      float d[8], xv[8];
+      unpack8(*(const u32x4*)(dy + off), d);
+      unpack8(*(const u32x4*)(x + off), xv);
+      if (y) {
+        float yv[8];
+        unpack8(*(const u32x4*)(y + off), yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s[e] += d[e]; q[e] += d[e] * (xv[e] - mean[e]); }
+    }
+  }
+  __shared__ float red[2][BN_T][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][tid][e] = s[e]; red[1][tid][e] = q[e]; }
+  __syncthreads();
+  for (int ch = tid; ch < C; ch += BN_T) {
+    const int cc = ch >> 3, e = ch & 7;
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < RPI; ++rr) { a += red[0][rr * CPR + cc][e]; b += red[1][rr * CPR + cc][e]; }
+    part[(int64_t)blockIdx.x * 2 * C + ch] = a;
+    part[(int64_t)blockIdx.x * 2 * C + C + ch] = b;
+  }
+}
+
+// bcoef: [3][C] = a, b, c  for dx = a*dz + b*x + c ; dgamma/dbeta accumulated (+=) into fp32 grads
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M, const float* __restrict__ gamma,
+                                       const float* __restrict__ coef, float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       float* __restrict__ bcoef) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < nb; ++b) {
+    s += part[(int64_t)b * 2 * C + ch];
+    q += part[(int64_t)b * 2 * C + C + ch];
+  }
+  const float mean = coef[2 * C + ch], invstd = coef[3 * C + ch];
+  const float g = gamma ? gamma[ch] : 1.f;
+  if (dgamma) dgamma[ch] += (float)(q * invstd);
+  if (dbeta) dbeta[ch] += (float)s;
+  const float k1 = g * invstd;
+  const float invM = 1.f / (float)M;
+  const float a = k1;
+  const float b = -k1 * invstd * invstd * (float)q * invM;
+  const float c = -k1 * (float)s * invM - b * mean;
+  bcoef[ch] = a;
+  bcoef[C + ch] = b;
+  bcoef[2 * C + ch] = c;
+}
+
+__global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+                                                            const uint16_t* __restrict__ x, const float* __restrict__ bcoef,
+                                                            uint16_t* __restrict__ dx, uint16_t* __restrict__ dz_out,
+                                                            int64_t nchunks, int C) {
+  const int CPR = C >> 3;
+  for (int64_t i = blockIdx.x * (int64_t)BN_T + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * BN_T) {
+    const int c8 = (int)(i % CPR) * 8;
+    float d[8], xv[8];
+    unpack8(*(const u32x4*)(dy + i * 8), d);
+    unpack8(*(const u32x4*)(x + i * 8), xv);
+    if (y) {
+      float yv[8];
+      unpack8(*(const u32x4*)(y + i * 8), yv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+    }
+    if (dz_out) *(u32x4*)(dz_out + i * 8) = pack8(d);
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = bcoef[c8 + e] * d[e] + bcoef[C + c8 + e] * xv[e] + bcoef[2 * C + c8 + e];
+    *(u32x4*)(dx + i * 8) = pack8(o);
+  }
+}
+
+}  // namespace dpe
+
+using namespace dpe;
+
+static int grid_for(int64_t nchunks) {
+  int64_t g = (nchunks + BN_T - 1) / BN_T;
+  return (int)(g < 4096 ? (g < 1 ? 1 : g) : 4096);
+}
+
+extern "C" int dpe_bn_stats_nblocks(int64_t M, int C) {
+  // target ~1024 partial blocks but at least 64 rows each
+  int64_t nb = M / 64;
+  if (nb > 1024) nb = 1024;
+  if (nb < 1) nb = 1;
+  (void)C;
+  return (int)nb;
+}
+
+extern "C" int dpe_bn_stats(const uint16_t* x, int64_t M, int C, int nb, float* part, hipStream_t st) {
+  if (C % 8 || C / 8 > BN_T) return -1;
+  const int64_t rpb = (M + nb - 1) / nb;
+  hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(nb), dim3(BN_T), 0, st, x, M, C, rpb, part);
+  return 0;
+}
+
+extern "C" int dpe_bn_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* beta,
+                               float* rmean, float* rvar, float momentum, float eps, float* coef, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, nb, C, M, gamma, beta, rmean, rvar,
+                     momentum, eps, coef);
+  return 0;
+}
+
+extern "C" int dpe_bn_eval_coeff(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                                 float eps, float* coef, hipStream_t st) {
+  hipLaunchKernelGGL(bn_eval_coeff_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma, beta, rmean, rvar, eps, coef);
+  return 0;
+}
+
+extern "C" int dpe_bn_apply(const uint16_t* x, const uint16_t* res, uint16_t* y, int64_t M, int C, const float* coef,
+                            int relu, hipStream_t st) {
+  const int64_t nch = M * C / 8;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, res, y, nch, C, coef, relu);
+  return 0;
+}
+
+extern "C" int dpe_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* coef, int64_t M,
+                                 int C, int nb, float* part, hipStream_t st) {
+  if (C % 8 || C / 8 > BN_T) return -1;
+  const int64_t rpb = (M + nb - 1) / nb;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(BN_T), 0, st, dy, y, x, coef, M, C, rpb, part);
+  return 0;
+}
+
+extern "C" int dpe_bn_bwd_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* coef,
+                                   float* dgamma, float* dbeta, float* bcoef, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, nb, C, M, gamma, coef, dgamma,
+                     dbeta, bcoef);
+  return 0;
+}
+
+extern "C" int dpe_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* bcoef, uint16_t* dx,
+                                uint16_t* dz_out, int64_t M, int C, hipStream_t st) {
+  const int64_t nch = M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(nch)), dim3(BN_T), 0, st, dy, y, x, bcoef, dx, dz_out, nch, C);
+  return 0;
+}

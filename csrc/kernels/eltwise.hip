@@ -1,0 +1,258 @@
+// Vectorised elementwise kernels (16 B per lane, grid-stride, capped grid):
+// casts, ReLU/GELU fwd+bwd, Philox dropout (mask regenerated in backward
+// from (seed, offset) -- no mask tensor), residual add, bias-grad column
+// sums, NCHW->NHWC input packing, embedding gather / scatter-add.
+#include "common.h"
+
+namespace dpe {
+
+constexpr int ET = 256;
+
+DPE_HOST_DEVICE int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+static inline int egrid(int64_t work) {
+  int64_t g = (work + ET - 1) / ET;
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+#define GRID_STRIDE(i, n) for (int64_t i = blockIdx.x * (int64_t)ET + threadIdx.x; i < (n); i += (int64_t)gridDim.x * ET)
+
+// ------------------------------------------------------------------ casts
+__global__ __launch_bounds__(ET) void f32_to_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, int64_t n) {
+  const int64_t n8 = n / 8;
+  GRID_STRIDE(i, n8) {
+    const f32x4 a = *(const f32x4*)(x + i * 8), b = *(const f32x4*)(x + i * 8 + 4);
+    u32x4 r;
+    r[0] = pack_bf2(a[0], a[1]); r[1] = pack_bf2(a[2], a[3]);
+    r[2] = pack_bf2(b[0], b[1]); r[3] = pack_bf2(b[2], b[3]);
+    *(u32x4*)(y + i * 8) = r;
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = n8 * 8 + threadIdx.x; i < n; i += ET) y[i] = f2bf(x[i]);
+}
+
+__global__ __launch_bounds__(ET) void bf16_to_f32_kernel(const uint16_t* __restrict__ x, float* __restrict__ y, int64_t n) {
+  const int64_t n8 = n / 8;
+  GRID_STRIDE(i, n8) {
+    float f[8];
+    unpack8(*(const u32x4*)(x + i * 8), f);
+    *(f32x4*)(y + i * 8) = f32x4{f[0], f[1], f[2], f[3]};
+    *(f32x4*)(y + i * 8 + 4) = f32x4{f[4], f[5], f[6], f[7]};
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = n8 * 8 + threadIdx.x; i < n; i += ET) y[i] = bf2f(x[i]);
+}
+
+// ----------------------------------------------------------- activations
+template <typename T> DPE_DEVICE float lf(const T* p, int64_t i);
+template <> DPE_DEVICE float lf<float>(const float* p, int64_t i) { return p[i]; }
+template <> DPE_DEVICE float lf<uint16_t>(const uint16_t* p, int64_t i) { return bf2f(p[i]); }
+template <typename T> DPE_DEVICE void sf(T* p, int64_t i, float v);
+template <> DPE_DEVICE void sf<float>(float* p, int64_t i, float v) { p[i] = v; }
+template <> DPE_DEVICE void sf<uint16_t>(uint16_t* p, int64_t i, float v) { p[i] = f2bf(v); }
+
+DPE_DEVICE float gelu_f(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+DPE_DEVICE float gelu_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  const float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+}
+
+// op: 0 relu fwd (y=f(x)), 1 relu bwd (dx = dy * (y>0)), 2 gelu fwd, 3 gelu bwd (dx = dy*gelu'(x))
+template <typename T>
+__global__ __launch_bounds__(ET) void act_kernel(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ out,
+                                                 int64_t n, int op) {
+  GRID_STRIDE(i, n) {
+    const float x = lf<T>(a, i);
+    float r;
+    if (op == 0) r = fmaxf(x, 0.f);
+    else if (op == 1) r = lf<T>(b, i) > 0.f ? x : 0.f;
+    else if (op == 2) r = gelu_f(x);
+    else r = x * gelu_grad(lf<T>(b, i));
+    sf<T>(out, i, r);
+  }
+}
+
+// bf16 fast path for the same ops, 8 per lane
+__global__ __launch_bounds__(ET) void act_bf16x8_kernel(const uint16_t* __restrict__ a, const uint16_t* __restrict__ b,
+                                                        uint16_t* __restrict__ out, int64_t n8, int op) {
+  GRID_STRIDE(i, n8) {
+    float x[8], y[8];
+    unpack8(*(const u32x4*)(a + i * 8), x);
+    if (op == 1 || op == 3) unpack8(*(const u32x4*)(b + i * 8), y);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (op == 0) x[e] = fmaxf(x[e], 0.f);
+      else if (op == 1) x[e] = y[e] > 0.f ? x[e] : 0.f;
+      else if (op == 2) x[e] = gelu_f(x[e]);
+      else x[e] = x[e] * gelu_grad(y[e]);
+    }
+    *(u32x4*)(out + i * 8) = pack8(x);
+  }
+}
+
+// ---------------------------------------------------------------- dropout
+// keep iff u >= p where u = philox(seed, offset + i/4)[i%4] / 2^32 ; scale 1/(1-p)
+template <typename T>
+__global__ __launch_bounds__(ET) void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n, float p,
+                                                     uint64_t seed, uint64_t offset) {
+  const uint32_t thr = (uint32_t)fminf(p * 4294967296.f, 4294967295.f);
+  const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  const int64_t n4 = (n + 3) / 4;
+  GRID_STRIDE(i, n4) {
+    const u32x4 r = philox4x32(seed, offset + (uint64_t)i, 0u);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t j = i * 4 + e;
+      if (j < n) sf<T>(y, j, (r[e] >= thr) ? lf<T>(x, j) * scale : 0.f);
+    }
+  }
+}
+
+// --------------------------------------------------------------- residual
+template <typename T>
+__global__ __launch_bounds__(ET) void add_kernel(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ out,
+                                                 int64_t n, float alpha) {
+  GRID_STRIDE(i, n) sf<T>(out, i, lf<T>(a, i) + alpha * lf<T>(b, i));
+}
+
+// ------------------------------------------------------ bias-grad col-sum
+// db[n] (+)= sum_m dy[m][n]; block = 256 threads over 64 columns x 4 row phases
+template <typename T>
+__global__ __launch_bounds__(ET) void colsum_kernel(const T* __restrict__ dy, int64_t M, int N, int64_t ld, float* __restrict__ db,
+                                                    int accumulate) {
+  __shared__ float red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int ph = threadIdx.x >> 6;
+  float s = 0.f;
+  if (col < N)
+    for (int64_t m = ph + 4 * (int64_t)blockIdx.y; m < M; m += 4 * (int64_t)gridDim.y) s += lf<T>(dy, m * ld + col);
+  red[ph][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (ph == 0 && col < N) {
+    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    if (gridDim.y == 1 && !accumulate) db[col] = t;
+    else atomicAdd(db + col, t);
+  }
+}
+
+// ------------------------------------------------------ input packing
+// x NCHW f32 -> y NHWC bf16 with channels padded to Cp (zeros)
+__global__ __launch_bounds__(ET) void nchw_to_nhwc_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, int N, int C,
+                                                          int HW, int Cp) {
+  const int64_t total = (int64_t)N * HW;
+  GRID_STRIDE(i, total) {
+    const int64_t n = i / HW, hw = i % HW;
+    for (int c = 0; c < Cp; ++c) y[i * Cp + c] = c < C ? f2bf(x[(n * C + c) * HW + hw]) : (uint16_t)0;
+  }
+}
+
+// ----------------------------------------------------------- embedding
+// out[r][:] = wte[idx[r]][:] (+ wpe[r % T][:]) ; D % 8 == 0, weights bf16, out f32
+__global__ __launch_bounds__(ET) void embedding_fwd_kernel(const int64_t* __restrict__ idx, const uint16_t* __restrict__ wte,
+                                                           const uint16_t* __restrict__ wpe, float* __restrict__ out,
+                                                           int64_t rows, int T, int D) {
+  const int CPR = D / 8;
+  GRID_STRIDE(i, rows * CPR) {
+    const int64_t r = i / CPR;
+    const int c8 = (int)(i % CPR) * 8;
+    float a[8];
+    unpack8(*(const u32x4*)(wte + idx[r] * D + c8), a);
+    if (wpe) {
+      float b[8];
+      unpack8(*(const u32x4*)(wpe + (r % T) * D + c8), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += b[e];
+    }
+    *(f32x4*)(out + r * D + c8) = f32x4{a[0], a[1], a[2], a[3]};
+    *(f32x4*)(out + r * D + c8 + 4) = f32x4{a[4], a[5], a[6], a[7]};
+  }
+}
+
+// dwte[idx[r]] += dout[r]; dwpe[r % T] += dout[r]   (fp32 atomics, 256-B wave segments)
+__global__ __launch_bounds__(ET) void embedding_bwd_kernel(const int64_t* __restrict__ idx, const float* __restrict__ dout,
+                                                           float* __restrict__ dwte, float* __restrict__ dwpe, int64_t rows,
+                                                           int T, int D) {
+  GRID_STRIDE(i, rows * D) {
+    const int64_t r = i / D;
+    const int d = (int)(i % D);
+    const float g = dout[i];
+    atomicAdd(dwte + idx[r] * D + d, g);
+    if (dwpe) atomicAdd(dwpe + (r % T) * D + d, g);
+  }
+}
+
+}  // namespace dpe
+
+using namespace dpe;
+
+extern "C" int dpe_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(egrid(n / 8 + 1)), dim3(ET), 0, st, x, y, n);
+  return 0;
+}
+extern "C" int dpe_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(egrid(n / 8 + 1)), dim3(ET), 0, st, x, y, n);
+  return 0;
+}
+extern "C" int dpe_act(const void* a, const void* b, void* out, int64_t n, int op, int bf16, hipStream_t st) {
+  if (bf16 && n % 8 == 0 && ((uintptr_t)a % 16 == 0) && ((uintptr_t)out % 16 == 0) && (!b || (uintptr_t)b % 16 == 0)) {
+    hipLaunchKernelGGL(act_bf16x8_kernel, dim3(egrid(n / 8)), dim3(ET), 0, st, (const uint16_t*)a, (const uint16_t*)b,
+                       (uint16_t*)out, n / 8, op);
+  } else if (bf16) {
+    hipLaunchKernelGGL((act_kernel<uint16_t>), dim3(egrid(n)), dim3(ET), 0, st, (const uint16_t*)a, (const uint16_t*)b,
+                       (uint16_t*)out, n, op);
+  } else {
+    hipLaunchKernelGGL((act_kernel<float>), dim3(egrid(n)), dim3(ET), 0, st, (const float*)a, (const float*)b, (float*)out, n,
+                       op);
+  }
+  return 0;
+}
+extern "C" int dpe_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset, int bf16,
+                           hipStream_t st) {
+  if (bf16)
+    hipLaunchKernelGGL((dropout_kernel<uint16_t>), dim3(egrid((n + 3) / 4)), dim3(ET), 0, st, (const uint16_t*)x, (uint16_t*)y,
+                       n, p, seed, offset);
+  else
+    hipLaunchKernelGGL((dropout_kernel<float>), dim3(egrid((n + 3) / 4)), dim3(ET), 0, st, (const float*)x, (float*)y, n, p,
+                       seed, offset);
+  return 0;
+}
+extern "C" int dpe_add(const void* a, const void* b, void* out, int64_t n, float alpha, int bf16, hipStream_t st) {
+  if (bf16)
+    hipLaunchKernelGGL((add_kernel<uint16_t>), dim3(egrid(n)), dim3(ET), 0, st, (const uint16_t*)a, (const uint16_t*)b,
+                       (uint16_t*)out, n, alpha);
+  else
+    hipLaunchKernelGGL((add_kernel<float>), dim3(egrid(n)), dim3(ET), 0, st, (const float*)a, (const float*)b, (float*)out, n,
+                       alpha);
+  return 0;
+}
+extern "C" int dpe_colsum(const void* dy, int64_t M, int N, int64_t ld, float* db, int accumulate, int bf16, hipStream_t st) {
+  int gy = (int)((M + 255) / 256);
+  if (gy > 64) gy = 64;
+  if (gy < 1) gy = 1;
+  dim3 grid((N + 63) / 64, gy);
+  if (bf16)
+    hipLaunchKernelGGL((colsum_kernel<uint16_t>), grid, dim3(ET), 0, st, (const uint16_t*)dy, M, N, ld, db, accumulate);
+  else
+    hipLaunchKernelGGL((colsum_kernel<float>), grid, dim3(ET), 0, st, (const float*)dy, M, N, ld, db, accumulate);
+  return 0;
+}
+extern "C" int dpe_nchw_to_nhwc(const float* x, uint16_t* y, int N, int C, int HW, int Cp, hipStream_t st) {
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(egrid((int64_t)N * HW)), dim3(ET), 0, st, x, y, N, C, HW, Cp);
+  return 0;
+}
+extern "C" int dpe_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* wpe, float* out, int64_t rows, int T,
+                                 int D, hipStream_t st) {
+  if (D % 8) return -1;
+  hipLaunchKernelGGL(embedding_fwd_kernel, dim3(egrid(rows * D / 8)), dim3(ET), 0, st, idx, wte, wpe, out, rows, T, D);
+  return 0;
+}
+extern "C" int dpe_embedding_bwd(const int64_t* idx, const float* dout, float* dwte, float* dwpe, int64_t rows, int T, int D,
+                                 hipStream_t st) {
+  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(egrid(rows * D)), dim3(ET), 0, st, idx, dout, dwte, dwpe, rows, T, D);
+  return 0;
+}

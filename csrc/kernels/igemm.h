@@ -1,0 +1,54 @@
+// Host-visible argument block for the implicit-GEMM kernels (igemm.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dpe {
+
+// How the A operand (M x K) is fetched.
+enum ALoad : int {
+  A_DENSE_K = 0,     // A[m][k] at A + m*lda + k         (K contiguous)
+  A_DENSE_M = 1,     // A[m][k] at A + k*lda + m         (M contiguous)
+  A_CONV_FWD = 2,    // im2col of NHWC x: m=(n,oh,ow), k=(r,s,ci)
+  A_CONV_DGRAD = 3,  // col2im-gather of NHWC dy: m=(n,h,w), k=(r,s,co)
+};
+// How the B operand (K x N) is fetched.
+enum BLoad : int {
+  B_DENSE_K = 0,     // B[k][n] at B + n*ldb + k         (K contiguous)
+  B_DENSE_N = 1,     // B[k][n] at B + k*ldb + n         (N contiguous)
+  B_CONV_DGRAD = 2,  // weights [Co][R][S][Ci] as B[k=(r,s,co)][n=ci]
+  B_CONV_WGRAD = 3,  // im2col of NHWC x as B[k=(n,oh,ow)][n=(r,s,ci)]
+};
+enum Epi : int {
+  EPI_BF16 = 0,        // C (bf16) = act(alpha*acc + bias) [+ residual]
+  EPI_F32 = 1,         // C (f32)  = act(alpha*acc + bias)
+  EPI_ATOMIC_F32 = 2,  // C (f32) += alpha*acc  (split-K / accumulate)
+};
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
+
+struct ConvGeom {
+  int N, H, W, C;      // input  NHWC
+  int OH, OW, K;       // output NHW(K)
+  int R, S;            // filter
+  int sh, sw, ph, pw, dh, dw;
+};
+
+struct IgemmArgs {
+  const uint16_t* A;
+  const uint16_t* B;
+  void* C;
+  const uint16_t* residual;  // bf16 [M][ldc] added in the EPI_BF16 epilogue (may alias C)
+  const float* bias;         // [N] or nullptr
+  float* col_stats;          // [2][N] per-column (sum, sumsq) of the stored bf16 output, or nullptr
+  int M, N, K;
+  int64_t lda, ldb, ldc;
+  float alpha;
+  int act;
+  int k_split;  // K elements per split (multiple of 32); >= K means no split
+  ConvGeom g;
+};
+
+}  // namespace dpe
+
+extern "C" int dpe_igemm_launch(const dpe::IgemmArgs* args, int bm, int bn, int aload, int bload, int epi,
+                                int splits, hipStream_t stream);

@@ -1,0 +1,174 @@
+// LayerNorm over the last dim (GPT-2 D=768), one wave per row, 16-B lanes.
+// fwd: x (f32 residual stream or bf16) -> y bf16 (feeds the next GEMM), mean/rstd f32.
+// bwd: dx = rstd*(g - mean(g) - xhat*mean(g*xhat)), g = dy*w; dw/db reduced
+//      per block into partials, then summed (+=) into the fp32 grads.
+//      dx is either written (x dtype) or ACCUMULATED into an f32 residual-stream grad.
+#include "common.h"
+
+namespace dpe {
+
+template <bool XBF>
+DPE_DEVICE void load8(const void* x, int64_t off, float* f) {
+  if constexpr (XBF) {
+    unpack8(*(const u32x4*)((const uint16_t*)x + off), f);
+  } else {
+    const f32x4 a = *(const f32x4*)((const float*)x + off), b = *(const f32x4*)((const float*)x + off + 4);
+    f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
+    f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+  }
+}
+
+template <bool XBF>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x, const float* __restrict__ w,
+                                                     const float* __restrict__ b, uint16_t* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out, int64_t rows,
+                                                     int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = blockIdx.x * 4ll + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int CH = D >> 3;
+  const int64_t base = row * D;
+  float s = 0.f;
+  for (int c = lane; c < CH; c += 64) {
+    float f[8];
+    load8<XBF>(x, base + c * 8, f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += f[e];
+  }
+  const float mean = warp_sum(s) / (float)D;
+  float v = 0.f;
+  for (int c = lane; c < CH; c += 64) {
+    float f[8];
+    load8<XBF>(x, base + c * 8, f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float d = f[e] - mean; v += d * d; }
+  }
+  const float rstd = rsqrtf(warp_sum(v) / (float)D + eps);
+  for (int c = lane; c < CH; c += 64) {
+    float f[8];
+    load8<XBF>(x, base + c * 8, f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = (f[e] - mean) * rstd * w[c * 8 + e] + (b ? b[c * 8 + e] : 0.f);
+    *(u32x4*)(y + base + c * 8) = pack8(f);
+  }
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
+// D <= 2048: each lane owns at most 4 chunks (32 columns) for the dw/db partials
+template <bool XBF>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict__ dy, const void* __restrict__ x,
+                                                     const float* __restrict__ w, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, void* __restrict__ dx, int dx_acc,
+                                                     float* __restrict__ part, int64_t rows, int D) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int CH = D >> 3;
+  float pw[4][8], pb[4][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { pw[j][e] = 0.f; pb[j][e] = 0.f; }
+  for (int64_t row = blockIdx.x * 4ll + wid; row < rows; row += (int64_t)gridDim.x * 4) {
+    const int64_t base = row * D;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = lane + 64 * j;
+      if (c < CH) {
+        float d[8], f[8];
+        unpack8(*(const u32x4*)(dy + base + c * 8), d);
+        load8<XBF>(x, base + c * 8, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xh = (f[e] - mean) * rstd;
+          const float g = d[e] * w[c * 8 + e];
+          sg += g;
+          sgx += g * xh;
+          pw[j][e] += d[e] * xh;
+          pb[j][e] += d[e];
+        }
+      }
+    }
+    sg = warp_sum(sg) / (float)D;
+    sgx = warp_sum(sgx) / (float)D;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = lane + 64 * j;
+      if (c < CH) {
+        float d[8], f[8], o[8];
+        unpack8(*(const u32x4*)(dy + base + c * 8), d);
+        load8<XBF>(x, base + c * 8, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xh = (f[e] - mean) * rstd;
+          o[e] = rstd * (d[e] * w[c * 8 + e] - sg - xh * sgx);
+        }
+        if (dx_acc) {
+          float* p = (float*)dx + base + c * 8;
+          f32x4 a = *(f32x4*)p, bb = *(f32x4*)(p + 4);
+          a[0] += o[0]; a[1] += o[1]; a[2] += o[2]; a[3] += o[3];
+          bb[0] += o[4]; bb[1] += o[5]; bb[2] += o[6]; bb[3] += o[7];
+          *(f32x4*)p = a;
+          *(f32x4*)(p + 4) = bb;
+        } else if (XBF) {
+          *(u32x4*)((uint16_t*)dx + base + c * 8) = pack8(o);
+        } else {
+          float* p = (float*)dx + base + c * 8;
+          *(f32x4*)p = f32x4{o[0], o[1], o[2], o[3]};
+          *(f32x4*)(p + 4) = f32x4{o[4], o[5], o[6], o[7]};
+        }
+      }
+    }
+  }
+  // block-reduce partials over 4 waves
+  __shared__ float red[2][4][2048];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = lane + 64 * j;
+    if (c < CH)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { red[0][wid][c * 8 + e] = pw[j][e]; red[1][wid][c * 8 + e] = pb[j][e]; }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < D; i += 256) {
+    part[(int64_t)blockIdx.x * 2 * D + i] = red[0][0][i] + red[0][1][i] + red[0][2][i] + red[0][3][i];
+    part[(int64_t)blockIdx.x * 2 * D + D + i] = red[1][0][i] + red[1][1][i] + red[1][2][i] + red[1][3][i];
+  }
+}
+
+__global__ void ln_bwd_finalize_kernel(const float* __restrict__ part, int nb, int D, float* __restrict__ dw,
+                                       float* __restrict__ db) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= D) return;
+  float a = 0.f, b = 0.f;
+  for (int k = 0; k < nb; ++k) { a += part[(int64_t)k * 2 * D + i]; b += part[(int64_t)k * 2 * D + D + i]; }
+  dw[i] += a;
+  if (db) db[i] += b;
+}
+
+}  // namespace dpe
+
+using namespace dpe;
+
+extern "C" int dpe_layernorm_fwd(const void* x, int x_bf16, const float* w, const float* b, uint16_t* y, float* mean,
+                                 float* rstd, int64_t rows, int D, float eps, hipStream_t st) {
+  if (D % 8) return -1;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  if (x_bf16) hipLaunchKernelGGL((ln_fwd_kernel<true>), grid, dim3(256), 0, st, x, w, b, y, mean, rstd, rows, D, eps);
+  else hipLaunchKernelGGL((ln_fwd_kernel<false>), grid, dim3(256), 0, st, x, w, b, y, mean, rstd, rows, D, eps);
+  return 0;
+}
+
+extern "C" int dpe_layernorm_bwd(const uint16_t* dy, const void* x, int x_bf16, const float* w, const float* mean,
+                                 const float* rstd, void* dx, int dx_acc, float* dw, float* db, float* part, int64_t rows,
+                                 int D, hipStream_t st) {
+  if (D % 8 || D > 2048) return -1;
+  const int nb = (int)(rows < 16384 ? (rows + 31) / 32 : 512);
+  const int nbc = nb > 512 ? 512 : nb;
+  if (x_bf16)
+    hipLaunchKernelGGL((ln_bwd_kernel<true>), dim3(nbc), dim3(256), 0, st, dy, x, w, mean, rstd, dx, dx_acc, part, rows, D);
+  else
+    hipLaunchKernelGGL((ln_bwd_kernel<false>), dim3(nbc), dim3(256), 0, st, dy, x, w, mean, rstd, dx, dx_acc, part, rows, D);
+  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 255) / 256), dim3(256), 0, st, part, nbc, D, dw, db);
+  return 0;
+}

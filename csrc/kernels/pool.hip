@@ -1,0 +1,159 @@
+// NHWC pooling: max-pool (with per-element argmax byte for an index-free
+// backward gather) and global average pool.  bf16 in/out, 8 channels/lane.
+#include "common.h"
+
+namespace dpe {
+
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                          uint8_t* __restrict__ idx, int N, int H, int W, int C, int OH,
+                                                          int OW, int k, int s, int p) {
+  const int CPR = C >> 3;
+  const int64_t total = (int64_t)N * OH * OW * CPR;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c8 = (int)(i % CPR) * 8;
+    int64_t t = i / CPR;
+    const int ow = (int)(t % OW); t /= OW;
+    const int oh = (int)(t % OH);
+    const int n = (int)(t / OH);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int r = 0; r < k; ++r) {
+      const int ih = oh * s - p + r;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int q = 0; q < k; ++q) {
+        const int iw = ow * s - p + q;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        float f[8];
+        unpack8(*(const u32x4*)(x + (((int64_t)n * H + ih) * W + iw) * C + c8), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (f[e] > best[e]) { best[e] = f[e]; bi[e] = (uint8_t)(r * k + q); }
+      }
+    }
+    *(u32x4*)(y + i * 8) = pack8(best);
+    u32x2 pk;
+    pk[0] = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    pk[1] = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *(u32x2*)(idx + i * 8) = pk;
+  }
+}
+
+// dx[n,h,w,c] = sum over windows (oh,ow) containing (h,w) whose argmax is (h,w)
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                          uint16_t* __restrict__ dx, int N, int H, int W, int C, int OH,
+                                                          int OW, int k, int s, int p) {
+  const int CPR = C >> 3;
+  const int64_t total = (int64_t)N * H * W * CPR;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c8 = (int)(i % CPR) * 8;
+    int64_t t = i / CPR;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    // oh*s - p <= h <= oh*s - p + k - 1
+    const int oh_lo = max(0, (h + p - k + s) / s), oh_hi = min(OH - 1, (h + p) / s);
+    const int ow_lo = max(0, (w + p - k + s) / s), ow_hi = min(OW - 1, (w + p) / s);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int r = h - (oh * s - p);
+      if (r < 0 || r >= k) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int q = w - (ow * s - p);
+        if (q < 0 || q >= k) continue;
+        const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c8;
+        const u32x2 pk = *(const u32x2*)(idx + o);
+        float g[8];
+        unpack8(*(const u32x4*)(dy + o), g);
+        const uint8_t want = (uint8_t)(r * k + q);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint8_t b = (uint8_t)((pk[e >> 2] >> ((e & 3) * 8)) & 0xff);
+          if (b == want) acc[e] += g[e];
+        }
+      }
+    }
+    *(u32x4*)(dx + i * 8) = pack8(acc);
+  }
+}
+
+// global average pool: x [N][HW][C] -> y [N][C] (bf16); one thread per (n, 8 channels)
+__global__ __launch_bounds__(256) void gavgpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int N,
+                                                           int HW, int C) {
+  const int CPR = C >> 3;
+  const int64_t total = (int64_t)N * CPR;
+  const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= total) return;
+  const int n = (int)(i / CPR), c8 = (int)(i % CPR) * 8;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  const uint16_t* base = x + (int64_t)n * HW * C + c8;
+  for (int j = 0; j < HW; ++j) {
+    float f[8];
+    unpack8(*(const u32x4*)(base + (int64_t)j * C), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += f[e];
+  }
+  const float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] *= inv;
+  *(u32x4*)(y + (int64_t)n * C + c8) = pack8(acc);
+}
+
+__global__ __launch_bounds__(256) void gavgpool_bwd_kernel(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx, int N,
+                                                           int HW, int C) {
+  const int CPR = C >> 3;
+  const int64_t total = (int64_t)N * HW * CPR;
+  const float inv = 1.f / (float)HW;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c8 = (int)(i % CPR) * 8;
+    const int n = (int)(i / ((int64_t)HW * CPR));
+    float f[8];
+    unpack8(*(const u32x4*)(dy + (int64_t)n * C + c8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] *= inv;
+    *(u32x4*)(dx + i * 8) = pack8(f);
+  }
+}
+
+}  // namespace dpe
+
+using namespace dpe;
+
+static int gs(int64_t n) {
+  int64_t g = (n + 255) / 256;
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+extern "C" int dpe_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH, int OW,
+                               int k, int s, int p, hipStream_t st) {
+  if (C % 8 || k * k > 255) return -1;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(gs((int64_t)N * OH * OW * C / 8)), dim3(256), 0, st, x, y, idx, N, H, W, C,
+                     OH, OW, k, s, p);
+  return 0;
+}
+
+extern "C" int dpe_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int OH,
+                               int OW, int k, int s, int p, hipStream_t st) {
+  if (C % 8) return -1;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(gs((int64_t)N * H * W * C / 8)), dim3(256), 0, st, dy, idx, dx, N, H, W, C,
+                     OH, OW, k, s, p);
+  return 0;
+}
+
+extern "C" int dpe_gavgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st) {
+  if (C % 8) return -1;
+  const int64_t total = (int64_t)N * C / 8;
+  hipLaunchKernelGGL(gavgpool_fwd_kernel, dim3((int)((total + 255) / 256)), dim3(256), 0, st, x, y, N, HW, C);
+  return 0;
+}
+
+extern "C" int dpe_gavgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st) {
+  if (C % 8) return -1;
+  hipLaunchKernelGGL(gavgpool_bwd_kernel, dim3(gs((int64_t)N * HW * C / 8)), dim3(256), 0, st, dy, dx, N, HW, C);
+  return 0;
+}

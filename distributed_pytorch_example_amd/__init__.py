@@ -1,0 +1,9 @@
+"""MI355X-native distributed data-parallel training framework.
+
+Same capabilities and CLI/env/checkpoint contract as
+northflank-examples/distributed-pytorch-example, rebuilt for AMD Instinct
+MI355X (gfx950): hand-written CDNA4 HIP kernels for the model ops, a C++
+RCCL communicator + bucketed reducer overlapped with backward on a side HIP
+stream, and a device-resident data path.
+"""
+__version__ = "0.1.0"

@@ -1,0 +1,94 @@
+"""ResNet-50 v1.5 (BASELINE.json configs 2, 3, 5) in NHWC for gfx950.
+
+Topology is torchvision's ``resnet50`` (stride on the 3x3 conv, 25,557,032
+parameters, zero-init of nothing) -- SURVEY §2.6.2 lists its 23 conv shapes.
+Execution is MI355X-native:
+
+* activations NHWC bf16, filters OHWI (implicit-GEMM K-contiguous);
+* every conv feeding a BatchNorm accumulates that BN's per-channel
+  (sum, sum^2) in its GEMM epilogue, so the BN statistics pass is skipped;
+* BN apply fuses ReLU and the residual add (one pass per BN);
+* the stem consumes an 8-channel-padded input image (16-B vector loads).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from ..ops import functional as Fx
+from ..ops.layers import BatchNorm2d, Conv2d, Linear
+
+
+def _stats(x: torch.Tensor, c: int) -> Optional[torch.Tensor]:
+    if x.is_cuda and torch.is_grad_enabled():
+        return torch.zeros(2 * c, dtype=torch.float32, device=x.device)
+    return None
+
+
+class ConvBN(nn.Module):
+    """conv -> BN (training stats from the conv epilogue) -> optional residual add -> optional ReLU."""
+
+    def __init__(self, cin, cout, k, stride=1, padding=0):
+        super().__init__()
+        self.conv = Conv2d(cin, cout, k, stride, padding)
+        self.bn = BatchNorm2d(cout)
+
+    def forward(self, x, relu=True, residual=None):
+        st = _stats(x, self.conv.out_channels) if self.bn.training else None
+        y = self.conv(x, st)
+        return self.bn(y, relu=relu, residual=residual, stats=st)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=False):
+        super().__init__()
+        width = planes
+        self.c1 = ConvBN(inplanes, width, 1)
+        self.c2 = ConvBN(width, width, 3, stride, 1)
+        self.c3 = ConvBN(width, planes * 4, 1)
+        self.down = ConvBN(inplanes, planes * 4, 1, stride) if downsample else None
+
+    def forward(self, x):
+        idn = self.down(x, relu=False) if self.down is not None else x
+        h = self.c1(x)
+        h = self.c2(h)
+        return self.c3(h, relu=True, residual=idn)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers: List[int] = (3, 4, 6, 3), num_classes: int = 1000, in_chans: int = 3, in_pad: int = 8):
+        super().__init__()
+        self.in_pad = in_pad
+        self.stem = ConvBN(in_chans, 64, 7, 2, 3)
+        blocks = []
+        inplanes = 64
+        for i, (n, planes) in enumerate(zip(layers, (64, 128, 256, 512))):
+            for j in range(n):
+                stride = 2 if (j == 0 and i > 0) else 1
+                blocks.append(Bottleneck(inplanes, planes, stride, downsample=(j == 0)))
+                inplanes = planes * 4
+        self.blocks = nn.Sequential(*blocks)
+        self.fc = Linear(512 * 4, num_classes, out_f32=True)
+
+    def forward(self, x):
+        """x: NCHW float images [N,3,H,W] or an already-packed NHWC tensor [N,H,W,in_pad]."""
+        if x.dim() == 4 and x.shape[1] != self.in_pad and x.shape[-1] != self.in_pad:
+            x = Fx.to_nhwc_input(x, self.in_pad)
+        h = self.stem(x)
+        h = Fx.max_pool2d_nhwc(h, 3, 2, 1)
+        h = self.blocks(h)
+        h = Fx.global_avg_pool_nhwc(h)
+        return self.fc(h)
+
+
+def resnet50(num_classes: int = 1000) -> ResNet:
+    return ResNet((3, 4, 6, 3), num_classes)
+
+
+def resnet18_like(num_classes: int = 10) -> ResNet:
+    """Small bottleneck ResNet for fast tests."""
+    return ResNet((1, 1, 1, 1), num_classes)

@@ -1,0 +1,98 @@
+"""Per-parameter runtime state shared by layers, optimizers and the DDP reducer.
+
+* bf16 compute shadows: layers keep fp32 master parameters; the MFMA kernels
+  read a bf16 copy.  The fused optimizer kernels write the shadow in the same
+  pass that updates the master (no cast pass per step).  A shadow is re-cast
+  whenever ``param._version`` moved (torch-side in-place edits such as
+  ``load_state_dict``) -- our own kernels write through raw pointers and
+  keep the version.  Shadows may be *padded* (extra trailing zero rows for
+  out_features % 8 != 0); the fused optimizer then still writes the prefix.
+  Shadows whose layout differs from the master (e.g. the ResNet stem's
+  channel-padded filter) register a ``derive`` function that the optimizer
+  re-runs after each step (``post_step`` hooks, graph-capturable).
+
+* direct gradients: when DDP runs with gradient-as-bucket-view, our backward
+  kernels accumulate weight gradients straight into ``param.grad`` (a view of
+  the flat bucket) and signal readiness to the reducer themselves, instead of
+  returning a fresh tensor that autograd would add into the bucket.
+"""
+from __future__ import annotations
+
+import torch
+
+_derived: list = []  # (param, shadow, fn)
+
+
+def shadow(p: torch.Tensor, pad_rows: int = 0) -> torch.Tensor:
+    """bf16 shadow of fp32 master ``p`` (optionally with zero pad rows)."""
+    sh = getattr(p, "_dpe_shadow", None)
+    if sh is None or getattr(p, "_dpe_shadow_ver", -1) != p._version or sh.device != p.device:
+        from ._ext import ext
+
+        rows = p.shape[0] + pad_rows
+        if sh is None or sh.device != p.device or sh.shape[0] != rows:
+            sh = torch.zeros((rows, *p.shape[1:]), dtype=torch.bfloat16, device=p.device)
+        ext().cast_bf16(p.detach().reshape(-1), sh.view(-1)[: p.numel()])
+        p._dpe_shadow = sh
+        p._dpe_shadow_ver = p._version
+    return sh
+
+
+def derived_shadow(p: torch.Tensor, key: str, fn) -> torch.Tensor:
+    """A shadow derived by ``fn(p) -> bf16 tensor`` (layout change), refreshed after optimizer steps."""
+    attr = "_dpe_dshadow_" + key
+    sh = getattr(p, attr, None)
+    stamp = (p._version, _step_counter[0])
+    if sh is None or getattr(p, attr + "_stamp", None) != stamp:
+        new = fn(p.detach())
+        if sh is None or sh.shape != new.shape:
+            sh = new
+        else:
+            sh.copy_(new)
+        setattr(p, attr, sh)
+        setattr(p, attr + "_stamp", stamp)
+        if not getattr(p, attr + "_reg", False):
+            _derived.append((p, attr, fn))
+            setattr(p, attr + "_reg", True)
+    return sh
+
+
+_step_counter = [0]
+
+
+def after_optimizer_step(params=None) -> None:
+    """Refresh derived shadows in place (called by the fused optimizers; capturable)."""
+    _step_counter[0] += 1
+    for p, attr, fn in _derived:
+        if params is not None and p not in params:
+            continue
+        sh = getattr(p, attr, None)
+        if sh is not None:
+            sh.copy_(fn(p.detach()))
+            setattr(p, attr + "_stamp", (p._version, _step_counter[0]))
+
+
+# ------------------------------------------------------------ direct grads
+def grad_sink(p: torch.Tensor):
+    """Return (buffer, direct).  direct=True: accumulate into p.grad (bucket view)."""
+    if getattr(p, "_dpe_direct", False) and p.grad is not None:
+        return p.grad, True
+    return torch.zeros_like(p, dtype=torch.float32), False
+
+
+def grad_done(p: torch.Tensor, direct: bool) -> None:
+    if not direct:
+        return
+    uses = getattr(p, "_dpe_uses", 1)
+    uses -= 1
+    p._dpe_uses = uses
+    if uses <= 0:
+        cb = getattr(p, "_dpe_ready", None)
+        if cb is not None:
+            cb(p)
+
+
+def note_use(p: torch.Tensor) -> None:
+    """Forward-side use counter so a weight used k times is 'ready' after k backward writes."""
+    if getattr(p, "_dpe_direct", False) and torch.is_grad_enabled():
+        p._dpe_uses = getattr(p, "_dpe_uses", 0) + 1

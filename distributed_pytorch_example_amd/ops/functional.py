@@ -1,0 +1,492 @@
+"""Autograd-level ops.  GPU tensors -> hand-written gfx950 kernels (``_C``);
+CPU tensors -> torch reference math with identical semantics (the CPU/gloo
+configuration of the reference, and the reference used by the numerics tests).
+
+Activation layout convention: convolutional activations are NHWC
+(``[N, H, W, C]``); on the GPU they are bf16.  Conv weights are stored
+``[Cout, R, S, Cin]`` (OHWI) so the forward implicit GEMM reads them K-contiguous.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence
+
+import torch
+import torch.nn.functional as F
+from torch.autograd import Function
+
+from ._ext import ext
+from ._state import grad_done, grad_sink, note_use, shadow
+
+ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
+
+
+def _pad8(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+# ===================================================================== Linear
+class _LinearFn(Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, act: int, out_f32: bool):
+        C = ext()
+        N = weight.shape[0]
+        Np = _pad8(N)
+        w16 = shadow(weight, Np - N)
+        xb = x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
+        xb = xb.contiguous()
+        if Np != N:
+            y = C.linear_fwd(xb, w16, None, 0, out_f32)[..., :N]
+            if bias is not None:
+                y = y + bias.to(y.dtype)
+            if act == ACT_RELU:
+                y = torch.relu(y)
+            y = y.contiguous()
+        else:
+            y = C.linear_fwd(xb, w16, bias.detach() if bias is not None else None, act, out_f32)
+        ctx.save_for_backward(xb, y if act != ACT_NONE else None)
+        ctx.weight, ctx.bias, ctx.act, ctx.N, ctx.Np = weight, bias, act, N, Np
+        ctx.x_dtype = x.dtype
+        note_use(weight)
+        if bias is not None:
+            note_use(bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = ext()
+        xb, y = ctx.saved_tensors
+        weight, bias, act, N, Np = ctx.weight, ctx.bias, ctx.act, ctx.N, ctx.Np
+        dy = dy.to(torch.bfloat16) if dy.dtype != torch.bfloat16 else dy
+        if act == ACT_RELU:
+            dy = C.act(dy.contiguous(), y.to(torch.bfloat16).contiguous() if y.dtype != torch.bfloat16 else y.contiguous(), 1)
+        dy = dy.contiguous()
+        if Np != N:
+            dyp = torch.zeros((*dy.shape[:-1], Np), dtype=dy.dtype, device=dy.device)
+            dyp[..., :N] = dy
+        else:
+            dyp = dy
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = C.linear_dgrad(dyp, shadow(weight, Np - N))
+            if ctx.x_dtype != torch.bfloat16:
+                dx = dx.to(ctx.x_dtype)
+        gw = None
+        if ctx.needs_input_grad[1]:
+            buf, direct = grad_sink(weight)
+            if Np != N:
+                tmp = torch.zeros((Np, weight.shape[1]), dtype=torch.float32, device=dy.device)
+                C.linear_wgrad(dyp, xb, tmp)
+                buf.add_(tmp[:N])
+            else:
+                C.linear_wgrad(dyp, xb, buf)
+            grad_done(weight, direct)
+            gw = None if direct else buf
+        gb = None
+        if bias is not None and ctx.needs_input_grad[2]:
+            bbuf, bdirect = grad_sink(bias)
+            C.colsum(dy, bbuf, True)
+            grad_done(bias, bdirect)
+            gb = None if bdirect else bbuf
+        return dx, gw, gb, None, None
+
+
+def linear(x, weight, bias=None, act: int = ACT_NONE, out_f32: bool = False):
+    if not x.is_cuda:
+        y = F.linear(x.float() if x.dtype != weight.dtype else x, weight, bias)
+        if act == ACT_RELU:
+            y = F.relu(y)
+        elif act == ACT_GELU:
+            y = F.gelu(y, approximate="tanh")
+        return y
+    if act == ACT_GELU:
+        return gelu(_LinearFn.apply(x, weight, bias, ACT_NONE, out_f32))
+    return _LinearFn.apply(x, weight, bias, act, out_f32)
+
+
+# ============================================================ activations
+class _ActFn(Function):
+    @staticmethod
+    def forward(ctx, x, op: int):
+        C = ext()
+        xc = x.contiguous()
+        y = C.act(xc, None, op)
+        ctx.op = op
+        ctx.save_for_backward(y if op == 0 else xc)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (s,) = ctx.saved_tensors
+        dy = dy.contiguous().to(s.dtype)
+        return ext().act(dy, s, 1 if ctx.op == 0 else 3), None
+
+
+def relu(x):
+    if not x.is_cuda:
+        return F.relu(x)
+    return _ActFn.apply(x, 0)
+
+
+def gelu(x):
+    if not x.is_cuda:
+        return F.gelu(x, approximate="tanh")
+    return _ActFn.apply(x, 2)
+
+
+class _RNG:
+    """Counter-based dropout RNG stream: (seed, offset) -> Philox; mask regenerated in backward."""
+
+    seed = None
+    offset = 0
+
+    @classmethod
+    def next(cls, n: int):
+        if cls.seed is None:
+            cls.seed = int(torch.initial_seed()) & 0xFFFFFFFFFFFF
+        off = cls.offset
+        cls.offset += (n + 3) // 4
+        return cls.seed, off
+
+
+class _DropoutFn(Function):
+    @staticmethod
+    def forward(ctx, x, p: float):
+        seed, off = _RNG.next(x.numel())
+        ctx.p, ctx.seed, ctx.off = p, seed, off
+        return ext().dropout(x.contiguous(), p, seed, off)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return ext().dropout(dy.contiguous(), ctx.p, ctx.seed, ctx.off), None
+
+
+def dropout(x, p: float, training: bool):
+    if not training or p == 0.0:
+        return x
+    if not x.is_cuda:
+        return F.dropout(x, p, True)
+    return _DropoutFn.apply(x, p)
+
+
+# ====================================================================== Conv
+def _conv_out(h, k, s, p, d):
+    return (h + 2 * p - d * (k - 1) - 1) // s + 1
+
+
+class _ConvFn(Function):
+    @staticmethod
+    def forward(ctx, x, weight, w16, stride, padding, dilation, stats):
+        C = ext()
+        y = C.conv_fwd(x, w16, list(stride), list(padding), list(dilation), stats, None)
+        ctx.save_for_backward(x)
+        ctx.w16, ctx.weight = w16, weight
+        ctx.conf = (list(stride), list(padding), list(dilation))
+        note_use(weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = ext()
+        (x,) = ctx.saved_tensors
+        stride, padding, dilation = ctx.conf
+        dy = dy.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = C.conv_dgrad(dy, ctx.w16, list(x.shape), stride, padding, dilation, None)
+        gw = None
+        weight = ctx.weight
+        if ctx.needs_input_grad[1]:
+            if tuple(ctx.w16.shape) == tuple(weight.shape):
+                buf, direct = grad_sink(weight)
+                C.conv_wgrad(dy, x, buf, stride, padding, dilation, 1.0)
+            else:  # channel-padded filter (stem): reduce in padded layout, keep the real channels
+                tmp = torch.zeros(ctx.w16.shape, dtype=torch.float32, device=dy.device)
+                C.conv_wgrad(dy, x, tmp, stride, padding, dilation, 1.0)
+                buf, direct = grad_sink(weight)
+                buf.add_(tmp[..., : weight.shape[-1]])
+            grad_done(weight, direct)
+            gw = None if direct else buf
+        return dx, gw, None, None, None, None, None
+
+
+def _pad_filter_channels(cp: int):
+    def fn(w):
+        out = torch.zeros((*w.shape[:-1], cp), dtype=torch.bfloat16, device=w.device)
+        out[..., : w.shape[-1]] = w
+        return out
+
+    return fn
+
+
+def conv2d_nhwc(x, weight, stride=(1, 1), padding=(0, 0), dilation=(1, 1), stats: Optional[torch.Tensor] = None):
+    """x: [N,H,W,Cin'] (Cin' >= Cin, zero-padded channels allowed), weight: [Cout,R,S,Cin] fp32 master."""
+    stride, padding, dilation = _pair(stride), _pair(padding), _pair(dilation)
+    if not x.is_cuda:
+        cin = weight.shape[-1]
+        xc = x[..., :cin].permute(0, 3, 1, 2).float()
+        y = F.conv2d(xc, weight.permute(0, 3, 1, 2), None, stride, padding, dilation)
+        return y.permute(0, 2, 3, 1).contiguous()
+    from ._state import derived_shadow
+
+    if x.shape[-1] != weight.shape[-1]:
+        w16 = derived_shadow(weight, f"cpad{x.shape[-1]}", _pad_filter_channels(x.shape[-1]))
+    else:
+        w16 = shadow(weight)
+    return _ConvFn.apply(x.contiguous(), weight, w16, stride, padding, dilation, stats)
+
+
+def _pair(v) -> tuple:
+    return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
+
+
+# ================================================================ BatchNorm
+class _BNFn(Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, rmean, rvar, momentum, eps, relu_, stats):
+        C = ext()
+        y, coef = C.bn_fwd_train(x, gamma.detach(), beta.detach(), rmean, rvar, momentum, eps, relu_, residual, stats)
+        ctx.save_for_backward(x, y if relu_ else None, coef)
+        ctx.gamma, ctx.beta, ctx.has_res = gamma, beta, residual is not None
+        note_use(gamma)
+        note_use(beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = ext()
+        x, y, coef = ctx.saved_tensors
+        gbuf, gdirect = grad_sink(ctx.gamma)
+        bbuf, bdirect = grad_sink(ctx.beta)
+        dx, dz = C.bn_bwd(dy.contiguous(), y, x, ctx.gamma.detach(), coef, gbuf, bbuf, ctx.has_res)
+        grad_done(ctx.gamma, gdirect)
+        grad_done(ctx.beta, bdirect)
+        return (dx, None if gdirect else gbuf, None if bdirect else bbuf, dz if ctx.has_res else None,
+                None, None, None, None, None, None)
+
+
+def batch_norm_nhwc(x, gamma, beta, running_mean, running_var, training: bool, momentum: float = 0.1,
+                    eps: float = 1e-5, relu: bool = False, residual=None, stats=None, num_batches_tracked=None):
+    """y = act(BN(x) [+ residual]) over the channel (last) dim of an NHWC tensor."""
+    if not x.is_cuda:
+        C_ = x.shape[-1]
+        xf = x.reshape(-1, C_).float()
+        yf = F.batch_norm(xf, running_mean, running_var, gamma, beta, training, momentum, eps)
+        y = yf.reshape(x.shape)
+        if residual is not None:
+            y = y + residual.float()
+        if relu:
+            y = F.relu(y)
+        if training and num_batches_tracked is not None:
+            num_batches_tracked.add_(1)
+        return y
+    if training:
+        if num_batches_tracked is not None:
+            num_batches_tracked.add_(1)
+        return _BNFn.apply(x.contiguous(), gamma, beta, residual.contiguous() if residual is not None else None,
+                           running_mean, running_var, momentum, eps, relu, stats)
+    return ext().bn_fwd_eval(x.contiguous(), gamma.detach(), beta.detach(), running_mean, running_var, eps, relu,
+                             residual.contiguous() if residual is not None else None)
+
+
+# ================================================================== pooling
+class _MaxPoolFn(Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        y, idx = ext().maxpool_fwd(x, k, s, p)
+        ctx.save_for_backward(idx)
+        ctx.conf = (list(x.shape), k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        xs, k, s, p = ctx.conf
+        return ext().maxpool_bwd(dy.contiguous(), idx, xs, k, s, p), None, None, None
+
+
+def max_pool2d_nhwc(x, kernel_size=3, stride=2, padding=1):
+    if not x.is_cuda:
+        return F.max_pool2d(x.permute(0, 3, 1, 2), kernel_size, stride, padding).permute(0, 2, 3, 1).contiguous()
+    return _MaxPoolFn.apply(x.contiguous(), kernel_size, stride, padding)
+
+
+class _GAvgPoolFn(Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = list(x.shape)
+        return ext().gavgpool_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return ext().gavgpool_bwd(dy.contiguous(), ctx.shape)
+
+
+def global_avg_pool_nhwc(x):
+    if not x.is_cuda:
+        return x.float().mean(dim=(1, 2))
+    return _GAvgPoolFn.apply(x.contiguous())
+
+
+# ===================================================================== loss
+class _CEFn(Function):
+    @staticmethod
+    def forward(ctx, logits, labels, num_classes: int, ignore_index: int):
+        rows, s, correct, d = ext().cross_entropy(logits.contiguous(), labels.contiguous(), num_classes, 1.0, True,
+                                                  logits.dtype == torch.bfloat16, ignore_index)
+        n = (labels != ignore_index).sum().clamp_min(1).to(torch.float32) if ignore_index >= 0 else labels.numel()
+        ctx.save_for_backward(d)
+        ctx.n = n
+        ctx.correct = correct
+        return s.reshape(()) / n
+
+    @staticmethod
+    def backward(ctx, g):
+        (d,) = ctx.saved_tensors
+        scale = g / ctx.n
+        return (d * scale.to(d.dtype)), None, None, None
+
+
+def cross_entropy(logits, labels, num_classes: Optional[int] = None, ignore_index: int = -100):
+    """Mean softmax cross-entropy over rows (torch.nn.CrossEntropyLoss semantics)."""
+    if num_classes is None:
+        num_classes = logits.shape[-1]
+    if not logits.is_cuda:
+        return F.cross_entropy(logits.reshape(-1, logits.shape[-1])[:, :num_classes].float(), labels.reshape(-1),
+                               ignore_index=ignore_index)
+    return _CEFn.apply(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1), num_classes, ignore_index)
+
+
+def cross_entropy_eval(logits, labels, num_classes: Optional[int] = None):
+    """(loss_sum, correct_count) as device scalars, one fused pass (no grad)."""
+    if num_classes is None:
+        num_classes = logits.shape[-1]
+    if not logits.is_cuda:
+        lf = logits.reshape(-1, logits.shape[-1])[:, :num_classes].float()
+        loss = F.cross_entropy(lf, labels.reshape(-1), reduction="sum")
+        return loss, (lf.argmax(1) == labels.reshape(-1)).sum().float()
+    _, s, correct, _ = ext().cross_entropy(logits.reshape(-1, logits.shape[-1]).contiguous(), labels.reshape(-1).contiguous(),
+                                           num_classes, 1.0, False, False, -100)
+    return s.reshape(()), correct.reshape(())
+
+
+# ================================================================ LayerNorm
+class _LNFn(Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        y, mean, rstd = ext().layernorm_fwd(x.contiguous(), w.detach(), b.detach() if b is not None else None, eps)
+        ctx.save_for_backward(x, mean, rstd)
+        ctx.w, ctx.b = w, b
+        note_use(w)
+        if b is not None:
+            note_use(b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd = ctx.saved_tensors
+        wbuf, wd = grad_sink(ctx.w)
+        bbuf, bd = (grad_sink(ctx.b) if ctx.b is not None else (None, False))
+        dx = ext().layernorm_bwd(dy.contiguous().to(torch.bfloat16), x.contiguous(), ctx.w.detach(), mean, rstd, wbuf, bbuf,
+                                 None)
+        grad_done(ctx.w, wd)
+        if ctx.b is not None:
+            grad_done(ctx.b, bd)
+        return dx, (None if wd else wbuf), (None if (bd or ctx.b is None) else bbuf), None
+
+
+def layer_norm(x, weight, bias=None, eps: float = 1e-5):
+    """LayerNorm over the last dim. GPU: f32/bf16 in -> bf16 out."""
+    if not x.is_cuda:
+        return F.layer_norm(x.float(), (x.shape[-1],), weight, bias, eps)
+    return _LNFn.apply(x, weight, bias, eps)
+
+
+# ================================================================ Embedding
+class _EmbFn(Function):
+    @staticmethod
+    def forward(ctx, idx, wte, wpe, wte16, wpe16):
+        out = ext().embedding_fwd(idx, wte16, wpe16)
+        ctx.save_for_backward(idx)
+        ctx.wte, ctx.wpe = wte, wpe
+        note_use(wte)
+        if wpe is not None:
+            note_use(wpe)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (idx,) = ctx.saved_tensors
+        tb, td = grad_sink(ctx.wte)
+        pb, pd = grad_sink(ctx.wpe) if ctx.wpe is not None else (None, False)
+        ext().embedding_bwd(idx, dout.contiguous().float(), tb, pb)
+        grad_done(ctx.wte, td)
+        if ctx.wpe is not None:
+            grad_done(ctx.wpe, pd)
+        return None, (None if td else tb), (None if (pd or ctx.wpe is None) else pb), None, None
+
+
+def embedding(idx, wte, wpe=None):
+    """tok + pos embedding -> f32 [B,T,D] residual stream."""
+    if not idx.is_cuda:
+        T = idx.shape[1]
+        x = F.embedding(idx, wte)
+        if wpe is not None:
+            x = x + wpe[:T].unsqueeze(0)
+        return x
+    return _EmbFn.apply(idx, wte, wpe, shadow(wte), shadow(wpe) if wpe is not None else None)
+
+
+# ================================================================ Attention
+class _AttnFn(Function):
+    @staticmethod
+    def forward(ctx, qkv, H: int, scale: float):
+        out, lse = ext().attn_fwd(qkv.contiguous(), H, scale, True)
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.H, ctx.scale = H, scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        dqkv = ext().attn_bwd(qkv, out, dout.contiguous().to(torch.bfloat16), lse, ctx.H, ctx.scale, True)
+        return dqkv, None, None
+
+
+def causal_attention(qkv, n_head: int):
+    """qkv: [B, T, 3*H*D] -> [B, T, H*D] causal softmax attention."""
+    B, T, three_hd = qkv.shape
+    D = three_hd // (3 * n_head)
+    scale = 1.0 / math.sqrt(D)
+    if not qkv.is_cuda:
+        q, k, v = qkv.float().view(B, T, 3, n_head, D).permute(2, 0, 3, 1, 4)
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        return o.transpose(1, 2).reshape(B, T, n_head * D)
+    out = _AttnFn.apply(qkv.reshape(B, T, 3, n_head, D), n_head, scale)
+    return out.reshape(B, T, n_head * D)
+
+
+def add(a, b):
+    if not a.is_cuda:
+        return a + b
+    return _AddFn.apply(a, b)
+
+
+class _AddFn(Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        return ext().add(a.contiguous(), b.contiguous(), 1.0)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
+def to_nhwc_input(x: torch.Tensor, cpad: int = 8) -> torch.Tensor:
+    """NCHW fp32 image batch -> NHWC (bf16 on GPU, channel-padded to ``cpad``)."""
+    if not x.is_cuda:
+        y = x.permute(0, 2, 3, 1).float()
+        if y.shape[-1] < cpad:
+            y = F.pad(y, (0, cpad - y.shape[-1]))
+        return y.contiguous()
+    return ext().nchw_to_nhwc(x.float().contiguous(), cpad)

@@ -1,0 +1,264 @@
+"""DistributedDataParallel for MI355X.
+
+API-compatible subset of ``torch.nn.parallel.DistributedDataParallel`` as the
+reference uses it (`train.py:12,233`: ``DDP(model)``, ``.module``, forward,
+implicit gradient averaging in backward) plus ``no_sync()``,
+``broadcast_buffers`` and bucket-size control.
+
+Design (MI355X-first, not a port of c10d::Reducer):
+
+* **Flat buckets, gradient-as-bucket-view.**  Every parameter's ``.grad`` is
+  a view into a flat fp32 bucket buffer for the whole run.  Our backward
+  kernels (Linear/Conv/BN/LN/Embedding) atomically accumulate weight
+  gradients *directly* into that view and announce readiness themselves --
+  there is no grad->bucket copy-and-scale (c10d's ``mul_out``, K18) and no
+  bucket->grad copy-back (K20).  Parameters of foreign modules still work via
+  ``register_post_accumulate_grad_hook``.
+* **Native reducer.**  On the rccl backend the per-bucket all-reduce is
+  issued by the C++ ``_C.Reducer`` on the communicator's high-priority side
+  stream behind an event recorded on the compute stream, so RCCL overlaps the
+  rest of backward; averaging uses ``ncclAvg`` (no scale kernel).  Buckets are
+  issued strictly in index order on every rank.  At the end of backward the
+  compute stream waits for the last bucket.
+* **gloo / CPU**: the same bucketing with async ``dist.all_reduce``.
+* **Init sync**: parameters and buffers are broadcast from rank 0 as one flat
+  buffer per dtype (c10d's coalesced broadcast, C3).
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import dist as pdist
+from .buckets import assign_buckets
+from ..utils.logging import get_logger
+
+log = get_logger(__name__)
+
+_DEFAULT_FIRST_BUCKET_BYTES = 1024 * 1024
+
+
+class _GlooReducer:
+    """Python reducer for the gloo backend (CPU plumbing path)."""
+
+    def __init__(self, buckets: List[torch.Tensor], bucket_params: List[List[int]], nparams: int):
+        self.buckets = buckets
+        self.bucket_of = {}
+        for b, ps in enumerate(bucket_params):
+            for p in ps:
+                self.bucket_of[p] = b
+        self.expected = [len(ps) for ps in bucket_params]
+        self.world = pdist.get_world_size()
+        self.prepare()
+
+    def prepare(self):
+        self.pending = list(self.expected)
+        self.ready = [False] * len(self.buckets)
+        self.seen = set()
+        self.next = 0
+        self.works = []
+        self.open = True
+
+    def _launch(self, b):
+        if self.world > 1:
+            self.works.append(dist.all_reduce(self.buckets[b], async_op=True))
+
+    def mark_ready(self, i: int):
+        if not self.open:
+            self.prepare()
+        if i in self.seen:
+            return
+        self.seen.add(i)
+        b = self.bucket_of.get(i)
+        if b is None:
+            return
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            self.ready[b] = True
+        while self.next < len(self.buckets) and self.ready[self.next]:
+            self._launch(self.next)
+            self.next += 1
+
+    def finalize(self):
+        if not self.open:
+            return
+        while self.next < len(self.buckets):
+            self._launch(self.next)
+            self.next += 1
+        for w in self.works:
+            w.wait()
+        if self.world > 1:
+            for t in self.buckets:
+                t.div_(self.world)
+        self.open = False
+
+    def last_timings(self):
+        return []
+
+
+class DistributedDataParallel(nn.Module):
+    def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers: bool = True,
+                 bucket_cap_mb: Optional[float] = 25.0, first_bucket_mb: float = 1.0,
+                 find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
+                 init_sync: bool = True, timing: bool = False):
+        super().__init__()
+        self.module = module
+        self.broadcast_buffers = broadcast_buffers
+        self.find_unused_parameters = find_unused_parameters
+        self.require_backward_grad_sync = True
+        self.world_size = pdist.get_world_size()
+        self._params = [p for p in module.parameters() if p.requires_grad]
+        self._index = {id(p): i for i, p in enumerate(self._params)}
+        cap = int((bucket_cap_mb if bucket_cap_mb is not None else 25.0) * 1024 * 1024)
+        first = int(first_bucket_mb * 1024 * 1024) if first_bucket_mb else cap
+        self.bucket_cap_bytes, self.first_bucket_bytes = cap, first
+        if init_sync and self.world_size > 1:
+            self._sync_module_states()
+        self._build_buckets()
+        self._queued = False
+        self._hooks = []
+        for p in self._params:
+            p._dpe_direct = True
+            p._dpe_ready = self._on_ready
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._on_ready))
+
+    # --------------------------------------------------------------- setup
+    @torch.no_grad()
+    def _sync_module_states(self):
+        """Broadcast params + buffers from rank 0, one flat buffer per dtype (reference C3, C9 at init)."""
+        tensors = [p.data for p in self.module.parameters()] + [b for b in self.module.buffers()]
+        by_dtype = {}
+        for t in tensors:
+            by_dtype.setdefault((t.dtype, t.device), []).append(t)
+        for (dt, dev), ts in by_dtype.items():
+            flat = torch.cat([t.reshape(-1) for t in ts])
+            pdist.broadcast(flat, 0)
+            off = 0
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[off: off + n].view_as(t))
+                off += n
+
+    def _build_buckets(self):
+        sizes = [p.numel() * 4 for p in self._params]  # fp32 grads
+        order = list(range(len(self._params)))[::-1]
+        keys = [(str(p.device),) for p in self._params]
+        self.bucket_indices = assign_buckets(sizes, order, self.bucket_cap_bytes, self.first_bucket_bytes, keys)
+        self.buckets: List[torch.Tensor] = []
+        self._views = {}
+        for bidx in self.bucket_indices:
+            n = sum(self._params[i].numel() for i in bidx)
+            dev = self._params[bidx[0]].device
+            buf = torch.zeros(n, dtype=torch.float32, device=dev)
+            off = 0
+            for i in bidx:
+                p = self._params[i]
+                self._views[i] = buf[off: off + p.numel()].view_as(p)
+                off += p.numel()
+            self.buckets.append(buf)
+        self._attach_grads(zero=True)
+        backend = pdist.backend()
+        if backend == "rccl" and self._params and self._params[0].is_cuda:
+            from ..ops._ext import ext
+
+            self.reducer = ext().Reducer(self.buckets, self.bucket_indices, len(self._params), pdist.comm(), False)
+            self._native = True
+        else:
+            self.reducer = _GlooReducer(self.buckets, self.bucket_indices, len(self._params))
+            self._native = False
+
+    def enable_timing(self, on: bool = True):
+        """Per-bucket comm timing (HIP events) for the overlap / bucket-size sweep."""
+        if self._native:
+            from ..ops._ext import ext
+
+            self.reducer = ext().Reducer(self.buckets, self.bucket_indices, len(self._params), pdist.comm(), on)
+
+    def bucket_timings(self):
+        return self.reducer.last_timings()
+
+    def _attach_grads(self, zero: bool):
+        reattached = False
+        for i, p in enumerate(self._params):
+            v = self._views[i]
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                if p.grad is not None:
+                    v.copy_(p.grad)
+                    p.grad = v
+                else:
+                    p.grad = v
+                    reattached = True
+        if zero or reattached:
+            # set_to_none=True zero_grad dropped the views: grads restart from zero
+            for b in self.buckets:
+                b.zero_()
+
+    # ---------------------------------------------------------- per-step
+    def _on_ready(self, p):
+        if not self.require_backward_grad_sync:
+            return
+        i = self._index.get(id(p))
+        if i is None:
+            return
+        if not self._queued:
+            self._queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+        self.reducer.mark_ready(i)
+
+    def _finalize(self):
+        self._queued = False
+        self.reducer.finalize()
+
+    def finish_gradient_sync(self):
+        """Explicit end-of-backward hook (also queued automatically)."""
+        if self.require_backward_grad_sync:
+            self.reducer.finalize()
+            self._queued = False
+
+    def forward(self, *args, **kwargs):
+        if torch.is_grad_enabled():
+            self._attach_grads(zero=False)
+            for p in self._params:
+                p._dpe_uses = 0
+            if self.require_backward_grad_sync:
+                self.reducer.prepare()
+        if self.broadcast_buffers and self.world_size > 1:
+            self._sync_buffers()
+        return self.module(*args, **kwargs)
+
+    @torch.no_grad()
+    def _sync_buffers(self):
+        bufs = [b for b in self.module.buffers() if b.is_floating_point()]
+        if not bufs:
+            return
+        flat = torch.cat([b.reshape(-1) for b in bufs])
+        pdist.broadcast(flat, 0)
+        off = 0
+        for b in bufs:
+            n = b.numel()
+            b.copy_(flat[off: off + n].view_as(b))
+            off += n
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Accumulate gradients locally (grad-accumulation micro-steps)."""
+        old = self.require_backward_grad_sync
+        self.require_backward_grad_sync = False
+        try:
+            yield
+        finally:
+            self.require_backward_grad_sync = old
+
+    # ------------------------------------------------------------- info
+    def num_buckets(self) -> int:
+        return len(self.buckets)
+
+    def bucket_bytes(self) -> List[int]:
+        return [b.numel() * b.element_size() for b in self.buckets]
+
+
+DDP = DistributedDataParallel

@@ -1,0 +1,160 @@
+"""Process-group setup and the collective API used by the training loop.
+
+Reference: `setup_distributed` / `cleanup_distributed` (`train.py:70-86`)
+hard-code ``init_process_group("gloo")`` and run every GPU collective through
+gloo's host-staged TCP ring.  Here:
+
+* ``backend="gloo"``  -- exactly the reference (CPU plumbing, BASELINE config 1).
+* ``backend="rccl"``  -- torch's c10d process group is initialised with gloo
+  as a *control plane only* (rendezvous, object broadcast, host barriers), and
+  a native RCCL communicator (``_C.Communicator``, C++) is bootstrapped from
+  its TCPStore: rank 0 calls ``ncclGetUniqueId`` and publishes it, peers read
+  it, everyone ``ncclCommInitRank``s.  All tensor collectives
+  (DDP buckets, init broadcast, metric all-reduce, barriers) then run on RCCL
+  over xGMI from a dedicated HIP stream.
+* ``backend="auto"``  -- rccl when a GPU is present, else gloo.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..utils.env import read_env
+from ..utils.logging import get_logger
+
+log = get_logger(__name__)
+
+_state = {"backend": None, "comm": None, "device": None}
+
+
+def resolve_backend(backend: str) -> str:
+    b = backend.lower()
+    if b == "nccl":
+        b = "rccl"
+    if b == "auto":
+        b = "rccl" if torch.cuda.is_available() else "gloo"
+    if b not in ("rccl", "gloo"):
+        raise ValueError(f"unknown backend {backend!r} (expected rccl|gloo|auto)")
+    if b == "rccl" and not torch.cuda.is_available():
+        raise RuntimeError("backend 'rccl' requires a GPU")
+    return b
+
+
+def init_process_group(backend: str = "auto", timeout_s: float = 1800.0) -> tuple[int, int, int]:
+    """Initialise the job.  Returns (rank, world_size, local_rank) like the reference's setup_distributed."""
+    env = read_env()
+    backend = resolve_backend(backend)
+    if not dist.is_initialized():
+        dist.init_process_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s))
+    rank, world = dist.get_rank(), dist.get_world_size()
+    local_rank = env.local_rank
+    _state["backend"] = backend
+    if backend == "rccl":
+        torch.cuda.set_device(local_rank)
+        _state["device"] = torch.device("cuda", local_rank)
+        _state["comm"] = _make_comm(rank, world, local_rank)
+    else:
+        _state["device"] = torch.device("cpu")
+    return rank, world, local_rank
+
+
+def _make_comm(rank: int, world: int, local_rank: int):
+    from ..ops._ext import ext
+
+    C = ext()
+    store = dist.distributed_c10d._get_default_store()
+    key = "dpe/rccl_uid"
+    if rank == 0:
+        uid = C.rccl_unique_id()
+        store.set(key, uid)
+    else:
+        uid = store.get(key)
+    comm = C.Communicator(bytes(uid), rank, world, local_rank)
+    return comm
+
+
+def backend() -> Optional[str]:
+    return _state["backend"]
+
+
+def comm():
+    """The native RCCL communicator (None on the gloo backend)."""
+    return _state["comm"]
+
+
+def is_initialized() -> bool:
+    return dist.is_initialized()
+
+
+def get_rank() -> int:
+    return dist.get_rank() if dist.is_initialized() else 0
+
+
+def get_world_size() -> int:
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
+def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    """In-place all-reduce of a tensor (RCCL for GPU tensors on the rccl backend)."""
+    c = _state["comm"]
+    if c is not None and t.is_cuda:
+        c.all_reduce(t, op)
+        return t
+    if not dist.is_initialized() or get_world_size() == 1:
+        return t
+    ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN, "avg": None}
+    if op == "avg":
+        dist.all_reduce(t, dist.ReduceOp.SUM)
+        t /= get_world_size()
+    else:
+        dist.all_reduce(t, ops[op])
+    return t
+
+
+def broadcast(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    c = _state["comm"]
+    if c is not None and t.is_cuda:
+        c.broadcast(t, src)
+        return t
+    if dist.is_initialized() and get_world_size() > 1:
+        dist.broadcast(t, src)
+    return t
+
+
+def barrier() -> None:
+    c = _state["comm"]
+    if c is not None:
+        c.barrier()
+    elif dist.is_initialized():
+        dist.barrier()
+
+
+def check_health() -> str:
+    """RCCL async-error watchdog probe ('' if healthy)."""
+    c = _state["comm"]
+    return c.async_error() if c is not None else ""
+
+
+def destroy_process_group() -> None:
+    if _state["comm"] is not None:
+        torch.cuda.synchronize()
+        _state["comm"] = None
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _state["backend"] = None
+
+
+def get_device(local_rank: int) -> torch.device:
+    """Reference `get_device` (`train.py:89-98`)."""
+    if torch.cuda.is_available():
+        device = torch.device(f"cuda:{local_rank}")
+        torch.cuda.set_device(device)
+        log.info(f"Using GPU: {torch.cuda.get_device_name(device)}")
+    else:
+        device = torch.device("cpu")
+        log.info("Using CPU for training")
+    return device

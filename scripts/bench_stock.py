@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""Comparison arm (b) of BASELINE.md §4: *stock* PyTorch-ROCm DDP on the same
+ResNet-50 v1.5 topology and synthetic data -- nn.Conv2d/BatchNorm2d (MIOpen),
+nn.Linear (hipBLASLt), channels_last, bf16 autocast, torch DDP with
+backend="nccl" (= RCCL), torch SGD (foreach).  Same step and timing protocol
+as bench.py; prints one JSON line.  This is the bar our framework must beat.
+"""
+import argparse
+import json
+import os
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class Bottleneck(nn.Module):
+    def __init__(self, inp, planes, stride, down):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inp, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.down = nn.Sequential(nn.Conv2d(inp, planes * 4, 1, stride, bias=False), nn.BatchNorm2d(planes * 4)) if down else None
+
+    def forward(self, x):
+        idn = self.down(x) if self.down is not None else x
+        h = F.relu(self.bn1(self.conv1(x)))
+        h = F.relu(self.bn2(self.conv2(h)))
+        return F.relu(self.bn3(self.conv3(h)) + idn)
+
+
+class ResNet50(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        layers, inp = [], 64
+        for i, (n, planes) in enumerate(zip((3, 4, 6, 3), (64, 128, 256, 512))):
+            for j in range(n):
+                layers.append(Bottleneck(inp, planes, 2 if (j == 0 and i > 0) else 1, j == 0))
+                inp = planes * 4
+        self.layers = nn.Sequential(*layers)
+        self.fc = nn.Linear(2048, 1000)
+
+    def forward(self, x):
+        x = F.max_pool2d(F.relu(self.bn1(self.conv1(x))), 3, 2, 1)
+        x = self.layers(x)
+        return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch-size", type=int, default=256)
+    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    args = ap.parse_args()
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    os.environ.setdefault("LOCAL_RANK", "0")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    local = int(os.environ["LOCAL_RANK"])
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = torch.device("cuda", local)
+    torch.backends.cudnn.benchmark = True
+    model = ResNet50().to(dev).to(memory_format=torch.channels_last)
+    ddp = nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=args.bucket_mb,
+                                              gradient_as_bucket_view=True)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)
+    xs = [torch.randn(args.batch_size, 3, 224, 224, device=dev).to(memory_format=torch.channels_last) for _ in range(4)]
+    ys = [torch.randint(0, 1000, (args.batch_size,), device=dev) for _ in range(4)]
+
+    def step(i):
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = ddp(xs[i % 4])
+            loss = F.cross_entropy(out.float(), ys[i % 4])
+        loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(); dist.barrier(); torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(i)
+    torch.cuda.synchronize(); dist.barrier(); torch.cuda.synchronize()
+    dt = torch.tensor([time.perf_counter() - t0], device=dev)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = dt.item()
+    if rank == 0:
+        print(json.dumps({"metric": "stock-pytorch resnet50 bf16 samples/s (whole node)",
+                          "value": round(args.batch_size * world * args.steps / dt, 2), "n_gpus": world,
+                          "ms_per_step": round(1000 * dt / args.steps, 3), "per_gpu_batch": args.batch_size,
+                          "loss": loss.item()}), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

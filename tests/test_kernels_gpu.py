@@ -1,0 +1,294 @@
+"""Numerics of every gfx950 kernel against a plain fp32 PyTorch reference of the
+same op (inputs rounded to bf16 first, so only accumulation/output rounding
+differs).  Random NON-zero data throughout."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def test_extension_is_native(C):
+    assert C.ARCH == "gfx950"
+
+
+# ------------------------------------------------------------------ GEMMs
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 192, 96), (1000, 520, 784), (64, 64, 32), (300, 1000, 2048),
+                                   (8, 24, 40)])
+def test_linear_fwd(C, M, N, K):
+    torch.manual_seed(0)
+    x = bf(torch.randn(M, K, device=dev))
+    w = bf(torch.randn(N, K, device=dev) / math.sqrt(K))
+    b = torch.randn(N, device=dev)
+    ref = x.float() @ w.float().t() + b
+    y = C.linear_fwd(x, w, b, 0, False)
+    assert y.dtype == torch.bfloat16 and rel_err(y, ref) < 1e-2
+    y32 = C.linear_fwd(x, w, b, 1, True)
+    assert rel_err(y32, F.relu(ref)) < 1e-3
+
+
+def test_linear_fwd_asymmetric_layout(C):
+    # integer data: exact; catches row/col swaps in the C write
+    M, N, K = 64, 64, 64
+    x = torch.zeros(M, K, device=dev)
+    x[torch.arange(M), torch.arange(M) % K] = 1.0
+    w = (torch.arange(N * K, device=dev).reshape(N, K) % 7).float()
+    y = C.linear_fwd(bf(x), bf(w), None, 0, True)
+    assert torch.equal(y, (x @ w.t()))
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 192, 96), (1000, 784, 520), (64, 256, 16 * 8)])
+def test_linear_dgrad(C, M, N, K):
+    torch.manual_seed(1)
+    dy = bf(torch.randn(M, N, device=dev))
+    w = bf(torch.randn(N, K, device=dev))
+    ref = dy.float() @ w.float()
+    assert rel_err(C.linear_dgrad(dy, w), ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (4096, 256, 128), (100, 64, 64), (2048, 1000 // 8 * 8, 2048)])
+def test_linear_wgrad(C, M, N, K):
+    torch.manual_seed(2)
+    dy = bf(torch.randn(M, N, device=dev))
+    x = bf(torch.randn(M, K, device=dev))
+    dw = torch.zeros(N, K, device=dev)
+    C.linear_wgrad(dy, x, dw, 1.0)
+    ref = dy.float().t() @ x.float()
+    assert rel_err(dw, ref) < 1e-3
+    C.linear_wgrad(dy, x, dw, 0.5)  # accumulate
+    assert rel_err(dw, 1.5 * ref) < 1e-3
+
+
+# ------------------------------------------------------------------- conv
+CONV_CASES = [
+    # N, H, W, Cin, Cout, k, stride, pad
+    (2, 8, 8, 64, 64, 1, 1, 0),
+    (2, 8, 8, 64, 64, 3, 1, 1),
+    (2, 14, 14, 128, 128, 3, 2, 1),
+    (2, 14, 14, 256, 512, 1, 2, 0),
+    (2, 28, 28, 8, 64, 7, 2, 3),     # stem (channel-padded input)
+    (3, 7, 7, 512, 128, 3, 1, 1),
+    (1, 9, 9, 32, 48, 3, 2, 1),
+]
+
+
+def _conv_ref(x, w, s, p):
+    return F.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), None, s, p).permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("N,H,W,Ci,Co,k,s,p", CONV_CASES)
+def test_conv_fwd(C, N, H, W, Ci, Co, k, s, p):
+    torch.manual_seed(3)
+    x = bf(torch.randn(N, H, W, Ci, device=dev))
+    w = bf(torch.randn(Co, k, k, Ci, device=dev) / math.sqrt(k * k * Ci))
+    ref = _conv_ref(x, w, s, p)
+    stats = torch.zeros(2 * Co, device=dev)
+    y = C.conv_fwd(x, w, [s, s], [p, p], [1, 1], stats, None)
+    assert y.shape == ref.shape and rel_err(y, ref) < 1e-2
+    yf = y.float().reshape(-1, Co)
+    assert rel_err(stats[:Co], yf.sum(0)) < 1e-3
+    assert rel_err(stats[Co:], (yf * yf).sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("N,H,W,Ci,Co,k,s,p", [c for c in CONV_CASES if c[3] != 8])
+def test_conv_dgrad(C, N, H, W, Ci, Co, k, s, p):
+    torch.manual_seed(4)
+    x = torch.randn(N, Ci, H, W, device=dev, requires_grad=True)
+    w = bf(torch.randn(Co, k, k, Ci, device=dev) / math.sqrt(k * k * Ci))
+    y = F.conv2d(x, w.permute(0, 3, 1, 2).float(), None, s, p)
+    dy = bf(torch.randn_like(y))
+    (ref,) = torch.autograd.grad(y, x, dy.float())
+    dx = C.conv_dgrad(dy.permute(0, 2, 3, 1).contiguous(), w, [N, H, W, Ci], [s, s], [p, p], [1, 1], None)
+    assert rel_err(dx, ref.permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,Ci,Co,k,s,p", CONV_CASES)
+def test_conv_wgrad(C, N, H, W, Ci, Co, k, s, p):
+    torch.manual_seed(5)
+    x = bf(torch.randn(N, H, W, Ci, device=dev))
+    w = torch.randn(Co, Ci, k, k, device=dev, requires_grad=True)
+    y = F.conv2d(x.permute(0, 3, 1, 2).float(), w, None, s, p)
+    dy = bf(torch.randn_like(y))
+    (ref,) = torch.autograd.grad(y, w, dy.float())
+    dw = torch.zeros(Co, k, k, Ci, device=dev)
+    C.conv_wgrad(dy.permute(0, 2, 3, 1).contiguous(), x, dw, [s, s], [p, p], [1, 1], 1.0)
+    assert rel_err(dw, ref.permute(0, 2, 3, 1)) < 1e-3
+
+
+def test_resnet_scale_shapes(C):
+    # a real ResNet-50 layer1 shape at batch 32: fwd/dgrad/wgrad
+    torch.manual_seed(6)
+    N, H, Ci, Co = 32, 56, 64, 256
+    x = bf(torch.randn(N, H, H, Ci, device=dev))
+    w = bf(torch.randn(Co, 1, 1, Ci, device=dev) / 8)
+    y = C.conv_fwd(x, w, [1, 1], [0, 0], [1, 1], None, None)
+    assert rel_err(y, _conv_ref(x, w, 1, 0)) < 1e-2
+    dy = bf(torch.randn_like(y.float()))
+    dw = torch.zeros(Co, 1, 1, Ci, device=dev)
+    C.conv_wgrad(dy, x, dw, [1, 1], [0, 0], [1, 1], 1.0)
+    ref = dy.float().reshape(-1, Co).t() @ x.float().reshape(-1, Ci)
+    assert rel_err(dw.reshape(Co, Ci), ref) < 1e-3
+
+
+# -------------------------------------------------------------- BatchNorm
+@pytest.mark.parametrize("M,Cc,relu,res", [(4096, 64, True, False), (1000, 256, False, True), (98, 2048, True, True),
+                                          (50000, 128, True, False)])
+def test_bn_train_fwd_bwd(C, M, Cc, relu, res):
+    torch.manual_seed(7)
+    x = bf(torch.randn(M, Cc, device=dev) * 2 + 0.5)
+    g = torch.rand(Cc, device=dev) + 0.5
+    b = torch.randn(Cc, device=dev)
+    r = bf(torch.randn(M, Cc, device=dev)) if res else None
+    rm, rv = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
+    y, coef = C.bn_fwd_train(x, g, b, rm, rv, 0.1, 1e-5, relu, r, None)
+    xf = x.float().requires_grad_(True)
+    gf, bfp = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    rf = r.float().requires_grad_(True) if res else None
+    rm2, rv2 = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
+    ref = F.batch_norm(xf, rm2, rv2, gf, bfp, True, 0.1, 1e-5)
+    if res:
+        ref = ref + rf
+    if relu:
+        ref = F.relu(ref)
+    assert rel_err(y, ref) < 1e-2
+    assert rel_err(rm, rm2) < 1e-4 and rel_err(rv, rv2) < 1e-4
+    dy = bf(torch.randn(M, Cc, device=dev))
+    grads = torch.autograd.grad(ref, [xf, gf, bfp] + ([rf] if res else []), dy.float())
+    dg, db = torch.zeros(Cc, device=dev), torch.zeros(Cc, device=dev)
+    dx, dz = C.bn_bwd(dy, y if relu else None, x, g, coef, dg, db, res)
+    assert rel_err(dx, grads[0]) < 2e-2
+    assert rel_err(dg, grads[1]) < 1e-2 and rel_err(db, grads[2]) < 1e-2
+    if res:
+        assert rel_err(dz, grads[3]) < 1e-2
+
+
+def test_bn_stats_from_conv_epilogue(C):
+    torch.manual_seed(8)
+    x = bf(torch.randn(4, 16, 16, 64, device=dev))
+    w = bf(torch.randn(128, 3, 3, 64, device=dev) / 24)
+    st = torch.zeros(256, device=dev)
+    y = C.conv_fwd(x, w, [1, 1], [1, 1], [1, 1], st, None)
+    g, b = torch.ones(128, device=dev), torch.zeros(128, device=dev)
+    y1, c1 = C.bn_fwd_train(y, g, b, None, None, 0.1, 1e-5, True, None, None)
+    y2, c2 = C.bn_fwd_train(y, g, b, None, None, 0.1, 1e-5, True, None, st)
+    assert rel_err(c1, c2) < 1e-4 and rel_err(y1, y2) < 1e-2
+
+
+def test_bn_eval(C):
+    x = bf(torch.randn(500, 64, device=dev))
+    g, b = torch.rand(64, device=dev), torch.randn(64, device=dev)
+    rm, rv = torch.randn(64, device=dev), torch.rand(64, device=dev) + 0.5
+    y = C.bn_fwd_eval(x, g, b, rm, rv, 1e-5, True, None)
+    ref = F.relu(F.batch_norm(x.float(), rm, rv, g, b, False, 0.1, 1e-5))
+    assert rel_err(y, ref) < 1e-2
+
+
+# ---------------------------------------------------------------- pooling
+def test_maxpool(C):
+    torch.manual_seed(9)
+    x = bf(torch.randn(2, 17, 17, 64, device=dev))
+    y, idx = C.maxpool_fwd(x, 3, 2, 1)
+    xf = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    ref = F.max_pool2d(xf, 3, 2, 1)
+    assert torch.equal(y.float(), ref.permute(0, 2, 3, 1))
+    dy = bf(torch.randn_like(y.float()))
+    (g,) = torch.autograd.grad(ref, xf, dy.float().permute(0, 3, 1, 2))
+    dx = C.maxpool_bwd(dy, idx, list(x.shape), 3, 2, 1)
+    assert rel_err(dx, g.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_gavgpool(C):
+    x = bf(torch.randn(4, 7, 7, 2048, device=dev))
+    y = C.gavgpool_fwd(x)
+    assert rel_err(y, x.float().mean((1, 2))) < 1e-2
+    dy = bf(torch.randn(4, 2048, device=dev))
+    dx = C.gavgpool_bwd(dy, list(x.shape))
+    assert rel_err(dx, (dy.float() / 49)[:, None, None, :].expand(4, 7, 7, 2048)) < 1e-2
+
+
+# ------------------------------------------------------------------- loss
+@pytest.mark.parametrize("B,V,ld,in_bf", [(64, 10, 10, False), (256, 1000, 1000, False), (32, 50257, 50304, True)])
+def test_cross_entropy(C, B, V, ld, in_bf):
+    torch.manual_seed(10)
+    z = torch.randn(B, ld, device=dev) * 3
+    if in_bf:
+        z = bf(z)
+    y = torch.randint(0, V, (B,), device=dev)
+    zf = z.float()[:, :V].requires_grad_(True)
+    ref = F.cross_entropy(zf, y, reduction="sum")
+    (g,) = torch.autograd.grad(ref, zf)
+    rows, s, correct, d = C.cross_entropy(z, y, V, 1.0, True, in_bf, -100)
+    assert abs(s.item() - ref.item()) / abs(ref.item()) < 1e-4
+    assert correct.item() == (zf.argmax(1) == y).sum().item()
+    assert rel_err(d[:, :V], g) < 1e-2
+    if ld > V:
+        assert d[:, V:].float().abs().max().item() == 0
+
+
+# ---------------------------------------------------------------- eltwise
+def test_cast_act_dropout(C):
+    x = torch.randn(1000003, device=dev)
+    assert torch.equal(C.cast_bf16(x, None), x.to(torch.bfloat16))
+    xb = bf(torch.randn(4096, 64, device=dev))
+    assert torch.equal(C.act(xb, None, 0), F.relu(xb))
+    g = C.act(xb, None, 2)
+    assert rel_err(g, F.gelu(xb.float(), approximate="tanh")) < 1e-2
+    dy = bf(torch.randn_like(xb.float()))
+    xr = xb.float().requires_grad_(True)
+    (ref,) = torch.autograd.grad(F.gelu(xr, approximate="tanh"), xr, dy.float())
+    assert rel_err(C.act(dy, xb, 3), ref) < 2e-2
+    y = C.dropout(torch.ones(100000, device=dev), 0.2, 1234, 0)
+    keep = (y != 0).float().mean().item()
+    assert abs(keep - 0.8) < 0.01 and torch.allclose(y[y != 0], torch.full_like(y[y != 0], 1.25))
+    y2 = C.dropout(torch.ones(100000, device=dev), 0.2, 1234, 0)
+    assert torch.equal(y, y2)
+
+
+def test_colsum(C):
+    dy = bf(torch.randn(3000, 520, device=dev))
+    db = torch.zeros(520, device=dev)
+    C.colsum(dy, db, False)
+    assert rel_err(db, dy.float().sum(0)) < 1e-4
+
+
+def test_layernorm(C):
+    torch.manual_seed(11)
+    x = torch.randn(333, 768, device=dev) * 2 + 1
+    w, b = torch.rand(768, device=dev) + 0.5, torch.randn(768, device=dev)
+    y, mean, rstd = C.layernorm_fwd(x, w, b, 1e-5)
+    xf = x.clone().requires_grad_(True)
+    wf, bfp = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    ref = F.layer_norm(xf, (768,), wf, bfp, 1e-5)
+    assert rel_err(y, ref) < 1e-2
+    dy = bf(torch.randn(333, 768, device=dev))
+    gx, gw, gb = torch.autograd.grad(ref, [xf, wf, bfp], dy.float())
+    dw, db = torch.zeros(768, device=dev), torch.zeros(768, device=dev)
+    dx = C.layernorm_bwd(dy, x, w, mean, rstd, dw, db, None)
+    assert rel_err(dx, gx) < 1e-2 and rel_err(dw, gw) < 1e-3 and rel_err(db, gb) < 1e-3
+    acc = torch.ones(333, 768, device=dev)
+    C.layernorm_bwd(dy, x, w, mean, rstd, torch.zeros(768, device=dev), None, acc)
+    assert rel_err(acc - 1, gx) < 1e-2
+
+
+def test_embedding(C):
+    idx = torch.randint(0, 1000, (4, 64), device=dev)
+    wte, wpe = bf(torch.randn(1000, 128, device=dev)), bf(torch.randn(64, 128, device=dev))
+    out = C.embedding_fwd(idx, wte, wpe)
+    assert rel_err(out, wte.float()[idx] + wpe.float()[None]) < 1e-6
+    dout = torch.randn(4, 64, 128, device=dev)
+    dwte, dwpe = torch.zeros(1000, 128, device=dev), torch.zeros(64, 128, device=dev)
+    C.embedding_bwd(idx, dout, dwte, dwpe)
+    ref = torch.zeros(1000, 128, device=dev).index_add_(0, idx.reshape(-1), dout.reshape(-1, 128))
+    assert rel_err(dwte, ref) < 1e-5 and rel_err(dwpe, dout.sum(0)) < 1e-5
