@@ -90,6 +90,19 @@ Cfg pick_cfg(int64_t M, int64_t N, int64_t K, bool allow_split) {
   Cfg c{128, N <= 64 ? 64 : 128, 1, (int)((K + 31) / 32 * 32)};
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   const int64_t target = 512;  // >= 2 workgroups per CU on 256 CUs
+  if (allow_split && K >= 32 * 64) {
+    // split-K (weight-grad) GEMMs: big K, small output.  Keep the largest
+    // tile (highest MFMA:LDS ratio) and let the K split supply parallelism.
+    c.bm = M <= 64 ? 64 : 128;
+    c.bn = N <= 64 ? 64 : 128;
+    const int64_t t = tiles(c.bm, c.bn);
+    const int64_t ksteps = (K + 31) / 32;
+    int64_t splits = std::max<int64_t>(1, std::min<int64_t>((512 + t - 1) / t, ksteps / 8));
+    const int64_t kps = (ksteps + splits - 1) / splits;
+    c.k_split = (int)(kps * 32);
+    c.splits = (int)((ksteps + kps - 1) / kps);
+    return c;
+  }
   if (tiles(c.bm, c.bn) < target && M <= 64) c.bm = 64;
   if (tiles(c.bm, c.bn) < target && c.bn == 128 && c.bm == 128 && tiles(128, 64) <= tiles(64, 128)) c.bn = 64;
   if (tiles(c.bm, c.bn) < target && c.bm == 128) c.bm = 64;

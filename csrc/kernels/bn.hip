@@ -47,22 +47,33 @@ __global__ __launch_bounds__(BN_T) void bn_stats_partial_kernel(const uint16_t* 
     const int cc = ch >> 3, e = ch & 7;
     float a = 0.f, b = 0.f;
     for (int rr = 0; rr < RPI; ++rr) { a += red[0][rr * CPR + cc][e]; b += red[1][rr * CPR + cc][e]; }
-    part[(int64_t)blockIdx.x * 2 * C + ch] = a;
-    part[(int64_t)blockIdx.x * 2 * C + C + ch] = b;
+    part[(int64_t)ch * gridDim.x + blockIdx.x] = a;
+    part[(int64_t)(C + ch) * gridDim.x + blockIdx.x] = b;
   }
+}
+
+// Sum channel ch's nb partials (layout [2][C][nb]) with one wave; fp64 accumulation per lane.
+DPE_DEVICE void wave_sum2(const float* __restrict__ part, int nb, int C, int ch, double& s, double& q) {
+  const int lane = threadIdx.x & 63;
+  double a = 0.0, b = 0.0;
+  const float* ps = part + (int64_t)ch * nb;
+  const float* pq = part + (int64_t)(C + ch) * nb;
+  for (int i = lane; i < nb; i += 64) { a += ps[i]; b += pq[i]; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
+  s = a;
+  q = b;
 }
 
 // out: [4][C] = scale, shift, mean, invstd
 __global__ void bn_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M, const float* __restrict__ gamma,
                                    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
                                    float momentum, float eps, float* __restrict__ out) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ch = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (ch >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nb; ++b) {
-    s += part[(int64_t)b * 2 * C + ch];
-    q += part[(int64_t)b * 2 * C + C + ch];
-  }
+  double s, q;
+  wave_sum2(part, nb, C, ch, s, q);
+  if ((threadIdx.x & 63) != 0) return;
   const double mean = s / (double)M;
   double var = q / (double)M - mean * mean;
   if (var < 0) var = 0;
@@ -156,8 +167,8 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const uint16_t* __r
     const int cc = ch >> 3, e = ch & 7;
     float a = 0.f, b = 0.f;
     for (int rr = 0; rr < RPI; ++rr) { a += red[0][rr * CPR + cc][e]; b += red[1][rr * CPR + cc][e]; }
-    part[(int64_t)blockIdx.x * 2 * C + ch] = a;
-    part[(int64_t)blockIdx.x * 2 * C + C + ch] = b;
+    part[(int64_t)ch * gridDim.x + blockIdx.x] = a;
+    part[(int64_t)(C + ch) * gridDim.x + blockIdx.x] = b;
   }
 }
 
@@ -165,13 +176,11 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const uint16_t* __r
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M, const float* __restrict__ gamma,
                                        const float* __restrict__ coef, float* __restrict__ dgamma, float* __restrict__ dbeta,
                                        float* __restrict__ bcoef) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ch = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (ch >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nb; ++b) {
-    s += part[(int64_t)b * 2 * C + ch];
-    q += part[(int64_t)b * 2 * C + C + ch];
-  }
+  double s, q;
+  wave_sum2(part, nb, C, ch, s, q);
+  if ((threadIdx.x & 63) != 0) return;
   const float mean = coef[2 * C + ch], invstd = coef[3 * C + ch];
   const float g = gamma ? gamma[ch] : 1.f;
   if (dgamma) dgamma[ch] += (float)(q * invstd);
@@ -237,7 +246,7 @@ extern "C" int dpe_bn_stats(const uint16_t* x, int64_t M, int C, int nb, float* 
 
 extern "C" int dpe_bn_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* beta,
                                float* rmean, float* rvar, float momentum, float eps, float* coef, hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, nb, C, M, gamma, beta, rmean, rvar,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, nb, C, M, gamma, beta, rmean, rvar,
                      momentum, eps, coef);
   return 0;
 }
@@ -265,7 +274,7 @@ extern "C" int dpe_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const ui
 
 extern "C" int dpe_bn_bwd_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* coef,
                                    float* dgamma, float* dbeta, float* bcoef, hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, nb, C, M, gamma, coef, dgamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, nb, C, M, gamma, coef, dgamma,
                      dbeta, bcoef);
   return 0;
 }

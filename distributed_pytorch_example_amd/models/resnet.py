@@ -51,8 +51,15 @@ class Bottleneck(nn.Module):
         self.c2 = ConvBN(width, width, 3, stride, 1)
         self.c3 = ConvBN(width, planes * 4, 1)
         self.down = ConvBN(inplanes, planes * 4, 1, stride) if downsample else None
+        cbs = [self.c1, self.c2, self.c3] + ([self.down] if downsample else [])
+        self._fused_params = [t for cb in cbs for t in (cb.conv.weight, cb.bn.weight, cb.bn.bias)]
+        self.fused = True
 
     def forward(self, x):
+        if x.is_cuda and self.training and self.fused:
+            from ._resnet_fused import bottleneck_forward
+
+            return bottleneck_forward(self, x)
         idn = self.down(x, relu=False) if self.down is not None else x
         h = self.c1(x)
         h = self.c2(h)

@@ -20,6 +20,30 @@ from ._state import grad_done, grad_sink, note_use, shadow
 
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 
+# CPU reference path: optionally round activations (forward) and their
+# gradients (backward) to bf16 at the same points the GPU kernels do, so the
+# GPU path can be validated against a reference with identical rounding
+# points (tests) instead of against pure fp32.
+EMULATE_BF16 = False
+
+
+class _RoundBF16(Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+def _emu(x):
+    return _RoundBF16.apply(x) if EMULATE_BF16 else x
+
+
+def _emu_w(w):
+    return w.to(torch.bfloat16).to(w.dtype) if EMULATE_BF16 else w
+
 
 def _pad8(n: int) -> int:
     return (n + 7) // 8 * 8
@@ -93,12 +117,14 @@ class _LinearFn(Function):
 
 def linear(x, weight, bias=None, act: int = ACT_NONE, out_f32: bool = False):
     if not x.is_cuda:
-        y = F.linear(x.float() if x.dtype != weight.dtype else x, weight, bias)
+        xin = _emu(x.float() if x.dtype != weight.dtype else x)
+        w = weight + (_emu_w(weight) - weight).detach() if EMULATE_BF16 else weight
+        y = F.linear(xin, w, bias)
         if act == ACT_RELU:
             y = F.relu(y)
         elif act == ACT_GELU:
             y = F.gelu(y, approximate="tanh")
-        return y
+        return y if out_f32 else _emu(y)
     if act == ACT_GELU:
         return gelu(_LinearFn.apply(x, weight, bias, ACT_NONE, out_f32))
     return _LinearFn.apply(x, weight, bias, act, out_f32)
@@ -224,9 +250,10 @@ def conv2d_nhwc(x, weight, stride=(1, 1), padding=(0, 0), dilation=(1, 1), stats
     stride, padding, dilation = _pair(stride), _pair(padding), _pair(dilation)
     if not x.is_cuda:
         cin = weight.shape[-1]
-        xc = x[..., :cin].permute(0, 3, 1, 2).float()
-        y = F.conv2d(xc, weight.permute(0, 3, 1, 2), None, stride, padding, dilation)
-        return y.permute(0, 2, 3, 1).contiguous()
+        xc = _emu(x[..., :cin].permute(0, 3, 1, 2).float())
+        w = weight + (_emu_w(weight) - weight).detach() if EMULATE_BF16 else weight
+        y = F.conv2d(xc, w.permute(0, 3, 1, 2), None, stride, padding, dilation)
+        return _emu(y.permute(0, 2, 3, 1).contiguous())
     from ._state import derived_shadow
 
     if x.shape[-1] != weight.shape[-1]:
@@ -279,7 +306,7 @@ def batch_norm_nhwc(x, gamma, beta, running_mean, running_var, training: bool, m
             y = F.relu(y)
         if training and num_batches_tracked is not None:
             num_batches_tracked.add_(1)
-        return y
+        return _emu(y)
     if training:
         if num_batches_tracked is not None:
             num_batches_tracked.add_(1)
@@ -307,7 +334,7 @@ class _MaxPoolFn(Function):
 
 def max_pool2d_nhwc(x, kernel_size=3, stride=2, padding=1):
     if not x.is_cuda:
-        return F.max_pool2d(x.permute(0, 3, 1, 2), kernel_size, stride, padding).permute(0, 2, 3, 1).contiguous()
+        return _emu(F.max_pool2d(x.permute(0, 3, 1, 2), kernel_size, stride, padding).permute(0, 2, 3, 1).contiguous())
     return _MaxPoolFn.apply(x.contiguous(), kernel_size, stride, padding)
 
 
@@ -324,7 +351,7 @@ class _GAvgPoolFn(Function):
 
 def global_avg_pool_nhwc(x):
     if not x.is_cuda:
-        return x.float().mean(dim=(1, 2))
+        return _emu(x.float().mean(dim=(1, 2)))
     return _GAvgPoolFn.apply(x.contiguous())
 
 

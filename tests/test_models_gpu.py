@@ -1,0 +1,121 @@
+"""Model-level GPU tests: the hand-scheduled ResNet bottleneck against the
+per-op autograd path, and GPU (bf16 kernels) against the CPU fp32 reference
+implementation of the same module with identical weights."""
+import copy
+
+import pytest
+import torch
+
+from distributed_pytorch_example_amd.models import get_model
+from distributed_pytorch_example_amd.ops import functional as Fx
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def cos(a, b):
+    a, b = a.float().flatten(), b.float().flatten()
+    return (a @ b / (a.norm() * b.norm() + 1e-12)).item()
+
+
+def _grads(model):
+    return {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+
+
+def test_fused_bottleneck_matches_per_op(C):
+    """One bottleneck block (shallow => well conditioned): hand-scheduled fused
+    fwd/bwd vs the per-op autograd path must agree tightly."""
+    from distributed_pytorch_example_amd.models.resnet import Bottleneck
+
+    torch.manual_seed(0)
+    for inpl, planes, stride, down in [(64, 64, 1, True), (256, 64, 1, False), (256, 128, 2, True)]:
+        b1 = Bottleneck(inpl, planes, stride, down).to(dev)
+        b2 = copy.deepcopy(b1)
+        b2.fused = False
+        x = torch.randn(16, 28, 28, inpl, device=dev).to(torch.bfloat16)
+        x1, x2 = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+        g = torch.randn(16, 28 // stride, 28 // stride, planes * 4, device=dev).to(torch.bfloat16)
+        y1, y2 = b1(x1), b2(x2)
+        assert rel(y1, y2) < 1e-2
+        y1.backward(g)
+        y2.backward(g)
+        assert rel(x1.grad, x2.grad) < 3e-2
+        for (n, p1), (_, p2) in zip(b1.named_parameters(), b2.named_parameters()):
+            assert rel(p1.grad, p2.grad) < 3e-2, n
+        for (n, r1), (_, r2) in zip(b1.named_buffers(), b2.named_buffers()):
+            assert rel(r1, r2) < 1e-2, n
+
+
+def test_resnet_gpu_vs_cpu_reference(C):
+    torch.manual_seed(1)
+    cpu = get_model("resnet_tiny", num_classes=10)
+    gpu = copy.deepcopy(cpu).to(dev)
+    x = torch.randn(8, 3, 32, 32)
+    y = torch.randint(0, 10, (8,))
+    lc = Fx.cross_entropy(cpu(x), y)
+    lc.backward()
+    lg = Fx.cross_entropy(gpu(x.to(dev)), y.to(dev))
+    lg.backward()
+    assert abs(lc.item() - lg.item()) < 5e-2 * abs(lc.item())
+    # bf16 rounding noise is amplified by every BN backward of a random-init net: the CPU
+    # bf16-emulation (tests/test_numerics_cpu.py) shows the same ~0.4 worst-case deviation
+    # from fp32, so deep layers are compared by direction and the head tightly.
+    gc = {n: p.grad for n, p in cpu.named_parameters()}
+    for n, p in gpu.named_parameters():
+        assert cos(p.grad.cpu(), gc[n]) > 0.8, n
+    assert rel(dict(gpu.named_parameters())["fc.bias"].grad.cpu(), gc["fc.bias"]) < 2e-2
+
+
+def test_simplenet_gpu_vs_cpu(C):
+    torch.manual_seed(2)
+    cpu = get_model("simplenet")
+    gpu = copy.deepcopy(cpu).to(dev)
+    cpu.eval(); gpu.eval()  # dropout off for a deterministic comparison
+    x = torch.randn(64, 784)
+    y = torch.randint(0, 10, (64,))
+    lc = Fx.cross_entropy(cpu(x), y)
+    lc.backward()
+    lg = Fx.cross_entropy(gpu(x.to(dev)), y.to(dev))
+    lg.backward()
+    assert abs(lc.item() - lg.item()) < 2e-2
+    gc = {n: p.grad for n, p in cpu.named_parameters()}
+    for n, p in gpu.named_parameters():  # bf16 emulation on CPU: ~5% on layers.0.weight
+        assert rel(p.grad.cpu(), gc[n]) < 0.1, n
+
+
+def test_fused_optimizers_match_torch(C):
+    from distributed_pytorch_example_amd.optim import SGD, Adam, AdamW
+
+    torch.manual_seed(3)
+    for ours_cls, ref_cls, kw in [(Adam, torch.optim.Adam, dict(lr=1e-2, weight_decay=0.01)),
+                                  (AdamW, torch.optim.AdamW, dict(lr=1e-2, weight_decay=0.1)),
+                                  (SGD, torch.optim.SGD, dict(lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True))]:
+        p1 = [torch.randn(1000, 37, device=dev, requires_grad=True), torch.randn(70001, device=dev, requires_grad=True)]
+        p2 = [p.detach().clone().requires_grad_(True) for p in p1]
+        o1, o2 = ours_cls(p1, **kw), ref_cls(p2, **kw)
+        for _ in range(3):
+            for a, b in zip(p1, p2):
+                g = torch.randn_like(a)
+                a.grad, b.grad = g.clone(), g.clone()
+            o1.step(); o2.step()
+        for a, b in zip(p1, p2):
+            assert rel(a.detach(), b.detach()) < 1e-5, ours_cls.__name__
+        sd = o1.state_dict()
+        assert set(sd["param_groups"][0].keys()) == set(o2.state_dict()["param_groups"][0].keys())
+
+
+def test_bf16_shadow_refreshed_by_fused_step(C):
+    from distributed_pytorch_example_amd.ops import _state
+    from distributed_pytorch_example_amd.optim import SGD
+
+    p = torch.randn(64, 32, device=dev, requires_grad=True)
+    sh = _state.shadow(p)
+    opt = SGD([p], lr=0.5)
+    p.grad = torch.ones_like(p)
+    opt.step()
+    assert torch.equal(_state.shadow(p), p.detach().to(torch.bfloat16))
+    assert _state.shadow(p).data_ptr() == sh.data_ptr()
