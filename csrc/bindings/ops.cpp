@@ -215,6 +215,9 @@ dpe::ConvGeom geom(const Tensor& x, const Tensor& w, int64_t sh, int64_t sw, int
   g.K = (int)w.size(0); g.R = (int)w.size(1); g.S = (int)w.size(2);
   g.sh = (int)sh; g.sw = (int)sw; g.ph = (int)ph; g.pw = (int)pw; g.dh = (int)dh; g.dw = (int)dw;
   g.OH = (int)OH; g.OW = (int)OW;
+  g.RR = g.R; g.SS = g.S;
+  g.pr0 = 0; g.ps0 = 0; g.psh = 1; g.psw = 1;
+  g.remap = 0; g.Hr = g.H; g.Wr = g.W; g.oa = 0; g.ob = 0;
   return g;
 }
 
@@ -223,8 +226,8 @@ bool is_pointwise(const dpe::ConvGeom& g) {
 }
 
 // x NHWC bf16 [N,H,W,C], w [K,R,S,C] bf16 -> y NHWC [N,OH,OW,K]
-Tensor conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64_t> stride, std::vector<int64_t> pad,
-                std::vector<int64_t> dil, const c10::optional<Tensor>& col_stats, const c10::optional<Tensor>& bias) {
+std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64_t> stride, std::vector<int64_t> pad,
+                             std::vector<int64_t> dil, bool want_stats, const c10::optional<Tensor>& bias) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && x.size(3) == w.size(3), "conv: NHWC x / KRSC w shape mismatch");
   TORCH_CHECK(x.size(3) % 8 == 0 && w.size(0) % 8 == 0, "conv: channels must be multiples of 8");
@@ -239,13 +242,16 @@ Tensor conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64_t> stride, s
   a.M = (int)(x.size(0) * OH * OW); a.N = g.K; a.K = (int)(R * S * g.C);
   a.lda = g.C; a.ldb = a.K; a.ldc = g.K;
   a.bias = fpo(bias);
-  if (col_stats.has_value() && col_stats->defined()) {
-    CHECK_F32((*col_stats));
-    TORCH_CHECK(col_stats->numel() >= 2 * g.K, "col_stats must hold 2*K floats");
-    a.col_stats = fp(*col_stats);
+  Tensor stats;
+  if (want_stats) {
+    // [2][K][tilesM] partial (sum, sumsq) per output channel and M-tile, reduced by bn_fwd_train
+    const Cfg c = pick_cfg(a.M, a.N, a.K, false);
+    const int64_t tilesM = (a.M + c.bm - 1) / c.bm;
+    stats = at::empty({2, g.K, tilesM}, x.options().dtype(at::kFloat));
+    a.col_stats = fp(stats);
   }
   run_igemm(a, is_pointwise(g) ? dpe::A_DENSE_K : dpe::A_CONV_FWD, dpe::B_DENSE_K, dpe::EPI_BF16, false);
-  return y;
+  return {y, stats};
 }
 
 // dx NHWC [N,H,W,C] = conv_transpose(dy, w); optional residual added into dx
@@ -261,8 +267,37 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape
   a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.K;
   a.lda = g.K; a.ldb = g.C; a.ldc = g.C;
   if (residual.has_value() && residual->defined()) { CHECK_BF16((*residual)); CHECK_CONTIG((*residual)); a.residual = bp(*residual); }
-  if (is_pointwise(g)) run_igemm(a, dpe::A_DENSE_K, dpe::B_DENSE_N, dpe::EPI_BF16, false);
-  else run_igemm(a, dpe::A_CONV_DGRAD, dpe::B_CONV_DGRAD, dpe::EPI_BF16, false);
+  if (is_pointwise(g)) {
+    run_igemm(a, dpe::A_DENSE_K, dpe::B_DENSE_N, dpe::EPI_BF16, false);
+  } else if (g.sh == 1 && g.sw == 1) {
+    run_igemm(a, dpe::A_CONV_DGRAD, dpe::B_CONV_DGRAD, dpe::EPI_BF16, false);
+  } else {
+    // Strided: one stride-1 sub-GEMM per output parity (a, b) over only the
+    // taps that reach it -- no MFMA work on structural zeros.  A parity with
+    // no taps is a K = 0 GEMM that stores zeros (+ residual).
+    for (int pa = 0; pa < g.sh; ++pa) {
+      for (int pb = 0; pb < g.sw; ++pb) {
+        dpe::ConvGeom v = g;
+        const int r0 = (pa + g.ph) % g.sh, s0 = (pb + g.pw) % g.sw;
+        const int Rp = g.R > r0 ? (g.R - r0 + g.sh - 1) / g.sh : 0;
+        const int Sp = g.S > s0 ? (g.S - s0 + g.sw - 1) / g.sw : 0;
+        const int Hp = (g.H - pa + g.sh - 1) / g.sh, Wp = (g.W - pb + g.sw - 1) / g.sw;
+        if (Hp <= 0 || Wp <= 0) continue;
+        TORCH_CHECK(g.dh == 1 && g.dw == 1, "strided dgrad with dilation is not supported");
+        v.H = Hp; v.W = Wp; v.R = Rp; v.S = Sp;
+        v.sh = 1; v.sw = 1;
+        v.ph = (pa + g.ph - r0) / g.sh;  // oh = hh + ph' - t
+        v.pw = (pb + g.pw - s0) / g.sw;
+        v.pr0 = r0; v.ps0 = s0; v.psh = g.sh; v.psw = g.sw;
+        v.remap = 1; v.Hr = g.H; v.Wr = g.W; v.oa = pa; v.ob = pb;
+        auto b = a;
+        b.g = v;
+        b.M = g.N * Hp * Wp;
+        b.K = Rp * Sp * g.K;
+        run_igemm(b, dpe::A_CONV_DGRAD, dpe::B_CONV_DGRAD, dpe::EPI_BF16, false);
+      }
+    }
+  }
   return dx;
 }
 
@@ -296,8 +331,9 @@ std::vector<Tensor> bn_fwd_train(const Tensor& x, const c10::optional<Tensor>& g
   Tensor coef = at::empty({4, C}, fo);
   hipStream_t st = cur_stream();
   if (stats.has_value() && stats->defined()) {
-    CHECK_RC(dpe_bn_finalize(fp(*stats), 1, (int)C, M, fpo(gamma), fpo(beta), fpom(rmean), fpom(rvar), (float)momentum,
-                             (float)eps, fp(coef), st), "bn_finalize");
+    TORCH_CHECK(stats->dim() == 3 && stats->size(0) == 2 && stats->size(1) == C, "stats must be [2][C][nb] partials");
+    CHECK_RC(dpe_bn_finalize(fp(*stats), (int)stats->size(2), (int)C, M, fpo(gamma), fpo(beta), fpom(rmean), fpom(rvar),
+                             (float)momentum, (float)eps, fp(coef), st), "bn_finalize");
   } else {
     const int nb = dpe_bn_stats_nblocks(M, (int)C);
     Tensor part = at::empty({nb, 2, C}, fo);
@@ -570,7 +606,7 @@ void register_ops(pybind11::module& m) {
   m.def("linear_dgrad", &linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("residual") = py::none());
   m.def("linear_wgrad", &linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("alpha") = 1.0);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
-        py::arg("col_stats") = py::none(), py::arg("bias") = py::none());
+        py::arg("want_stats") = false, py::arg("bias") = py::none());
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), py::arg("residual") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),

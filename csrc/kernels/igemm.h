@@ -31,6 +31,13 @@ struct ConvGeom {
   int OH, OW, K;       // output NHW(K)
   int R, S;            // filter
   int sh, sw, ph, pw, dh, dw;
+  // Phase-decomposed data-grad (stride > 1): the GEMM runs on a virtual
+  // stride-1 problem over one output parity (a, b); taps t map to real filter
+  // rows r = pr0 + psh*t (same for columns), and output row (n, hh, ww) is
+  // stored at dX[n, oa + psh*hh, ob + psw*ww].  remap = 0: identity.
+  int RR, SS;          // real filter dims (weight addressing)
+  int pr0, ps0, psh, psw;
+  int remap, Hr, Wr, oa, ob;
 };
 
 struct IgemmArgs {
@@ -39,7 +46,7 @@ struct IgemmArgs {
   void* C;
   const uint16_t* residual;  // bf16 [M][ldc] added in the EPI_BF16 epilogue (may alias C)
   const float* bias;         // [N] or nullptr
-  float* col_stats;          // [2][N] per-column (sum, sumsq) of the stored bf16 output, or nullptr
+  float* col_stats;          // [2][N][tilesM] per-(column, M-tile) (sum, sumsq) of the stored bf16 output, or nullptr
   int M, N, K;
   int64_t lda, ldb, ldc;
   float alpha;

@@ -188,8 +188,8 @@ struct MNLoader {
   int krow[NC], cc[NC];
   bool vcol[NC];
   int kk[NC];
-  // dgrad weights: k = (r,s,co) -> co, rs
-  int co[NC], rs[NC];
+  // dgrad weights: k = (t,u,co) -> co, virtual taps (t,u) -> real (r,s)
+  int co[NC], tt[NC], uu[NC];
   // wgrad im2col: k = pixel -> (img, oh, ow); column chunk -> (r, s, ci)
   int img[NC], oh[NC], ow[NC];
   int roff[NC], soff[NC];
@@ -209,8 +209,10 @@ struct MNLoader {
       } else if constexpr (KIND == B_CONV_DGRAD) {
         const ConvGeom& g = p.g;
         co[i] = kk[i] % g.K;
-        rs[i] = kk[i] / g.K;
-        base[i] = ptr + gcc;  // + co*RSC + rs*C
+        const int rs = kk[i] / g.K;
+        tt[i] = rs / g.S;
+        uu[i] = rs % g.S;
+        base[i] = ptr + gcc;  // + co*RR*SS*C + (r*SS + s)*C
       } else {  // B_CONV_WGRAD
         const ConvGeom& g = p.g;
         const int cin = gcc % g.C, t = gcc / g.C;
@@ -235,7 +237,8 @@ struct MNLoader {
         regs[i] = v ? ld16(base[i]) : zero16();
       } else if constexpr (KIND == B_CONV_DGRAD) {
         const ConvGeom& g = p.g;
-        regs[i] = v ? ld16(base[i] + (int64_t)co[i] * g.R * g.S * g.C + (int64_t)rs[i] * g.C) : zero16();
+        const int r = g.pr0 + g.psh * tt[i], s_ = g.ps0 + g.psw * uu[i];
+        regs[i] = v ? ld16(base[i] + (int64_t)co[i] * g.RR * g.SS * g.C + (int64_t)(r * g.SS + s_) * g.C) : zero16();
       } else {
         const ConvGeom& g = p.g;
         const int ih = oh[i] * g.sh + roff[i], iw = ow[i] * g.sw + soff[i];
@@ -253,7 +256,10 @@ struct MNLoader {
         base[i] += BK * ld;
       } else if constexpr (KIND == B_CONV_DGRAD) {
         co[i] += BK;
-        while (co[i] >= p.g.K) { co[i] -= p.g.K; ++rs[i]; }
+        while (co[i] >= p.g.K) {
+          co[i] -= p.g.K;
+          if (++uu[i] == p.g.S) { uu[i] = 0; ++tt[i]; }
+        }
       } else {
         ow[i] += BK;
         while (ow[i] >= p.g.OW) {
@@ -467,11 +473,16 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
       const int m = m0 + rr;
       if (m >= p.M) break;
       u32x4 v = *(const u32x4*)(smem + rr * CROW + c * 16);
-      uint16_t* dst = C + (int64_t)m * p.ldc + n;
+      int64_t orow = m;
+      if (p.g.remap) {  // phase dgrad: virtual row (n, hh, ww) -> real dX pixel
+        const int ww = m % p.g.W, t = m / p.g.W, hh = t % p.g.H, nn = t / p.g.H;
+        orow = ((int64_t)nn * p.g.Hr + p.g.oa + p.g.psh * hh) * p.g.Wr + p.g.ob + p.g.psw * ww;
+      }
+      uint16_t* dst = C + orow * p.ldc + n;
       if (p.residual) {
         float f[8], g[8];
         unpack8(v, f);
-        const uint16_t* src = p.residual + (int64_t)m * p.ldc + n;
+        const uint16_t* src = p.residual + orow * p.ldc + n;
         if (vec) {
           unpack8(ld16(src), g);
         } else {
@@ -516,12 +527,14 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
         }
       }
       __syncthreads();
+      // per-(M-tile) partials, layout [2][N][tilesM]: no atomics, deterministic;
+      // the BatchNorm finalize reduces the tilesM partials of each channel.
       if (tid < BN && n0 + tid < p.N) {
         float a = 0.f, b = 0.f;
 #pragma unroll
         for (int w = 0; w < 4; ++w) { a += red[w * BN + tid]; b += red[4 * BN + w * BN + tid]; }
-        atomicAdd(p.col_stats + n0 + tid, a);
-        atomicAdd(p.col_stats + p.N + n0 + tid, b);
+        p.col_stats[(int64_t)(n0 + tid) * tilesM + tm] = a;
+        p.col_stats[(int64_t)(p.N + n0 + tid) * tilesM + tm] = b;
       }
     }
   }

@@ -40,19 +40,15 @@ class BottleneckFn(Function):
         C = ext()
         convs = [block.c1, block.c2, block.c3] + ([block.down] if block.down is not None else [])
         ws = [shadow(cb.conv.weight) for cb in convs]
-        stat_sizes = [cb.conv.out_channels * 2 for cb in convs]
-        stats = torch.zeros(sum(stat_sizes), dtype=torch.float32, device=x.device)
-        st = list(torch.split(stats, stat_sizes))
-        saved = [x]
         coefs = []
 
         def convbn(i, inp, relu, residual=None):
             cb = convs[i]
             s, p, d = _conv_conf(cb.conv)
-            h = C.conv_fwd(inp, ws[i], s, p, d, st[i], None)
+            h, st = C.conv_fwd(inp, ws[i], s, p, d, True, None)   # BN stats partials from the epilogue
             bn = cb.bn
             y, coef = C.bn_fwd_train(h, bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var,
-                                     bn.momentum, bn.eps, relu, residual, st[i])
+                                     bn.momentum, bn.eps, relu, residual, st)
             coefs.append(coef)
             return h, y
 

@@ -21,12 +21,6 @@ from ..ops import functional as Fx
 from ..ops.layers import BatchNorm2d, Conv2d, Linear
 
 
-def _stats(x: torch.Tensor, c: int) -> Optional[torch.Tensor]:
-    if x.is_cuda and torch.is_grad_enabled():
-        return torch.zeros(2 * c, dtype=torch.float32, device=x.device)
-    return None
-
-
 class ConvBN(nn.Module):
     """conv -> BN (training stats from the conv epilogue) -> optional residual add -> optional ReLU."""
 
@@ -36,8 +30,10 @@ class ConvBN(nn.Module):
         self.bn = BatchNorm2d(cout)
 
     def forward(self, x, relu=True, residual=None):
-        st = _stats(x, self.conv.out_channels) if self.bn.training else None
-        y = self.conv(x, st)
+        if self.bn.training and x.is_cuda:
+            y, st = self.conv(x, want_stats=True)   # BN statistics from the conv epilogue
+        else:
+            y, st = self.conv(x), None
         return self.bn(y, relu=relu, residual=residual, stats=st)
 
 

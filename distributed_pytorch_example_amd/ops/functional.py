@@ -202,17 +202,20 @@ def _conv_out(h, k, s, p, d):
 
 class _ConvFn(Function):
     @staticmethod
-    def forward(ctx, x, weight, w16, stride, padding, dilation, stats):
+    def forward(ctx, x, weight, w16, stride, padding, dilation, want_stats):
         C = ext()
-        y = C.conv_fwd(x, w16, list(stride), list(padding), list(dilation), stats, None)
+        y, st = C.conv_fwd(x, w16, list(stride), list(padding), list(dilation), want_stats, None)
         ctx.save_for_backward(x)
         ctx.w16, ctx.weight = w16, weight
         ctx.conf = (list(stride), list(padding), list(dilation))
         note_use(weight)
+        if want_stats:
+            ctx.mark_non_differentiable(st)
+            return y, st
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, *unused):
         C = ext()
         (x,) = ctx.saved_tensors
         stride, padding, dilation = ctx.conf
@@ -245,22 +248,26 @@ def _pad_filter_channels(cp: int):
     return fn
 
 
-def conv2d_nhwc(x, weight, stride=(1, 1), padding=(0, 0), dilation=(1, 1), stats: Optional[torch.Tensor] = None):
-    """x: [N,H,W,Cin'] (Cin' >= Cin, zero-padded channels allowed), weight: [Cout,R,S,Cin] fp32 master."""
+def conv2d_nhwc(x, weight, stride=(1, 1), padding=(0, 0), dilation=(1, 1), want_stats: bool = False):
+    """x: [N,H,W,Cin'] (Cin' >= Cin, zero-padded channels allowed), weight: [Cout,R,S,Cin] fp32 master.
+
+    With ``want_stats`` (GPU) returns ``(y, stats)`` where ``stats`` holds per-channel
+    partial (sum, sum^2) of y from the GEMM epilogue, consumed by ``batch_norm_nhwc``."""
     stride, padding, dilation = _pair(stride), _pair(padding), _pair(dilation)
     if not x.is_cuda:
         cin = weight.shape[-1]
         xc = _emu(x[..., :cin].permute(0, 3, 1, 2).float())
         w = weight + (_emu_w(weight) - weight).detach() if EMULATE_BF16 else weight
         y = F.conv2d(xc, w.permute(0, 3, 1, 2), None, stride, padding, dilation)
-        return _emu(y.permute(0, 2, 3, 1).contiguous())
+        y = _emu(y.permute(0, 2, 3, 1).contiguous())
+        return (y, None) if want_stats else y
     from ._state import derived_shadow
 
     if x.shape[-1] != weight.shape[-1]:
         w16 = derived_shadow(weight, f"cpad{x.shape[-1]}", _pad_filter_channels(x.shape[-1]))
     else:
         w16 = shadow(weight)
-    return _ConvFn.apply(x.contiguous(), weight, w16, stride, padding, dilation, stats)
+    return _ConvFn.apply(x.contiguous(), weight, w16, stride, padding, dilation, want_stats)
 
 
 def _pair(v) -> tuple:

@@ -87,8 +87,8 @@ class Conv2d(nn.Module):
         with torch.no_grad():
             self.weight.normal_(0, std)
 
-    def forward(self, x, stats=None):
-        return Fx.conv2d_nhwc(x, self.weight, self.stride, self.padding, self.dilation, stats)
+    def forward(self, x, want_stats: bool = False):
+        return Fx.conv2d_nhwc(x, self.weight, self.stride, self.padding, self.dilation, want_stats)
 
     def extra_repr(self):
         return (f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, stride={self.stride}, "

@@ -94,12 +94,12 @@ def test_conv_fwd(C, N, H, W, Ci, Co, k, s, p):
     x = bf(torch.randn(N, H, W, Ci, device=dev))
     w = bf(torch.randn(Co, k, k, Ci, device=dev) / math.sqrt(k * k * Ci))
     ref = _conv_ref(x, w, s, p)
-    stats = torch.zeros(2 * Co, device=dev)
-    y = C.conv_fwd(x, w, [s, s], [p, p], [1, 1], stats, None)
+    y, stats = C.conv_fwd(x, w, [s, s], [p, p], [1, 1], True, None)
     assert y.shape == ref.shape and rel_err(y, ref) < 1e-2
     yf = y.float().reshape(-1, Co)
-    assert rel_err(stats[:Co], yf.sum(0)) < 1e-3
-    assert rel_err(stats[Co:], (yf * yf).sum(0)) < 1e-3
+    tot = stats.sum(-1)
+    assert rel_err(tot[0], yf.sum(0)) < 1e-3
+    assert rel_err(tot[1], (yf * yf).sum(0)) < 1e-3
 
 
 @pytest.mark.parametrize("N,H,W,Ci,Co,k,s,p", [c for c in CONV_CASES if c[3] != 8])
@@ -133,7 +133,7 @@ def test_resnet_scale_shapes(C):
     N, H, Ci, Co = 32, 56, 64, 256
     x = bf(torch.randn(N, H, H, Ci, device=dev))
     w = bf(torch.randn(Co, 1, 1, Ci, device=dev) / 8)
-    y = C.conv_fwd(x, w, [1, 1], [0, 0], [1, 1], None, None)
+    y, _ = C.conv_fwd(x, w, [1, 1], [0, 0], [1, 1], False, None)
     assert rel_err(y, _conv_ref(x, w, 1, 0)) < 1e-2
     dy = bf(torch.randn_like(y.float()))
     dw = torch.zeros(Co, 1, 1, Ci, device=dev)
@@ -178,8 +178,7 @@ def test_bn_stats_from_conv_epilogue(C):
     torch.manual_seed(8)
     x = bf(torch.randn(4, 16, 16, 64, device=dev))
     w = bf(torch.randn(128, 3, 3, 64, device=dev) / 24)
-    st = torch.zeros(256, device=dev)
-    y = C.conv_fwd(x, w, [1, 1], [1, 1], [1, 1], st, None)
+    y, st = C.conv_fwd(x, w, [1, 1], [1, 1], [1, 1], True, None)
     g, b = torch.ones(128, device=dev), torch.zeros(128, device=dev)
     y1, c1 = C.bn_fwd_train(y, g, b, None, None, 0.1, 1e-5, True, None, None)
     y2, c2 = C.bn_fwd_train(y, g, b, None, None, 0.1, 1e-5, True, None, st)
