@@ -1,0 +1,236 @@
+"""Training application -- CLI-, log- and checkpoint-compatible with the
+reference `train.py` (`train.py:212-318`), executed on the MI355X stack.
+
+Same 6 flags with the same defaults (`train.py:213-221`), the same log lines
+(`train.py:77-80,226-247,285-316`), the same per-epoch flow (set_epoch ->
+train -> validate -> metric all-reduce / world -> rank-0 checkpoints ->
+barrier) and the same checkpoint files/keys.  Additive flags select the
+BASELINE-scope models, backend, bucket size, grad accumulation, etc.
+
+Deliberate fixes: resume is read by rank 0 and broadcast; the
+training loss is accumulated on the device (the reference forces a device
+sync with ``loss.item()`` every step, `train.py:141`); synthetic data lives in
+HBM (no DataLoader worker processes, no per-batch H2D) unless ``--loader torch``.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import time
+
+import torch
+from torch.distributed.elastic.multiprocessing.errors import record
+
+from .data import SyntheticDataset, SyntheticTokens, create_data_loader
+from .models import get_model
+from .ops import functional as Fx
+from .optim import build_optimizer
+from .parallel import DDP
+from .parallel import dist as pdist
+from .utils.checkpoint import load_checkpoint, resume_exists, save_checkpoint, wait_pending
+from .utils.env import ensure_single_process_env
+from .utils.logging import get_logger
+from .utils import fault
+
+logger = get_logger("__main__")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser()
+    # ---- reference flags (train.py:213-221), identical names and defaults
+    p.add_argument("--epochs", type=int, default=10)
+    p.add_argument("--batch-size", type=int, default=64)
+    p.add_argument("--lr", type=float, default=0.001)
+    p.add_argument("--num-samples", type=int, default=10000)
+    p.add_argument("--checkpoint-dir", type=str, default="./checkpoints")
+    p.add_argument("--resume", type=str, default=None)
+    # ---- additive
+    p.add_argument("--model", default="simplenet", choices=["simplenet", "resnet50", "resnet_tiny", "gpt2", "gpt2-tiny"])
+    p.add_argument("--backend", default="auto", choices=["auto", "rccl", "nccl", "gloo"])
+    p.add_argument("--optimizer", default=None, choices=[None, "adam", "adamw", "sgd"])
+    p.add_argument("--weight-decay", type=float, default=0.0)
+    p.add_argument("--bucket-mb", type=float, default=25.0)
+    p.add_argument("--grad-accum", type=int, default=1)
+    p.add_argument("--seed", type=int, default=None, help="seed the synthetic data (reference: unseeded)")
+    p.add_argument("--loader", default="auto", choices=["auto", "device", "torch"])
+    p.add_argument("--image-size", type=int, default=224)
+    p.add_argument("--seq-len", type=int, default=1024)
+    p.add_argument("--max-steps", type=int, default=None, help="stop each epoch after this many steps")
+    p.add_argument("--async-checkpoint", action="store_true")
+    p.add_argument("--auto-resume", action="store_true", help="resume from <checkpoint-dir>/latest_model.pt if present")
+    p.add_argument("--profile", type=str, default=None, help="write a torch.profiler chrome trace to this path")
+    return p
+
+
+def _datasets(args, device):
+    if args.model == "simplenet":
+        tr = SyntheticDataset(args.num_samples, 784, 10, seed=args.seed)
+        va = SyntheticDataset(args.num_samples // 10, 784, 10, seed=None if args.seed is None else args.seed + 1)
+        return tr, va, 10
+    if args.model.startswith("resnet"):
+        shp = (3, args.image_size, args.image_size)
+        ncls = 1000 if args.model == "resnet50" else 10
+        tr = SyntheticDataset(args.num_samples, shp, ncls, seed=args.seed)
+        va = SyntheticDataset(max(1, args.num_samples // 10), shp, ncls, seed=None if args.seed is None else args.seed + 1)
+        return tr, va, ncls
+    vocab = 50257 if args.model == "gpt2" else 512
+    tr = SyntheticTokens(args.num_samples, args.seq_len, vocab, seed=args.seed)
+    va = SyntheticTokens(max(1, args.num_samples // 10), args.seq_len, vocab, seed=None if args.seed is None else args.seed + 1)
+    return tr, va, vocab
+
+
+def train_epoch(model, loader, optimizer, criterion, device, epoch, rank, grad_accum=1, max_steps=None):
+    """Reference `train_epoch` (`train.py:119-151`); loss accumulated on device."""
+    model.train()
+    total_loss = torch.zeros((), dtype=torch.float64, device=device)
+    num_batches = 0
+    nb = len(loader)
+    for batch_idx, (data, target) in enumerate(loader):
+        if max_steps is not None and batch_idx >= max_steps:
+            break
+        fault.maybe_inject(epoch, batch_idx)
+        data, target = data.to(device, non_blocking=True), target.to(device, non_blocking=True)
+        sync = (batch_idx + 1) % grad_accum == 0 or batch_idx + 1 == nb
+        ctx = model.no_sync() if (not sync and hasattr(model, "no_sync")) else _null()
+        with ctx:
+            output = model(data)
+            loss = criterion(output, target)
+            (loss / grad_accum if grad_accum > 1 else loss).backward()
+        if sync:
+            optimizer.step()
+            optimizer.zero_grad()
+        total_loss += loss.detach()
+        num_batches += 1
+        if batch_idx % 10 == 0 and rank == 0:
+            logger.info(f"Epoch {epoch}, Batch {batch_idx}/{nb}, Loss: {loss.item():.4f}")
+    return (total_loss / max(1, num_batches)).item()
+
+
+@torch.no_grad()
+def validate(model, loader, criterion, device, num_classes, max_steps=None):
+    """Reference `validate` (`train.py:154-175`): mean of per-batch losses, accuracy in %."""
+    model.eval()
+    total_loss = torch.zeros((), dtype=torch.float64, device=device)
+    correct = torch.zeros((), dtype=torch.float64, device=device)
+    total = 0
+    nbatches = 0
+    for i, (data, target) in enumerate(loader):
+        if max_steps is not None and i >= max_steps:
+            break
+        data, target = data.to(device), target.to(device)
+        output = model(data)
+        s, c = Fx.cross_entropy_eval(output, target, num_classes)
+        total_loss += s / target.numel()
+        correct += c
+        total += target.numel()
+        nbatches += 1
+    return (total_loss / max(1, nbatches)).item(), (100.0 * correct / max(1, total)).item()
+
+
+@record
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    ensure_single_process_env()
+    rank, world_size, local_rank = pdist.init_process_group(args.backend)
+    logger.info(f"Initialized process group: rank={rank}, world_size={world_size}, local_rank={local_rank}")
+    device = pdist.get_device(local_rank)
+
+    logger.info(f"Starting distributed training with {world_size} processes")
+    logger.info(f"Configuration: epochs={args.epochs}, batch_size={args.batch_size}, lr={args.lr}")
+
+    model = get_model(args.model).to(device)
+    model = DDP(model, bucket_cap_mb=args.bucket_mb)
+    logger.info(f"Model parameters: {sum(p.numel() for p in model.parameters()):,}")
+
+    train_dataset, val_dataset, num_classes = _datasets(args, device)
+    mode = args.loader if args.loader != "auto" else ("device" if device.type == "cuda" else "torch")
+    train_loader, train_sampler = create_data_loader(train_dataset, args.batch_size, rank, world_size, mode=mode,
+                                                     device=device)
+    val_loader, _ = create_data_loader(val_dataset, args.batch_size, rank, world_size, mode=mode, device=device)
+    logger.info(f"Dataset size: {len(train_dataset)}, batches per epoch: {len(train_loader)}")
+
+    opt_name = args.optimizer or ("adam" if args.model == "simplenet" else ("sgd" if args.model.startswith("resnet") else "adamw"))
+    optimizer = build_optimizer(opt_name, model.parameters(), lr=args.lr, weight_decay=args.weight_decay)
+
+    def criterion(out, tgt):
+        return Fx.cross_entropy(out, tgt, num_classes)
+
+    start_epoch = 0
+    if rank == 0:
+        os.makedirs(args.checkpoint_dir, exist_ok=True)
+    resume = args.resume
+    if resume is None and args.auto_resume:
+        resume = os.path.join(args.checkpoint_dir, "latest_model.pt")
+    if resume_exists(resume):
+        start_epoch = load_checkpoint(model, optimizer, resume, device)
+
+    pdist.barrier()
+
+    best_accuracy = 0.0
+    start_time = time.time()
+    prof = _profiler(args.profile, rank)
+
+    for epoch in range(start_epoch, args.epochs):
+        epoch_start = time.time()
+        train_sampler.set_epoch(epoch)
+        train_loss = train_epoch(model, train_loader, optimizer, criterion, device, epoch, rank, args.grad_accum,
+                                 args.max_steps)
+        val_loss, val_accuracy = validate(model, val_loader, criterion, device, num_classes, args.max_steps)
+
+        metrics = torch.tensor([train_loss, val_loss, val_accuracy], device=device)
+        pdist.all_reduce(metrics, "sum")
+        metrics /= world_size
+        avg_train_loss, avg_val_loss, avg_val_accuracy = (v.item() for v in metrics)
+
+        epoch_time = time.time() - epoch_start
+        if rank == 0:
+            logger.info(f"Epoch {epoch} completed in {epoch_time:.2f}s")
+            logger.info(f"  Train Loss: {avg_train_loss:.4f}")
+            logger.info(f"  Val Loss: {avg_val_loss:.4f}, Val Accuracy: {avg_val_accuracy:.2f}%")
+            nb = min(len(train_loader), args.max_steps or len(train_loader))
+            logger.info(f"  Throughput: {nb * args.batch_size * world_size / epoch_time:.1f} samples/s (incl. validation)")
+            if avg_val_accuracy > best_accuracy:
+                best_accuracy = avg_val_accuracy
+                save_checkpoint(model, optimizer, epoch, avg_train_loss,
+                                os.path.join(args.checkpoint_dir, "best_model.pt"), args.async_checkpoint)
+            save_checkpoint(model, optimizer, epoch, avg_train_loss,
+                            os.path.join(args.checkpoint_dir, "latest_model.pt"), args.async_checkpoint)
+        if prof is not None:
+            prof.step()
+        pdist.barrier()
+
+    wait_pending()
+    total_time = time.time() - start_time
+    if prof is not None:
+        prof.__exit__(None, None, None)
+    if rank == 0:
+        logger.info(f"Training completed in {total_time:.2f}s")
+        logger.info(f"Best validation accuracy: {best_accuracy:.2f}%")
+    pdist.destroy_process_group()
+
+
+def _profiler(path, rank):
+    if not path:
+        return None
+    from torch.profiler import ProfilerActivity, profile
+
+    acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if torch.cuda.is_available() else [])
+
+    def handler(p):
+        p.export_chrome_trace(path.replace(".json", f".rank{rank}.json"))
+
+    prof = profile(activities=acts, on_trace_ready=handler)
+    prof.__enter__()
+    return prof
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,53 @@
+"""CLI / env / logging contract parity with the reference."""
+import logging
+import os
+
+import pytest
+
+from distributed_pytorch_example_amd.train import build_parser
+from distributed_pytorch_example_amd.utils.env import read_env
+from distributed_pytorch_example_amd.utils.logging import LOG_FORMAT, RankLogFilter
+
+
+def test_reference_flags_and_defaults():
+    a = build_parser().parse_args([])
+    assert (a.epochs, a.batch_size, a.lr, a.num_samples, a.checkpoint_dir, a.resume) == (
+        10, 64, 0.001, 10000, "./checkpoints", None)
+    b = build_parser().parse_args("--epochs 3 --batch-size 32 --lr 0.01 --num-samples 500 --checkpoint-dir /x --resume y".split())
+    assert (b.epochs, b.batch_size, b.lr, b.num_samples, b.checkpoint_dir, b.resume) == (3, 32, 0.01, 500, "/x", "y")
+
+
+def test_log_format_matches_reference():
+    assert LOG_FORMAT == "%(asctime)s - %(name)s - %(levelname)s - [Rank %(rank)s] %(message)s"
+    rec = logging.LogRecord("__main__", logging.INFO, __file__, 1, "hello", None, None)
+    os.environ["RANK"] = "3"
+    try:
+        RankLogFilter().filter(rec)
+        assert rec.rank == "3"
+    finally:
+        del os.environ["RANK"]
+    RankLogFilter().filter(rec)
+    assert rec.rank == "?"
+
+
+def test_env_contract():
+    e = read_env({"RANK": "5", "LOCAL_RANK": "1", "WORLD_SIZE": "8", "LOCAL_WORLD_SIZE": "4", "GROUP_RANK": "1",
+                  "MASTER_ADDR": "10.0.0.1", "MASTER_PORT": "1234"})
+    assert (e.rank, e.local_rank, e.world_size, e.local_world_size, e.group_rank, e.master_addr, e.master_port) == (
+        5, 1, 8, 4, 1, "10.0.0.1", 1234)
+    assert read_env({}).world_size == 1
+    with pytest.raises(ValueError):
+        read_env({"RANK": "8", "WORLD_SIZE": "8"})
+    with pytest.raises(ValueError):
+        read_env({"RANK": "x", "WORLD_SIZE": "2"})
+
+
+def test_launcher_worker_env():
+    from distributed_pytorch_example_amd.launch.__main__ import parse, worker_env
+
+    a = parse(["--nnodes=2", "--nproc-per-node=4", "--node-rank=1", "--master-addr=h0", "--master-port=777", "t.py", "--x"])
+    env = worker_env(a, 2, base={})
+    assert env["RANK"] == "6" and env["LOCAL_RANK"] == "2" and env["WORLD_SIZE"] == "8"
+    assert env["LOCAL_WORLD_SIZE"] == "4" and env["GROUP_RANK"] == "1"
+    assert env["MASTER_ADDR"] == "h0" and env["MASTER_PORT"] == "777" and env["OMP_NUM_THREADS"] == "1"
+    assert a.script == "t.py" and a.script_args == ["--x"]

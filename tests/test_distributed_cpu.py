@@ -1,0 +1,171 @@
+"""Multi-process DDP plumbing on CPU/gloo (world 2/4) and launcher behaviour:
+gradient averaging, no_sync accumulation, init broadcast, buffer broadcast,
+end-to-end train + resume, fail-fast fault injection."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _setup(rank, world, port):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank), "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": str(port)})
+    from distributed_pytorch_example_amd.parallel import dist as pdist
+
+    torch.set_num_threads(1)
+    return pdist.init_process_group("gloo")
+
+
+def _w_grad_avg(rank, world, port, q):
+    _setup(rank, world, port)
+    import torch.distributed as dist
+
+    from distributed_pytorch_example_amd.models import SimpleNet
+    from distributed_pytorch_example_amd.parallel import DDP
+
+    torch.manual_seed(100 + rank)  # different init per rank -> DDP must broadcast rank 0's
+    m = SimpleNet()
+    m.eval()  # no dropout: deterministic grads
+    ddp = DDP(m)
+    # init sync: every rank now holds rank 0's parameters
+    for p in m.parameters():
+        ref = p.detach().clone()
+        dist.broadcast(ref, 0)
+        assert torch.equal(p.detach(), ref)
+    torch.manual_seed(7 + rank)
+    x, y = torch.randn(8, 784), torch.randint(0, 10, (8,))
+    # independent local grad for comparison
+    local = [torch.autograd.grad(torch.nn.functional.cross_entropy(m(x), y), list(m.parameters()))]
+    loss = torch.nn.functional.cross_entropy(ddp(x), y)
+    loss.backward()
+    for g_local, p in zip(local[0], m.parameters()):
+        avg = g_local.clone()
+        dist.all_reduce(avg)
+        avg /= world
+        assert torch.allclose(p.grad, avg, atol=1e-6)
+    # no_sync: two local micro-batches then a synced one == average of the sum
+    for p in m.parameters():
+        p.grad = None
+    grads_sum = [torch.zeros_like(p) for p in m.parameters()]
+    for i in range(3):
+        torch.manual_seed(50 + 10 * i + rank)
+        xi, yi = torch.randn(4, 784), torch.randint(0, 10, (4,))
+        gi = torch.autograd.grad(torch.nn.functional.cross_entropy(m(xi), yi), list(m.parameters()))
+        for a, b in zip(grads_sum, gi):
+            a += b
+        if i < 2:
+            with ddp.no_sync():
+                torch.nn.functional.cross_entropy(ddp(xi), yi).backward()
+        else:
+            torch.nn.functional.cross_entropy(ddp(xi), yi).backward()
+    for a, p in zip(grads_sum, m.parameters()):
+        dist.all_reduce(a)
+        a /= world
+        assert torch.allclose(p.grad, a, atol=1e-5)
+    q.put(("ok", rank))
+    dist.destroy_process_group()
+
+
+def _w_buffers(rank, world, port, q):
+    _setup(rank, world, port)
+    import torch.distributed as dist
+
+    from distributed_pytorch_example_amd.models import resnet18_like
+    from distributed_pytorch_example_amd.parallel import DDP
+
+    torch.manual_seed(rank)
+    m = resnet18_like(num_classes=4)
+    ddp = DDP(m, broadcast_buffers=True)
+    torch.manual_seed(rank + 11)
+    out = ddp(torch.randn(2, 3, 32, 32))
+    out.sum().backward()
+    # forward 2 broadcasts rank 0's running stats before running
+    ddp(torch.randn(2, 3, 32, 32))
+    for b in m.buffers():
+        if b.is_floating_point():
+            ref = b.clone()
+            dist.broadcast(ref, 0)
+    q.put(("ok", rank))
+    dist.destroy_process_group()
+
+
+def _spawn(fn, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=fn, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * world, codes
+    res = [q.get(timeout=5) for _ in range(world)]
+    assert sorted(r[1] for r in res) == list(range(world))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ddp_gradient_average_and_no_sync(world):
+    _spawn(_w_grad_avg, world)
+
+
+def test_ddp_buffers_broadcast():
+    _spawn(_w_buffers, 2)
+
+
+def _launch(args, env=None, timeout=300):
+    e = dict(os.environ)
+    e["PYTHONPATH"] = ROOT
+    e.update(env or {})
+    cmd = [sys.executable, "-m", "distributed_pytorch_example_amd.launch", "--nproc-per-node", "2",
+           "--master-port", str(_port()), os.path.join(ROOT, "train.py")] + args
+    return subprocess.run(cmd, env=e, capture_output=True, text=True, timeout=timeout)
+
+
+def test_train_e2e_and_resume(tmp_path):
+    ck = str(tmp_path / "ck")
+    r = _launch(["--epochs", "1", "--num-samples", "512", "--checkpoint-dir", ck, "--backend", "gloo"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    log = r.stdout + r.stderr
+    assert "Starting distributed training with 2 processes" in log
+    assert "Dataset size: 512, batches per epoch: 4" in log
+    assert "Model parameters: 269,322" in log
+    assert os.path.exists(os.path.join(ck, "latest_model.pt")) and os.path.exists(os.path.join(ck, "best_model.pt"))
+    # resume: rank 0 reads, both ranks restart at the saved epoch (re-run semantics)
+    r2 = _launch(["--epochs", "2", "--num-samples", "512", "--checkpoint-dir", ck, "--backend", "gloo", "--resume",
+                  os.path.join(ck, "latest_model.pt")])
+    assert r2.returncode == 0, r2.stderr[-2000:]
+    log2 = r2.stdout + r2.stderr
+    assert log2.count("Checkpoint loaded from") == 2      # both ranks received the state
+    assert "Epoch 0 completed" in log2 and "Epoch 1 completed" in log2
+
+
+def test_fault_injection_fails_fast(tmp_path):
+    r = _launch(["--epochs", "3", "--num-samples", "2048", "--checkpoint-dir", str(tmp_path), "--backend", "gloo"],
+                env={"DPE_FAULT_INJECT": "1:0:3:kill"}, timeout=120)
+    assert r.returncode == 1
+    assert "rank 1 (local_rank 1): exitcode -9" in r.stderr
+
+
+def test_fault_injection_exception_recorded(tmp_path):
+    r = _launch(["--epochs", "1", "--num-samples", "1024", "--checkpoint-dir", str(tmp_path), "--backend", "gloo"],
+                env={"DPE_FAULT_INJECT": "0:0:2:raise"}, timeout=120)
+    assert r.returncode == 1
+    assert "injected fault at rank 0" in r.stderr
