@@ -165,9 +165,15 @@ Tensor linear_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>&
   a.bias = fpo(bias);
   a.act = (int)act;
   if (residual.has_value() && residual->defined()) {
-    TORCH_CHECK(!out_f32, "residual add only for bf16 outputs");
-    CHECK_BF16((*residual)); CHECK_CONTIG((*residual));
-    a.residual = bp(*residual);
+    CHECK_CONTIG((*residual));
+    TORCH_CHECK(residual->numel() == M * N, "residual shape mismatch");
+    if (out_f32) {
+      CHECK_F32((*residual));
+      a.residual_f32 = (const float*)residual->data_ptr();
+    } else {
+      CHECK_BF16((*residual));
+      a.residual = bp(*residual);
+    }
   }
   run_igemm(a, dpe::A_DENSE_K, dpe::B_DENSE_K, out_f32 ? dpe::EPI_F32 : dpe::EPI_BF16, false);
   return y;
@@ -193,16 +199,18 @@ Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const c10::optional<Tenso
 }
 
 // dw[N,K] (+)= dy[M,N]^T @ x[M,K]   (fp32, atomic split-K; dw must be zeroed or hold an accumulation)
+// dy may be column-padded (row stride ldy >= N, ldy % 8 == 0, pad columns zero): then N need not be a
+// multiple of 8 (vocab-padded LM head: N = 50257, ldy = 50304).
 void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(x); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
-  const int64_t N = dw.size(0), K = dw.size(1);
-  TORCH_CHECK(dy.size(-1) == N && x.size(-1) == K && dy.numel() / N == x.numel() / K, "linear_wgrad: shape mismatch");
-  TORCH_CHECK(N % 8 == 0 && K % 8 == 0, "linear_wgrad: features must be multiples of 8");
-  const int64_t M = dy.numel() / N;
+  const int64_t N = dw.size(0), K = dw.size(1), ldy = dy.size(-1);
+  TORCH_CHECK(ldy >= N && x.size(-1) == K && dy.numel() / ldy == x.numel() / K, "linear_wgrad: shape mismatch");
+  TORCH_CHECK(ldy % 8 == 0 && K % 8 == 0, "linear_wgrad: dy row stride and in_features must be multiples of 8");
+  const int64_t M = dy.numel() / ldy;
   auto a = base_args();
   a.A = bp(dy); a.B = bp(x); a.C = dw.data_ptr();
   a.M = (int)N; a.N = (int)K; a.K = (int)M;
-  a.lda = N; a.ldb = K; a.ldc = K;
+  a.lda = ldy; a.ldb = K; a.ldc = K;
   a.alpha = (float)alpha;
   run_igemm(a, dpe::A_DENSE_M, dpe::B_DENSE_N, dpe::EPI_ATOMIC_F32, true);
 }

@@ -1,8 +1,397 @@
-// Causal flash attention (GPT-2 path).  Filled in by the attention milestone.
+// Causal flash attention for GPT-2 (head dim 64) on gfx950 bf16 MFMA
+// (v_mfma_f32_16x16x32_bf16).  qkv is the QKV projection output [B, T, 3, H, 64]
+// (no split/transpose copies); out is [B, T, H, 64] (feeds the out-projection).
+//
+// Forward (one workgroup = 64 queries of one (b, h), 4 waves x 16 queries):
+//   S^T = K . Q^T with K as the A operand, so each lane holds ONE query (lane&15)
+//   and 16 keys in registers: the online-softmax max/sum are lane-local plus
+//   two xor-shuffles (cdna_hip_programming.md App. B, "swapped QK^T").
+//   P is converted to bf16 in registers and used directly as the B operand of
+//   O^T += V^T . P; the key order inside each 32-key MFMA step is permuted
+//   ({4g..4g+3} u {16+4g..}) and the V operand is read with transposing
+//   ds_read_b64_tr_b16 from exactly those rows (§3 "accumulator tile as the
+//   next MFMA's operand").  K/V tiles are register-prefetched one tile ahead
+//   into double-buffered, XOR-swizzled LDS.  Heaviest (latest) query tiles are
+//   scheduled first.  Saves lse2 = m + log2(l) (log2 units, scale folded).
+// Backward (one workgroup = 64 keys, 4 waves x 16 keys; loops over query tiles):
+//   key-on-the-lane: S = Q.K^T and dP = dO.V^T have the key on the lane, so
+//   their accumulators ARE the B operands of dV^T += dO^T.P and
+//   dK^T += Q^T.dS (permuted-k trick again, Q/dO read transposed from LDS).
+//   dS crosses LDS once for dQ = dS.K, summed over key tiles with fp32 atomics
+//   shaped as full 256-B rows.  D = rowsum(dO*O) is precomputed.
 #include "common.h"
 
-extern "C" int dpe_attn_fwd(const uint16_t*, uint16_t*, float*, int, int, int, int, float, int, hipStream_t) { return -1; }
-extern "C" int dpe_attn_bwd(const uint16_t*, const uint16_t*, const uint16_t*, const float*, float*, float*, uint16_t*, int,
-                            int, int, int, float, int, hipStream_t) {
-  return -1;
+namespace dpe {
+
+constexpr int AD = 64;      // head dim
+constexpr int AQ = 64;      // queries per tile
+constexpr int AKV = 64;     // keys per tile
+
+typedef __attribute__((address_space(3))) s16x4 lds4;
+
+// [64 rows][32 bf16] K-contiguous image (64-B rows), swizzled for ds_read_b128 (as igemm)
+DPE_DEVICE int kimg(int row, int chunk) {
+  const int g = (0x78 >> (((row >> 2) & 3) << 1)) & 3;
+  return row * 64 + ((chunk ^ g) << 4);
+}
+// [rows][64 bf16] image (128-B rows) read transposed.  GEMM-style rows {8g+q, 8g+4+q}.
+DPE_DEVICE int mnimg(int k, int chunk) {
+  const int h = (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1;
+  return k * 128 + ((chunk ^ h) << 4);
+}
+// same, for the permuted-key reads (rows {4g+q, 16+4g+q}): conflict-free with h = 2*((k>>1)&3)
+DPE_DEVICE int pimg(int k, int chunk) {
+  const int h = ((k >> 1) & 3) << 1;
+  return k * 128 + ((chunk ^ h) << 4);
+}
+
+DPE_DEVICE bf16x8 kfrag64(const char* img, int r0) {
+  const int lane = threadIdx.x & 63;
+  const int row = r0 + (lane & 15);
+  return __builtin_bit_cast(bf16x8, *(const u32x4*)(img + kimg(row, lane >> 4)));
+}
+
+// A/B operand with k = rows (rows k0 + [perm]), cols c0..c0+15 = lane&15
+template <bool PERM>
+DPE_DEVICE bf16x8 trfrag(const char* img, int k0, int c0) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  int r1, r2;
+  if constexpr (PERM) { r1 = k0 + 4 * g + q; r2 = r1 + 16; }
+  else { r1 = k0 + 8 * g + q; r2 = r1 + 4; }
+  const int ch = (c0 >> 3) + (p >> 1), sub = (p & 1) * 8;
+  const char* a1 = img + (PERM ? pimg(r1, ch) : mnimg(r1, ch)) + sub;
+  const char* a2 = img + (PERM ? pimg(r2, ch) : mnimg(r2, ch)) + sub;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)a1);
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)a2);
+  s16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+DPE_DEVICE bf16x8 pack_frag(const f32x4& a, const f32x4& b) {
+  u32x4 u;
+  u[0] = pack_bf2(a[0], a[1]); u[1] = pack_bf2(a[2], a[3]);
+  u[2] = pack_bf2(b[0], b[1]); u[3] = pack_bf2(b[2], b[3]);
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+#define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
+
+// ======================================================================= fwd
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+                                                       float* __restrict__ lse2, int B, int T, int H, float sl2) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * AKV * 64 + AKV * 128)];  // 2 x (K halves 8K + V 8K)
+  constexpr int KB = 2 * AKV * 64, STG = KB + AKV * 128;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int nq = T / AQ, BH = B * H;
+  const int qt = nq - 1 - (int)(blockIdx.x / BH);
+  const int bh = blockIdx.x % BH, b = bh / H, h = bh % H;
+  const int64_t RS = 3LL * H * AD;
+  const uint16_t* qb = qkv + (int64_t)b * T * RS + (int64_t)h * AD;
+  const uint16_t* kb = qb + H * AD;
+  const uint16_t* vb = qb + 2 * H * AD;
+  const int q0w = qt * AQ + 16 * w;
+  const int myq = q0w + li;
+
+  bf16x8 qf[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+    qf[kk] = __builtin_bit_cast(bf16x8, *(const u32x4*)(qb + (int64_t)myq * RS + 32 * kk + 8 * g));
+
+  // K/V tile chunk ownership: chunk c in [0,512): key = c>>3, dchunk = c&7
+  u32x4 rk[2], rv[2];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, key = c >> 3, dc = c & 7;
+      const int64_t off = (int64_t)(kt * AKV + key) * RS + dc * 8;
+      rk[i] = *(const u32x4*)(kb + off);
+      rv[i] = *(const u32x4*)(vb + off);
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* s = smem + buf * STG;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, key = c >> 3, dc = c & 7;
+      *(u32x4*)(s + (dc >> 2) * (AKV * 64) + kimg(key, dc & 3)) = rk[i];
+      *(u32x4*)(s + KB + pimg(key, dc)) = rv[i];
+    }
+  };
+
+  f32x4 acc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt <= qt; ++kt) {
+    const bool more = kt < qt;
+    if (more) gload(kt + 1);
+    const char* s = smem + cur * STG;
+    f32x4 sc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) sc[nt] = MFMA(kfrag64(s + kk * (AKV * 64), 16 * nt), qf[kk], sc[nt]);
+    }
+    // scale (log2 domain), causal mask on the diagonal tile
+    float mx = -INFINITY;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = sc[nt][e] * sl2;
+        if (kt == qt) {
+          const int key = kt * AKV + 16 * nt + 4 * g + e;
+          if (key > myq) v = -INFINITY;
+        }
+        sc[nt][e] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f(m - mn);
+    float ps = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pv = exp2f(sc[nt][e] - mn);
+        sc[nt][e] = pv;
+        ps += pv;
+      }
+    lsum = lsum * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc[d] *= alpha;
+    const bf16x8 p0 = pack_frag(sc[0], sc[1]), p1 = pack_frag(sc[2], sc[3]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      acc[d] = MFMA(trfrag<true>(s + KB, 0, 16 * d), p0, acc[d]);
+      acc[d] = MFMA(trfrag<true>(s + KB, 32, 16 * d), p1, acc[d]);
+    }
+    if (more) lstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+  float l = lsum + __shfl_xor(lsum, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.f / l;
+  uint16_t* o = out + ((int64_t)(b * T + myq) * H + h) * AD;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    u32x2 pk;
+    pk[0] = pack_bf2(acc[d][0] * inv, acc[d][1] * inv);
+    pk[1] = pack_bf2(acc[d][2] * inv, acc[d][3] * inv);
+    *(u32x2*)(o + 16 * d + 4 * g) = pk;
+  }
+  if (g == 0) lse2[(int64_t)bh * T + myq] = m + __log2f(l);
+}
+
+// ======================================================================= bwd
+// delta[bh][t] = sum_d dO * O
+__global__ __launch_bounds__(256) void attn_delta_kernel(const uint16_t* __restrict__ o, const uint16_t* __restrict__ dout,
+                                                         float* __restrict__ delta, int B, int T, int H) {
+  const int64_t row = blockIdx.x * 32ll + (threadIdx.x >> 3);  // 8 lanes per (b, t, h) row
+  if (row >= (int64_t)B * T * H) return;
+  const int sub = threadIdx.x & 7;
+  float a[8], c[8];
+  unpack8(*(const u32x4*)(o + row * AD + sub * 8), a);
+  unpack8(*(const u32x4*)(dout + row * AD + sub * 8), c);
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s += a[e] * c[e];
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 4, 64);
+  if (sub == 0) {
+    const int h = (int)(row % H);
+    const int64_t bt = row / H;
+    const int t = (int)(bt % T), b = (int)(bt / T);
+    delta[((int64_t)b * H + h) * T + t] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dout,
+                                                       const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                       float* __restrict__ dq_acc, uint16_t* __restrict__ dqkv, int B,
+                                                       int T, int H, float sl2, float scale) {
+  // LDS: Qk (8K) Qmn (8K) dOk (8K) dOmn (8K) Kmn (8K) dS (8K) lse/delta (512 B); dQ staging reuses Qk+Qmn (16K)
+  __shared__ __attribute__((aligned(16))) char smem[6 * 8192 + 512];
+  char* Qk = smem;
+  char* Qm = smem + 8192;
+  char* Ok = smem + 2 * 8192;
+  char* Om = smem + 3 * 8192;
+  char* Km = smem + 4 * 8192;
+  char* dS = smem + 5 * 8192;
+  float* sl = (float*)(smem + 6 * 8192);
+  float* sd = sl + 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int nk = T / AKV, BH = B * H;
+  const int kt = (int)(blockIdx.x / BH);  // key tile (light-first order would be kt = nk-1-...)
+  const int bh = blockIdx.x % BH, b = bh / H, h = bh % H;
+  const int64_t RS = 3LL * H * AD;
+  const uint16_t* qb = qkv + (int64_t)b * T * RS + (int64_t)h * AD;
+  const uint16_t* kb = qb + H * AD;
+  const uint16_t* vb = qb + 2 * H * AD;
+  const int64_t ORS = (int64_t)H * AD;  // dO / O row stride
+  const uint16_t* ob = dout + (int64_t)b * T * ORS + (int64_t)h * AD;
+  const int mykey = kt * AKV + 16 * w + li;
+
+  // wave's own 16 keys as B operands (key on lane)
+  bf16x8 kf[2], vf[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    kf[kk] = __builtin_bit_cast(bf16x8, *(const u32x4*)(kb + (int64_t)mykey * RS + 32 * kk + 8 * g));
+    vf[kk] = __builtin_bit_cast(bf16x8, *(const u32x4*)(vb + (int64_t)mykey * RS + 32 * kk + 8 * g));
+  }
+  // block's K tile as an [key][d] image for dQ = dS . K (B operand, k = key, read transposed)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i, key = c >> 3, dc = c & 7;
+    *(u32x4*)(Km + mnimg(key, dc)) = *(const u32x4*)(kb + (int64_t)(kt * AKV + key) * RS + dc * 8);
+  }
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
+
+  for (int qt = kt; qt < nk; ++qt) {
+    __syncthreads();  // previous iteration's readers are done with Q/dO/dS/staging
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, q = c >> 3, dc = c & 7;
+      const u32x4 qv = *(const u32x4*)(qb + (int64_t)(qt * AQ + q) * RS + dc * 8);
+      const u32x4 ov = *(const u32x4*)(ob + (int64_t)(qt * AQ + q) * ORS + dc * 8);
+      *(u32x4*)(Qk + (dc >> 2) * 4096 + kimg(q, dc & 3)) = qv;
+      *(u32x4*)(Qm + pimg(q, dc)) = qv;
+      *(u32x4*)(Ok + (dc >> 2) * 4096 + kimg(q, dc & 3)) = ov;
+      *(u32x4*)(Om + pimg(q, dc)) = ov;
+    }
+    if (tid < 64) sl[tid] = lse2[(int64_t)bh * T + qt * AQ + tid];
+    else if (tid < 128) sd[tid - 64] = delta[(int64_t)bh * T + qt * AQ + tid - 64];
+    __syncthreads();
+    // S[q][key], dP[q][key]: lane = key, rows q = 16mt + 4g + e
+    f32x4 ps[4], dp[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      ps[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[mt] = ps[mt];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        ps[mt] = MFMA(kfrag64(Qk + kk * 4096, 16 * mt), kf[kk], ps[mt]);
+        dp[mt] = MFMA(kfrag64(Ok + kk * 4096, 16 * mt), vf[kk], dp[mt]);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int ql = 16 * mt + 4 * g + e;
+        float p = exp2f(ps[mt][e] * sl2 - sl[ql]);
+        if (qt == kt && mykey > qt * AQ + ql) p = 0.f;
+        ps[mt][e] = p;                        // P
+        dp[mt][e] = p * (dp[mt][e] - sd[ql]);  // dS (unscaled)
+      }
+    // dV^T += dO^T . P ; dK^T += Q^T . dS   (k = q, permuted order matches the accumulators)
+    const bf16x8 p0 = pack_frag(ps[0], ps[1]), p1 = pack_frag(ps[2], ps[3]);
+    const bf16x8 s0 = pack_frag(dp[0], dp[1]), s1 = pack_frag(dp[2], dp[3]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      dv[d] = MFMA(trfrag<true>(Om, 0, 16 * d), p0, dv[d]);
+      dv[d] = MFMA(trfrag<true>(Om, 32, 16 * d), p1, dv[d]);
+      dk[d] = MFMA(trfrag<true>(Qm, 0, 16 * d), s0, dk[d]);
+      dk[d] = MFMA(trfrag<true>(Qm, 32, 16 * d), s1, dk[d]);
+    }
+    // dS -> LDS as [q][key] K-contiguous image (rows q, key halves) for dQ = dS . K
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int ql = 16 * mt + 4 * g + e, kl = 16 * w + li;
+        char* a = dS + (kl >> 5) * 4096 + kimg(ql, (kl & 31) >> 3) + (kl & 7) * 2;
+        *(uint16_t*)a = f2bf(dp[mt][e]);
+      }
+    __syncthreads();
+    // dQ tile rows 16w..16w+15 : D[q][d] (lane = d, rows q = 4g + e)
+    f32x4 dqa[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      dqa[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) dqa[d] = MFMA(kfrag64(dS + kk * 4096, 16 * w), trfrag<false>(Km, 32 * kk, 16 * d), dqa[d]);
+    }
+    // stage (Qk+Qm region, 64x64 fp32 = 16 KB) and add whole 256-B rows atomically
+    __syncthreads();
+    float* stg = (float*)smem;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) stg[(16 * w + 4 * g + e) * 64 + 16 * d + li] = dqa[d][e] * scale;
+    __syncthreads();
+    for (int r = w; r < 64; r += 4) {
+      float* dst = dq_acc + ((int64_t)(b * T + qt * AQ + r) * H + h) * AD;
+      atomicAdd(dst + lane, stg[r * 64 + lane]);
+    }
+  }
+  // dK, dV (bf16) -> dqkv[b, key, 1|2, h, :]
+  uint16_t* dkb = dqkv + (int64_t)b * T * RS + (int64_t)mykey * RS + H * AD + (int64_t)h * AD;
+  uint16_t* dvb = dkb + H * AD;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    u32x2 a, c;
+    a[0] = pack_bf2(dk[d][0] * scale, dk[d][1] * scale);
+    a[1] = pack_bf2(dk[d][2] * scale, dk[d][3] * scale);
+    c[0] = pack_bf2(dv[d][0], dv[d][1]);
+    c[1] = pack_bf2(dv[d][2], dv[d][3]);
+    *(u32x2*)(dkb + 16 * d + 4 * g) = a;
+    *(u32x2*)(dvb + 16 * d + 4 * g) = c;
+  }
+}
+
+// dq (fp32 [B,T,H,64]) -> dqkv[:, :, 0] (bf16)
+__global__ __launch_bounds__(256) void attn_dq_store_kernel(const float* __restrict__ dq, uint16_t* __restrict__ dqkv, int B,
+                                                            int T, int H) {
+  const int64_t n8 = (int64_t)B * T * H * AD / 8;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int64_t e = i * 8;
+    const int64_t bt = e / (H * AD);
+    const int64_t rem = e % (H * AD);
+    const f32x4 a = *(const f32x4*)(dq + e), c = *(const f32x4*)(dq + e + 4);
+    float f[8] = {a[0], a[1], a[2], a[3], c[0], c[1], c[2], c[3]};
+    *(u32x4*)(dqkv + bt * 3 * H * AD + rem) = pack8(f);
+  }
+}
+
+}  // namespace dpe
+
+using namespace dpe;
+
+extern "C" int dpe_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int T, int H, int D, float scale, int causal,
+                            hipStream_t st) {
+  if (D != AD || T % AQ != 0 || !causal) return -1;
+  const float sl2 = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * H * (T / AQ)), dim3(256), 0, st, qkv, out, lse, B, T, H, sl2);
+  return 0;
+}
+
+extern "C" int dpe_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
+                            float* dq_acc, uint16_t* dqkv, int B, int T, int H, int D, float scale, int causal,
+                            hipStream_t st) {
+  if (D != AD || T % AQ != 0 || !causal) return -1;
+  const float sl2 = scale * 1.4426950408889634f;
+  const int64_t rows = (int64_t)B * T * H;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, st, out, dout, delta, B, T, H);
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(B * H * (T / AKV)), dim3(256), 0, st, qkv, dout, lse, delta, dq_acc, dqkv, B, T,
+                     H, sl2, scale);
+  int64_t g = rows * AD / 8 / 256 + 1;
+  hipLaunchKernelGGL(attn_dq_store_kernel, dim3((unsigned)(g > 8192 ? 8192 : g)), dim3(256), 0, st, dq_acc, dqkv, B, T, H);
+  return 0;
 }

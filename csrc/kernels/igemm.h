@@ -46,6 +46,7 @@ struct IgemmArgs {
   void* C;
   const uint16_t* residual;  // bf16 [M][ldc] added in the EPI_BF16 epilogue (may alias C)
   const float* bias;         // [N] or nullptr
+  const float* residual_f32; // f32 [M][ldc] added in the EPI_F32 epilogue (x + f(a) on an fp32 residual stream)
   float* col_stats;          // [2][N][tilesM] per-(column, M-tile) (sum, sumsq) of the stored bf16 output, or nullptr
   int M, N, K;
   int64_t lda, ldb, ldc;

@@ -428,6 +428,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
         for (int e = 0; e < 4; ++e) {
           float b = (p.bias && n + e < p.N) ? p.bias[n + e] : 0.f;
           v[e] = act_fn(p.alpha * acc[i][j][e] + b, p.act);
+          if (p.residual_f32 && n + e < p.N) v[e] += p.residual_f32[(int64_t)m * p.ldc + n + e];
         }
         float* dst = C + (int64_t)m * p.ldc + n;
         if (n + 4 <= p.N && (p.ldc & 3) == 0) {

@@ -26,16 +26,18 @@ _derived: list = []  # (param, shadow, fn)
 def shadow(p: torch.Tensor, pad_rows: int = 0) -> torch.Tensor:
     """bf16 shadow of fp32 master ``p`` (optionally with zero pad rows)."""
     sh = getattr(p, "_dpe_shadow", None)
-    if sh is None or getattr(p, "_dpe_shadow_ver", -1) != p._version or sh.device != p.device:
+    rows = p.shape[0] + pad_rows
+    if sh is None or sh.device != p.device or sh.shape[0] < rows:
+        sh = torch.zeros((rows, *p.shape[1:]), dtype=torch.bfloat16, device=p.device)
+        p._dpe_shadow = sh
+        p._dpe_shadow_ver = -1
+    if getattr(p, "_dpe_shadow_ver", -1) != p._version:
         from ._ext import ext
 
-        rows = p.shape[0] + pad_rows
-        if sh is None or sh.device != p.device or sh.shape[0] != rows:
-            sh = torch.zeros((rows, *p.shape[1:]), dtype=torch.bfloat16, device=p.device)
         ext().cast_bf16(p.detach().reshape(-1), sh.view(-1)[: p.numel()])
-        p._dpe_shadow = sh
         p._dpe_shadow_ver = p._version
-    return sh
+    # one shadow per parameter: a padded (larger) shadow also serves unpadded users
+    return sh if sh.shape[0] == rows else sh[:rows]
 
 
 def derived_shadow(p: torch.Tensor, key: str, fn) -> torch.Tensor:

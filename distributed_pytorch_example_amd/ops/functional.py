@@ -524,3 +524,84 @@ def to_nhwc_input(x: torch.Tensor, cpad: int = 8) -> torch.Tensor:
             y = F.pad(y, (0, cpad - y.shape[-1]))
         return y.contiguous()
     return ext().nchw_to_nhwc(x.float().contiguous(), cpad)
+
+
+# ====================================================== residual-stream linear
+class _LinearResidualFn(Function):
+    """y = x_res + a @ W^T + b  with a bf16 activations and x_res the fp32 residual stream,
+    one GEMM launch (fp32-residual epilogue)."""
+
+    @staticmethod
+    def forward(ctx, a, weight, bias, x_res):
+        C = ext()
+        w16 = shadow(weight)
+        ab = a.contiguous() if a.dtype == torch.bfloat16 else a.to(torch.bfloat16).contiguous()
+        y = C.linear_fwd(ab, w16, bias.detach() if bias is not None else None, 0, True, x_res.contiguous(), None)
+        ctx.save_for_backward(ab)
+        ctx.weight, ctx.bias = weight, bias
+        note_use(weight)
+        if bias is not None:
+            note_use(bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = ext()
+        (ab,) = ctx.saved_tensors
+        weight, bias = ctx.weight, ctx.bias
+        dyb = dy.to(torch.bfloat16).contiguous()
+        da = C.linear_dgrad(dyb, shadow(weight)) if ctx.needs_input_grad[0] else None
+        buf, direct = grad_sink(weight)
+        C.linear_wgrad(dyb, ab, buf, 1.0)
+        grad_done(weight, direct)
+        gb = None
+        if bias is not None:
+            bb, bd = grad_sink(bias)
+            C.colsum(dy.contiguous(), bb, True)
+            grad_done(bias, bd)
+            gb = None if bd else bb
+        return da, (None if direct else buf), gb, dy
+
+
+def linear_residual(a, weight, bias, x_res):
+    """x_res (fp32) + linear(a)."""
+    if not a.is_cuda:
+        return x_res + F.linear(a.float(), weight, bias)
+    return _LinearResidualFn.apply(a, weight, bias, x_res)
+
+
+# ================================================================ LM head
+class _LMHeadFn(Function):
+    """logits[.., Vp] = x @ wte_pad^T, wte tied with the token embedding; the
+    vocab is padded to a multiple of 64 inside the bf16 shadow only (zero pad
+    rows), the fp32 master keeps the canonical [V, D] shape."""
+
+    @staticmethod
+    def forward(ctx, x, wte, pad_rows: int):
+        C = ext()
+        w16 = shadow(wte, pad_rows)
+        xb = x.contiguous() if x.dtype == torch.bfloat16 else x.to(torch.bfloat16).contiguous()
+        y = C.linear_fwd(xb, w16, None, 0, False, None, None)
+        ctx.save_for_backward(xb)
+        ctx.wte, ctx.pad = wte, pad_rows
+        note_use(wte)
+        return y
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        C = ext()
+        (xb,) = ctx.saved_tensors
+        d = dlogits.to(torch.bfloat16).contiguous()
+        dx = C.linear_dgrad(d, shadow(ctx.wte, ctx.pad))
+        buf, direct = grad_sink(ctx.wte)
+        C.linear_wgrad(d, xb, buf, 1.0)  # padded leading dim, only the V real rows are produced
+        grad_done(ctx.wte, direct)
+        return dx, (None if direct else buf), None
+
+
+def lm_head(x, wte, vocab_pad_to: int = 64):
+    V = wte.shape[0]
+    Vp = (V + vocab_pad_to - 1) // vocab_pad_to * vocab_pad_to
+    if not x.is_cuda:
+        return F.linear(x.float(), wte)
+    return _LMHeadFn.apply(x, wte, Vp - V)

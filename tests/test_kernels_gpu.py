@@ -291,3 +291,26 @@ def test_embedding(C):
     C.embedding_bwd(idx, dout, dwte, dwpe)
     ref = torch.zeros(1000, 128, device=dev).index_add_(0, idx.reshape(-1), dout.reshape(-1, 128))
     assert rel_err(dwte, ref) < 1e-5 and rel_err(dwpe, dout.sum(0)) < 1e-5
+
+
+# -------------------------------------------------------------- attention
+@pytest.mark.parametrize("B,T,H", [(2, 128, 2), (1, 1024, 3), (2, 256, 12)])
+def test_attention_fwd_bwd(C, B, T, H):
+    torch.manual_seed(12)
+    D = 64
+    qkv = bf(torch.randn(B, T, 3, H, D, device=dev))
+    scale = 1.0 / math.sqrt(D)
+    out, lse = C.attn_fwd(qkv, H, scale, True)
+    q, k, v = qkv.float().permute(2, 0, 3, 1, 4).requires_grad_(True).unbind(0)
+    qf, kf, vf = [t.detach().clone().requires_grad_(True) for t in (q, k, v)]
+    ref = F.scaled_dot_product_attention(qf, kf, vf, is_causal=True)  # [B,H,T,D]
+    assert rel_err(out.permute(0, 2, 1, 3), ref) < 1e-2
+    # lse2 = log2-domain logsumexp of the scaled scores
+    s = (qf @ kf.transpose(-1, -2)) * scale
+    s = s.masked_fill(torch.triu(torch.ones(T, T, device=dev, dtype=torch.bool), 1), float("-inf"))
+    assert rel_err(lse, torch.logsumexp(s, -1) / math.log(2)) < 1e-4
+    do = bf(torch.randn(B, T, H, D, device=dev))
+    gq, gk, gv = torch.autograd.grad(ref, [qf, kf, vf], do.float().permute(0, 2, 1, 3))
+    dqkv = C.attn_bwd(qkv, out, do, lse, H, scale, True)
+    for i, g in enumerate((gq, gk, gv)):
+        assert rel_err(dqkv[:, :, i].permute(0, 2, 1, 3), g) < 2e-2, i
