@@ -162,8 +162,9 @@ void Communicator::abort() {
 
 // ------------------------------------------------------------------ Reducer
 Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params, int64_t nparams,
-                 std::shared_ptr<Communicator> comm, bool timing)
-    : buckets_(std::move(buckets)), bparams_(std::move(bucket_params)), comm_(std::move(comm)), timing_(timing) {
+                 std::shared_ptr<Communicator> comm, bool timing, bool force)
+    : buckets_(std::move(buckets)), bparams_(std::move(bucket_params)), comm_(std::move(comm)), timing_(timing),
+      force_(force) {
   TORCH_CHECK(buckets_.size() == bparams_.size(), "bucket/param list size mismatch");
   param_bucket_.assign(nparams, -1);
   expected_.resize(buckets_.size());
@@ -206,13 +207,15 @@ void Reducer::prepare() {
   std::fill(ready_.begin(), ready_.end(), 0);
   std::fill(seen_.begin(), seen_.end(), 0);
   next_ = 0;
+  launch_order_.clear();
   step_open_ = true;
   if (timing_) HIP_CHECK(hipEventRecord(ev_step_begin_, c10::hip::getCurrentHIPStream().stream()));
 }
 
 void Reducer::launch(int64_t b) {
   hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
-  if (!comm_ || comm_->world() == 1) return;
+  launch_order_.push_back(b);
+  if (!comm_ || (comm_->world() == 1 && !force_)) return;
   hipStream_t cs = comm_->comm_stream().stream();
   HIP_CHECK(hipEventRecord(ev_ready_[b], cur));
   HIP_CHECK(hipStreamWaitEvent(cs, ev_ready_[b], 0));
@@ -240,7 +243,7 @@ void Reducer::finalize() {
   // Unused parameters: their (zero / stale-accumulated) slices are reduced
   // anyway so every rank issues the same collective sequence.
   while (next_ < (int64_t)buckets_.size()) launch(next_++);
-  if (comm_ && comm_->world() > 1) {
+  if (comm_ && (comm_->world() > 1 || force_)) {
     HIP_CHECK(hipEventRecord(ev_done_, comm_->comm_stream().stream()));
     HIP_CHECK(hipStreamWaitEvent(cur, ev_done_, 0));
   }
@@ -249,7 +252,7 @@ void Reducer::finalize() {
 
 std::vector<std::tuple<int64_t, double, double>> Reducer::last_timings() {
   std::vector<std::tuple<int64_t, double, double>> out;
-  if (!timing_ || !comm_ || comm_->world() == 1) return out;
+  if (!timing_ || !comm_ || (comm_->world() == 1 && !force_)) return out;
   HIP_CHECK(hipEventSynchronize(ev_done_));
   for (size_t b = 0; b < buckets_.size(); ++b) {
     float ms = 0.f, rel = 0.f;
@@ -286,8 +289,11 @@ void register_comm(pybind11::module& m) {
       .def("abort", &Communicator::abort)
       .def("comm_stream_ptr", [](Communicator& c) { return (uint64_t)(uintptr_t)c.comm_stream().stream(); });
   py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
-      .def(py::init<std::vector<at::Tensor>, std::vector<std::vector<int64_t>>, int64_t, std::shared_ptr<Communicator>, bool>(),
-           py::arg("buckets"), py::arg("bucket_params"), py::arg("nparams"), py::arg("comm"), py::arg("timing") = false)
+      .def(py::init<std::vector<at::Tensor>, std::vector<std::vector<int64_t>>, int64_t, std::shared_ptr<Communicator>, bool,
+                    bool>(),
+           py::arg("buckets"), py::arg("bucket_params"), py::arg("nparams"), py::arg("comm"), py::arg("timing") = false,
+           py::arg("force") = false)
+      .def("launch_order", &Reducer::launch_order)
       .def("prepare", &Reducer::prepare)
       .def("mark_ready", &Reducer::mark_ready)
       .def("finalize", &Reducer::finalize)

@@ -71,7 +71,7 @@ ncclRedOp_t to_nccl_op(const std::string& op);
 class Reducer {
  public:
   Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params, int64_t nparams,
-          std::shared_ptr<Communicator> comm, bool timing);
+          std::shared_ptr<Communicator> comm, bool timing, bool force = false);
   ~Reducer();
   void prepare();
   void mark_ready(int64_t param);
@@ -80,6 +80,7 @@ class Reducer {
   std::vector<std::tuple<int64_t, double, double>> last_timings();
   int64_t num_buckets() const { return (int64_t)buckets_.size(); }
   int64_t buckets_launched() const { return next_; }
+  std::vector<int64_t> launch_order() const { return launch_order_; }
 
  private:
   void launch(int64_t b);
@@ -91,6 +92,8 @@ class Reducer {
   int64_t next_ = 0;
   std::shared_ptr<Communicator> comm_;
   bool timing_;
+  bool force_;  // issue collectives even at world size 1 (exercises the comm path on a 1-GPU box)
+  std::vector<int64_t> launch_order_;
   std::vector<hipEvent_t> ev_ready_, ev_start_, ev_end_;
   hipEvent_t ev_bwd_end_ = nullptr, ev_done_ = nullptr, ev_step_begin_ = nullptr;
   bool step_open_ = false;

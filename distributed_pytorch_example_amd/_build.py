@@ -72,7 +72,11 @@ def build(verbose: bool = True, jobs: int | None = None, force: bool = False) ->
         objs.append(obj)
         if force or _needs(obj, src, hdr):
             tasks.append([os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-                          "-ffp-contract=fast", "-munsafe-fp-atomics", "-c", src, "-o", obj])
+                          "-ffp-contract=fast", "-munsafe-fp-atomics",
+                          # MFMA C/D in arch VGPRs (gfx950 unified file): avoids per-K-step
+                          # v_accvgpr_read/write shuffles of the accumulators in the main loops
+                          "-mllvm", "-amdgpu-mfma-vgpr-form",
+                          "-c", src, "-o", obj])
     for src in cpp_srcs:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)

@@ -104,7 +104,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers: bool = True,
                  bucket_cap_mb: Optional[float] = 25.0, first_bucket_mb: float = 1.0,
                  find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
-                 init_sync: bool = True, timing: bool = False):
+                 init_sync: bool = True, timing: bool = False, comm=None, force_comm: bool = False):
         super().__init__()
         self.module = module
         self.broadcast_buffers = broadcast_buffers
@@ -116,6 +116,9 @@ class DistributedDataParallel(nn.Module):
         cap = int((bucket_cap_mb if bucket_cap_mb is not None else 25.0) * 1024 * 1024)
         first = int(first_bucket_mb * 1024 * 1024) if first_bucket_mb else cap
         self.bucket_cap_bytes, self.first_bucket_bytes = cap, first
+        self._comm = comm if comm is not None else pdist.comm()
+        self._force = force_comm
+        self._timing = timing
         if init_sync and self.world_size > 1:
             self._sync_module_states()
         self._build_buckets()
@@ -161,11 +164,11 @@ class DistributedDataParallel(nn.Module):
                 off += p.numel()
             self.buckets.append(buf)
         self._attach_grads(zero=True)
-        backend = pdist.backend()
-        if backend == "rccl" and self._params and self._params[0].is_cuda:
+        if self._comm is not None and self._params and self._params[0].is_cuda:
             from ..ops._ext import ext
 
-            self.reducer = ext().Reducer(self.buckets, self.bucket_indices, len(self._params), pdist.comm(), False)
+            self.reducer = ext().Reducer(self.buckets, self.bucket_indices, len(self._params), self._comm, self._timing,
+                                         self._force)
             self._native = True
         else:
             self.reducer = _GlooReducer(self.buckets, self.bucket_indices, len(self._params))
@@ -176,7 +179,8 @@ class DistributedDataParallel(nn.Module):
         if self._native:
             from ..ops._ext import ext
 
-            self.reducer = ext().Reducer(self.buckets, self.bucket_indices, len(self._params), pdist.comm(), on)
+            self._timing = on
+            self.reducer = ext().Reducer(self.buckets, self.bucket_indices, len(self._params), self._comm, on, self._force)
 
     def bucket_timings(self):
         return self.reducer.last_timings()

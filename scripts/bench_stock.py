@@ -53,6 +53,36 @@ class ResNet50(nn.Module):
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
 
 
+class GPT2Block(nn.Module):
+    def __init__(self, d=768, h=12):
+        super().__init__()
+        self.h = h
+        self.ln_1, self.ln_2 = nn.LayerNorm(d), nn.LayerNorm(d)
+        self.c_attn, self.c_proj = nn.Linear(d, 3 * d), nn.Linear(d, d)
+        self.c_fc, self.mlp_proj = nn.Linear(d, 4 * d), nn.Linear(4 * d, d)
+
+    def forward(self, x):
+        B, T, C = x.shape
+        q, k, v = self.c_attn(self.ln_1(x)).view(B, T, 3, self.h, C // self.h).permute(2, 0, 3, 1, 4)
+        a = F.scaled_dot_product_attention(q, k, v, is_causal=True).transpose(1, 2).reshape(B, T, C)
+        x = x + self.c_proj(a)
+        return x + self.mlp_proj(F.gelu(self.c_fc(self.ln_2(x)), approximate="tanh"))
+
+
+class GPT2(nn.Module):
+    def __init__(self, V=50257, T=1024, d=768, L=12):
+        super().__init__()
+        self.wte, self.wpe = nn.Embedding(V, d), nn.Embedding(T, d)
+        self.h = nn.ModuleList([GPT2Block(d) for _ in range(L)])
+        self.ln_f = nn.LayerNorm(d)
+
+    def forward(self, idx):
+        x = self.wte(idx) + self.wpe(torch.arange(idx.shape[1], device=idx.device))
+        for b in self.h:
+            x = b(x)
+        return F.linear(self.ln_f(x), self.wte.weight)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -60,6 +90,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch-size", type=int, default=256)
     ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "gpt2"])
     args = ap.parse_args()
     os.environ.setdefault("RANK", "0")
     os.environ.setdefault("WORLD_SIZE", "1")
@@ -72,18 +103,26 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = torch.device("cuda", local)
     torch.backends.cudnn.benchmark = True
-    model = ResNet50().to(dev).to(memory_format=torch.channels_last)
+    if args.model == "gpt2":
+        model = GPT2().to(dev)
+        opt = torch.optim.AdamW(model.parameters(), lr=6e-4, weight_decay=0.1, fused=True)
+        toks = [torch.randint(0, 50257, (args.batch_size, 1025), device=dev) for _ in range(4)]
+        xs, ys = [t[:, :-1] for t in toks], [t[:, 1:] for t in toks]
+        unit = 1024
+    else:
+        model = ResNet50().to(dev).to(memory_format=torch.channels_last)
+        opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)
+        xs = [torch.randn(args.batch_size, 3, 224, 224, device=dev).to(memory_format=torch.channels_last) for _ in range(4)]
+        ys = [torch.randint(0, 1000, (args.batch_size,), device=dev) for _ in range(4)]
+        unit = 1
     ddp = nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=args.bucket_mb,
                                               gradient_as_bucket_view=True)
-    opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)
-    xs = [torch.randn(args.batch_size, 3, 224, 224, device=dev).to(memory_format=torch.channels_last) for _ in range(4)]
-    ys = [torch.randint(0, 1000, (args.batch_size,), device=dev) for _ in range(4)]
 
     def step(i):
         opt.zero_grad(set_to_none=True)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             out = ddp(xs[i % 4])
-            loss = F.cross_entropy(out.float(), ys[i % 4])
+            loss = F.cross_entropy(out.float().reshape(-1, out.shape[-1]), ys[i % 4].reshape(-1))
         loss.backward()
         opt.step()
         return loss
@@ -99,8 +138,8 @@ def main():
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = dt.item()
     if rank == 0:
-        print(json.dumps({"metric": "stock-pytorch resnet50 bf16 samples/s (whole node)",
-                          "value": round(args.batch_size * world * args.steps / dt, 2), "n_gpus": world,
+        print(json.dumps({"metric": f"stock-pytorch {args.model} bf16 {'tokens' if unit > 1 else 'samples'}/s (whole node)",
+                          "value": round(unit * args.batch_size * world * args.steps / dt, 2), "n_gpus": world,
                           "ms_per_step": round(1000 * dt / args.steps, 3), "per_gpu_batch": args.batch_size,
                           "loss": loss.item()}), flush=True)
     dist.destroy_process_group()
