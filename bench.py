@@ -113,6 +113,7 @@ def main():
         metric, unit = "samples/sec (whole node), SimpleNet MLP", "samples/s"
         num_classes = 10
 
+    fused_loss = args.model == "gpt2"
     ddp = DDP(model, bucket_cap_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb)
     opt = build_optimizer(opt_name, model.parameters(), lr=lr, weight_decay=wd)
 
@@ -122,8 +123,10 @@ def main():
             last = a == args.grad_accum - 1
             ctx = ddp.no_sync() if not last else _null()
             with ctx:
-                out = ddp(x)
-                loss = Fx.cross_entropy(out, y, num_classes)
+                if fused_loss:
+                    loss = ddp(x, y)  # GPT-2: fused LM head + CE (logits stay inside the op)
+                else:
+                    loss = Fx.cross_entropy(ddp(x), y, num_classes)
                 if args.grad_accum > 1:
                     loss = loss / args.grad_accum
                 loss.backward()

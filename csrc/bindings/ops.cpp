@@ -4,6 +4,8 @@
 // HIP stream, so the ops compose with the caching allocator and hipGraph
 // capture (no host sync, no hipMalloc inside).
 #include <torch/extension.h>
+#include <map>
+#include <string>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
@@ -121,7 +123,57 @@ Cfg pick_cfg(int64_t M, int64_t N, int64_t K, bool allow_split) {
   return c;
 }
 
+// Large dense GEMMs go to the 256-tile LDS-DMA kernel when the shape fills
+// the chip (>= 192 tiles, or split-K for atomic weight-grads).  Mode:
+// 0 auto, 1 never (A/B testing, DPE_GEMM256=0), 2 always when supported.
+int g_g256_mode = -1;
+int g256_mode() {
+  if (g_g256_mode < 0) {
+    const char* e = getenv("DPE_GEMM256");
+    g_g256_mode = (e && e[0] == '0') ? 1 : (e && e[0] == '2') ? 2 : 0;
+  }
+  return g_g256_mode;
+}
+
+int g_g256_override = -1;  // set by the per-shape autotuner: 0 off, 1 force
+
+bool try_gemm256(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_split) {
+  int mode = g256_mode();
+  if (g_g256_override == 0) return false;
+  if (g_g256_override == 1 && mode != 1) mode = 2;
+  if (mode == 1) return false;
+  int ak, bk;
+  if (aload == dpe::A_DENSE_K && bload == dpe::B_DENSE_K) { ak = 1; bk = 1; }
+  else if (aload == dpe::A_DENSE_K && bload == dpe::B_DENSE_N) { ak = 1; bk = 0; }
+  else if (aload == dpe::A_DENSE_M && bload == dpe::B_DENSE_N) { ak = 0; bk = 0; }
+  else return false;
+  if (!ak && epi == dpe::EPI_BF16) return false;
+  if (a.K % 64 || a.K == 0 || a.col_stats || (a.act != 0 && a.act != 2)) return false;
+  if (a.lda % 8 || a.ldb % 8 || (!bk && a.N % 8) || (!ak && a.M % 8)) return false;
+  // 32-bit per-lane source offsets
+  const int64_t abytes = (ak ? (int64_t)a.M * a.lda : (int64_t)a.K * a.lda) * 2;
+  const int64_t bbytes = (bk ? (int64_t)a.N * a.ldb : (int64_t)a.K * a.ldb) * 2;
+  if (abytes >= (1ll << 32) || bbytes >= (1ll << 32)) return false;
+  const int64_t tiles = ((a.M + 255) / 256) * ((int64_t)(a.N + 255) / 256);
+  const int64_t ktiles = a.K / 64;
+  int64_t splits = 1;
+  if (epi == dpe::EPI_ATOMIC_F32 && allow_split) {
+    // fill >= 1.5 waves of 256 CUs, keep >= 8 K-tiles (512) per split
+    splits = std::max<int64_t>(1, std::min<int64_t>((384 + tiles - 1) / tiles, ktiles / 8));
+  }
+  // tile-quantisation waste: the 256x256 tile must be >= 75 % useful
+  if (mode == 0 && ((double)a.M * a.N < 0.75 * 65536.0 * tiles || tiles * splits < 192)) return false;
+  const int64_t kps = (ktiles + splits - 1) / splits;
+  splits = (ktiles + kps - 1) / kps;
+  a.k_split = (int)(kps * 64);
+  const int rc = dpe_gemm256_launch(&a, ak, bk, epi, (int)splits, cur_stream());
+  const hipError_t e = hipGetLastError();
+  TORCH_CHECK(e == hipSuccess, "gemm256 launch failed: ", hipGetErrorString(e));
+  return rc == 0;
+}
+
 void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_split) {
+  if (try_gemm256(a, aload, bload, epi, allow_split)) return;
   Cfg c = pick_cfg(a.M, a.N, a.K, allow_split && epi == dpe::EPI_ATOMIC_F32);
   a.k_split = c.k_split;
   const int rc = dpe_igemm_launch(&a, c.bm, c.bn, aload, bload, epi, c.splits, cur_stream());
@@ -130,11 +182,88 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
   TORCH_CHECK(rc == 0, "igemm: unsupported configuration (aload=", aload, " bload=", bload, " epi=", epi, ") rc=", rc);
 }
 
+// optional device scalar (f32, 1 element) multiplied into the GEMM alpha
+const float* alpha_ptr_of(const c10::optional<Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  CHECK_GPU((*t)); CHECK_F32((*t));
+  TORCH_CHECK(t->numel() == 1, "alpha tensor must have one element");
+  return (const float*)t->data_ptr();
+}
+
 dpe::IgemmArgs base_args() {
   dpe::IgemmArgs a;
   memset(&a, 0, sizeof(a));
   a.alpha = 1.f;
   return a;
+}
+
+
+// ------------------------------------------------ vendor-library arm (plain GEMMs)
+// A GEMM whose epilogue the library can express exactly (no activation, no
+// fp32 residual stream, no BN statistics) is autotuned once per shape between
+// our MFMA kernels and hipBLASLt (through ATen): both run a few times into
+// scratch outputs, timed with HIP events, and the faster one is cached.
+// DPE_GEMM_BACKEND = auto (default) | native | blas.
+int g_blas_mode = -1;  // 0 auto, 1 native only, 2 blas whenever eligible
+int blas_mode() {
+  if (g_blas_mode < 0) {
+    const char* e = getenv("DPE_GEMM_BACKEND");
+    const std::string v = e ? e : "auto";
+    g_blas_mode = v == "native" ? 1 : v == "blas" ? 2 : 0;
+  }
+  return g_blas_mode;
+}
+std::map<std::tuple<int, int64_t, int64_t, int64_t, int>, int> g_blas_choice;
+
+template <class F>
+double time_ms(F& f, int reps) {
+  hipStream_t st = cur_stream();
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  f();  // warm-up (first-call library heuristics, caches)
+  hipEventRecord(e0, st);
+  for (int i = 0; i < reps; ++i) f();
+  hipEventRecord(e1, st);
+  hipEventSynchronize(e1);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, e0, e1);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  return ms / reps;
+}
+
+// kind: 0 fwd, 1 dgrad, 2 wgrad, 3 fwd+f32 residual.  Returns 0 = native 128-tile
+// igemm, 1 = native 256-tile LDS-DMA kernel, 2 = library.  native/blas write
+// into a scratch output while being timed.
+template <class FN, class FB>
+int pick_backend(int kind, int64_t M, int64_t N, int64_t K, int flags, FN&& native_into_scratch,
+                 FB&& blas_into_scratch) {
+  const int mode = blas_mode();
+  if (mode == 2) return 2;
+  if (mode == 1 || g256_mode() != 0) return g256_mode() == 2 ? 1 : (g256_mode() == 1 ? 0 : -1);
+  auto key = std::make_tuple(kind, M, N, K, flags);
+  auto it = g_blas_choice.find(key);
+  if (it != g_blas_choice.end()) return it->second;
+  g_g256_override = 0;
+  const double t0 = time_ms(native_into_scratch, 3);
+  g_g256_override = 1;
+  const double t1 = time_ms(native_into_scratch, 3);
+  g_g256_override = -1;
+  const double t2 = time_ms(blas_into_scratch, 3);
+  int best = t1 < t0 ? 1 : 0;
+  const double tn = std::min(t0, t1);
+  if (t2 < 0.97 * tn) best = 2;
+  g_blas_choice[key] = best;
+  return best;
+}
+
+// run the native arm with the autotuner's tile choice (-1 = heuristic)
+template <class F>
+void run_native(int choice, F&& f) {
+  g_g256_override = choice == 0 ? 0 : choice == 1 ? 1 : -1;
+  f();
+  g_g256_override = -1;
 }
 
 // -------------------------------------------------------------- dense GEMMs
@@ -175,12 +304,55 @@ Tensor linear_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>&
       a.residual = bp(*residual);
     }
   }
+  const bool plain = !out_f32 && act == 0 && !a.residual;
+  if (plain) {
+    Tensor y2 = y.view({M, N});
+    Tensor bb = bias.has_value() && bias->defined() ? bias->to(at::kBFloat16) : Tensor();
+    auto blas = [&](Tensor& out) {
+      if (bb.defined()) at::addmm_out(out, bb, x2, w.t());
+      else at::mm_out(out, x2, w.t());
+    };
+    auto native = [&](Tensor& out) {
+      auto b = a;
+      b.C = out.data_ptr();
+      run_igemm(b, dpe::A_DENSE_K, dpe::B_DENSE_K, dpe::EPI_BF16, false);
+    };
+    Tensor tmp;
+    auto get_tmp = [&]() -> Tensor& { if (!tmp.defined()) tmp = at::empty_like(y2); return tmp; };
+    const int c = pick_backend(0, M, N, K, bb.defined(), [&] { native(get_tmp()); }, [&] { blas(get_tmp()); });
+    if (c == 2) blas(y2);
+    else run_native(c, [&] { native(y2); });
+    return y;
+  }
+  if (out_f32 && act == 0 && a.residual_f32) {
+    // x + (x_in @ w^T + b) on the fp32 residual stream: library arm = fp32-out addmm onto the residual
+    Tensor y2 = y.view({M, N});
+    Tensor res2 = residual->view({M, N});
+    auto blas = [&](Tensor& out) {
+      at::addmm_out(out, res2, x2, w.t(), at::kFloat);
+      if (bias.has_value() && bias->defined()) out.add_(*bias);
+    };
+    auto native = [&](Tensor& out) {
+      auto b = a;
+      b.C = out.data_ptr();
+      run_igemm(b, dpe::A_DENSE_K, dpe::B_DENSE_K, dpe::EPI_F32, false);
+    };
+    const bool aliased = y.data_ptr() == residual->data_ptr();
+    Tensor tmp;
+    auto get_tmp = [&]() -> Tensor& { if (!tmp.defined()) tmp = at::empty_like(y2); return tmp; };
+    const int c = aliased ? 0 : pick_backend(3, M, N, K, bias.has_value() && bias->defined(), [&] { native(get_tmp()); },
+                                             [&] { blas(get_tmp()); });
+    if (c == 2) blas(y2);
+    else run_native(c, [&] { native(y2); });
+    return y;
+  }
   run_igemm(a, dpe::A_DENSE_K, dpe::B_DENSE_K, out_f32 ? dpe::EPI_F32 : dpe::EPI_BF16, false);
   return y;
 }
 
 // dx[M,K] = dy[M,N] @ w[N,K]
-Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const c10::optional<Tensor>& residual) {
+Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const c10::optional<Tensor>& residual,
+                    const c10::optional<Tensor>& alpha_t) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(dy);
   const int64_t N = w.size(0), K = w.size(1);
   TORCH_CHECK(dy.size(-1) == N, "linear_dgrad: shape mismatch");
@@ -194,6 +366,33 @@ Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const c10::optional<Tenso
   a.M = (int)M; a.N = (int)K; a.K = (int)N;
   a.lda = N; a.ldb = K; a.ldc = K;
   if (residual.has_value() && residual->defined()) { CHECK_BF16((*residual)); CHECK_CONTIG((*residual)); a.residual = bp(*residual); }
+  a.alpha_ptr = alpha_ptr_of(alpha_t);
+  {
+    Tensor dy2 = dy.reshape({M, N}), dx2 = dx.view({M, K});
+    Tensor res2 = a.residual ? residual->reshape({M, K}) : Tensor();
+    auto blas = [&](Tensor& out) {
+      if (res2.defined()) at::addmm_out(out, res2, dy2, w);
+      else at::mm_out(out, dy2, w);
+      if (a.alpha_ptr) {
+        TORCH_CHECK(!res2.defined(), "linear_dgrad: alpha_t with residual unsupported on the library arm");
+        out.mul_(*alpha_t);
+      }
+    };
+    auto native = [&](Tensor& out) {
+      auto b = a;
+      b.C = out.data_ptr();
+      run_igemm(b, dpe::A_DENSE_K, dpe::B_DENSE_N, dpe::EPI_BF16, false);
+    };
+    Tensor tmp;
+    auto get_tmp = [&]() -> Tensor& { if (!tmp.defined()) tmp = at::empty_like(dx2); return tmp; };
+    const bool ok = !(a.alpha_ptr && res2.defined());
+    const int c = ok ? pick_backend(1, M, K, N, (res2.defined() ? 1 : 0) | (a.alpha_ptr ? 2 : 0), [&] { native(get_tmp()); },
+                                    [&] { blas(get_tmp()); })
+                     : -1;
+    if (c == 2) blas(dx2);
+    else run_native(c, [&] { native(dx2); });
+    return dx;
+  }
   run_igemm(a, dpe::A_DENSE_K, dpe::B_DENSE_N, dpe::EPI_BF16, false);
   return dx;
 }
@@ -201,7 +400,7 @@ Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const c10::optional<Tenso
 // dw[N,K] (+)= dy[M,N]^T @ x[M,K]   (fp32, atomic split-K; dw must be zeroed or hold an accumulation)
 // dy may be column-padded (row stride ldy >= N, ldy % 8 == 0, pad columns zero): then N need not be a
 // multiple of 8 (vocab-padded LM head: N = 50257, ldy = 50304).
-void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha) {
+void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha, const c10::optional<Tensor>& alpha_t) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(x); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
   const int64_t N = dw.size(0), K = dw.size(1), ldy = dy.size(-1);
   TORCH_CHECK(ldy >= N && x.size(-1) == K && dy.numel() / ldy == x.numel() / K, "linear_wgrad: shape mismatch");
@@ -212,7 +411,25 @@ void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha) {
   a.M = (int)N; a.N = (int)K; a.K = (int)M;
   a.lda = ldy; a.ldb = K; a.ldc = K;
   a.alpha = (float)alpha;
-  run_igemm(a, dpe::A_DENSE_M, dpe::B_DENSE_N, dpe::EPI_ATOMIC_F32, true);
+  a.alpha_ptr = alpha_ptr_of(alpha_t);
+  {
+    Tensor dyT = dy.reshape({M, ldy}).narrow(1, 0, N).t();
+    Tensor x2 = x.reshape({M, K});
+    auto blas = [&](Tensor& out) {
+      Tensor xs = a.alpha_ptr ? (x2 * *alpha_t).to(at::kBFloat16) : x2;  // device-scalar scale folded into the small operand
+      at::addmm_out(out, out, dyT, xs, at::kFloat, 1.0, alpha);
+    };
+    auto native = [&](Tensor& out) {
+      auto b = a;
+      b.C = out.data_ptr();
+      run_igemm(b, dpe::A_DENSE_M, dpe::B_DENSE_N, dpe::EPI_ATOMIC_F32, true);
+    };
+    Tensor tmp;
+    auto get_tmp = [&]() -> Tensor& { if (!tmp.defined()) tmp = at::zeros_like(dw); return tmp; };
+    const int c = pick_backend(2, N, K, M, a.alpha_ptr ? 2 : 0, [&] { native(get_tmp()); }, [&] { blas(get_tmp()); });
+    if (c == 2) blas(dw);
+    else run_native(c, [&] { native(dw); });
+  }
 }
 
 // ------------------------------------------------------------------- conv
@@ -433,7 +650,7 @@ Tensor gavgpool_bwd(const Tensor& dy, std::vector<int64_t> xshape) {
 // ------------------------------------------------------------------- loss
 // returns (loss_rows [B] f32, loss_sum [1], correct [1], dlogits or empty)
 std::vector<Tensor> cross_entropy(const Tensor& logits, const Tensor& labels, int64_t V, double grad_scale, bool want_grad,
-                                  bool grad_bf16, int64_t ignore_index) {
+                                  bool grad_bf16, int64_t ignore_index, bool inplace) {
   CHECK_GPU(logits); CHECK_CONTIG(logits); CHECK_CONTIG(labels);
   TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
   const bool in_bf16 = logits.scalar_type() == at::kBFloat16;
@@ -444,7 +661,12 @@ std::vector<Tensor> cross_entropy(const Tensor& logits, const Tensor& labels, in
   Tensor rows = at::empty({B}, fo);
   Tensor sums = at::zeros({2}, fo);
   Tensor d;
-  if (want_grad) d = at::empty(logits.sizes(), logits.options().dtype(grad_bf16 ? at::kBFloat16 : at::kFloat));
+  if (want_grad && inplace) {
+    TORCH_CHECK(grad_bf16 == in_bf16, "cross_entropy: in-place gradient needs the logits dtype");
+    d = logits;  // the row is held in registers: the gradient overwrites the logits
+  } else if (want_grad) {
+    d = at::empty(logits.sizes(), logits.options().dtype(grad_bf16 ? at::kBFloat16 : at::kFloat));
+  }
   CHECK_RC(dpe_cross_entropy(logits.data_ptr(), in_bf16, (const int64_t*)labels.data_ptr(), (int)B, (int)V, ld,
                              (float)grad_scale, want_grad ? d.data_ptr() : nullptr, grad_bf16, fp(rows), fp(sums),
                              fp(sums) + 1, (int)ignore_index, cur_stream()), "cross_entropy");
@@ -611,8 +833,10 @@ void register_ops(pybind11::module& m) {
   using c10::optional;
   m.def("linear_fwd", &linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("out_f32") = false, py::arg("residual") = py::none(), py::arg("out") = py::none());
-  m.def("linear_dgrad", &linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("residual") = py::none());
-  m.def("linear_wgrad", &linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("alpha") = 1.0);
+  m.def("linear_dgrad", &linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("residual") = py::none(),
+        py::arg("alpha_t") = py::none());
+  m.def("linear_wgrad", &linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("alpha") = 1.0,
+        py::arg("alpha_t") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("want_stats") = false, py::arg("bias") = py::none());
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"), py::arg("pad"),
@@ -630,7 +854,7 @@ void register_ops(pybind11::module& m) {
   m.def("gavgpool_fwd", &gavgpool_fwd);
   m.def("gavgpool_bwd", &gavgpool_bwd);
   m.def("cross_entropy", &cross_entropy, py::arg("logits"), py::arg("labels"), py::arg("V"), py::arg("grad_scale"),
-        py::arg("want_grad"), py::arg("grad_bf16"), py::arg("ignore_index") = -100);
+        py::arg("want_grad"), py::arg("grad_bf16"), py::arg("ignore_index") = -100, py::arg("inplace") = false);
   m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("out") = py::none());
   m.def("cast_f32", &cast_f32);
   m.def("act", &act, py::arg("a"), py::arg("b") = py::none(), py::arg("op") = 0);
@@ -649,6 +873,16 @@ void register_ops(pybind11::module& m) {
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("H"), py::arg("scale"), py::arg("causal") = true);
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("H"),
         py::arg("scale"), py::arg("causal") = true);
+  m.def("set_gemm_backend", [](int64_t mode) { g_blas_mode = (int)mode; g_blas_choice.clear(); },
+        "0 auto (per-shape autotune vs hipBLASLt), 1 native kernels only, 2 library whenever eligible");
+  m.def("gemm_backend_choices", []() {
+    std::vector<std::tuple<int, int64_t, int64_t, int64_t, int, int>> v;
+    for (auto& kv : g_blas_choice)
+      v.emplace_back(std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first), std::get<3>(kv.first),
+                     std::get<4>(kv.first), kv.second);
+    return v;
+  });
+  m.def("set_gemm256_mode", [](int64_t mode) { g_g256_mode = (int)mode; }, "0 auto, 1 off, 2 force (when supported)");
   m.def("pick_gemm_cfg", [](int64_t M, int64_t N, int64_t K, bool split) {
     auto c = pick_cfg(M, N, K, split);
     return std::make_tuple(c.bm, c.bn, c.splits, c.k_split);

@@ -51,6 +51,7 @@ struct IgemmArgs {
   int M, N, K;
   int64_t lda, ldb, ldc;
   float alpha;
+  const float* alpha_ptr;     // optional device scalar multiplied into alpha (loss-scale from autograd)
   int act;
   int k_split;  // K elements per split (multiple of 32); >= K means no split
   ConvGeom g;
@@ -60,3 +61,7 @@ struct IgemmArgs {
 
 extern "C" int dpe_igemm_launch(const dpe::IgemmArgs* args, int bm, int bn, int aload, int bload, int epi,
                                 int splits, hipStream_t stream);
+
+// 256x256x64 LDS-DMA / 8-phase GEMM (gemm256.hip) for large dense shapes.
+// a_k / b_k: operand K-contiguous (1) or M/N-contiguous (0); K % 64 == 0.
+extern "C" int dpe_gemm256_launch(const dpe::IgemmArgs* args, int a_k, int b_k, int epi, int splits, hipStream_t stream);

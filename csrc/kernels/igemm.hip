@@ -378,6 +378,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
 
   // ---------------------------------------------------------------- epilogue
   // acc[i][j][e]: m = m0 + wm + 16i + (lane&15), n = n0 + wn + 16j + (lane>>4)*4 + e
+  if (p.alpha_ptr) p.alpha *= *p.alpha_ptr;
   const int lm = lane & 15, ln4 = (lane >> 4) * 4;
   if constexpr (EPI == EPI_ATOMIC_F32) {
     // Stage the fp32 tile through LDS, half the rows at a time (the two

@@ -29,6 +29,9 @@ __global__ __launch_bounds__(1024) void ce_kernel(const TIn* __restrict__ logits
   const TIn* z = logits + (int64_t)row * ld;
   const int64_t label = labels[row];
   const bool ignored = (label == ignore_index);
+  // z_y read up front (before any thread can overwrite it when dlogits aliases logits)
+  __shared__ float s_zy;
+  if (threadIdx.x == 0) s_zy = (label >= 0 && label < V) ? ldv<TIn>(z, label) : 0.f;
   // pass 1: max + argmax
   float m = -INFINITY;
   int am = 0;
@@ -56,7 +59,7 @@ __global__ __launch_bounds__(1024) void ce_kernel(const TIn* __restrict__ logits
   for (int j = threadIdx.x; j < V; j += blockDim.x) s += __expf(ldv<TIn>(z, j) - m);
   s = block_sum(s, sh);
   const float lse = m + __logf(s);
-  const float zy = (label >= 0 && label < V) ? ldv<TIn>(z, label) : 0.f;
+  const float zy = s_zy;  // published by the barriers inside block_sum
   const float li = ignored ? 0.f : lse - zy;
   if (threadIdx.x == 0) {
     if (loss_rows) loss_rows[row] = li;
@@ -75,6 +78,133 @@ __global__ __launch_bounds__(1024) void ce_kernel(const TIn* __restrict__ logits
   }
 }
 
+// Vectorised row-in-registers variant (ld % 8 == 0, ld <= NT*8*MAXC): each
+// thread loads its 16-B chunks ONCE into registers, so the row is read from
+// HBM once and the gradient written once (the scalar kernel above reads it
+// three times).  dlogits may alias logits: every thread only rewrites the
+// chunks it alone read, and z_y is taken from registers, not re-read.
+template <typename TIn>
+DPE_DEVICE void ce_load8(const TIn* p, float* f);
+template <>
+DPE_DEVICE void ce_load8<uint16_t>(const uint16_t* p, float* f) { unpack8(*(const u32x4*)p, f); }
+template <>
+DPE_DEVICE void ce_load8<float>(const float* p, float* f) {
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+  f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3]; f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+}
+
+template <typename TIn, typename TOut, int NT, int MAXC>
+__global__ __launch_bounds__(NT) void ce_vec_kernel(const TIn* logits, const int64_t* __restrict__ labels, int V,
+                                                    int64_t ld, float grad_scale, TOut* dlogits,
+                                                    float* __restrict__ loss_rows, float* __restrict__ loss_sum,
+                                                    float* __restrict__ correct, int ignore_index) {
+  constexpr int NW = NT / 64;
+  __shared__ float shm[NW], shs[NW], shz[NW];
+  __shared__ int sha[NW];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const TIn* z = logits + (int64_t)row * ld;
+  const int nch = (int)(ld >> 3);
+  const int64_t label = labels[row];
+  const bool ignored = (label == ignore_index);
+  float f[MAXC][8];
+  float m = -INFINITY, zy = 0.f;
+  int am = 0x7fffffff;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = tid + c * NT;
+    if (ch < nch) {
+      ce_load8<TIn>(z + (int64_t)ch * 8, f[c]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int col = ch * 8 + e;
+        if (col >= V) f[c][e] = -INFINITY;
+        if (col == label) zy = f[c][e];
+        if (f[c][e] > m) { m = f[c][e]; am = col; }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[c][e] = -INFINITY;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64);
+    const int oa = __shfl_xor(am, o, 64);
+    if (om > m || (om == m && oa < am)) { m = om; am = oa; }
+  }
+  if (lane == 0) { shm[wid] = m; sha[wid] = am; }
+  __syncthreads();
+  m = shm[0];
+  am = sha[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w)
+    if (shm[w] > m || (shm[w] == m && sha[w] < am)) { m = shm[w]; am = sha[w]; }
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += __expf(f[c][e] - m);
+  s = warp_sum(s);
+  zy = warp_sum(zy);
+  if (lane == 0) { shs[wid] = s; shz[wid] = zy; }
+  __syncthreads();
+  s = 0.f;
+  zy = 0.f;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) { s += shs[w]; zy += shz[w]; }
+  const float lse = m + __logf(s);
+  const float li = ignored ? 0.f : lse - zy;
+  if (tid == 0) {
+    if (loss_rows) loss_rows[row] = li;
+    if (loss_sum) atomicAdd(loss_sum, li);
+    if (correct && !ignored) atomicAdd(correct, (am == label) ? 1.f : 0.f);
+  }
+  if (dlogits) {
+    TOut* d = dlogits + (int64_t)row * ld;
+    const float k = ignored ? 0.f : grad_scale / s;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = tid + c * NT;
+      if (ch < nch) {
+        float g[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int col = ch * 8 + e;
+          g[e] = __expf(f[c][e] - m) * k - ((col == label && !ignored) ? grad_scale : 0.f);
+        }
+        if constexpr (sizeof(TOut) == 2) {
+          *(u32x4*)(d + (int64_t)ch * 8) = pack8(g);
+        } else {
+          *(f32x4*)(d + (int64_t)ch * 8) = f32x4{g[0], g[1], g[2], g[3]};
+          *(f32x4*)(d + (int64_t)ch * 8 + 4) = f32x4{g[4], g[5], g[6], g[7]};
+        }
+      }
+    }
+  }
+}
+
+template <typename TIn, typename TOut>
+bool ce_vec_launch(const TIn* logits, const int64_t* labels, int B, int V, int64_t ld, float gs, TOut* d, float* lr,
+                   float* ls, float* cor, int ign, hipStream_t st) {
+  if (ld % 8) return false;
+  const int64_t nch = ld / 8;
+#define DPE_CE_VEC(NT, MC)                                                                                         \
+  if (nch <= (int64_t)(NT) * (MC)) {                                                                               \
+    hipLaunchKernelGGL((ce_vec_kernel<TIn, TOut, NT, MC>), dim3(B), dim3(NT), 0, st, logits, labels, V, ld, gs, d, lr, \
+                       ls, cor, ign);                                                                              \
+    return true;                                                                                                   \
+  }
+  DPE_CE_VEC(64, 1)
+  DPE_CE_VEC(128, 1)
+  DPE_CE_VEC(256, 1)
+  DPE_CE_VEC(256, 2)
+  DPE_CE_VEC(1024, 1)
+  DPE_CE_VEC(1024, 2)
+  DPE_CE_VEC(1024, 4)
+  DPE_CE_VEC(1024, 8)
+#undef DPE_CE_VEC
+  return false;
+}
+
 }  // namespace dpe
 
 using namespace dpe;
@@ -83,6 +213,16 @@ using namespace dpe;
 extern "C" int dpe_cross_entropy(const void* logits, int in_bf16, const int64_t* labels, int B, int V, int64_t ld,
                                  float grad_scale, void* dlogits, int out_bf16, float* loss_rows, float* loss_sum,
                                  float* correct, int ignore_index, hipStream_t st) {
+  if (dlogits == logits && in_bf16 != out_bf16) return -2;  // in-place needs equal dtypes
+  if (in_bf16 ? (out_bf16 ? ce_vec_launch((const uint16_t*)logits, labels, B, V, ld, grad_scale, (uint16_t*)dlogits,
+                                           loss_rows, loss_sum, correct, ignore_index, st)
+                           : ce_vec_launch((const uint16_t*)logits, labels, B, V, ld, grad_scale, (float*)dlogits,
+                                           loss_rows, loss_sum, correct, ignore_index, st))
+              : (out_bf16 ? ce_vec_launch((const float*)logits, labels, B, V, ld, grad_scale, (uint16_t*)dlogits,
+                                          loss_rows, loss_sum, correct, ignore_index, st)
+                          : ce_vec_launch((const float*)logits, labels, B, V, ld, grad_scale, (float*)dlogits,
+                                          loss_rows, loss_sum, correct, ignore_index, st)))
+    return 0;
   const int threads = V >= 4096 ? 1024 : 256;
   if (in_bf16) {
     if (out_bf16)

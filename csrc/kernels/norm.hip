@@ -136,14 +136,34 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
   }
 }
 
-__global__ void ln_bwd_finalize_kernel(const float* __restrict__ part, int nb, int D, float* __restrict__ dw,
-                                       float* __restrict__ db) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= D) return;
-  float a = 0.f, b = 0.f;
-  for (int k = 0; k < nb; ++k) { a += part[(int64_t)k * 2 * D + i]; b += part[(int64_t)k * 2 * D + D + i]; }
-  dw[i] += a;
-  if (db) db[i] += b;
+// Column-parallel reduction of the [nb][2][D] partials: block = 64 columns x
+// 4 waves splitting the nb rows (coalesced 256-B row reads), blockIdx.y picks
+// dw (0) or db (1).  Replaces a serial per-column loop (1.7 ms/step on GPT-2).
+__global__ __launch_bounds__(256) void ln_bwd_finalize_kernel(const float* __restrict__ part, int nb, int D,
+                                                              float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int which = blockIdx.y;
+  const int col = blockIdx.x * 64 + lane;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (col < D) {
+    const float* src = part + (int64_t)which * D + col;
+    int k = wid;
+    for (; k + 12 < nb; k += 16) {
+      a0 += src[(int64_t)k * 2 * D];
+      a1 += src[(int64_t)(k + 4) * 2 * D];
+      a2 += src[(int64_t)(k + 8) * 2 * D];
+      a3 += src[(int64_t)(k + 12) * 2 * D];
+    }
+    for (; k < nb; k += 4) a0 += src[(int64_t)k * 2 * D];
+  }
+  red[wid][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (wid == 0 && col < D) {
+    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    if (which == 0) dw[col] += t;
+    else if (db) db[col] += t;
+  }
 }
 
 }  // namespace dpe
@@ -169,6 +189,6 @@ extern "C" int dpe_layernorm_bwd(const uint16_t* dy, const void* x, int x_bf16, 
     hipLaunchKernelGGL((ln_bwd_kernel<true>), dim3(nbc), dim3(256), 0, st, dy, x, w, mean, rstd, dx, dx_acc, part, rows, D);
   else
     hipLaunchKernelGGL((ln_bwd_kernel<false>), dim3(nbc), dim3(256), 0, st, dy, x, w, mean, rstd, dx, dx_acc, part, rows, D);
-  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 255) / 256), dim3(256), 0, st, part, nbc, D, dw, db);
+  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 63) / 64, db ? 2 : 1), dim3(256), 0, st, part, nbc, D, dw, db);
   return 0;
 }

@@ -88,13 +88,18 @@ class GPT2(nn.Module):
                     lin.weight.normal_(0, std / math.sqrt(2 * self.cfg.n_layer))
                     lin.bias.zero_()
 
-    def forward(self, idx):
+    def forward(self, idx, targets=None):
+        """Logits [B, T, V(p)], or -- with ``targets`` -- the mean next-token
+        cross-entropy through the fused LM-head + CE op (logits never materialise
+        outside it)."""
         B, T = idx.shape
         assert T <= self.cfg.block_size, "sequence longer than block_size"
         x = Fx.embedding(idx, self.wte, self.wpe[:T] if not idx.is_cuda else self.wpe)
         for blk in self.h:
             x = blk(x)
         x = self.ln_f(x)
+        if targets is not None:
+            return Fx.lm_head_ce(x, self.wte, targets)
         return Fx.lm_head(x, self.wte)
 
     def num_params(self) -> int:

@@ -368,7 +368,7 @@ class _CEFn(Function):
     def forward(ctx, logits, labels, num_classes: int, ignore_index: int):
         rows, s, correct, d = ext().cross_entropy(logits.contiguous(), labels.contiguous(), num_classes, 1.0, True,
                                                   logits.dtype == torch.bfloat16, ignore_index)
-        n = (labels != ignore_index).sum().clamp_min(1).to(torch.float32) if ignore_index >= 0 else labels.numel()
+        n = (labels != ignore_index).sum().clamp_min(1).to(torch.float32)
         ctx.save_for_backward(d)
         ctx.n = n
         ctx.correct = correct
@@ -597,6 +597,53 @@ class _LMHeadFn(Function):
         C.linear_wgrad(d, xb, buf, 1.0)  # padded leading dim, only the V real rows are produced
         grad_done(ctx.wte, direct)
         return dx, (None if direct else buf), None
+
+
+class _LMHeadCEFn(Function):
+    """Fused tied LM head + mean cross-entropy (GPT-2 training path).
+
+    The logits never leave the op: the CE kernel holds each row in registers
+    and overwrites the logits with (softmax - onehot) in place (one HBM read +
+    one write of the [tokens, Vp] matrix); backward feeds that straight to the
+    dgrad/wgrad GEMMs, which read the incoming loss gradient / N as a device
+    scalar (``alpha_t``) -- no separate scaling pass over the 0.8 GB gradient.
+    """
+
+    @staticmethod
+    def forward(ctx, x, wte, labels, pad_rows: int, ignore_index: int):
+        C = ext()
+        w16 = shadow(wte, pad_rows)
+        xb = x.contiguous() if x.dtype == torch.bfloat16 else x.to(torch.bfloat16).contiguous()
+        xb = xb.reshape(-1, xb.shape[-1])
+        logits = C.linear_fwd(xb, w16, None, 0, False, None, None)
+        lab = labels.reshape(-1).contiguous()
+        _, s, _, d = C.cross_entropy(logits, lab, wte.shape[0], 1.0, True, True, ignore_index, True)
+        n = (lab != ignore_index).sum().clamp_min(1).to(torch.float32)
+        ctx.save_for_backward(xb, d, n)
+        ctx.wte, ctx.pad, ctx.xshape = wte, pad_rows, x.shape
+        note_use(wte)
+        return s.reshape(()) / n
+
+    @staticmethod
+    def backward(ctx, g):
+        C = ext()
+        xb, d, n = ctx.saved_tensors
+        scale = (g.float() / n).reshape(1).contiguous()
+        dx = C.linear_dgrad(d, shadow(ctx.wte, ctx.pad), None, scale)
+        buf, direct = grad_sink(ctx.wte)
+        C.linear_wgrad(d, xb, buf, 1.0, scale)
+        grad_done(ctx.wte, direct)
+        return dx.reshape(ctx.xshape), (None if direct else buf), None, None, None
+
+
+def lm_head_ce(x, wte, labels, vocab_pad_to: int = 64, ignore_index: int = -100):
+    """Mean CE of the tied LM head logits ``x @ wte^T`` against ``labels`` (fused)."""
+    if not x.is_cuda:
+        logits = F.linear(x.float(), wte)
+        return F.cross_entropy(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1), ignore_index=ignore_index)
+    V = wte.shape[0]
+    Vp = (V + vocab_pad_to - 1) // vocab_pad_to * vocab_pad_to
+    return _LMHeadCEFn.apply(x, wte, labels, Vp - V, ignore_index)
 
 
 def lm_head(x, wte, vocab_pad_to: int = 64):

@@ -218,7 +218,8 @@ def test_gavgpool(C):
 
 
 # ------------------------------------------------------------------- loss
-@pytest.mark.parametrize("B,V,ld,in_bf", [(64, 10, 10, False), (256, 1000, 1000, False), (32, 50257, 50304, True)])
+@pytest.mark.parametrize("B,V,ld,in_bf", [(64, 16, 16, False), (256, 1000, 1000, False), (32, 50257, 50304, True),
+                                         (16, 3000, 3000, True), (8, 100000, 100000, True)])
 def test_cross_entropy(C, B, V, ld, in_bf):
     torch.manual_seed(10)
     z = torch.randn(B, ld, device=dev) * 3
@@ -234,6 +235,11 @@ def test_cross_entropy(C, B, V, ld, in_bf):
     assert rel_err(d[:, :V], g) < 1e-2
     if ld > V:
         assert d[:, V:].float().abs().max().item() == 0
+    # in-place (row held in registers): gradient overwrites the logits
+    z2 = z.clone()
+    _, s2, _, d2 = C.cross_entropy(z2, y, V, 1.0, True, in_bf, -100, True)
+    assert d2.data_ptr() == z2.data_ptr() and abs(s2.item() - s.item()) <= 1e-5 * abs(s.item())
+    assert torch.equal(d2, d)
 
 
 # ---------------------------------------------------------------- eltwise
@@ -314,3 +320,113 @@ def test_attention_fwd_bwd(C, B, T, H):
     dqkv = C.attn_bwd(qkv, out, do, lse, H, scale, True)
     for i, g in enumerate((gq, gk, gv)):
         assert rel_err(dqkv[:, :, i].permute(0, 2, 1, 3), g) < 2e-2, i
+
+
+# ------------------------------------------- 256-tile LDS-DMA GEMM (gemm256.hip)
+@pytest.fixture
+def g256(C):
+    C.set_gemm_backend(1)  # native kernels only (no hipBLASLt autotune arm)
+    C.set_gemm256_mode(2)  # force the 256-tile kernel whenever the layout is supported
+    yield C
+    C.set_gemm256_mode(0)
+    C.set_gemm_backend(0)
+
+
+@pytest.mark.parametrize("backend", [1, 2])
+def test_gemm_backends_plain(C, backend):
+    """Native (1) and library (2) arms of the plain-GEMM dispatch agree with fp32 torch."""
+    C.set_gemm_backend(backend)
+    try:
+        torch.manual_seed(8)
+        M, N, K = 1024, 776, 512
+        x = bf(torch.randn(M, K, device=dev))
+        w = bf(torch.randn(N, K, device=dev) / math.sqrt(K))
+        b = torch.randn(N, device=dev)
+        assert rel_err(C.linear_fwd(x, w, b, 0, False), x.float() @ w.float().t() + b) < 1e-2
+        dy = bf(torch.randn(M, N, device=dev))
+        s = torch.tensor([0.5], device=dev)
+        assert rel_err(C.linear_dgrad(dy, w, None, s), 0.5 * (dy.float() @ w.float())) < 1e-2
+        dw = torch.randn(N, K, device=dev)
+        ref = dw + 0.5 * (dy.float().t() @ x.float())
+        C.linear_wgrad(dy, x, dw, 1.0, s)
+        assert rel_err(dw, ref) < 1e-3
+        # fp32 residual stream: y = res + x @ w^T + b
+        res = torch.randn(M, N, device=dev)
+        y = C.linear_fwd(x, w, b, 0, True, res)
+        assert rel_err(y, res + x.float() @ w.float().t() + b) < 1e-4
+        # column-padded dy (vocab-padded LM head): only the first N columns are real
+        dyp = bf(torch.randn(M, N + 56, device=dev))
+        dw2 = torch.zeros(N, K, device=dev)
+        C.linear_wgrad(dyp, x, dw2, 1.0)
+        assert rel_err(dw2, dyp[:, :N].float().t() @ x.float()) < 1e-3
+    finally:
+        C.set_gemm_backend(0)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 256), (8192 // 8 + 64, 2304 // 4 + 8, 768), (300, 520, 128)])
+def test_gemm256_fwd(g256, M, N, K):
+    C = g256
+    torch.manual_seed(3)
+    x = bf(torch.randn(M, K, device=dev))
+    w = bf(torch.randn(N, K, device=dev) / math.sqrt(K))
+    b = torch.randn(N, device=dev)
+    ref = x.float() @ w.float().t() + b
+    y = C.linear_fwd(x, w, b, 0, False)
+    assert rel_err(y, ref) < 1e-2
+    yg = C.linear_fwd(x, w, b, 2, False)  # fused tanh-GELU epilogue
+    assert rel_err(yg, F.gelu(ref, approximate="tanh")) < 1e-2
+    res = torch.randn(M, N, device=dev)
+    y32 = C.linear_fwd(x, w, b, 0, True, res)  # fp32 out + fp32 residual
+    assert rel_err(y32, ref + res) < 1e-4
+    rb = bf(torch.randn(M, N, device=dev))
+    yr = C.linear_fwd(x, w, None, 0, False, rb)  # bf16 residual
+    assert rel_err(yr, x.float() @ w.float().t() + rb.float()) < 1e-2
+
+
+def test_gemm256_asymmetric_layout(g256):
+    C = g256
+    M, N, K = 256, 256, 128
+    x = torch.zeros(M, K, device=dev)
+    x[torch.arange(M), torch.arange(M) % K] = 1.0
+    w = (torch.arange(N * K, device=dev).reshape(N, K) % 7).float()
+    assert torch.equal(C.linear_fwd(bf(x), bf(w), None, 0, True), x @ w.t())
+    # dgrad layout (B N-contiguous): dx = dy @ w
+    dy = (torch.arange(M * N, device=dev).reshape(M, N) % 5).float()
+    w2 = torch.zeros(N, K, device=dev)
+    w2[torch.arange(N), torch.arange(N) % K] = 1.0
+    assert torch.equal(C.linear_dgrad(bf(dy), bf(w2)).float(), dy @ w2)
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 256, 768), (1024, 768, 2304), (320, 520, 192)])
+def test_gemm256_dgrad(g256, M, N, K):
+    C = g256
+    torch.manual_seed(4)
+    dy = bf(torch.randn(M, N, device=dev))
+    w = bf(torch.randn(N, K, device=dev))
+    assert rel_err(C.linear_dgrad(dy, w), dy.float() @ w.float()) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 768, 256), (4096, 2304, 768), (1024, 520, 264)])
+def test_gemm256_wgrad(g256, M, N, K):
+    C = g256
+    torch.manual_seed(5)
+    dy = bf(torch.randn(M, N, device=dev))
+    x = bf(torch.randn(M, K, device=dev))
+    dw = torch.randn(N, K, device=dev)
+    ref = dw + dy.float().t() @ x.float()
+    C.linear_wgrad(dy, x, dw, 1.0)  # accumulates (split-K atomics)
+    assert rel_err(dw, ref) < 1e-3
+
+
+def test_gemm256_alpha_tensor(g256):
+    C = g256
+    torch.manual_seed(6)
+    M, N, K = 512, 512, 256
+    dy = bf(torch.randn(M, N, device=dev))
+    w = bf(torch.randn(N, K, device=dev))
+    x = bf(torch.randn(M, K, device=dev))
+    s = torch.tensor([0.25], device=dev)
+    assert rel_err(C.linear_dgrad(dy, w, None, s), 0.25 * (dy.float() @ w.float())) < 1e-2
+    dw = torch.zeros(N, K, device=dev)
+    C.linear_wgrad(dy, x, dw, 2.0, s)
+    assert rel_err(dw, 0.5 * (dy.float().t() @ x.float())) < 1e-3

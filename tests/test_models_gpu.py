@@ -138,6 +138,24 @@ def test_gpt2_tiny_gpu_vs_cpu(C):
         assert rel(p.grad.cpu(), gc[n].grad) < 0.1, n
 
 
+def test_gpt2_fused_lm_head_ce(C):
+    """model(idx, targets) (fused LM head + in-place CE + alpha-scaled GEMMs) == unfused logits + CE."""
+    torch.manual_seed(7)
+    m1 = get_model("gpt2-tiny").to(dev)
+    m2 = copy.deepcopy(m1)
+    idx = torch.randint(0, 512, (2, 128), device=dev)
+    tgt = torch.randint(0, 512, (2, 128), device=dev)
+    l1 = Fx.cross_entropy(m1(idx), tgt)
+    (3.0 * l1).backward()
+    l2 = m2(idx, tgt)
+    (3.0 * l2).backward()
+    assert abs(l1.item() - l2.item()) < 1e-3 * abs(l1.item())
+    g1 = dict(m1.named_parameters())
+    for n, p in m2.named_parameters():
+        assert cos(p.grad, g1[n].grad) > 0.999, n
+        assert rel(p.grad, g1[n].grad) < 0.02, n
+
+
 def test_gpt2_small_step(C):
     from distributed_pytorch_example_amd.optim import AdamW
 
@@ -148,7 +166,7 @@ def test_gpt2_small_step(C):
     idx = torch.randint(0, 50257, (2, 1024), device=dev)
     losses = []
     for _ in range(3):
-        loss = Fx.cross_entropy(m(idx), idx)  # learn the identity: loss must drop
+        loss = m(idx, idx)  # fused LM head + CE; learn the identity: loss must drop
         loss.backward()
         opt.step()
         for p in m.parameters():
