@@ -27,7 +27,7 @@ int dpe_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, 
 int dpe_bn_bwd_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* coef, float* dgamma,
                         float* dbeta, float* bcoef, hipStream_t st);
 int dpe_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* bcoef, uint16_t* dx,
-                     uint16_t* dz_out, int64_t M, int C, hipStream_t st);
+                     uint16_t* dz_out, int64_t M, int C, const float* mcoef, hipStream_t st);
 int dpe_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int k, int s,
                     int p, hipStream_t st);
 int dpe_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int OH, int OW, int k,
@@ -172,8 +172,10 @@ bool try_gemm256(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_sp
   return rc == 0;
 }
 
-void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_split) {
-  if (try_gemm256(a, aload, bload, epi, allow_split)) return;
+// conv_*: the 128-tile kernel measured faster than the 256-tile one on every
+// ResNet-50 1x1 shape (small K / N), so convolutions opt out of it unless forced.
+void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_split, bool conv = false) {
+  if ((!conv || g_g256_override == 1 || g256_mode() == 2) && try_gemm256(a, aload, bload, epi, allow_split)) return;
   Cfg c = pick_cfg(a.M, a.N, a.K, allow_split && epi == dpe::EPI_ATOMIC_F32);
   a.k_split = c.k_split;
   const int rc = dpe_igemm_launch(&a, c.bm, c.bn, aload, bload, epi, c.splits, cur_stream());
@@ -475,13 +477,18 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
     stats = at::empty({2, g.K, tilesM}, x.options().dtype(at::kFloat));
     a.col_stats = fp(stats);
   }
-  run_igemm(a, is_pointwise(g) ? dpe::A_DENSE_K : dpe::A_CONV_FWD, dpe::B_DENSE_K, dpe::EPI_BF16, false);
+  run_igemm(a, is_pointwise(g) ? dpe::A_DENSE_K : dpe::A_CONV_FWD, dpe::B_DENSE_K, dpe::EPI_BF16, false, true);
   return {y, stats};
 }
 
 // dx NHWC [N,H,W,C] = conv_transpose(dy, w); optional residual added into dx
-Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape, std::vector<int64_t> stride,
-                  std::vector<int64_t> pad, std::vector<int64_t> dil, const c10::optional<Tensor>& residual) {
+// dx NHWC [N,H,W,C] = conv_transpose(dy, w); optional residual added into dx.
+// With bn_x/bn_coef (dx is dL/d relu(BN(bn_x))), the epilogue also emits the
+// BatchNorm-backward partials [2][C][tiles] (sum dz, sum dz*(x-mean)).
+std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape,
+                                    std::vector<int64_t> stride, std::vector<int64_t> pad, std::vector<int64_t> dil,
+                                    const c10::optional<Tensor>& residual, const c10::optional<Tensor>& bn_x,
+                                    const c10::optional<Tensor>& bn_coef) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(w); CHECK_CONTIG(dy); CHECK_CONTIG(w);
   Tensor dx = at::empty(xshape, dy.options());
   auto g = geom(dx, w, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], dy.size(1), dy.size(2));
@@ -492,14 +499,33 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape
   a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.K;
   a.lda = g.K; a.ldb = g.C; a.ldc = g.C;
   if (residual.has_value() && residual->defined()) { CHECK_BF16((*residual)); CHECK_CONTIG((*residual)); a.residual = bp(*residual); }
-  if (is_pointwise(g)) {
-    run_igemm(a, dpe::A_DENSE_K, dpe::B_DENSE_N, dpe::EPI_BF16, false);
-  } else if (g.sh == 1 && g.sw == 1) {
-    run_igemm(a, dpe::A_CONV_DGRAD, dpe::B_CONV_DGRAD, dpe::EPI_BF16, false);
+  const bool want_bn = bn_x.has_value() && bn_x->defined();
+  if (want_bn) {
+    CHECK_BF16((*bn_x)); CHECK_CONTIG((*bn_x)); CHECK_F32((*bn_coef));
+    TORCH_CHECK(bn_x->sizes() == dx.sizes(), "conv_dgrad: bn_x must have dx's shape");
+    TORCH_CHECK(bn_coef->numel() == 4 * g.C, "conv_dgrad: bn_coef must be [4][C]");
+    a.st_x = bp(*bn_x);
+    a.st_coef = fp(*bn_coef);
+  }
+  Tensor part;
+  auto tiles_of = [&](int64_t M, int64_t K) { const Cfg c = pick_cfg(M, g.C, K, false); return (M + c.bm - 1) / c.bm; };
+  if (is_pointwise(g) || (g.sh == 1 && g.sw == 1)) {
+    if (want_bn) {
+      const int64_t t = tiles_of(a.M, a.K);
+      part = at::empty({2, g.C, t}, dy.options().dtype(at::kFloat));
+      a.col_stats = fp(part);
+      a.stats_ld = (int)t;
+    }
+    const int epi = want_bn ? dpe::EPI_BF16_BNB : dpe::EPI_BF16;
+    if (is_pointwise(g)) run_igemm(a, dpe::A_DENSE_K, dpe::B_DENSE_N, epi, false, true);
+    else run_igemm(a, dpe::A_CONV_DGRAD, dpe::B_CONV_DGRAD, epi, false, true);
   } else {
     // Strided: one stride-1 sub-GEMM per output parity (a, b) over only the
     // taps that reach it -- no MFMA work on structural zeros.  A parity with
     // no taps is a K = 0 GEMM that stores zeros (+ residual).
+    TORCH_CHECK(g.dh == 1 && g.dw == 1, "strided dgrad with dilation is not supported");
+    std::vector<dpe::IgemmArgs> subs;
+    int64_t total_tiles = 0;
     for (int pa = 0; pa < g.sh; ++pa) {
       for (int pb = 0; pb < g.sw; ++pb) {
         dpe::ConvGeom v = g;
@@ -508,7 +534,6 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape
         const int Sp = g.S > s0 ? (g.S - s0 + g.sw - 1) / g.sw : 0;
         const int Hp = (g.H - pa + g.sh - 1) / g.sh, Wp = (g.W - pb + g.sw - 1) / g.sw;
         if (Hp <= 0 || Wp <= 0) continue;
-        TORCH_CHECK(g.dh == 1 && g.dw == 1, "strided dgrad with dilation is not supported");
         v.H = Hp; v.W = Wp; v.R = Rp; v.S = Sp;
         v.sh = 1; v.sw = 1;
         v.ph = (pa + g.ph - r0) / g.sh;  // oh = hh + ph' - t
@@ -519,11 +544,23 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape
         b.g = v;
         b.M = g.N * Hp * Wp;
         b.K = Rp * Sp * g.K;
-        run_igemm(b, dpe::A_CONV_DGRAD, dpe::B_CONV_DGRAD, dpe::EPI_BF16, false);
+        b.stats_off = (int)total_tiles;
+        total_tiles += tiles_of(b.M, b.K);
+        subs.push_back(b);
       }
     }
+    if (want_bn) part = at::empty({2, g.C, total_tiles}, dy.options().dtype(at::kFloat));
+    for (auto& b : subs) {
+      if (want_bn) { b.col_stats = fp(part); b.stats_ld = (int)total_tiles; }
+      run_igemm(b, dpe::A_CONV_DGRAD, dpe::B_CONV_DGRAD, want_bn ? dpe::EPI_BF16_BNB : dpe::EPI_BF16, false, true);
+    }
   }
-  return dx;
+  return {dx, part};
+}
+
+Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape, std::vector<int64_t> stride,
+                  std::vector<int64_t> pad, std::vector<int64_t> dil, const c10::optional<Tensor>& residual) {
+  return conv_dgrad_impl(dy, w, xshape, stride, pad, dil, residual, c10::nullopt, c10::nullopt)[0];
 }
 
 // dw [K,R,S,C] fp32 (+)= alpha * dy^T (x) im2col(x)
@@ -538,7 +575,7 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64
   a.M = g.K; a.N = g.R * g.S * g.C; a.K = g.N * g.OH * g.OW;
   a.lda = g.K; a.ldb = g.C; a.ldc = a.N;
   a.alpha = (float)alpha;
-  run_igemm(a, dpe::A_DENSE_M, is_pointwise(g) ? dpe::B_DENSE_N : dpe::B_CONV_WGRAD, dpe::EPI_ATOMIC_F32, true);
+  run_igemm(a, dpe::A_DENSE_M, is_pointwise(g) ? dpe::B_DENSE_N : dpe::B_CONV_WGRAD, dpe::EPI_ATOMIC_F32, true, true);
 }
 
 // --------------------------------------------------------------- BatchNorm
@@ -605,9 +642,41 @@ std::vector<Tensor> bn_bwd(const Tensor& dy, const c10::optional<Tensor>& y, con
   Tensor dx = at::empty_like(x);
   Tensor dz;
   if (want_dz) dz = at::empty_like(x);
-  CHECK_RC(dpe_bn_bwd_apply(bp(dy), yp, bp(x), fp(bcoef), bpm(dx), want_dz ? bpm(dz) : nullptr, M, (int)C, st),
+  CHECK_RC(dpe_bn_bwd_apply(bp(dy), yp, bp(x), fp(bcoef), bpm(dx), want_dz ? bpm(dz) : nullptr, M, (int)C, nullptr, st),
            "bn_bwd_apply");
   return {dx, dz};
+}
+
+// BatchNorm coefficients [4][C] (scale, shift, mean, invstd) from conv-epilogue
+// partials WITHOUT applying them: the consumer conv applies relu(x*scale+shift)
+// in its load prologue.  Updates running stats like bn_fwd_train.
+Tensor bn_coef(const Tensor& stats, int64_t M, const c10::optional<Tensor>& gamma, const c10::optional<Tensor>& beta,
+               const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar, double momentum, double eps) {
+  CHECK_GPU(stats); CHECK_F32(stats);
+  TORCH_CHECK(stats.dim() == 3 && stats.size(0) == 2, "stats must be [2][C][nb] partials");
+  const int64_t C = stats.size(1);
+  Tensor coef = at::empty({4, C}, stats.options());
+  CHECK_RC(dpe_bn_finalize(fp(stats), (int)stats.size(2), (int)C, M, fpo(gamma), fpo(beta), fpom(rmean), fpom(rvar),
+                           (float)momentum, (float)eps, fp(coef), cur_stream()), "bn_finalize");
+  return coef;
+}
+
+// Backward of y = relu(BN(x)) given the (sum dz, sum dz*(x-mean)) partials
+// [2][C][nb] produced by the dgrad epilogue that computed dy; the ReLU mask is
+// recomputed from x and the forward coefficients.  dgamma/dbeta accumulate.
+Tensor bn_bwd_partials(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& gamma, const Tensor& coef,
+                       const Tensor& partials, const c10::optional<Tensor>& dgamma, const c10::optional<Tensor>& dbeta) {
+  CHECK_GPU(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_BF16(x);
+  TORCH_CHECK(dy.sizes() == x.sizes(), "bn_bwd_partials: dy/x shape mismatch");
+  const int64_t C = x.size(-1), M = rows_of(x);
+  TORCH_CHECK(partials.dim() == 3 && partials.size(0) == 2 && partials.size(1) == C, "partials must be [2][C][nb]");
+  hipStream_t st = cur_stream();
+  Tensor bcoef = at::empty({3, C}, x.options().dtype(at::kFloat));
+  CHECK_RC(dpe_bn_bwd_finalize(fp(partials), (int)partials.size(2), (int)C, M, fpo(gamma), fp(coef), fpom(dgamma),
+                               fpom(dbeta), fp(bcoef), st), "bn_bwd_finalize");
+  Tensor dx = at::empty_like(x);
+  CHECK_RC(dpe_bn_bwd_apply(bp(dy), nullptr, bp(x), fp(bcoef), bpm(dx), nullptr, M, (int)C, fp(coef), st), "bn_bwd_apply");
+  return dx;
 }
 
 // ----------------------------------------------------------------- pooling
@@ -839,6 +908,13 @@ void register_ops(pybind11::module& m) {
         py::arg("alpha_t") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("want_stats") = false, py::arg("bias") = py::none());
+  m.def("conv_dgrad_bn", &conv_dgrad_impl, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"),
+        py::arg("pad"), py::arg("dil"), py::arg("residual") = py::none(), py::arg("bn_x") = py::none(),
+        py::arg("bn_coef") = py::none());
+  m.def("bn_coef", &bn_coef, py::arg("stats"), py::arg("M"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
+        py::arg("running_var"), py::arg("momentum"), py::arg("eps"));
+  m.def("bn_bwd_partials", &bn_bwd_partials, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("coef"),
+        py::arg("partials"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), py::arg("residual") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),

@@ -52,28 +52,33 @@ __global__ __launch_bounds__(BN_T) void bn_stats_partial_kernel(const uint16_t* 
   }
 }
 
-// Sum channel ch's nb partials (layout [2][C][nb]) with one wave; fp64 accumulation per lane.
-DPE_DEVICE void wave_sum2(const float* __restrict__ part, int nb, int C, int ch, double& s, double& q) {
-  const int lane = threadIdx.x & 63;
+// Sum channel ch's nb partials (layout [2][C][nb]) with the whole 256-thread
+// block (the conv-epilogue partials number M/BM -- thousands for the early
+// layers -- so one wave per channel was latency-bound); fp64 accumulation.
+// Result valid in thread 0.
+DPE_DEVICE void block_sum2(const float* __restrict__ part, int nb, int C, int ch, double& s, double& q) {
+  __shared__ double red[2][4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   double a = 0.0, b = 0.0;
   const float* ps = part + (int64_t)ch * nb;
   const float* pq = part + (int64_t)(C + ch) * nb;
-  for (int i = lane; i < nb; i += 64) { a += ps[i]; b += pq[i]; }
+  for (int i = threadIdx.x; i < nb; i += 256) { a += ps[i]; b += pq[i]; }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
-  s = a;
-  q = b;
+  if (lane == 0) { red[0][wid] = a; red[1][wid] = b; }
+  __syncthreads();
+  s = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+  q = red[1][0] + red[1][1] + red[1][2] + red[1][3];
 }
 
 // out: [4][C] = scale, shift, mean, invstd
 __global__ void bn_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M, const float* __restrict__ gamma,
                                    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
                                    float momentum, float eps, float* __restrict__ out) {
-  const int ch = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (ch >= C) return;
+  const int ch = blockIdx.x;
   double s, q;
-  wave_sum2(part, nb, C, ch, s, q);
-  if ((threadIdx.x & 63) != 0) return;
+  block_sum2(part, nb, C, ch, s, q);
+  if (threadIdx.x != 0) return;
   const double mean = s / (double)M;
   double var = q / (double)M - mean * mean;
   if (var < 0) var = 0;
@@ -176,11 +181,10 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const uint16_t* __r
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M, const float* __restrict__ gamma,
                                        const float* __restrict__ coef, float* __restrict__ dgamma, float* __restrict__ dbeta,
                                        float* __restrict__ bcoef) {
-  const int ch = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (ch >= C) return;
+  const int ch = blockIdx.x;
   double s, q;
-  wave_sum2(part, nb, C, ch, s, q);
-  if ((threadIdx.x & 63) != 0) return;
+  block_sum2(part, nb, C, ch, s, q);
+  if (threadIdx.x != 0) return;
   const float mean = coef[2 * C + ch], invstd = coef[3 * C + ch];
   const float g = gamma ? gamma[ch] : 1.f;
   if (dgamma) dgamma[ch] += (float)(q * invstd);
@@ -195,10 +199,13 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nb, i
   bcoef[2 * C + ch] = c;
 }
 
+// ReLU mask: from y (y > 0) when y is given, else from the pre-BN input and the
+// forward coefficients (x*scale + shift > 0) when mcoef is given (the BN output
+// was never materialised: it was applied in the consumer's load prologue).
 __global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
                                                             const uint16_t* __restrict__ x, const float* __restrict__ bcoef,
                                                             uint16_t* __restrict__ dx, uint16_t* __restrict__ dz_out,
-                                                            int64_t nchunks, int C) {
+                                                            int64_t nchunks, int C, const float* __restrict__ mcoef) {
   const int CPR = C >> 3;
   for (int64_t i = blockIdx.x * (int64_t)BN_T + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * BN_T) {
     const int c8 = (int)(i % CPR) * 8;
@@ -210,6 +217,9 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const uint16_t* __re
       unpack8(*(const u32x4*)(y + i * 8), yv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+    } else if (mcoef) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = fmaf(xv[e], mcoef[c8 + e], mcoef[C + c8 + e]) > 0.f ? d[e] : 0.f;
     }
     if (dz_out) *(u32x4*)(dz_out + i * 8) = pack8(d);
     float o[8];
@@ -246,7 +256,7 @@ extern "C" int dpe_bn_stats(const uint16_t* x, int64_t M, int C, int nb, float* 
 
 extern "C" int dpe_bn_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* beta,
                                float* rmean, float* rvar, float momentum, float eps, float* coef, hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, nb, C, M, gamma, beta, rmean, rvar,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, part, nb, C, M, gamma, beta, rmean, rvar,
                      momentum, eps, coef);
   return 0;
 }
@@ -274,14 +284,15 @@ extern "C" int dpe_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const ui
 
 extern "C" int dpe_bn_bwd_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* coef,
                                    float* dgamma, float* dbeta, float* bcoef, hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, nb, C, M, gamma, coef, dgamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, nb, C, M, gamma, coef, dgamma,
                      dbeta, bcoef);
   return 0;
 }
 
 extern "C" int dpe_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* bcoef, uint16_t* dx,
-                                uint16_t* dz_out, int64_t M, int C, hipStream_t st) {
+                                uint16_t* dz_out, int64_t M, int C, const float* mcoef, hipStream_t st) {
   const int64_t nch = M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(nch)), dim3(BN_T), 0, st, dy, y, x, bcoef, dx, dz_out, nch, C);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(nch)), dim3(BN_T), 0, st, dy, y, x, bcoef, dx, dz_out, nch, C,
+                     mcoef);
   return 0;
 }

@@ -3,6 +3,7 @@
 // from (seed, offset) -- no mask tensor), residual add, bias-grad column
 // sums, NCHW->NHWC input packing, embedding gather / scatter-add.
 #include "common.h"
+#include <algorithm>
 
 namespace dpe {
 
@@ -140,6 +141,45 @@ __global__ __launch_bounds__(ET) void colsum_kernel(const T* __restrict__ dy, in
   }
 }
 
+// Vectorised form (N % 8 == 0, ld % 8 == 0): a wave covers 512 columns with
+// 16-B loads, 4 waves x gridDim.y blocks split the rows; LDS reduce over the
+// waves, then one atomic per column per block.
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_vec_kernel(const T* __restrict__ dy, int64_t M, int N, int64_t ld,
+                                                         float* __restrict__ db, int accumulate) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c8 = blockIdx.x * 512 + lane * 8;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c8 < N) {
+    int64_t m = wid + 4 * (int64_t)blockIdx.y;
+    const int64_t step = 4 * (int64_t)gridDim.y;
+#pragma unroll 4
+    for (; m < M; m += step) {
+      float f[8];
+      if constexpr (sizeof(T) == 2) {
+        unpack8(*(const u32x4*)((const uint16_t*)dy + m * ld + c8), f);
+      } else {
+        const f32x4 a = *(const f32x4*)((const float*)dy + m * ld + c8), b = *(const f32x4*)((const float*)dy + m * ld + c8 + 4);
+        f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3]; f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += f[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[wid][lane * 8 + e] = s[e];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int col = blockIdx.x * 512 + i;
+    if (col < N) {
+      const float t = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+      if (gridDim.y == 1 && !accumulate) db[col] = t;
+      else atomicAdd(db + col, t);
+    }
+  }
+}
+
 // ------------------------------------------------------ input packing
 // x NCHW f32 -> y NHWC bf16 with channels padded to Cp (zeros)
 __global__ __launch_bounds__(ET) void nchw_to_nhwc_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, int N, int C,
@@ -231,6 +271,17 @@ extern "C" int dpe_add(const void* a, const void* b, void* out, int64_t n, float
   return 0;
 }
 extern "C" int dpe_colsum(const void* dy, int64_t M, int N, int64_t ld, float* db, int accumulate, int bf16, hipStream_t st) {
+  if (N % 8 == 0 && ld % 8 == 0) {
+    const int gx = (N + 511) / 512;
+    int64_t gy = std::max<int64_t>(1, std::min<int64_t>((M + 63) / 64, 1024 / gx));
+    if (!accumulate && gy > 1) hipMemsetAsync(db, 0, (size_t)N * sizeof(float), st);
+    const dim3 grid(gx, (unsigned)gy);
+    if (bf16)
+      hipLaunchKernelGGL((colsum_vec_kernel<uint16_t>), grid, dim3(256), 0, st, (const uint16_t*)dy, M, N, ld, db, accumulate);
+    else
+      hipLaunchKernelGGL((colsum_vec_kernel<float>), grid, dim3(256), 0, st, (const float*)dy, M, N, ld, db, accumulate);
+    return 0;
+  }
   int gy = (int)((M + 255) / 256);
   if (gy > 64) gy = 64;
   if (gy < 1) gy = 1;

@@ -23,6 +23,7 @@ enum Epi : int {
   EPI_BF16 = 0,        // C (bf16) = act(alpha*acc + bias) [+ residual]
   EPI_F32 = 1,         // C (f32)  = act(alpha*acc + bias)
   EPI_ATOMIC_F32 = 2,  // C (f32) += alpha*acc  (split-K / accumulate)
+  EPI_BF16_BNB = 3,    // EPI_BF16 + BatchNorm-backward partials of dL/dy in the epilogue (data-grad of a BN+ReLU input)
 };
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
 
@@ -47,7 +48,14 @@ struct IgemmArgs {
   const uint16_t* residual;  // bf16 [M][ldc] added in the EPI_BF16 epilogue (may alias C)
   const float* bias;         // [N] or nullptr
   const float* residual_f32; // f32 [M][ldc] added in the EPI_F32 epilogue (x + f(a) on an fp32 residual stream)
-  float* col_stats;          // [2][N][tilesM] per-(column, M-tile) (sum, sumsq) of the stored bf16 output, or nullptr
+  float* col_stats;          // [2][N][stats_ld] per-(column, M-tile) partial statistics of the stored bf16 output, or nullptr:
+                             //   EPI_BF16:      (sum v, sum v^2)                      (BatchNorm forward)
+                             //   EPI_BF16_BNB:  (sum dz, sum dz*(x - mean)),  dz = v * [x*scale+shift > 0],
+                             //                  x = st_x, [scale|shift|mean|invstd] = st_coef  (BN+ReLU backward)
+  const uint16_t* st_x;      // [M][ldc] bf16 pre-BN input (row indexing as C, incl. phase remap)  (EPI_BF16_BNB)
+  const float* st_coef;      // [4][N]                                                            (EPI_BF16_BNB)
+  int stats_ld;              // partial columns per channel (0 -> tilesM of this launch)
+  int stats_off;             // first partial column written by this launch (phase-decomposed dgrad)
   int M, N, K;
   int64_t lda, ldb, ldc;
   float alpha;

@@ -298,7 +298,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int CROW = BN * 2 + 16;
   constexpr int LDS_MAIN = 2 * STAGE;
-  constexpr int LDS_C = (EPI == EPI_BF16) ? (BM * CROW + 2 * 4 * BN * 4)
+  constexpr int LDS_C = (EPI == EPI_BF16 || EPI == EPI_BF16_BNB) ? (BM * CROW + 2 * 4 * BN * 4)
                         : (EPI == EPI_ATOMIC_F32 ? (BM / 2) * (BN + 4) * 4 : 0);
   constexpr int LDS = LDS_MAIN > LDS_C ? LDS_MAIN : LDS_C;
   constexpr int RM = BM / 32, RN = BN / 32;
@@ -442,6 +442,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
     }
     return;
   } else {
+    constexpr bool BNB = (EPI == EPI_BF16_BNB);
     // Stage bf16 tile in LDS (row stride CROW), then coalesced 16-B stores.
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
@@ -471,6 +472,16 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
     float s[8], ss[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
+    float bsc[8], bsh[8], bmu[8];  // BN forward coefficients of this thread's 8 columns (EPI_BF16_BNB)
+    if constexpr (BNB) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int ch = min(n + e, p.N - 1);
+        bsc[e] = p.st_coef[ch];
+        bsh[e] = p.st_coef[p.N + ch];
+        bmu[e] = p.st_coef[2 * p.N + ch];
+      }
+    }
     for (int rr = r0; rr < BM; rr += RPP) {
       const int m = m0 + rr;
       if (m >= p.M) break;
@@ -498,8 +509,24 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
       if (p.col_stats) {
         float f[8];
         unpack8(v, f);
+        if constexpr (BNB) {  // (sum dz, sum dz*(x - mean)), dz = f * relu'(x*scale + shift)
+          float xv[8];
+          if (vec) {
+            unpack8(ld16(p.st_x + orow * p.ldc + n), xv);
+          } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { s[e] += f[e]; ss[e] += f[e] * f[e]; }
+            for (int e = 0; e < 8; ++e) xv[e] = (n + e < p.N) ? bf2f(p.st_x[orow * p.ldc + n + e]) : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float dz = fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? f[e] : 0.f;
+            s[e] += dz;
+            ss[e] += dz * (xv[e] - bmu[e]);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { s[e] += f[e]; ss[e] += f[e] * f[e]; }
+        }
       }
       if (vec) {
         *(u32x4*)dst = v;
@@ -535,8 +562,9 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
         float a = 0.f, b = 0.f;
 #pragma unroll
         for (int w = 0; w < 4; ++w) { a += red[w * BN + tid]; b += red[4 * BN + w * BN + tid]; }
-        p.col_stats[(int64_t)(n0 + tid) * tilesM + tm] = a;
-        p.col_stats[(int64_t)(p.N + n0 + tid) * tilesM + tm] = b;
+        const int sld = p.stats_ld ? p.stats_ld : tilesM;
+        p.col_stats[(int64_t)(n0 + tid) * sld + p.stats_off + tm] = a;
+        p.col_stats[(int64_t)(p.N + n0 + tid) * sld + p.stats_off + tm] = b;
       }
     }
   }
@@ -580,6 +608,9 @@ extern "C" int dpe_igemm_launch(const IgemmArgs* args, int bm, int bn, int aload
   // conv
   DPE_CASE(A_CONV_FWD, B_DENSE_K, EPI_BF16)
   DPE_CASE(A_CONV_DGRAD, B_CONV_DGRAD, EPI_BF16)
+  // data-grad feeding a BN+ReLU backward (partials from the epilogue)
+  DPE_CASE(A_DENSE_K, B_DENSE_N, EPI_BF16_BNB)
+  DPE_CASE(A_CONV_DGRAD, B_CONV_DGRAD, EPI_BF16_BNB)
   DPE_CASE(A_DENSE_M, B_CONV_WGRAD, EPI_ATOMIC_F32)
 #undef DPE_CASE
   return -1;

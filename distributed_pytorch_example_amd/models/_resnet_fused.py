@@ -9,12 +9,18 @@ forward  (x NHWC bf16)
     h3 = conv3(a2) -> out = relu(BN3(h3) + idn)
 backward (dout)
     dh3, dz3 = BN3'(dout; out, h3)            dz3 = dout*relu'(out) is also d(idn)
-    dW3 += dh3 (x) a2 ;  da2 = dh3 . W3
-    dh2 = BN2'(da2; a2, h2) ; dW2 += dh2 (x) a1 ; da1 = dh2 . W2
-    dh1 = BN1'(da1; a1, h1) ; dW1 += dh1 (x) x
+    dW3 += dh3 (x) a2 ;  da2 = dh3 . W3       the dgrad epilogue also emits BN2's backward
+                                              sums (sum dz, sum dz*(h2-mean)), ReLU mask from h2
+    dh2 = BN2'(da2; h2)                       one elementwise pass: no separate reduce pass over da2
+    dW2 += dh2 (x) a1 ; da1 = dh2 . W2 (+ BN1 sums) ; dh1 = BN1'(da1; h1) ; dW1 += dh1 (x) x
     identity block:   dx = dh1 . W1 + dz3            (residual add fused in the dgrad epilogue)
     downsample block: dhd = BN_d'(dz3; hd); dW_d += dhd (x) x
                       dx = dh1 . W1 + dhd . W_d      (second dgrad accumulates the first)
+
+(A variant that also fused BN1/BN2 + ReLU into the consumer convs' load
+prologues, never materialising a1/a2, measured slower on MI355X: the
+transform sits on the loaders' critical path and the inner BN tensors carry
+only 1/4 of the block's channels -- so the outputs are materialised.)
 
 Weight gradients are accumulated straight into the DDP bucket views and each
 parameter is announced to the reducer as soon as its gradient is final, in
@@ -23,11 +29,16 @@ still in backward.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch.autograd import Function
 
 from ..ops._ext import ext
 from ..ops._state import grad_done, grad_sink, note_use, shadow
+
+# DPE_BN_EPI=0: inner BN backward through the standalone reduce kernel (A/B reference)
+_EPI_BNB = os.environ.get("DPE_BN_EPI", "1") != "0"
 
 
 def _conv_conf(conv):
@@ -40,26 +51,24 @@ class BottleneckFn(Function):
         C = ext()
         convs = [block.c1, block.c2, block.c3] + ([block.down] if block.down is not None else [])
         ws = [shadow(cb.conv.weight) for cb in convs]
-        coefs = []
 
         def convbn(i, inp, relu, residual=None):
             cb = convs[i]
             s, p, d = _conv_conf(cb.conv)
-            h, st = C.conv_fwd(inp, ws[i], s, p, d, True, None)   # BN stats partials from the epilogue
+            h, st = C.conv_fwd(inp, ws[i], s, p, d, True, None)  # BN stats partials from the epilogue
             bn = cb.bn
             y, coef = C.bn_fwd_train(h, bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var,
                                      bn.momentum, bn.eps, relu, residual, st)
-            coefs.append(coef)
-            return h, y
+            return h, y, coef
 
         if block.down is not None:
-            hd, idn = convbn(3, x, False)
+            hd, idn, cd = convbn(3, x, False)
         else:
-            hd, idn = None, x
-        h1, a1 = convbn(0, x, True)
-        h2, a2 = convbn(1, a1, True)
-        h3, out = convbn(2, a2, True, idn)
-        ctx.save_for_backward(x, h1, a1, h2, a2, h3, out, hd, *coefs)
+            hd, idn, cd = None, x, None
+        h1, a1, c1 = convbn(0, x, True)
+        h2, a2, c2 = convbn(1, a1, True)
+        h3, out, c3 = convbn(2, a2, True, idn)
+        ctx.save_for_backward(x, h1, a1, h2, a2, h3, out, hd, c1, c2, c3, cd)
         ctx.block = block
         ctx.convs = convs
         ctx.ws = ws
@@ -72,20 +81,28 @@ class BottleneckFn(Function):
     @staticmethod
     def backward(ctx, dout):
         C = ext()
-        x, h1, a1, h2, a2, h3, out, hd, *coefs = ctx.saved_tensors
+        x, h1, a1, h2, a2, h3, out, hd, c1, c2, c3, cd = ctx.saved_tensors
         convs, ws = ctx.convs, ctx.ws
         has_down = len(convs) == 4
         dout = dout.contiguous()
+        grads = {}
 
-        def bn_bwd(i, dy, y, h, want_dz):
+        def bn_sinks(i):
             bn = convs[i].bn
             gb, gd = grad_sink(bn.weight)
             bb, bd = grad_sink(bn.bias)
-            dh, dz = C.bn_bwd(dy, y, h, bn.weight.detach(), coefs[i], gb, bb, want_dz)
+            return bn, gb, gd, bb, bd
+
+        def bn_done(bn, gb, gd, bb, bd):
             grad_done(bn.weight, gd)
             grad_done(bn.bias, bd)
             grads[id(bn.weight)] = None if gd else gb
             grads[id(bn.bias)] = None if bd else bb
+
+        def bn_bwd(i, dy, y, h, coef, want_dz):
+            bn, gb, gd, bb, bd = bn_sinks(i)
+            dh, dz = C.bn_bwd(dy, y, h, bn.weight.detach(), coef, gb, bb, want_dz)
+            bn_done(bn, gb, gd, bb, bd)
             return dh, dz
 
         def wgrad(i, dy, inp):
@@ -100,30 +117,36 @@ class BottleneckFn(Function):
             s, p, d = _conv_conf(convs[i].conv)
             return C.conv_dgrad(dy, ws[i], shape, s, p, d, residual)
 
-        grads = {}
-        # coefs are in forward order: [down], c1, c2, c3
-        order = ([3] if has_down else []) + [0, 1, 2]
-        coefs = {order[k]: coefs[k] for k in range(len(order))}
+        def dgrad_bnb(i, dy, j, y, h, coef):
+            """dL/dy of conv i's input, then BN j's backward.  With the fused epilogue the
+            BN sums come out of the dgrad kernel and the ReLU mask is recomputed from h."""
+            if not _EPI_BNB:
+                da = dgrad(i, dy, list(h.shape))
+                return bn_bwd(j, da, y, h, coef, False)[0]
+            s, p, d = _conv_conf(convs[i].conv)
+            da, part = C.conv_dgrad_bn(dy, ws[i], list(h.shape), s, p, d, None, h, coef)
+            bn, gb, gd, bb, bd = bn_sinks(j)
+            dh = C.bn_bwd_partials(da, h, bn.weight.detach(), coef, part, gb, bb)
+            bn_done(bn, gb, gd, bb, bd)
+            return dh
 
-        dh3, dz3 = bn_bwd(2, dout, out, h3, True)
+        dh3, dz3 = bn_bwd(2, dout, out, h3, c3, True)
         wgrad(2, dh3, a2)
-        da2 = dgrad(2, dh3, list(a2.shape))
-        dh2, _ = bn_bwd(1, da2, a2, h2, False)
+        dh2 = dgrad_bnb(2, dh3, 1, a2, h2, c2)
         wgrad(1, dh2, a1)
-        da1 = dgrad(1, dh2, list(a1.shape))
-        dh1, _ = bn_bwd(0, da1, a1, h1, False)
+        dh1 = dgrad_bnb(1, dh2, 0, a1, h1, c1)
         wgrad(0, dh1, x)
         dx = None
         if ctx.needs_input_grad[0]:
             if has_down:
-                dhd, _ = bn_bwd(3, dz3, None, hd, False)
+                dhd, _ = bn_bwd(3, dz3, None, hd, cd, False)
                 wgrad(3, dhd, x)
                 dxd = dgrad(3, dhd, list(x.shape))
                 dx = dgrad(0, dh1, list(x.shape), dxd)
             else:
                 dx = dgrad(0, dh1, list(x.shape), dz3)
         elif has_down:
-            dhd, _ = bn_bwd(3, dz3, None, hd, False)
+            dhd, _ = bn_bwd(3, dz3, None, hd, cd, False)
             wgrad(3, dhd, x)
         pgrads = [grads.get(id(p)) for p in ctx.block._fused_params]
         return (dx, None, *pgrads)

@@ -261,29 +261,36 @@ def test_cast_act_dropout(C):
     assert torch.equal(y, y2)
 
 
-def test_colsum(C):
-    dy = bf(torch.randn(3000, 520, device=dev))
-    db = torch.zeros(520, device=dev)
-    C.colsum(dy, db, False)
+@pytest.mark.parametrize("M,N,dt", [(3000, 520, torch.bfloat16), (8192, 768, torch.float32), (8192, 3072, torch.bfloat16),
+                                    (100, 36, torch.float32), (7, 1000, torch.bfloat16)])
+def test_colsum(C, M, N, dt):
+    dy = torch.randn(M, N, device=dev).to(dt)
+    db = torch.full((N,), 7.0, device=dev)
+    C.colsum(dy, db, False)  # overwrite
     assert rel_err(db, dy.float().sum(0)) < 1e-4
+    C.colsum(dy, db, True)  # accumulate
+    assert rel_err(db, 2 * dy.float().sum(0)) < 1e-4
 
 
-def test_layernorm(C):
+@pytest.mark.parametrize("D", [768, 64, 1024, 2048, 4096])
+def test_layernorm(C, D):
     torch.manual_seed(11)
-    x = torch.randn(333, 768, device=dev) * 2 + 1
-    w, b = torch.rand(768, device=dev) + 0.5, torch.randn(768, device=dev)
+    x = torch.randn(333, D, device=dev) * 2 + 1
+    w, b = torch.rand(D, device=dev) + 0.5, torch.randn(D, device=dev)
     y, mean, rstd = C.layernorm_fwd(x, w, b, 1e-5)
     xf = x.clone().requires_grad_(True)
     wf, bfp = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
-    ref = F.layer_norm(xf, (768,), wf, bfp, 1e-5)
+    ref = F.layer_norm(xf, (D,), wf, bfp, 1e-5)
     assert rel_err(y, ref) < 1e-2
-    dy = bf(torch.randn(333, 768, device=dev))
+    if D > 2048:
+        return  # backward supports D <= 2048
+    dy = bf(torch.randn(333, D, device=dev))
     gx, gw, gb = torch.autograd.grad(ref, [xf, wf, bfp], dy.float())
-    dw, db = torch.zeros(768, device=dev), torch.zeros(768, device=dev)
+    dw, db = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
     dx = C.layernorm_bwd(dy, x, w, mean, rstd, dw, db, None)
     assert rel_err(dx, gx) < 1e-2 and rel_err(dw, gw) < 1e-3 and rel_err(db, gb) < 1e-3
-    acc = torch.ones(333, 768, device=dev)
-    C.layernorm_bwd(dy, x, w, mean, rstd, torch.zeros(768, device=dev), None, acc)
+    acc = torch.ones(333, D, device=dev)
+    C.layernorm_bwd(dy, x, w, mean, rstd, torch.zeros(D, device=dev), None, acc)
     assert rel_err(acc - 1, gx) < 1e-2
 
 
@@ -430,3 +437,44 @@ def test_gemm256_alpha_tensor(g256):
     dw = torch.zeros(N, K, device=dev)
     C.linear_wgrad(dy, x, dw, 2.0, s)
     assert rel_err(dw, 0.5 * (dy.float().t() @ x.float())) < 1e-3
+
+
+# ------------------------------------- BatchNorm backward fused into dgrad epilogues
+def _bn_coef(C_, Cc):
+    scale = torch.rand(Cc, device=dev) + 0.5
+    shift = torch.randn(Cc, device=dev) * 0.5
+    mean = torch.randn(Cc, device=dev) * 0.3
+    invstd = torch.rand(Cc, device=dev) + 0.5
+    return torch.stack([scale, shift, mean, invstd]).contiguous()
+
+
+def _bn_relu(h, coef):
+    return torch.relu(h.float() * coef[0] + coef[1]).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("N,H,W,Ci,Co,k,s,p", [(2, 14, 14, 64, 128, 3, 1, 1), (2, 14, 14, 64, 128, 3, 2, 1),
+                                               (4, 7, 7, 256, 64, 1, 1, 0), (2, 28, 28, 128, 128, 3, 2, 1)])
+def test_dgrad_bn_backward_partials(C, N, H, W, Ci, Co, k, s, p):
+    """dgrad epilogue partials + bn_bwd_partials == the standalone BN backward (mask from y)."""
+    torch.manual_seed(13)
+    h = bf(torch.randn(N, H, W, Ci, device=dev))  # pre-BN input of the BN+ReLU feeding this conv
+    coef = _bn_coef(C, Ci)
+    w = bf(torch.randn(Co, k, k, Ci, device=dev) / math.sqrt(k * k * Ci))
+    OH = (H + 2 * p - k) // s + 1
+    dy = bf(torch.randn(N, OH, OH, Co, device=dev))
+    da_ref = C.conv_dgrad(dy, w, [N, H, W, Ci], [s, s], [p, p], [1, 1], None)
+    da, part = C.conv_dgrad_bn(dy, w, [N, H, W, Ci], [s, s], [p, p], [1, 1], None, h, coef)
+    assert torch.equal(da, da_ref)
+    df = da.float().reshape(-1, Ci)
+    hf = h.float().reshape(-1, Ci)
+    dz = torch.where(hf * coef[0] + coef[1] > 0, df, torch.zeros_like(df))
+    tot = part.sum(-1)
+    assert rel_err(tot[0], dz.sum(0)) < 1e-3
+    assert rel_err(tot[1], (dz * (hf - coef[2])).sum(0)) < 1e-3
+    gamma = torch.rand(Ci, device=dev) + 0.5
+    dg1, db1 = torch.zeros(Ci, device=dev), torch.zeros(Ci, device=dev)
+    dh = C.bn_bwd_partials(da, h, gamma, coef, part, dg1, db1)
+    y = _bn_relu(h, coef)
+    dg2, db2 = torch.zeros(Ci, device=dev), torch.zeros(Ci, device=dev)
+    dh_ref, _ = C.bn_bwd(da, y, h, gamma, coef, dg2, db2, False)
+    assert rel_err(dh, dh_ref) < 2e-2 and rel_err(dg1, dg2) < 1e-3 and rel_err(db1, db2) < 1e-3
