@@ -12,6 +12,9 @@
 
 #include <stdexcept>
 
+extern "C" int dpe_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st);
+extern "C" int dpe_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
+
 namespace dpe {
 
 #define NCCL_CHECK(cmd)                                                                       \
@@ -162,9 +165,9 @@ void Communicator::abort() {
 
 // ------------------------------------------------------------------ Reducer
 Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params, int64_t nparams,
-                 std::shared_ptr<Communicator> comm, bool timing, bool force)
+                 std::shared_ptr<Communicator> comm, bool timing, bool force, bool comm_bf16, bool sync_debug)
     : buckets_(std::move(buckets)), bparams_(std::move(bucket_params)), comm_(std::move(comm)), timing_(timing),
-      force_(force) {
+      force_(force), comm_bf16_(comm_bf16), sync_debug_(sync_debug) {
   TORCH_CHECK(buckets_.size() == bparams_.size(), "bucket/param list size mismatch");
   param_bucket_.assign(nparams, -1);
   expected_.resize(buckets_.size());
@@ -188,6 +191,11 @@ Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_
     HIP_CHECK(hipEventCreateWithFlags(&ev_start_[b], flags));
     HIP_CHECK(hipEventCreateWithFlags(&ev_end_[b], flags));
     if (comm_) c10::hip::HIPCachingAllocator::recordStream(buckets_[b].storage().data_ptr(), comm_->comm_stream());
+    if (comm_bf16_) {
+      TORCH_CHECK(buckets_[b].scalar_type() == at::kFloat, "comm_bf16 needs fp32 buckets");
+      staging_.push_back(at::empty({buckets_[b].numel()}, buckets_[b].options().dtype(at::kBFloat16)));
+      if (comm_) c10::hip::HIPCachingAllocator::recordStream(staging_.back().storage().data_ptr(), comm_->comm_stream());
+    }
   }
   HIP_CHECK(hipEventCreateWithFlags(&ev_bwd_end_, flags));
   HIP_CHECK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
@@ -221,8 +229,20 @@ void Reducer::launch(int64_t b) {
   HIP_CHECK(hipStreamWaitEvent(cs, ev_ready_[b], 0));
   if (timing_) HIP_CHECK(hipEventRecord(ev_start_[b], cs));
   auto& t = buckets_[b];
-  comm_->all_reduce_raw(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), ncclAvg, cs);
+  if (comm_bf16_) {
+    auto& h = staging_[b];
+    TORCH_CHECK(dpe_cast_f32_bf16((const float*)t.data_ptr(), (uint16_t*)h.data_ptr(), t.numel(), cs) == 0, "bf16 cast");
+    comm_->all_reduce_raw(h.data_ptr(), h.numel(), ncclBfloat16, ncclAvg, cs);
+    TORCH_CHECK(dpe_cast_bf16_f32((const uint16_t*)h.data_ptr(), (float*)t.data_ptr(), t.numel(), cs) == 0, "f32 cast");
+  } else {
+    comm_->all_reduce_raw(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), ncclAvg, cs);
+  }
   if (timing_) HIP_CHECK(hipEventRecord(ev_end_[b], cs));
+  if (sync_debug_) {
+    HIP_CHECK(hipStreamSynchronize(cs));
+    const std::string err = comm_->async_error();
+    TORCH_CHECK(err.empty(), "RCCL error after bucket ", b, ": ", err);
+  }
 }
 
 void Reducer::mark_ready(int64_t p) {
@@ -290,9 +310,9 @@ void register_comm(pybind11::module& m) {
       .def("comm_stream_ptr", [](Communicator& c) { return (uint64_t)(uintptr_t)c.comm_stream().stream(); });
   py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
       .def(py::init<std::vector<at::Tensor>, std::vector<std::vector<int64_t>>, int64_t, std::shared_ptr<Communicator>, bool,
-                    bool>(),
+                    bool, bool, bool>(),
            py::arg("buckets"), py::arg("bucket_params"), py::arg("nparams"), py::arg("comm"), py::arg("timing") = false,
-           py::arg("force") = false)
+           py::arg("force") = false, py::arg("comm_bf16") = false, py::arg("sync_debug") = false)
       .def("launch_order", &Reducer::launch_order)
       .def("prepare", &Reducer::prepare)
       .def("mark_ready", &Reducer::mark_ready)

@@ -70,8 +70,13 @@ ncclRedOp_t to_nccl_op(const std::string& op);
 // for the last one (optimizer ordering).
 class Reducer {
  public:
+  // comm_bf16: all-reduce a bf16 copy of each fp32 bucket (cast -> ncclAvg in bf16 -> cast back, all on the
+  //   comm stream): half the xGMI bytes, the gradient-compression hook of SURVEY §2.2 I5 / B3.
+  // sync_debug: synchronise the comm stream after every bucket and raise on an RCCL async error (SURVEY §5.2
+  //   stream-ordering assertion mode).
   Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params, int64_t nparams,
-          std::shared_ptr<Communicator> comm, bool timing, bool force = false);
+          std::shared_ptr<Communicator> comm, bool timing, bool force = false, bool comm_bf16 = false,
+          bool sync_debug = false);
   ~Reducer();
   void prepare();
   void mark_ready(int64_t param);
@@ -93,6 +98,8 @@ class Reducer {
   std::shared_ptr<Communicator> comm_;
   bool timing_;
   bool force_;  // issue collectives even at world size 1 (exercises the comm path on a 1-GPU box)
+  bool comm_bf16_, sync_debug_;
+  std::vector<at::Tensor> staging_;  // bf16 copies of the buckets (comm_bf16)
   std::vector<int64_t> launch_order_;
   std::vector<hipEvent_t> ev_ready_, ev_start_, ev_end_;
   hipEvent_t ev_bwd_end_ = nullptr, ev_done_ = nullptr, ev_step_begin_ = nullptr;

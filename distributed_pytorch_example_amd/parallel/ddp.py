@@ -3,7 +3,9 @@
 API-compatible subset of ``torch.nn.parallel.DistributedDataParallel`` as the
 reference uses it (`train.py:12,233`: ``DDP(model)``, ``.module``, forward,
 implicit gradient averaging in backward) plus ``no_sync()``,
-``broadcast_buffers`` and bucket-size control.
+``broadcast_buffers``, bucket-size control, ``register_comm_hook`` and the
+one-time bucket rebuild from the observed gradient-ready order (SURVEY §2.2
+I4/I5).
 
 Design (MI355X-first, not a port of c10d::Reducer):
 
@@ -19,21 +21,34 @@ Design (MI355X-first, not a port of c10d::Reducer):
   stream behind an event recorded on the compute stream, so RCCL overlaps the
   rest of backward; averaging uses ``ncclAvg`` (no scale kernel).  Buckets are
   issued strictly in index order on every rank.  At the end of backward the
-  compute stream waits for the last bucket.
-* **gloo / CPU**: the same bucketing with async ``dist.all_reduce``.
+  compute stream waits for the last bucket.  ``gradient_compression="bf16"``
+  (or ``register_comm_hook(None, bf16_compress_hook)``) all-reduces bf16
+  copies cast on the comm stream.
+* **Bucket rebuild.**  Like c10d (`distributed.py:1201-1206`), the buckets
+  are rebuilt once, before the second forward, in the order gradients were
+  observed to become ready in the first backward -- rank 0's order is
+  broadcast so every rank builds identical buckets.
+* **Desync guard.**  ``debug=True`` (or ``DPE_DDP_DEBUG=1``) fingerprints the
+  bucket layout at every (re)build and compares it across ranks through the
+  control plane (fail fast instead of hanging in mismatched collectives), and
+  synchronises the comm stream after every bucket.
+* **gloo / CPU / custom hooks**: the same bucketing with a Python reducer.
 * **Init sync**: parameters and buffers are broadcast from rank 0 as one flat
   buffer per dtype (c10d's coalesced broadcast, C3).
 """
 from __future__ import annotations
 
 import contextlib
-from typing import List, Optional
+import hashlib
+import os
+from typing import Callable, List, Optional
 
 import torch
 import torch.distributed as dist
 import torch.nn as nn
 
 from . import dist as pdist
+from . import hooks as _hooks
 from .buckets import assign_buckets
 from ..utils.logging import get_logger
 
@@ -42,17 +57,25 @@ log = get_logger(__name__)
 _DEFAULT_FIRST_BUCKET_BYTES = 1024 * 1024
 
 
-class _GlooReducer:
-    """Python reducer for the gloo backend (CPU plumbing path)."""
+class _PyReducer:
+    """Python reducer: gloo backend, or any backend with a user comm hook.
 
-    def __init__(self, buckets: List[torch.Tensor], bucket_params: List[List[int]], nparams: int):
+    Buckets are handed to the hook (default: async all-reduce + average) in
+    index order as they complete; ``finalize`` waits for all of them."""
+
+    def __init__(self, buckets: List[torch.Tensor], bucket_params: List[List[int]], nparams: int, params,
+                 hook: Optional[Callable] = None, state=None, compression: Optional[str] = None):
         self.buckets = buckets
+        self.bucket_params = bucket_params
+        self.params = params
         self.bucket_of = {}
         for b, ps in enumerate(bucket_params):
             for p in ps:
                 self.bucket_of[p] = b
         self.expected = [len(ps) for ps in bucket_params]
         self.world = pdist.get_world_size()
+        self.hook, self.state, self.compression = hook, state, compression
+        self.order: List[int] = []
         self.prepare()
 
     def prepare(self):
@@ -62,10 +85,22 @@ class _GlooReducer:
         self.next = 0
         self.works = []
         self.open = True
+        self.order = []
 
     def _launch(self, b):
-        if self.world > 1:
-            self.works.append(dist.all_reduce(self.buckets[b], async_op=True))
+        self.order.append(b)
+        t = self.buckets[b]
+        if self.hook is not None:
+            gb = _hooks.GradBucket(b, t, [self.params[i] for i in self.bucket_params[b]], b == len(self.buckets) - 1)
+            self.works.append((b, self.hook(self.state, gb)))
+            return
+        if self.world == 1:
+            return
+        if self.compression == "bf16":
+            c = t.to(torch.bfloat16)
+            self.works.append((b, ("bf16", c, dist.all_reduce(c, async_op=True))))
+        else:
+            self.works.append((b, dist.all_reduce(t, async_op=True)))
 
     def mark_ready(self, i: int):
         if not self.open:
@@ -89,22 +124,37 @@ class _GlooReducer:
         while self.next < len(self.buckets):
             self._launch(self.next)
             self.next += 1
-        for w in self.works:
-            w.wait()
-        if self.world > 1:
-            for t in self.buckets:
+        for b, w in self.works:
+            t = self.buckets[b]
+            if self.hook is not None:
+                r = w.wait() if isinstance(w, torch.futures.Future) else w
+                if isinstance(r, (list, tuple)):
+                    r = r[0]
+                if isinstance(r, torch.Tensor) and r.data_ptr() != t.data_ptr():
+                    t.copy_(r)
+            elif isinstance(w, tuple):  # bf16 compressed
+                _, c, work = w
+                work.wait()
+                t.copy_(c.float().div_(self.world))
+            else:
+                w.wait()
                 t.div_(self.world)
         self.open = False
 
     def last_timings(self):
         return []
 
+    def launch_order(self):
+        return list(self.order)
+
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers: bool = True,
                  bucket_cap_mb: Optional[float] = 25.0, first_bucket_mb: float = 1.0,
                  find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
-                 init_sync: bool = True, timing: bool = False, comm=None, force_comm: bool = False):
+                 init_sync: bool = True, timing: bool = False, comm=None, force_comm: bool = False,
+                 gradient_compression: Optional[str] = None, rebuild_buckets: bool = True,
+                 debug: Optional[bool] = None):
         super().__init__()
         self.module = module
         self.broadcast_buffers = broadcast_buffers
@@ -119,9 +169,20 @@ class DistributedDataParallel(nn.Module):
         self._comm = comm if comm is not None else pdist.comm()
         self._force = force_comm
         self._timing = timing
+        if gradient_compression not in (None, "none", "bf16"):
+            raise ValueError(f"gradient_compression must be None or 'bf16', got {gradient_compression!r}")
+        self._compression = None if gradient_compression in (None, "none") else gradient_compression
+        self._hook, self._hook_state = None, None
+        self._debug = (os.environ.get("DPE_DDP_DEBUG", "0") == "1") if debug is None else debug
+        # one-time rebuild from the observed ready order (c10d: after iteration 0)
+        self._rebuild_pending = False
+        self._rebuild_enabled = rebuild_buckets
+        self._record_order = rebuild_buckets
+        self._ready_order: List[int] = []
+        self.bucket_rebuilds = 0
         if init_sync and self.world_size > 1:
             self._sync_module_states()
-        self._build_buckets()
+        self._build_buckets(None)
         self._queued = False
         self._hooks = []
         for p in self._params:
@@ -146,41 +207,80 @@ class DistributedDataParallel(nn.Module):
                 t.copy_(flat[off: off + n].view_as(t))
                 off += n
 
-    def _build_buckets(self):
+    @torch.no_grad()
+    def _build_buckets(self, order: Optional[List[int]]):
+        n = len(self._params)
+        if order is None:
+            order = list(range(n))[::-1]
         sizes = [p.numel() * 4 for p in self._params]  # fp32 grads
-        order = list(range(len(self._params)))[::-1]
         keys = [(str(p.device),) for p in self._params]
+        old = None
+        if getattr(self, "buckets", None) is not None:
+            old = [p.grad.detach().clone() if p.grad is not None else None for p in self._params]
         self.bucket_indices = assign_buckets(sizes, order, self.bucket_cap_bytes, self.first_bucket_bytes, keys)
         self.buckets: List[torch.Tensor] = []
         self._views = {}
         for bidx in self.bucket_indices:
-            n = sum(self._params[i].numel() for i in bidx)
+            total = sum(self._params[i].numel() for i in bidx)
             dev = self._params[bidx[0]].device
-            buf = torch.zeros(n, dtype=torch.float32, device=dev)
+            buf = torch.zeros(total, dtype=torch.float32, device=dev)
             off = 0
             for i in bidx:
                 p = self._params[i]
                 self._views[i] = buf[off: off + p.numel()].view_as(p)
                 off += p.numel()
             self.buckets.append(buf)
-        self._attach_grads(zero=True)
-        if self._comm is not None and self._params and self._params[0].is_cuda:
+        for i, p in enumerate(self._params):
+            p.grad = self._views[i]
+            if old is not None and old[i] is not None:
+                self._views[i].copy_(old[i])
+        self._make_reducer()
+        if self._debug:
+            self._check_layout()
+
+    def _make_reducer(self):
+        native_ok = self._comm is not None and self._params and self._params[0].is_cuda and self._hook is None
+        if native_ok:
             from ..ops._ext import ext
 
             self.reducer = ext().Reducer(self.buckets, self.bucket_indices, len(self._params), self._comm, self._timing,
-                                         self._force)
+                                         self._force, self._compression == "bf16", self._debug)
             self._native = True
         else:
-            self.reducer = _GlooReducer(self.buckets, self.bucket_indices, len(self._params))
+            self.reducer = _PyReducer(self.buckets, self.bucket_indices, len(self._params), self._params, self._hook,
+                                      self._hook_state, self._compression)
             self._native = False
+
+    def layout_fingerprint(self) -> str:
+        h = hashlib.sha1()
+        for bidx, buf in zip(self.bucket_indices, self.buckets):
+            h.update(repr((tuple(bidx), buf.numel(), str(buf.dtype))).encode())
+        return h.hexdigest()
+
+    def _check_layout(self):
+        """Fail fast on a cross-rank bucket-layout mismatch (would otherwise hang in RCCL)."""
+        if self.world_size == 1 or not dist.is_initialized():
+            return
+        mine = self.layout_fingerprint()
+        allfp = [None] * self.world_size
+        dist.all_gather_object(allfp, mine)
+        if len(set(allfp)) != 1:
+            raise RuntimeError(f"DDP bucket layout differs across ranks: {allfp}")
+
+    def register_comm_hook(self, state, hook: Callable):
+        """torch DDP API.  Built-in hooks run on the native reducer; custom ones on the Python reducer."""
+        if hook in _hooks.BUILTIN:
+            self._compression = _hooks.BUILTIN[hook]
+            self._hook, self._hook_state = None, None
+        else:
+            self._hook, self._hook_state = hook, state
+        self._make_reducer()
 
     def enable_timing(self, on: bool = True):
         """Per-bucket comm timing (HIP events) for the overlap / bucket-size sweep."""
+        self._timing = on
         if self._native:
-            from ..ops._ext import ext
-
-            self._timing = on
-            self.reducer = ext().Reducer(self.buckets, self.bucket_indices, len(self._params), self._comm, on, self._force)
+            self._make_reducer()
 
     def bucket_timings(self):
         return self.reducer.last_timings()
@@ -208,6 +308,8 @@ class DistributedDataParallel(nn.Module):
         i = self._index.get(id(p))
         if i is None:
             return
+        if self._record_order:
+            self._ready_order.append(i)
         if not self._queued:
             self._queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
@@ -216,6 +318,9 @@ class DistributedDataParallel(nn.Module):
     def _finalize(self):
         self._queued = False
         self.reducer.finalize()
+        if self._record_order:
+            self._record_order = False
+            self._rebuild_pending = self._rebuild_enabled
 
     def finish_gradient_sync(self):
         """Explicit end-of-backward hook (also queued automatically)."""
@@ -223,8 +328,27 @@ class DistributedDataParallel(nn.Module):
             self.reducer.finalize()
             self._queued = False
 
+    def _rebuild_from_observed_order(self):
+        seen = set()
+        order = []
+        for i in self._ready_order:
+            if i not in seen:
+                seen.add(i)
+                order.append(i)
+        order += [i for i in range(len(self._params))[::-1] if i not in seen]  # unused params last
+        if self.world_size > 1 and dist.is_initialized():
+            box = [order]
+            dist.broadcast_object_list(box, src=0)  # identical buckets on every rank (C5)
+            order = box[0]
+        if order != list(range(len(self._params)))[::-1] or self.bucket_rebuilds == 0:
+            self._build_buckets(order)
+        self.bucket_rebuilds += 1
+        self._rebuild_pending = False
+
     def forward(self, *args, **kwargs):
         if torch.is_grad_enabled():
+            if self._rebuild_pending and self.require_backward_grad_sync:
+                self._rebuild_from_observed_order()
             self._attach_grads(zero=False)
             for p in self._params:
                 p._dpe_uses = 0

@@ -139,6 +139,58 @@ def check_health() -> str:
     return c.async_error() if c is not None else ""
 
 
+class Watchdog:
+    """Failure detector: a daemon thread that polls the RCCL
+    communicator's async error (``ncclCommGetAsyncError``) and a heartbeat the
+    training loop refreshes every step.  On an RCCL error, or no heartbeat for
+    ``timeout_s`` (a peer died mid-collective, a hang), it logs, aborts the
+    communicator (``ncclCommAbort`` releases ranks blocked in collectives) and
+    exits the process non-zero so the launcher's fail-fast path tears the job
+    down -- instead of the reference's 30-minute gloo timeout."""
+
+    def __init__(self, timeout_s: float = 600.0, interval_s: float = 2.0, on_fail=None):
+        import threading
+        import time
+
+        self.timeout_s, self.interval_s = timeout_s, interval_s
+        self._time = time
+        self._last = time.monotonic()
+        self._stop = threading.Event()
+        self._on_fail = on_fail
+        self.failure: Optional[str] = None
+        self._thread = threading.Thread(target=self._run, name="dpe-watchdog", daemon=True)
+        self._thread.start()
+
+    def beat(self) -> None:
+        self._last = self._time.monotonic()
+
+    def stop(self) -> None:
+        self._stop.set()
+        self._thread.join(timeout=5)
+
+    def _run(self):
+        while not self._stop.wait(self.interval_s):
+            err = check_health()
+            stalled = self._time.monotonic() - self._last
+            if err or stalled > self.timeout_s:
+                self.failure = f"RCCL async error: {err}" if err else f"no progress for {stalled:.0f}s"
+                log.error(f"watchdog: {self.failure}; aborting communicator")
+                c = _state["comm"]
+                if c is not None:
+                    try:
+                        c.abort()
+                    except Exception:  # noqa: BLE001
+                        pass
+                if self._on_fail is not None:
+                    self._on_fail(self.failure)
+                    return
+                os._exit(1)
+
+
+def start_watchdog(timeout_s: float = 600.0, interval_s: float = 2.0, on_fail=None) -> Watchdog:
+    return Watchdog(timeout_s, interval_s, on_fail)
+
+
 def destroy_process_group() -> None:
     if _state["comm"] is not None:
         torch.cuda.synchronize()

@@ -30,7 +30,7 @@ from .parallel import dist as pdist
 from .utils.checkpoint import load_checkpoint, resume_exists, save_checkpoint, wait_pending
 from .utils.env import ensure_single_process_env
 from .utils.logging import get_logger
-from .utils import fault
+from .utils import fault, tracing
 
 logger = get_logger("__main__")
 
@@ -59,6 +59,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--async-checkpoint", action="store_true")
     p.add_argument("--auto-resume", action="store_true", help="resume from <checkpoint-dir>/latest_model.pt if present")
     p.add_argument("--profile", type=str, default=None, help="write a torch.profiler chrome trace to this path")
+    p.add_argument("--roctx", action="store_true", help="roctx ranges (forward/backward/optimizer) for rocprofv3")
+    p.add_argument("--gradient-compression", default="none", choices=["none", "bf16"],
+                   help="all-reduce bf16 copies of the fp32 gradient buckets")
+    p.add_argument("--ddp-debug", action="store_true", help="cross-rank bucket-layout check + per-bucket stream sync")
+    p.add_argument("--watchdog-timeout", type=float, default=0.0,
+                   help="abort the job when no training step completes for this many seconds or RCCL reports an "
+                        "async error (0 = off)")
     return p
 
 
@@ -79,7 +86,7 @@ def _datasets(args, device):
     return tr, va, vocab
 
 
-def train_epoch(model, loader, optimizer, criterion, device, epoch, rank, grad_accum=1, max_steps=None):
+def train_epoch(model, loader, optimizer, criterion, device, epoch, rank, grad_accum=1, max_steps=None, watchdog=None):
     """Reference `train_epoch` (`train.py:119-151`); loss accumulated on device."""
     model.train()
     total_loss = torch.zeros((), dtype=torch.float64, device=device)
@@ -93,12 +100,17 @@ def train_epoch(model, loader, optimizer, criterion, device, epoch, rank, grad_a
         sync = (batch_idx + 1) % grad_accum == 0 or batch_idx + 1 == nb
         ctx = model.no_sync() if (not sync and hasattr(model, "no_sync")) else _null()
         with ctx:
-            output = model(data)
-            loss = criterion(output, target)
-            (loss / grad_accum if grad_accum > 1 else loss).backward()
+            with tracing.range("forward"):
+                output = model(data)
+                loss = criterion(output, target)
+            with tracing.range("backward"):
+                (loss / grad_accum if grad_accum > 1 else loss).backward()
         if sync:
-            optimizer.step()
-            optimizer.zero_grad()
+            with tracing.range("optimizer"):
+                optimizer.step()
+                optimizer.zero_grad()
+        if watchdog is not None:
+            watchdog.beat()
         total_loss += loss.detach()
         num_batches += 1
         if batch_idx % 10 == 0 and rank == 0:
@@ -139,7 +151,12 @@ def main(argv=None):
     logger.info(f"Configuration: epochs={args.epochs}, batch_size={args.batch_size}, lr={args.lr}")
 
     model = get_model(args.model).to(device)
-    model = DDP(model, bucket_cap_mb=args.bucket_mb)
+    model = DDP(model, bucket_cap_mb=args.bucket_mb,
+                gradient_compression=None if args.gradient_compression == "none" else args.gradient_compression,
+                debug=args.ddp_debug or None)
+    if args.roctx:
+        tracing.enable(True)
+    watchdog = pdist.start_watchdog(args.watchdog_timeout) if args.watchdog_timeout > 0 else None
     logger.info(f"Model parameters: {sum(p.numel() for p in model.parameters()):,}")
 
     train_dataset, val_dataset, num_classes = _datasets(args, device)
@@ -174,7 +191,7 @@ def main(argv=None):
         epoch_start = time.time()
         train_sampler.set_epoch(epoch)
         train_loss = train_epoch(model, train_loader, optimizer, criterion, device, epoch, rank, args.grad_accum,
-                                 args.max_steps)
+                                 args.max_steps, watchdog)
         val_loss, val_accuracy = validate(model, val_loader, criterion, device, num_classes, args.max_steps)
 
         metrics = torch.tensor([train_loss, val_loss, val_accuracy], device=device)
@@ -200,6 +217,8 @@ def main(argv=None):
         pdist.barrier()
 
     wait_pending()
+    if watchdog is not None:
+        watchdog.stop()
     total_time = time.time() - start_time
     if prof is not None:
         prof.__exit__(None, None, None)

@@ -64,6 +64,7 @@ def test_reducer_order_and_grads(C, comm):
         p.grad = None
     Fx.cross_entropy(ddp(x), y).backward()
     torch.cuda.synchronize()
+    assert ddp.bucket_rebuilds == 1  # rebuilt from the observed ready order before this step
     assert ddp.reducer.launch_order() == list(range(ddp.num_buckets()))
 
 
@@ -83,3 +84,24 @@ def test_ddp_no_sync_world1(C, comm):
     Fx.cross_entropy(ddp(x), y).backward()
     for a, p in zip(g1, m.parameters()):
         assert torch.allclose(p.grad, 2 * a, rtol=2e-2, atol=1e-4)
+
+
+def test_reducer_bf16_compression_and_sync_debug(C, comm):
+    """Native reducer: bf16 all-reduce of fp32 buckets (cast on the comm stream) and the
+    per-bucket stream-sync debug mode; grads match the uncompressed ones to bf16 precision."""
+    from distributed_pytorch_example_amd.models import resnet18_like
+    from distributed_pytorch_example_amd.ops import functional as Fx
+    from distributed_pytorch_example_amd.parallel import DDP
+
+    torch.manual_seed(3)
+    m1 = resnet18_like(num_classes=10).to(dev)
+    m2 = copy.deepcopy(m1)
+    ddp = DDP(m2, comm=comm, force_comm=True, bucket_cap_mb=2, gradient_compression="bf16", debug=True)
+    x = torch.randn(8, 3, 32, 32, device=dev)
+    y = torch.randint(0, 10, (8,), device=dev)
+    Fx.cross_entropy(m1(x), y).backward()
+    Fx.cross_entropy(ddp(x), y).backward()
+    torch.cuda.synchronize()
+    assert comm.async_error() == ""
+    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert ((a.grad - b.grad).norm() / (a.grad.norm() + 1e-12)).item() < 3e-2, n

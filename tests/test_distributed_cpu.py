@@ -169,3 +169,117 @@ def test_fault_injection_exception_recorded(tmp_path):
                 env={"DPE_FAULT_INJECT": "0:0:2:raise"}, timeout=120)
     assert r.returncode == 1
     assert "injected fault at rank 0" in r.stderr
+
+
+class _TwoPath(torch.nn.Module):
+    """Gradients become ready in an order unlike reverse registration order:
+    `late` is registered last but used first in forward, so it is ready last."""
+
+    def __init__(self):
+        super().__init__()
+        self.b = torch.nn.Linear(16, 4)
+        self.a = torch.nn.Linear(16, 16)
+        self.late = torch.nn.Linear(16, 16)
+
+    def forward(self, x):
+        return self.b(torch.relu(self.a(torch.relu(self.late(x)))))
+
+
+def _w_rebuild_and_hooks(rank, world, port, q):
+    _setup(rank, world, port)
+    import torch.distributed as dist
+
+    from distributed_pytorch_example_amd.parallel import DDP, hooks
+
+    def local_avg(m, x, y):
+        g = torch.autograd.grad(torch.nn.functional.cross_entropy(m(x), y), list(m.parameters()))
+        out = []
+        for t in g:
+            t = t.clone()
+            dist.all_reduce(t)
+            out.append(t / world)
+        return out
+
+    torch.manual_seed(0)
+    m = _TwoPath()
+    ddp = DDP(m, bucket_cap_mb=0.0005, first_bucket_mb=0.0005, debug=True)  # ~1 param per bucket
+    n0 = ddp.num_buckets()
+    order0 = [list(b) for b in ddp.bucket_indices]
+    for step in range(3):
+        torch.manual_seed(10 * step + rank)
+        x, y = torch.randn(8, 16), torch.randint(0, 4, (8,))
+        ref = local_avg(m, x, y)
+        for p in m.parameters():
+            p.grad = None
+        torch.nn.functional.cross_entropy(ddp(x), y).backward()
+        for r, p in zip(ref, m.parameters()):
+            assert torch.allclose(p.grad, r, atol=1e-6)
+    # rebuilt once, from the observed ready order (late.* last), identically on all ranks
+    assert ddp.bucket_rebuilds == 1, ddp.bucket_rebuilds
+    assert [list(b) for b in ddp.bucket_indices] != order0
+    fps = [None] * world
+    dist.all_gather_object(fps, ddp.layout_fingerprint())
+    assert len(set(fps)) == 1
+    # gradient compression (bf16 all-reduce) and a custom hook
+    ddp.register_comm_hook(None, hooks.bf16_compress_hook)
+    x, y = torch.randn(8, 16), torch.randint(0, 4, (8,))
+    ref = local_avg(m, x, y)
+    for p in m.parameters():
+        p.grad = None
+    torch.nn.functional.cross_entropy(ddp(x), y).backward()
+    for r, p in zip(ref, m.parameters()):
+        assert torch.allclose(p.grad, r, atol=2e-2, rtol=2e-2)
+    calls = []
+
+    def scaled_hook(state, bucket):
+        calls.append(bucket.index())
+        t = bucket.buffer()
+        dist.all_reduce(t)
+        t.mul_(state["scale"] / world)
+        fut = torch.futures.Future()
+        fut.set_result(t)
+        return fut
+
+    ddp.register_comm_hook({"scale": 2.0}, scaled_hook)
+    ref = local_avg(m, x, y)
+    for p in m.parameters():
+        p.grad = None
+    torch.nn.functional.cross_entropy(ddp(x), y).backward()
+    assert calls == list(range(ddp.num_buckets()))
+    for r, p in zip(ref, m.parameters()):
+        assert torch.allclose(p.grad, 2.0 * r, atol=1e-6)
+    q.put(("ok", rank))
+    dist.destroy_process_group()
+
+
+def test_ddp_bucket_rebuild_and_comm_hooks():
+    _spawn(_w_rebuild_and_hooks, 2)
+
+
+def _w_layout_mismatch(rank, world, port, q):
+    _setup(rank, world, port)
+    import torch.distributed as dist
+
+    from distributed_pytorch_example_amd.models import SimpleNet
+    from distributed_pytorch_example_amd.parallel import DDP
+
+    try:
+        DDP(SimpleNet(), bucket_cap_mb=0.1 if rank == 0 else 25.0, debug=True)
+        q.put(("no-error", rank))
+    except RuntimeError as e:
+        q.put(("ok" if "layout differs" in str(e) else f"wrong: {e}", rank))
+    dist.destroy_process_group()
+
+
+def test_ddp_debug_detects_bucket_layout_mismatch():
+    _spawn(_w_layout_mismatch, 2)
+
+
+def test_train_runtime_options(tmp_path):
+    """Additive runtime flags on the reference CLI: bf16 gradient compression,
+    DDP desync guard, watchdog heartbeat, roctx ranges, grad accumulation."""
+    r = _launch(["--epochs", "1", "--num-samples", "512", "--checkpoint-dir", str(tmp_path), "--backend", "gloo",
+                 "--gradient-compression", "bf16", "--ddp-debug", "--watchdog-timeout", "120", "--roctx",
+                 "--grad-accum", "2"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Epoch 0 completed" in (r.stdout + r.stderr)
