@@ -17,8 +17,11 @@
 //   key-on-the-lane: S = Q.K^T and dP = dO.V^T have the key on the lane, so
 //   their accumulators ARE the B operands of dV^T += dO^T.P and
 //   dK^T += Q^T.dS (permuted-k trick again, Q/dO read transposed from LDS).
-//   dS crosses LDS once for dQ = dS.K, summed over key tiles with fp32 atomics
-//   shaped as full 256-B rows.  D = rowsum(dO*O) is precomputed.
+//   dS crosses LDS once (as a [key][q] image written with 8-B stores, read
+//   transposed) for dQ = dS.K, summed over key tiles with fp32 atomics shaped
+//   as full 256-B rows.  The next query tile's Q/dO/lse/delta are prefetched
+//   into registers during the current tile's MFMAs; two barriers per tile.
+//   D = rowsum(dO*O) is precomputed.
 #include "common.h"
 
 namespace dpe {
@@ -224,19 +227,20 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
                                                        const float* __restrict__ lse2, const float* __restrict__ delta,
                                                        float* __restrict__ dq_acc, uint16_t* __restrict__ dqkv, int B,
                                                        int T, int H, float sl2, float scale) {
-  // LDS: Qk (8K) Qmn (8K) dOk (8K) dOmn (8K) Kmn (8K) dS (8K) lse/delta (512 B); dQ staging reuses Qk+Qmn (16K)
-  __shared__ __attribute__((aligned(16))) char smem[6 * 8192 + 512];
+  // LDS: Qk Qm dOk dOm Km dS^T (8 KB each) | dQ staging (16 KB) | lse, delta (512 B)
+  __shared__ __attribute__((aligned(16))) char smem[6 * 8192 + 16384 + 512];
   char* Qk = smem;
   char* Qm = smem + 8192;
   char* Ok = smem + 2 * 8192;
   char* Om = smem + 3 * 8192;
   char* Km = smem + 4 * 8192;
-  char* dS = smem + 5 * 8192;
-  float* sl = (float*)(smem + 6 * 8192);
+  char* dSt = smem + 5 * 8192;
+  float* stg = (float*)(smem + 6 * 8192);
+  float* sl = (float*)(smem + 6 * 8192 + 16384);
   float* sd = sl + 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
   const int nk = T / AKV, BH = B * H;
-  const int kt = (int)(blockIdx.x / BH);  // key tile (light-first order would be kt = nk-1-...)
+  const int kt = (int)(blockIdx.x / BH);  // heaviest key tiles (most query tiles) first
   const int bh = blockIdx.x % BH, b = bh / H, h = bh % H;
   const int64_t RS = 3LL * H * AD;
   const uint16_t* qb = qkv + (int64_t)b * T * RS + (int64_t)h * AD;
@@ -259,25 +263,40 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
     const int c = tid + 256 * i, key = c >> 3, dc = c & 7;
     *(u32x4*)(Km + mnimg(key, dc)) = *(const u32x4*)(kb + (int64_t)(kt * AKV + key) * RS + dc * 8);
   }
-  f32x4 dk[4], dv[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
-
-  for (int qt = kt; qt < nk; ++qt) {
-    __syncthreads();  // previous iteration's readers are done with Q/dO/dS/staging
+  // Q / dO / lse / delta of a query tile: global -> registers (prefetched one tile ahead) -> LDS
+  u32x4 qv[2], ov[2];
+  float lv = 0.f;
+  auto fetch = [&](int qt) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = tid + 256 * i, q = c >> 3, dc = c & 7;
-      const u32x4 qv = *(const u32x4*)(qb + (int64_t)(qt * AQ + q) * RS + dc * 8);
-      const u32x4 ov = *(const u32x4*)(ob + (int64_t)(qt * AQ + q) * ORS + dc * 8);
-      *(u32x4*)(Qk + (dc >> 2) * 4096 + kimg(q, dc & 3)) = qv;
-      *(u32x4*)(Qm + pimg(q, dc)) = qv;
-      *(u32x4*)(Ok + (dc >> 2) * 4096 + kimg(q, dc & 3)) = ov;
-      *(u32x4*)(Om + pimg(q, dc)) = ov;
+      qv[i] = *(const u32x4*)(qb + (int64_t)(qt * AQ + q) * RS + dc * 8);
+      ov[i] = *(const u32x4*)(ob + (int64_t)(qt * AQ + q) * ORS + dc * 8);
     }
-    if (tid < 64) sl[tid] = lse2[(int64_t)bh * T + qt * AQ + tid];
-    else if (tid < 128) sd[tid - 64] = delta[(int64_t)bh * T + qt * AQ + tid - 64];
-    __syncthreads();
+    if (tid < 64) lv = lse2[(int64_t)bh * T + qt * AQ + tid];
+    else if (tid < 128) lv = delta[(int64_t)bh * T + qt * AQ + tid - 64];
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, q = c >> 3, dc = c & 7;
+      *(u32x4*)(Qk + (dc >> 2) * 4096 + kimg(q, dc & 3)) = qv[i];
+      *(u32x4*)(Qm + pimg(q, dc)) = qv[i];
+      *(u32x4*)(Ok + (dc >> 2) * 4096 + kimg(q, dc & 3)) = ov[i];
+      *(u32x4*)(Om + pimg(q, dc)) = ov[i];
+    }
+    if (tid < 128) sl[tid] = lv;  // sl[0..63] = lse, sd = sl + 64: delta
+  };
+  fetch(kt);
+  stash();
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
+  __syncthreads();
+
+  for (int qt = kt; qt < nk; ++qt) {
+    const bool more = qt + 1 < nk;
+    if (more) fetch(qt + 1);  // in flight during this tile's MFMAs
     // S[q][key], dP[q][key]: lane = key, rows q = 16mt + 4g + e
     f32x4 ps[4], dp[4];
 #pragma unroll
@@ -310,32 +329,31 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
       dk[d] = MFMA(trfrag<true>(Qm, 0, 16 * d), s0, dk[d]);
       dk[d] = MFMA(trfrag<true>(Qm, 32, 16 * d), s1, dk[d]);
     }
-    // dS -> LDS as [q][key] K-contiguous image (rows q, key halves) for dQ = dS . K
+    // dS^T -> LDS as a [key][q] image: each lane owns 4 consecutive q of its key -> 8-B stores
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int ql = 16 * mt + 4 * g + e, kl = 16 * w + li;
-        char* a = dS + (kl >> 5) * 4096 + kimg(ql, (kl & 31) >> 3) + (kl & 7) * 2;
-        *(uint16_t*)a = f2bf(dp[mt][e]);
-      }
-    __syncthreads();
-    // dQ tile rows 16w..16w+15 : D[q][d] (lane = d, rows q = 4g + e)
+    for (int mt = 0; mt < 4; ++mt) {
+      u32x2 pk;
+      pk[0] = pack_bf2(dp[mt][0], dp[mt][1]);
+      pk[1] = pack_bf2(dp[mt][2], dp[mt][3]);
+      *(u32x2*)(dSt + mnimg(16 * w + li, 2 * mt + (g >> 1)) + (g & 1) * 8) = pk;
+    }
+    __syncthreads();  // dS^T complete; every wave is done with this tile's Q/dO/lse/delta
+    if (more) stash();
+    // dQ tile rows 16w..16w+15 : D[q][d] (lane = d, rows q = 4g + e);  A = dS (read transposed from dS^T)
     f32x4 dqa[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       dqa[d] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) dqa[d] = MFMA(kfrag64(dS + kk * 4096, 16 * w), trfrag<false>(Km, 32 * kk, 16 * d), dqa[d]);
+      for (int kk = 0; kk < 2; ++kk)
+        dqa[d] = MFMA(trfrag<false>(dSt, 32 * kk, 16 * w), trfrag<false>(Km, 32 * kk, 16 * d), dqa[d]);
     }
-    // stage (Qk+Qm region, 64x64 fp32 = 16 KB) and add whole 256-B rows atomically
-    __syncthreads();
-    float* stg = (float*)smem;
 #pragma unroll
     for (int d = 0; d < 4; ++d)
 #pragma unroll
       for (int e = 0; e < 4; ++e) stg[(16 * w + 4 * g + e) * 64 + 16 * d + li] = dqa[d][e] * scale;
-    __syncthreads();
+    __syncthreads();  // staging complete; next tile's Q/dO images complete
+    // add whole 256-B rows atomically (full-rate atomic shape)
     for (int r = w; r < 64; r += 4) {
       float* dst = dq_acc + ((int64_t)(b * T + qt * AQ + r) * H + h) * AD;
       atomicAdd(dst + lane, stg[r * 64 + lane]);
