@@ -55,8 +55,8 @@ int dpe_optim_step(int kind, const void* desc, const void* chunks, int nchunks, 
 int dpe_layernorm_fwd(const void* x, int x_bf16, const float* w, const float* b, uint16_t* y, float* mean, float* rstd,
                       int64_t rows, int D, float eps, hipStream_t st);
 int dpe_layernorm_bwd(const uint16_t* dy, const void* x, int x_bf16, const float* w, const float* mean, const float* rstd,
-                      void* dx, int dx_accumulate_f32, float* dw, float* db, float* part, int64_t rows, int D,
-                      hipStream_t st);
+                      void* dx, int dx_accumulate_f32, const float* res_in, uint16_t* dx_bf16, float* dw, float* db,
+                      float* part, int64_t rows, int D, hipStream_t st);
 int dpe_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int T, int H, int D, float scale, int causal,
                  hipStream_t st);
 int dpe_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
@@ -864,9 +864,29 @@ Tensor layernorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const T
   }
   const int nb = (int)std::min<int64_t>(512, (rows + 31) / 32);
   Tensor part = at::empty({nb, 2, D}, x.options().dtype(at::kFloat));
-  CHECK_RC(dpe_layernorm_bwd(bp(dy), x.data_ptr(), xb, fp(w), fp(mean), fp(rstd), dx.data_ptr(), acc ? 1 : 0, fp(dw),
-                             fpom(db), fp(part), rows, (int)D, cur_stream()), "layernorm_bwd");
+  CHECK_RC(dpe_layernorm_bwd(bp(dy), x.data_ptr(), xb, fp(w), fp(mean), fp(rstd), dx.data_ptr(), acc ? 1 : 0, nullptr,
+                             nullptr, fp(dw), fpom(db), fp(part), rows, (int)D, cur_stream()), "layernorm_bwd");
   return dx;
+}
+
+// Residual-stream form (pre-LN transformer block): dx = res_in + dLN(dy) in fp32 (a new tensor,
+// res_in untouched) plus its bf16 copy for the next data/weight-grad GEMMs -- one pass instead of
+// LN-bwd + add + cast.
+std::vector<Tensor> layernorm_bwd_residual(const Tensor& dy, const Tensor& x, const Tensor& w, const Tensor& mean,
+                                           const Tensor& rstd, Tensor& dw, const c10::optional<Tensor>& db,
+                                           const Tensor& res_in) {
+  CHECK_GPU(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw);
+  CHECK_F32(res_in); CHECK_CONTIG(res_in);
+  const bool xb = x.scalar_type() == at::kBFloat16;
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  TORCH_CHECK(res_in.numel() == x.numel(), "layernorm_bwd_residual: res_in shape mismatch");
+  Tensor dx = at::empty(x.sizes(), x.options().dtype(at::kFloat));
+  Tensor dxb = at::empty(x.sizes(), x.options().dtype(at::kBFloat16));
+  const int nb = (int)std::min<int64_t>(512, (rows + 31) / 32);
+  Tensor part = at::empty({nb, 2, D}, x.options().dtype(at::kFloat));
+  CHECK_RC(dpe_layernorm_bwd(bp(dy), x.data_ptr(), xb, fp(w), fp(mean), fp(rstd), dx.data_ptr(), 1, fp(res_in), bpm(dxb),
+                             fp(dw), fpom(db), fp(part), rows, (int)D, cur_stream()), "layernorm_bwd_residual");
+  return {dx, dxb};
 }
 
 // ---------------------------------------------------------------- attention
@@ -943,6 +963,8 @@ void register_ops(pybind11::module& m) {
   m.def("optim_step", &optim_step);
   m.def("optim_chunk_size", []() { return dpe_optim_chunk_size(); });
   m.def("optim_desc_bytes", []() { return dpe_optim_desc_bytes(); });
+  m.def("layernorm_bwd_residual", &layernorm_bwd_residual, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"),
+        py::arg("rstd"), py::arg("dw"), py::arg("db"), py::arg("res_in"));
   m.def("layernorm_fwd", &layernorm_fwd, py::arg("x"), py::arg("w"), py::arg("b") = py::none(), py::arg("eps") = 1e-5);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
         py::arg("dw"), py::arg("db") = py::none(), py::arg("dx_out") = py::none());

@@ -80,6 +80,11 @@ DPE_DEVICE bf16x8 mnfrag(const char* img, int c0) {
 DPE_DEVICE u32x4 ld16(const uint16_t* p) { return *(const u32x4*)p; }
 DPE_DEVICE u32x4 zero16() { u32x4 z; z[0] = z[1] = z[2] = z[3] = 0u; return z; }
 
+// Out-of-range chunks (conv padding, M/N/K tails) load from this zero page: the
+// address is selected (v_cndmask), the load is unconditional -- no branch per chunk.
+__device__ __attribute__((aligned(64))) uint16_t igemm_zero_page[32];
+DPE_DEVICE u32x4 ld16z(bool v, const uint16_t* p) { return *(const u32x4*)(v ? p : igemm_zero_page); }
+
 // ------------------------------------------------------------------ loaders
 // K-contiguous loaders: tile [ROWS][32]; chunk c -> row c>>2, kchunk c&3.
 template <int ROWS, int KIND>
@@ -137,18 +142,18 @@ struct KLoader {
     for (int i = 0; i < NC; ++i) {
       bool v = vrow[i] && kk[i] < kend;
       if constexpr (KIND == A_DENSE_K || KIND == B_DENSE_K) {
-        regs[i] = v ? ld16(base[i]) : zero16();
+        regs[i] = ld16z(v, base[i]);
       } else if constexpr (KIND == A_CONV_FWD) {
         const ConvGeom& g = p.g;
         const int ih = ihb[i] + r[i] * g.dh, iw = iwb[i] + s[i] * g.dw;
         v = v && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-        regs[i] = v ? ld16(base[i] + ((int64_t)ih * g.W + iw) * g.C + ci[i]) : zero16();
+        regs[i] = ld16z(v, base[i] + ((int64_t)ih * g.W + iw) * g.C + ci[i]);
       } else {  // A_CONV_DGRAD
         const ConvGeom& g = p.g;
         const int oh_ = ihb[i] - r[i] * g.dh, ow_ = iwb[i] - s[i] * g.dw;
         const int oh = oh_ / g.sh, ow = ow_ / g.sw;
         v = v && oh_ >= 0 && ow_ >= 0 && oh * g.sh == oh_ && ow * g.sw == ow_ && oh < g.OH && ow < g.OW;
-        regs[i] = v ? ld16(base[i] + ((int64_t)oh * g.OW + ow) * g.K + ci[i]) : zero16();
+        regs[i] = ld16z(v, base[i] + ((int64_t)oh * g.OW + ow) * g.K + ci[i]);
       }
     }
   }
@@ -234,16 +239,16 @@ struct MNLoader {
     for (int i = 0; i < NC; ++i) {
       bool v = vcol[i] && kk[i] < kend;
       if constexpr (KIND == A_DENSE_M || KIND == B_DENSE_N) {
-        regs[i] = v ? ld16(base[i]) : zero16();
+        regs[i] = ld16z(v, base[i]);
       } else if constexpr (KIND == B_CONV_DGRAD) {
         const ConvGeom& g = p.g;
         const int r = g.pr0 + g.psh * tt[i], s_ = g.ps0 + g.psw * uu[i];
-        regs[i] = v ? ld16(base[i] + (int64_t)co[i] * g.RR * g.SS * g.C + (int64_t)(r * g.SS + s_) * g.C) : zero16();
+        regs[i] = ld16z(v, base[i] + (int64_t)co[i] * g.RR * g.SS * g.C + (int64_t)(r * g.SS + s_) * g.C);
       } else {
         const ConvGeom& g = p.g;
         const int ih = oh[i] * g.sh + roff[i], iw = ow[i] * g.sw + soff[i];
         v = v && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-        regs[i] = v ? ld16(base[i] + (((int64_t)img[i] * g.H + ih) * g.W + iw) * g.C) : zero16();
+        regs[i] = ld16z(v, base[i] + (((int64_t)img[i] * g.H + ih) * g.W + iw) * g.C);
       }
     }
   }

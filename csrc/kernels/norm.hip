@@ -79,6 +79,7 @@ template <bool XBF>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict__ dy, const void* __restrict__ x,
                                                      const float* __restrict__ w, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, void* __restrict__ dx, int dx_acc,
+                                                     const float* __restrict__ res_in, uint16_t* __restrict__ dx_bf16,
                                                      float* __restrict__ part, int64_t rows, int D) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int CH = D >> 3;
@@ -119,13 +120,18 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
         float o[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = rstd * (dd[j][e] * w[c * 8 + e] - sg - xh[j][e] * sgx);
-        if (dx_acc) {
+        if (dx_acc) {  // fp32 residual-stream grad: dx = (res_in or dx) + dLN, optional bf16 copy
           float* p = (float*)dx + base + c * 8;
-          f32x4 a = *(f32x4*)p, bb = *(f32x4*)(p + 4);
+          const float* q = res_in ? res_in + base + c * 8 : p;
+          f32x4 a = *(const f32x4*)q, bb = *(const f32x4*)(q + 4);
           a[0] += o[0]; a[1] += o[1]; a[2] += o[2]; a[3] += o[3];
           bb[0] += o[4]; bb[1] += o[5]; bb[2] += o[6]; bb[3] += o[7];
           *(f32x4*)p = a;
           *(f32x4*)(p + 4) = bb;
+          if (dx_bf16) {
+            const float t[8] = {a[0], a[1], a[2], a[3], bb[0], bb[1], bb[2], bb[3]};
+            *(u32x4*)(dx_bf16 + base + c * 8) = pack8(t);
+          }
         } else if (XBF) {
           *(u32x4*)((uint16_t*)dx + base + c * 8) = pack8(o);
         } else {
@@ -207,15 +213,17 @@ extern "C" int dpe_layernorm_fwd(const void* x, int x_bf16, const float* w, cons
 }
 
 extern "C" int dpe_layernorm_bwd(const uint16_t* dy, const void* x, int x_bf16, const float* w, const float* mean,
-                                 const float* rstd, void* dx, int dx_acc, float* dw, float* db, float* part, int64_t rows,
-                                 int D, hipStream_t st) {
+                                 const float* rstd, void* dx, int dx_acc, const float* res_in, uint16_t* dx_bf16, float* dw,
+                                 float* db, float* part, int64_t rows, int D, hipStream_t st) {
   if (D % 8 || D > 2048) return -1;
   const int nb = (int)(rows < 16384 ? (rows + 31) / 32 : 512);
   const int nbc = nb > 512 ? 512 : nb;
   if (x_bf16)
-    hipLaunchKernelGGL((ln_bwd_kernel<true>), dim3(nbc), dim3(256), 0, st, dy, x, w, mean, rstd, dx, dx_acc, part, rows, D);
+    hipLaunchKernelGGL((ln_bwd_kernel<true>), dim3(nbc), dim3(256), 0, st, dy, x, w, mean, rstd, dx, dx_acc, res_in, dx_bf16,
+                       part, rows, D);
   else
-    hipLaunchKernelGGL((ln_bwd_kernel<false>), dim3(nbc), dim3(256), 0, st, dy, x, w, mean, rstd, dx, dx_acc, part, rows, D);
+    hipLaunchKernelGGL((ln_bwd_kernel<false>), dim3(nbc), dim3(256), 0, st, dy, x, w, mean, rstd, dx, dx_acc, res_in, dx_bf16,
+                       part, rows, D);
   hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 63) / 64, db ? 2 : 1), dim3(256), 0, st, part, nbc, D, dw, db);
   return 0;
 }

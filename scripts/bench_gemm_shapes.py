@@ -15,6 +15,8 @@ C = ext()
 dev = "cuda"
 SHAPES = [(256 * 56 * 56, 64, 576), (256 * 28 * 28, 128, 1152), (256 * 14 * 14, 256, 2304), (256 * 7 * 7, 512, 4608),
           (256 * 56 * 56, 256, 64), (256 * 28 * 28, 512, 128), (256 * 14 * 14, 1024, 256), (256 * 14 * 14, 256, 1024)]
+if len(sys.argv) > 1 and sys.argv[1] == "square":
+    SHAPES = [(4096, 4096, 4096), (8192, 8192, 8192), (8192, 8192, 1024), (16384, 4096, 4096)]
 
 
 def timeit(fn, iters=20):
