@@ -1,0 +1,147 @@
+"""Hand-scheduled forward/backward of a GPT-2 pre-LN transformer block on gfx950.
+
+One autograd node per block instead of eight per-op nodes.  The per-op graph
+pays, per block, two fp32->bf16 casts of the residual-stream gradient and two
+fp32 adds where autograd joins the residual branch with the LayerNorm branch;
+here both disappear into the LayerNorm backward kernel (residual form: it reads
+the incoming stream gradient, adds the LN input gradient and writes the result
+in fp32 *and* bf16 in one pass):
+
+forward  (x fp32 residual stream [B, T, D])
+    h1 = LN1(x)                     bf16
+    qkv = h1 W_qkv^T + b            bf16 [B, T, 3, H, 64], read in place by attention
+    a, lse = attn(qkv)              causal flash attention
+    x2 = x + a W_o^T + b            fp32, residual add in the GEMM epilogue
+    h2 = LN2(x2) ; v = h2 W_fc^T + b ; u = gelu(v)
+    y  = x2 + u W_p^T + b           fp32
+backward (g = dL/dy fp32, gb its bf16 copy)
+    dW_p += gb^T u ; db_p += colsum(gb) ; du = gb W_p ; dv = gelu'(v) du
+    dW_fc += dv^T h2 ; db_fc ; dh2 = dv W_fc
+    g2, g2b = g + LN2'(dh2)         one kernel: fp32 stream grad + bf16 copy
+    dW_o += g2b^T a ; db_o ; da = g2b W_o ; dqkv = attn'(da)
+    dW_qkv += dqkv^T h1 ; db_qkv ; dh1 = dqkv W_qkv
+    g1, g1b = g2 + LN1'(dh1)        -> returned; g1b handed to the previous block
+
+The bf16 copy of the returned gradient is passed to the next backward node
+(the previous block) through ``_carry``: it is used only if that node receives
+exactly the tensor this node returned (same storage, shape and version), else
+the node casts itself.  Weight gradients go straight into the DDP bucket views
+and are announced in reverse-forward order, as in the per-op path.
+
+Reference parity: the reference trains only SimpleNet (``train.py``); GPT-2 is
+BASELINE.json config 4 -- same math as ``models/gpt2.py:Block``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch.autograd import Function
+
+from ..ops._ext import ext
+from ..ops._state import grad_done, grad_sink, note_use, shadow
+
+# (fp32 grad, its bf16 copy, version) produced by the most recent block backward
+_carry: list = [None]
+
+
+def _bf16_of(g: torch.Tensor) -> torch.Tensor:
+    c = _carry[0]
+    _carry[0] = None
+    if c is not None:
+        g32, gb, ver = c
+        if (g32.data_ptr() == g.data_ptr() and g32.shape == g.shape and g.dtype == torch.float32
+                and g._version == ver and g.is_contiguous()):
+            return gb
+    return g.to(torch.bfloat16).contiguous()
+
+
+def block_params(blk):
+    """Parameters of ``blk`` in the order BlockFn takes them (None biases skipped)."""
+    mods = (blk.ln_1, blk.c_attn, blk.attn_proj, blk.ln_2, blk.c_fc, blk.mlp_proj)
+    return [t for m in mods for t in (m.weight, m.bias) if t is not None]
+
+
+class BlockFn(Function):
+    @staticmethod
+    def forward(ctx, x, blk, *params):
+        C = ext()
+        B, T, D = x.shape
+        H = blk.n_head
+        hd = D // H
+        scale = 1.0 / math.sqrt(hd)
+        x = x.contiguous()
+
+        def opt(t):
+            return t.detach() if t is not None else None
+
+        h1, m1, r1 = C.layernorm_fwd(x, blk.ln_1.weight.detach(), opt(blk.ln_1.bias), blk.ln_1.eps)
+        qkv = C.linear_fwd(h1, shadow(blk.c_attn.weight), opt(blk.c_attn.bias), 0, False, None, None)
+        qkv5 = qkv.view(B, T, 3, H, hd)
+        a, lse = C.attn_fwd(qkv5, H, scale, True)
+        a = a.view(B, T, D)
+        x2 = C.linear_fwd(a, shadow(blk.attn_proj.weight), opt(blk.attn_proj.bias), 0, True, x, None)
+        h2, m2, r2 = C.layernorm_fwd(x2, blk.ln_2.weight.detach(), opt(blk.ln_2.bias), blk.ln_2.eps)
+        v = C.linear_fwd(h2, shadow(blk.c_fc.weight), opt(blk.c_fc.bias), 0, False, None, None)
+        u = C.act(v, None, 2)
+        y = C.linear_fwd(u, shadow(blk.mlp_proj.weight), opt(blk.mlp_proj.bias), 0, True, x2, None)
+        ctx.save_for_backward(x, h1, m1, r1, qkv5, a, lse, x2, h2, m2, r2, v, u)
+        ctx.blk, ctx.scale = blk, scale
+        for p in params:
+            note_use(p)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        C = ext()
+        x, h1, m1, r1, qkv5, a, lse, x2, h2, m2, r2, v, u = ctx.saved_tensors
+        blk = ctx.blk
+        g = g.contiguous()
+        gb = _bf16_of(g)
+        grads = {}
+
+        def sink(p):
+            buf, direct = grad_sink(p)
+            return buf, direct
+
+        def done(p, buf, direct):
+            grad_done(p, direct)
+            grads[id(p)] = None if direct else buf
+
+        def linear_bwd(lin, dyb, inp, want_dx=True):
+            """dW += dyb^T inp ; db += colsum(dyb) ; return dyb W (bf16)."""
+            buf, d = sink(lin.weight)
+            C.linear_wgrad(dyb, inp, buf, 1.0)
+            done(lin.weight, buf, d)
+            if lin.bias is not None:
+                bb, bd = sink(lin.bias)
+                C.colsum(dyb, bb, True)
+                done(lin.bias, bb, bd)
+            return C.linear_dgrad(dyb, shadow(lin.weight)) if want_dx else None
+
+        def ln_bwd(ln, dy, xin, mean, rstd, res):
+            wb, wd = sink(ln.weight)
+            bb, bd = sink(ln.bias) if ln.bias is not None else (None, False)
+            dx, dxb = C.layernorm_bwd_residual(dy, xin, ln.weight.detach(), mean, rstd, wb, bb, res)
+            done(ln.weight, wb, wd)
+            if ln.bias is not None:
+                done(ln.bias, bb, bd)
+            return dx, dxb
+
+        du = linear_bwd(blk.mlp_proj, gb, u)
+        dv = C.act(du, v, 3)
+        dh2 = linear_bwd(blk.c_fc, dv, h2)
+        g2, g2b = ln_bwd(blk.ln_2, dh2, x2, m2, r2, g)
+        da = linear_bwd(blk.attn_proj, g2b, a)
+        dqkv = C.attn_bwd(qkv5, a.view(qkv5.shape[0], qkv5.shape[1], qkv5.shape[3], qkv5.shape[4]), da, lse,
+                          blk.n_head, ctx.scale, True)
+        dqkv = dqkv.view(a.shape[0], a.shape[1], -1)
+        dh1 = linear_bwd(blk.c_attn, dqkv, h1)
+        g1, g1b = ln_bwd(blk.ln_1, dh1, x, m1, r1, g2)
+        _carry[0] = (g1, g1b, g1._version)
+        pgrads = [grads.get(id(p)) for p in block_params(blk)]
+        return (g1, None, *pgrads)
+
+
+def block_forward(blk, x):
+    return BlockFn.apply(x, blk, *block_params(blk))

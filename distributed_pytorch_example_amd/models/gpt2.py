@@ -16,6 +16,7 @@ parameterisation as HF/nanoGPT ``GPT2``), executed on gfx950 kernels:
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -23,6 +24,9 @@ import torch.nn as nn
 
 from ..ops import functional as Fx
 from ..ops.layers import LayerNorm, Linear
+
+# DPE_GPT2_FUSED=0: per-op autograd graph for the blocks (A/B reference)
+_FUSED = os.environ.get("DPE_GPT2_FUSED", "1") != "0"
 
 
 @dataclass
@@ -53,8 +57,13 @@ class Block(nn.Module):
         self.ln_2 = LayerNorm(d, bias=cfg.bias)
         self.c_fc = Linear(d, 4 * d, bias=cfg.bias)
         self.mlp_proj = Linear(4 * d, d, bias=cfg.bias)
+        self.fused = _FUSED
 
     def forward(self, x):
+        if x.is_cuda and self.fused and torch.is_grad_enabled():
+            from ._gpt2_fused import block_forward  # hand-scheduled fwd/bwd, one autograd node
+
+            return block_forward(self, x)
         h = self.ln_1(x)
         qkv = self.c_attn(h)
         a = Fx.causal_attention(qkv, self.n_head)
@@ -83,10 +92,12 @@ class GPT2(nn.Module):
             for blk in self.h:
                 for lin in (blk.c_attn, blk.c_fc):
                     lin.weight.normal_(0, std)
-                    lin.bias.zero_()
+                    if lin.bias is not None:
+                        lin.bias.zero_()
                 for lin in (blk.attn_proj, blk.mlp_proj):
                     lin.weight.normal_(0, std / math.sqrt(2 * self.cfg.n_layer))
-                    lin.bias.zero_()
+                    if lin.bias is not None:
+                        lin.bias.zero_()
 
     def forward(self, idx, targets=None):
         """Logits [B, T, V(p)], or -- with ``targets`` -- the mean next-token

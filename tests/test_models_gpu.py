@@ -174,3 +174,25 @@ def test_gpt2_small_step(C):
         losses.append(loss.item())
     # ~ln(50257)=10.8 minus the tied-embedding self-similarity bonus of predicting the input token
     assert 9.0 < losses[0] < 11.5 and losses[-1] < losses[0]
+
+
+def test_gpt2_fused_block_matches_per_op(C):
+    """Hand-scheduled transformer block (one autograd node, residual-form LN backward with
+    the bf16 gradient copy carried between blocks) == per-op autograd graph."""
+    torch.manual_seed(8)
+    for bias in (True, False):
+        m1 = get_model("gpt2-tiny", n_layer=3, bias=bias).to(dev)
+        m2 = copy.deepcopy(m1)
+        for b in m2.h:
+            b.fused = False
+        assert all(b.fused for b in m1.h)
+        idx = torch.randint(0, 512, (2, 128), device=dev)
+        tgt = torch.randint(0, 512, (2, 128), device=dev)
+        l1, l2 = m1(idx, tgt), m2(idx, tgt)
+        assert abs(l1.item() - l2.item()) < 1e-4 * abs(l2.item())
+        l1.backward()
+        l2.backward()
+        g2 = dict(m2.named_parameters())
+        for n, p in m1.named_parameters():
+            assert cos(p.grad, g2[n].grad) > 0.999, n
+            assert rel(p.grad, g2[n].grad) < 0.02, n
