@@ -72,9 +72,10 @@ def main():
         g = torch.Generator(device=dev)
         g.manual_seed(99 + rank)
         if dev.type == "cuda":
-            xs = [torch.randn(bs, 224, 224, 8, device=dev, generator=g).to(torch.bfloat16) for _ in range(args.nbatches)]
-            for x in xs:
-                x[..., 3:] = 0
+            # device-resident batches in the stem's packed input layout (space-to-depth bf16)
+            from distributed_pytorch_example_amd.ops import functional as Fx
+
+            xs = [Fx.to_s2d_input(torch.randn(bs, 3, 224, 224, device=dev, generator=g)) for _ in range(args.nbatches)]
         else:
             xs = [torch.randn(bs, 3, 224, 224, generator=g, device=dev) for _ in range(args.nbatches)]
         ys = [torch.randint(0, 1000, (bs,), device=dev, generator=g) for _ in range(args.nbatches)]

@@ -43,6 +43,8 @@ int dpe_act(const void* a, const void* b, void* out, int64_t n, int op, int bf16
 int dpe_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset, int bf16, hipStream_t st);
 int dpe_add(const void* a, const void* b, void* out, int64_t n, float alpha, int bf16, hipStream_t st);
 int dpe_colsum(const void* dy, int64_t M, int N, int64_t ld, float* db, int accumulate, int bf16, hipStream_t st);
+int dpe_nchw_to_s2d(const float* x, uint16_t* y, int N, int C, int H, int W, hipStream_t st);
+int dpe_conv_w_flipT(const uint16_t* w, uint16_t* wt, int K, int R, int S, int C, hipStream_t st);
 int dpe_nchw_to_nhwc(const float* x, uint16_t* y, int N, int C, int HW, int Cp, hipStream_t st);
 int dpe_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* wpe, float* out, int64_t rows, int T, int D,
                       hipStream_t st);
@@ -458,9 +460,11 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && x.size(3) == w.size(3), "conv: NHWC x / KRSC w shape mismatch");
   TORCH_CHECK(x.size(3) % 8 == 0 && w.size(0) % 8 == 0, "conv: channels must be multiples of 8");
+  TORCH_CHECK(pad.size() == 2 || pad.size() == 4, "conv: pad is [ph, pw] or [top, left, bottom, right]");
   const int64_t H = x.size(1), W = x.size(2), R = w.size(1), S = w.size(2);
-  const int64_t OH = (H + 2 * pad[0] - dil[0] * (R - 1) - 1) / stride[0] + 1;
-  const int64_t OW = (W + 2 * pad[1] - dil[1] * (S - 1) - 1) / stride[1] + 1;
+  const int64_t pb = pad.size() == 4 ? pad[2] : pad[0], pr = pad.size() == 4 ? pad[3] : pad[1];
+  const int64_t OH = (H + pad[0] + pb - dil[0] * (R - 1) - 1) / stride[0] + 1;
+  const int64_t OW = (W + pad[1] + pr - dil[1] * (S - 1) - 1) / stride[1] + 1;
   Tensor y = at::empty({x.size(0), OH, OW, w.size(0)}, x.options());
   auto g = geom(x, w, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], OH, OW);
   auto a = base_args();
@@ -485,6 +489,12 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
 // dx NHWC [N,H,W,C] = conv_transpose(dy, w); optional residual added into dx.
 // With bn_x/bn_coef (dx is dL/d relu(BN(bn_x))), the epilogue also emits the
 // BatchNorm-backward partials [2][C][tiles] (sum dz, sum dz*(x-mean)).
+// DPE_DGRAD_FWD=0: stride-1 data grads on the transposed-filter loaders (A/B reference)
+bool dgrad_as_fwd() {
+  static const bool on = [] { const char* e = getenv("DPE_DGRAD_FWD"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape,
                                     std::vector<int64_t> stride, std::vector<int64_t> pad, std::vector<int64_t> dil,
                                     const c10::optional<Tensor>& residual, const c10::optional<Tensor>& bn_x,
@@ -509,7 +519,24 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
   }
   Tensor part;
   auto tiles_of = [&](int64_t M, int64_t K) { const Cfg c = pick_cfg(M, g.C, K, false); return (M + c.bm - 1) / c.bm; };
-  if (is_pointwise(g) || (g.sh == 1 && g.sw == 1)) {
+  if (!is_pointwise(g) && g.sh == 1 && g.sw == 1 && g.dh == 1 && g.dw == 1 && dgrad_as_fwd()) {
+    // Stride-1 data grad as a forward conv: dx = conv(dy, flipT(w), pad R-1-p) on the
+    // forward loaders (K-contiguous filter, im2col gather of dy).
+    Tensor wt = at::empty({g.C, g.R, g.S, g.K}, w.options());
+    CHECK_RC(dpe_conv_w_flipT(bp(w), bpm(wt), g.K, g.R, g.S, g.C, cur_stream()), "conv_w_flipT");
+    auto f = geom(dy, wt, 1, 1, g.R - 1 - g.ph, g.S - 1 - g.pw, 1, 1, g.H, g.W);
+    auto b = a;
+    b.g = f;
+    b.B = bp(wt);
+    b.lda = g.K; b.ldb = a.K; b.ldc = g.C;
+    if (want_bn) {
+      const int64_t t = tiles_of(b.M, b.K);
+      part = at::empty({2, g.C, t}, dy.options().dtype(at::kFloat));
+      b.col_stats = fp(part);
+      b.stats_ld = (int)t;
+    }
+    run_igemm(b, dpe::A_CONV_FWD, dpe::B_DENSE_K, want_bn ? dpe::EPI_BF16_BNB : dpe::EPI_BF16, false, true);
+  } else if (is_pointwise(g) || (g.sh == 1 && g.sw == 1)) {
     if (want_bn) {
       const int64_t t = tiles_of(a.M, a.K);
       part = at::empty({2, g.C, t}, dy.options().dtype(at::kFloat));
@@ -805,6 +832,15 @@ Tensor nchw_to_nhwc(const Tensor& x, int64_t cpad) {
   return y;
 }
 
+Tensor nchw_to_s2d(const Tensor& x) {
+  CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C <= 4 && H % 2 == 0 && W % 2 == 0, "nchw_to_s2d: needs C <= 4 and even H, W");
+  Tensor y = at::empty({N, H / 2, W / 2, 16}, x.options().dtype(at::kBFloat16));
+  CHECK_RC(dpe_nchw_to_s2d(fp(x), bpm(y), (int)N, (int)C, (int)H, (int)W, cur_stream()), "nchw_to_s2d");
+  return y;
+}
+
 Tensor embedding_fwd(const Tensor& idx, const Tensor& wte, const c10::optional<Tensor>& wpe) {
   CHECK_GPU(idx); CHECK_CONTIG(idx); CHECK_BF16(wte); CHECK_CONTIG(wte);
   TORCH_CHECK(idx.scalar_type() == at::kLong && idx.dim() == 2, "embedding: idx must be int64 [B,T]");
@@ -957,6 +993,7 @@ void register_ops(pybind11::module& m) {
   m.def("dropout", &dropout);
   m.def("add", &add, py::arg("a"), py::arg("b"), py::arg("alpha") = 1.0);
   m.def("colsum", &colsum, py::arg("dy"), py::arg("db"), py::arg("accumulate") = false);
+  m.def("nchw_to_s2d", &nchw_to_s2d, py::arg("x"));
   m.def("nchw_to_nhwc", &nchw_to_nhwc, py::arg("x"), py::arg("cpad") = 8);
   m.def("embedding_fwd", &embedding_fwd, py::arg("idx"), py::arg("wte"), py::arg("wpe") = py::none());
   m.def("embedding_bwd", &embedding_bwd, py::arg("idx"), py::arg("dout"), py::arg("dwte"), py::arg("dwpe") = py::none());

@@ -191,6 +191,49 @@ __global__ __launch_bounds__(ET) void nchw_to_nhwc_kernel(const float* __restric
   }
 }
 
+// x NCHW f32 [N,C<=4,H,W] -> space-to-depth NHWC bf16 [N,H/2,W/2,16],
+// channel (ay*2+ax)*4+c = x[n][c][2q+ay][2p+ax] (zeros for c >= C).  The 7x7/s2
+// stem then runs as a 4x4/s1 conv over 16 channels (K 256 instead of 392, two
+// 16-B chunks per tap).
+__global__ __launch_bounds__(ET) void nchw_to_s2d_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, int N, int C,
+                                                         int H, int W) {
+  const int Ho = H / 2, Wo = W / 2;
+  const int64_t total = (int64_t)N * Ho * Wo;
+  GRID_STRIDE(i, total) {
+    const int p = (int)(i % Wo);
+    const int64_t t = i / Wo;
+    const int q = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int c = j & 3, ax = (j >> 2) & 1, ay = j >> 3;
+      v[j] = c < C ? x[(((int64_t)n * C + c) * H + 2 * q + ay) * W + 2 * p + ax] : 0.f;
+    }
+    u32x4* o = (u32x4*)(y + i * 16);
+    o[0] = pack8(v);
+    o[1] = pack8(v + 8);
+  }
+}
+
+// ------------------------------------------- data-grad filter layout
+// wt[c][r][s][k] = w[k][R-1-r][S-1-s][c]: the stride-1 data grad of a conv is a
+// forward conv of dy with this filter (pad R-1-p), so it can run on the
+// forward loaders (K-contiguous filter rows) instead of the transposed ones.
+__global__ __launch_bounds__(ET) void conv_w_flipT_kernel(const uint16_t* __restrict__ w, uint16_t* __restrict__ wt, int K,
+                                                          int R, int S, int C) {
+  const int64_t total = (int64_t)K * R * S * C;
+  GRID_STRIDE(i, total) {
+    const int k = (int)(i % K);
+    int64_t t = i / K;
+    const int s = (int)(t % S);
+    t /= S;
+    const int r = (int)(t % R);
+    const int c = (int)(t / R);
+    wt[i] = w[(((int64_t)k * R + (R - 1 - r)) * S + (S - 1 - s)) * C + c];
+  }
+}
+
 // ----------------------------------------------------------- embedding
 // out[r][:] = wte[idx[r]][:] (+ wpe[r % T][:]) ; D % 8 == 0, weights bf16, out f32
 __global__ __launch_bounds__(ET) void embedding_fwd_kernel(const int64_t* __restrict__ idx, const uint16_t* __restrict__ wte,
@@ -292,6 +335,17 @@ extern "C" int dpe_colsum(const void* dy, int64_t M, int N, int64_t ld, float* d
     hipLaunchKernelGGL((colsum_kernel<float>), grid, dim3(ET), 0, st, (const float*)dy, M, N, ld, db, accumulate);
   return 0;
 }
+extern "C" int dpe_nchw_to_s2d(const float* x, uint16_t* y, int N, int C, int H, int W, hipStream_t st) {
+  if (C > 4 || (H & 1) || (W & 1)) return -1;
+  hipLaunchKernelGGL(nchw_to_s2d_kernel, dim3(egrid((int64_t)N * (H / 2) * (W / 2))), dim3(ET), 0, st, x, y, N, C, H, W);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dpe_conv_w_flipT(const uint16_t* w, uint16_t* wt, int K, int R, int S, int C, hipStream_t st) {
+  hipLaunchKernelGGL(conv_w_flipT_kernel, dim3(egrid((int64_t)K * R * S * C)), dim3(ET), 0, st, w, wt, K, R, S, C);
+  return (int)hipGetLastError();
+}
+
 extern "C" int dpe_nchw_to_nhwc(const float* x, uint16_t* y, int N, int C, int HW, int Cp, hipStream_t st) {
   hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(egrid((int64_t)N * HW)), dim3(ET), 0, st, x, y, N, C, HW, Cp);
   return 0;

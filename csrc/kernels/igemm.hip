@@ -616,6 +616,7 @@ extern "C" int dpe_igemm_launch(const IgemmArgs* args, int bm, int bn, int aload
   // data-grad feeding a BN+ReLU backward (partials from the epilogue)
   DPE_CASE(A_DENSE_K, B_DENSE_N, EPI_BF16_BNB)
   DPE_CASE(A_CONV_DGRAD, B_CONV_DGRAD, EPI_BF16_BNB)
+  DPE_CASE(A_CONV_FWD, B_DENSE_K, EPI_BF16_BNB)
   DPE_CASE(A_DENSE_M, B_CONV_WGRAD, EPI_ATOMIC_F32)
 #undef DPE_CASE
   return -1;

@@ -270,6 +270,82 @@ def conv2d_nhwc(x, weight, stride=(1, 1), padding=(0, 0), dilation=(1, 1), want_
     return _ConvFn.apply(x.contiguous(), weight, w16, stride, padding, dilation, want_stats)
 
 
+# ================================================ space-to-depth ResNet stem
+# A 7x7/s2/p3 conv over x equals a 4x4/s1 conv over the space-to-depth image
+# x'[q][p][(ay,ax,c)] = x[2q+ay][2p+ax][c], padded 2 (top/left) and 1
+# (bottom/right), with filter w'[o][dy][dx][(ay,ax,c)] = w[o][2dy+ay-1][2dx+ax-1][c]
+# (zero outside 7x7).  Each 7x7 tap appears exactly once in w', so the weight
+# gradient maps back by a gather.
+_S2D_IDX: dict = {}
+
+
+def _s2d_index(cin: int, device):
+    key = (cin, str(device))
+    if key not in _S2D_IDX:
+        dst, src = [], []
+        for dy in range(4):
+            for dx in range(4):
+                for ay in range(2):
+                    for ax in range(2):
+                        for c in range(4):
+                            r, s_ = 2 * dy + ay - 1, 2 * dx + ax - 1
+                            if 0 <= r < 7 and 0 <= s_ < 7 and c < cin:
+                                dst.append(((dy * 4 + dx) * 4 + ay * 2 + ax) * 4 + c)
+                                src.append((r * 7 + s_) * cin + c)
+        order = sorted(range(len(src)), key=lambda i: src[i])
+        inv = torch.tensor([dst[i] for i in order], dtype=torch.long, device=device)  # w-flat index -> w'-flat index
+        _S2D_IDX[key] = (torch.tensor(dst, dtype=torch.long, device=device),
+                         torch.tensor(src, dtype=torch.long, device=device), inv)
+    return _S2D_IDX[key]
+
+
+def _s2d_filter(w):
+    co, cin = w.shape[0], w.shape[-1]
+    dst, src, _ = _s2d_index(cin, w.device)
+    out = torch.zeros((co, 256), dtype=torch.bfloat16, device=w.device)
+    out[:, dst] = w.reshape(co, -1)[:, src].to(torch.bfloat16)
+    return out.view(co, 4, 4, 16)
+
+
+class _S2DStemFn(Function):
+    @staticmethod
+    def forward(ctx, xs, weight, w16, want_stats):
+        y, st = ext().conv_fwd(xs, w16, [1, 1], [2, 2, 1, 1], [1, 1], want_stats, None)
+        ctx.save_for_backward(xs)
+        ctx.weight = weight
+        note_use(weight)
+        if want_stats:
+            ctx.mark_non_differentiable(st)
+            return y, st
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, *unused):
+        (xs,) = ctx.saved_tensors
+        weight = ctx.weight
+        co = weight.shape[0]
+        tmp = torch.zeros((co, 4, 4, 16), dtype=torch.float32, device=dy.device)
+        ext().conv_wgrad(dy.contiguous(), xs, tmp, [1, 1], [2, 2], [1, 1], 1.0)
+        buf, direct = grad_sink(weight)
+        buf.view(co, -1).add_(tmp.view(co, 256)[:, _s2d_index(weight.shape[-1], dy.device)[2]])
+        grad_done(weight, direct)
+        return None, (None if direct else buf), None, None
+
+
+def to_s2d_input(x: torch.Tensor) -> torch.Tensor:
+    """NCHW fp32 images [N,3,H,W] -> space-to-depth NHWC bf16 [N,H/2,W/2,16] (GPU stem input)."""
+    return ext().nchw_to_s2d(x.float().contiguous())
+
+
+def stem_conv_s2d(xs, weight, want_stats: bool = False):
+    """7x7/s2/p3 conv (filter ``weight`` [Co,7,7,Cin<=4]) over a space-to-depth input ``xs``."""
+    from ._state import derived_shadow
+
+    assert tuple(weight.shape[1:3]) == (7, 7) and weight.shape[-1] <= 4 and xs.shape[-1] == 16
+    w16 = derived_shadow(weight, "s2d", _s2d_filter)
+    return _S2DStemFn.apply(xs.contiguous(), weight, w16, want_stats)
+
+
 def _pair(v) -> tuple:
     return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
 

@@ -81,6 +81,8 @@ CONV_CASES = [
     (2, 28, 28, 8, 64, 7, 2, 3),     # stem (channel-padded input)
     (3, 7, 7, 512, 128, 3, 1, 1),
     (1, 9, 9, 32, 48, 3, 2, 1),
+    (2, 10, 10, 16, 32, 5, 1, 2),    # stride-1 data grad as a forward conv (pad R-1-p)
+    (2, 9, 9, 64, 64, 3, 1, 0),
 ]
 
 
@@ -478,3 +480,27 @@ def test_dgrad_bn_backward_partials(C, N, H, W, Ci, Co, k, s, p):
     dg2, db2 = torch.zeros(Ci, device=dev), torch.zeros(Ci, device=dev)
     dh_ref, _ = C.bn_bwd(da, y, h, gamma, coef, dg2, db2, False)
     assert rel_err(dh, dh_ref) < 2e-2 and rel_err(dg1, dg2) < 1e-3 and rel_err(db1, db2) < 1e-3
+
+
+def test_s2d_stem_conv(C):
+    """Space-to-depth packing + 4x4/s1 stem conv (fwd, BN stats, weight grad) == 7x7/s2/p3 conv."""
+    from distributed_pytorch_example_amd.ops import functional as Fx
+
+    torch.manual_seed(21)
+    x = torch.randn(4, 3, 64, 64, device=dev)
+    w = torch.randn(64, 7, 7, 3, device=dev) / math.sqrt(147)
+    w16 = w.to(torch.bfloat16)
+    xb = x.to(torch.bfloat16).float()
+    ref = F.conv2d(xb, w16.permute(0, 3, 1, 2).float(), None, 2, 3).permute(0, 2, 3, 1)
+    xs = Fx.to_s2d_input(x)
+    assert xs.shape == (4, 32, 32, 16) and torch.equal(xs[0, 3, 5, 4 * 3 + 1], x[0, 1, 7, 11].to(torch.bfloat16))
+    wp = torch.nn.Parameter(w.clone())
+    y, st = Fx.stem_conv_s2d(xs, wp, want_stats=True)
+    assert y.shape == ref.shape and rel_err(y, ref) < 1e-2
+    s = st.sum(-1)
+    assert rel_err(s[0], ref.reshape(-1, 64).sum(0)) < 1e-2
+    dy = bf(torch.randn_like(ref))
+    y.backward(dy)
+    wr = w16.float().permute(0, 3, 1, 2).requires_grad_(True)
+    (gref,) = torch.autograd.grad(F.conv2d(xb, wr, None, 2, 3), wr, dy.float().permute(0, 3, 1, 2))
+    assert rel_err(wp.grad, gref.permute(0, 2, 3, 1)) < 1e-2
