@@ -44,7 +44,8 @@ int dpe_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint6
 int dpe_add(const void* a, const void* b, void* out, int64_t n, float alpha, int bf16, hipStream_t st);
 int dpe_colsum(const void* dy, int64_t M, int N, int64_t ld, float* db, int accumulate, int bf16, hipStream_t st);
 int dpe_nchw_to_s2d(const float* x, uint16_t* y, int N, int C, int H, int W, hipStream_t st);
-int dpe_conv_w_flipT(const uint16_t* w, uint16_t* wt, int K, int R, int S, int C, hipStream_t st);
+int dpe_conv_w_flipT(const uint16_t* w, uint16_t* wt, int K, int R, int S, int C, int r0, int rs, int Rp, int s0, int ss,
+                     int Sp, hipStream_t st);
 int dpe_nchw_to_nhwc(const float* x, uint16_t* y, int N, int C, int HW, int Cp, hipStream_t st);
 int dpe_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* wpe, float* out, int64_t rows, int T, int D,
                       hipStream_t st);
@@ -498,9 +499,11 @@ bool dgrad_as_fwd() {
 std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape,
                                     std::vector<int64_t> stride, std::vector<int64_t> pad, std::vector<int64_t> dil,
                                     const c10::optional<Tensor>& residual, const c10::optional<Tensor>& bn_x,
-                                    const c10::optional<Tensor>& bn_coef) {
+                                    const c10::optional<Tensor>& bn_coef, const Tensor* acc_into = nullptr) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(w); CHECK_CONTIG(dy); CHECK_CONTIG(w);
-  Tensor dx = at::empty(xshape, dy.options());
+  // acc_into: dx += dgrad in place (the epilogue reads each element as its residual
+  // right before overwriting it); parities no tap reaches are left untouched.
+  Tensor dx = acc_into ? *acc_into : at::empty(xshape, dy.options());
   auto g = geom(dx, w, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], dy.size(1), dy.size(2));
   TORCH_CHECK(dy.size(3) == g.K && dy.size(0) == g.N, "conv_dgrad: dy shape mismatch");
   auto a = base_args();
@@ -509,6 +512,12 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
   a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.K;
   a.lda = g.K; a.ldb = g.C; a.ldc = g.C;
   if (residual.has_value() && residual->defined()) { CHECK_BF16((*residual)); CHECK_CONTIG((*residual)); a.residual = bp(*residual); }
+  if (acc_into) {
+    TORCH_CHECK(!a.residual && !(bn_x.has_value() && bn_x->defined()), "conv_dgrad_acc: no residual / BN with accumulate");
+    CHECK_BF16(dx); CHECK_CONTIG(dx);
+    TORCH_CHECK(dx.sizes().vec() == xshape, "conv_dgrad_acc: dx shape mismatch");
+    a.residual = bp(dx);
+  }
   const bool want_bn = bn_x.has_value() && bn_x->defined();
   if (want_bn) {
     CHECK_BF16((*bn_x)); CHECK_CONTIG((*bn_x)); CHECK_F32((*bn_coef));
@@ -523,7 +532,7 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
     // Stride-1 data grad as a forward conv: dx = conv(dy, flipT(w), pad R-1-p) on the
     // forward loaders (K-contiguous filter, im2col gather of dy).
     Tensor wt = at::empty({g.C, g.R, g.S, g.K}, w.options());
-    CHECK_RC(dpe_conv_w_flipT(bp(w), bpm(wt), g.K, g.R, g.S, g.C, cur_stream()), "conv_w_flipT");
+    CHECK_RC(dpe_conv_w_flipT(bp(w), bpm(wt), g.K, g.R, g.S, g.C, 0, 1, g.R, 0, 1, g.S, cur_stream()), "conv_w_flipT");
     auto f = geom(dy, wt, 1, 1, g.R - 1 - g.ph, g.S - 1 - g.pw, 1, 1, g.H, g.W);
     auto b = a;
     b.g = f;
@@ -552,6 +561,8 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
     // no taps is a K = 0 GEMM that stores zeros (+ residual).
     TORCH_CHECK(g.dh == 1 && g.dw == 1, "strided dgrad with dilation is not supported");
     std::vector<dpe::IgemmArgs> subs;
+    std::vector<bool> sub_fwd;
+    std::vector<Tensor> phase_w;  // keeps the per-parity filters alive until the launches are queued
     int64_t total_tiles = 0;
     for (int pa = 0; pa < g.sh; ++pa) {
       for (int pb = 0; pb < g.sw; ++pb) {
@@ -561,6 +572,7 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
         const int Sp = g.S > s0 ? (g.S - s0 + g.sw - 1) / g.sw : 0;
         const int Hp = (g.H - pa + g.sh - 1) / g.sh, Wp = (g.W - pb + g.sw - 1) / g.sw;
         if (Hp <= 0 || Wp <= 0) continue;
+        if (acc_into && (g.R <= r0 || g.S <= s0)) continue;  // no taps: dx += 0
         v.H = Hp; v.W = Wp; v.R = Rp; v.S = Sp;
         v.sh = 1; v.sw = 1;
         v.ph = (pa + g.ph - r0) / g.sh;  // oh = hh + ph' - t
@@ -573,16 +585,40 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
         b.K = Rp * Sp * g.K;
         b.stats_off = (int)total_tiles;
         total_tiles += tiles_of(b.M, b.K);
+        bool fwd_form = false;
+        if (Rp > 0 && Sp > 0 && dgrad_as_fwd()) {
+          // this parity as a forward conv of dy with its own flipped tap subset:
+          // oh = hh + ph' - t = hh - (Rp-1-ph') + (Rp-1-t)
+          Tensor wt = at::empty({g.C, Rp, Sp, g.K}, w.options());
+          CHECK_RC(dpe_conv_w_flipT(bp(w), bpm(wt), g.K, g.R, g.S, g.C, r0, g.sh, Rp, s0, g.sw, Sp, cur_stream()),
+                   "conv_w_flipT");
+          phase_w.push_back(wt);
+          auto f = geom(dy, wt, 1, 1, Rp - 1 - v.ph, Sp - 1 - v.pw, 1, 1, Hp, Wp);
+          f.remap = 2; f.Hr = g.H; f.Wr = g.W; f.oa = pa; f.ob = pb; f.psh = g.sh; f.psw = g.sw;
+          b.g = f;
+          b.B = bp(wt);
+          b.lda = g.K; b.ldb = b.K;
+          fwd_form = true;
+        }
         subs.push_back(b);
+        sub_fwd.push_back(fwd_form);
       }
     }
     if (want_bn) part = at::empty({2, g.C, total_tiles}, dy.options().dtype(at::kFloat));
-    for (auto& b : subs) {
+    for (size_t i = 0; i < subs.size(); ++i) {
+      auto& b = subs[i];
       if (want_bn) { b.col_stats = fp(part); b.stats_ld = (int)total_tiles; }
-      run_igemm(b, dpe::A_CONV_DGRAD, dpe::B_CONV_DGRAD, want_bn ? dpe::EPI_BF16_BNB : dpe::EPI_BF16, false, true);
+      const int epi = want_bn ? dpe::EPI_BF16_BNB : dpe::EPI_BF16;
+      if (sub_fwd[i]) run_igemm(b, dpe::A_CONV_FWD, dpe::B_DENSE_K, epi, false, true);
+      else run_igemm(b, dpe::A_CONV_DGRAD, dpe::B_CONV_DGRAD, epi, false, true);
     }
   }
   return {dx, part};
+}
+
+void conv_dgrad_acc(const Tensor& dy, const Tensor& w, Tensor& dx, std::vector<int64_t> stride, std::vector<int64_t> pad,
+                    std::vector<int64_t> dil) {
+  conv_dgrad_impl(dy, w, dx.sizes().vec(), stride, pad, dil, c10::nullopt, c10::nullopt, c10::nullopt, &dx);
 }
 
 Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape, std::vector<int64_t> stride,
@@ -964,7 +1000,13 @@ void register_ops(pybind11::module& m) {
         py::arg("alpha_t") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("want_stats") = false, py::arg("bias") = py::none());
-  m.def("conv_dgrad_bn", &conv_dgrad_impl, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"),
+  m.def("conv_dgrad_acc", &conv_dgrad_acc, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"),
+        py::arg("dil"), "dx += data grad of conv(w) in place (parities without taps untouched)");
+  m.def("conv_dgrad_bn", [](const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape, std::vector<int64_t> stride,
+                            std::vector<int64_t> pad, std::vector<int64_t> dil, const c10::optional<Tensor>& residual,
+                            const c10::optional<Tensor>& bn_x, const c10::optional<Tensor>& bn_coef) {
+          return conv_dgrad_impl(dy, w, xshape, stride, pad, dil, residual, bn_x, bn_coef);
+        }, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"),
         py::arg("pad"), py::arg("dil"), py::arg("residual") = py::none(), py::arg("bn_x") = py::none(),
         py::arg("bn_coef") = py::none());
   m.def("bn_coef", &bn_coef, py::arg("stats"), py::arg("M"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),

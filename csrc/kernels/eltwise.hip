@@ -217,20 +217,24 @@ __global__ __launch_bounds__(ET) void nchw_to_s2d_kernel(const float* __restrict
 }
 
 // ------------------------------------------- data-grad filter layout
-// wt[c][r][s][k] = w[k][R-1-r][S-1-s][c]: the stride-1 data grad of a conv is a
-// forward conv of dy with this filter (pad R-1-p), so it can run on the
-// forward loaders (K-contiguous filter rows) instead of the transposed ones.
+// wt[c][r][s][k] = w[k][r0 + rs*(Rp-1-r)][s0 + ss*(Sp-1-s)][c], r < Rp, s < Sp.
+// With (r0, rs, Rp) = (0, 1, R): the flipped/transposed filter -- the stride-1
+// data grad of a conv is a forward conv of dy with it (pad R-1-p), so it runs on
+// the forward loaders (K-contiguous filter rows) instead of the transposed ones.
+// With a stride > 1, one such filter per output parity holds only the taps that
+// reach that parity (phase-decomposed data grad).
 __global__ __launch_bounds__(ET) void conv_w_flipT_kernel(const uint16_t* __restrict__ w, uint16_t* __restrict__ wt, int K,
-                                                          int R, int S, int C) {
-  const int64_t total = (int64_t)K * R * S * C;
+                                                          int R, int S, int C, int r0, int rs, int Rp, int s0, int ss,
+                                                          int Sp) {
+  const int64_t total = (int64_t)K * Rp * Sp * C;
   GRID_STRIDE(i, total) {
     const int k = (int)(i % K);
     int64_t t = i / K;
-    const int s = (int)(t % S);
-    t /= S;
-    const int r = (int)(t % R);
-    const int c = (int)(t / R);
-    wt[i] = w[(((int64_t)k * R + (R - 1 - r)) * S + (S - 1 - s)) * C + c];
+    const int s = (int)(t % Sp);
+    t /= Sp;
+    const int r = (int)(t % Rp);
+    const int c = (int)(t / Rp);
+    wt[i] = w[(((int64_t)k * R + r0 + rs * (Rp - 1 - r)) * S + s0 + ss * (Sp - 1 - s)) * C + c];
   }
 }
 
@@ -341,8 +345,11 @@ extern "C" int dpe_nchw_to_s2d(const float* x, uint16_t* y, int N, int C, int H,
   return (int)hipGetLastError();
 }
 
-extern "C" int dpe_conv_w_flipT(const uint16_t* w, uint16_t* wt, int K, int R, int S, int C, hipStream_t st) {
-  hipLaunchKernelGGL(conv_w_flipT_kernel, dim3(egrid((int64_t)K * R * S * C)), dim3(ET), 0, st, w, wt, K, R, S, C);
+extern "C" int dpe_conv_w_flipT(const uint16_t* w, uint16_t* wt, int K, int R, int S, int C, int r0, int rs, int Rp,
+                                int s0, int ss, int Sp, hipStream_t st) {
+  if (Rp <= 0 || Sp <= 0 || r0 + rs * (Rp - 1) >= R || s0 + ss * (Sp - 1) >= S) return -1;
+  hipLaunchKernelGGL(conv_w_flipT_kernel, dim3(egrid((int64_t)K * Rp * Sp * C)), dim3(ET), 0, st, w, wt, K, R, S, C, r0, rs,
+                     Rp, s0, ss, Sp);
   return (int)hipGetLastError();
 }
 

@@ -493,7 +493,9 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
       u32x4 v = *(const u32x4*)(smem + rr * CROW + c * 16);
       int64_t orow = m;
       if (p.g.remap) {  // phase dgrad: virtual row (n, hh, ww) -> real dX pixel
-        const int ww = m % p.g.W, t = m / p.g.W, hh = t % p.g.H, nn = t / p.g.H;
+        // remap 1: dgrad-form geometry (virtual output = H x W); 2: forward-form (OH x OW)
+        const int VW = p.g.remap == 2 ? p.g.OW : p.g.W, VH = p.g.remap == 2 ? p.g.OH : p.g.H;
+        const int ww = m % VW, t = m / VW, hh = t % VH, nn = t / VH;
         orow = ((int64_t)nn * p.g.Hr + p.g.oa + p.g.psh * hh) * p.g.Wr + p.g.ob + p.g.psw * ww;
       }
       uint16_t* dst = C + orow * p.ldc + n;

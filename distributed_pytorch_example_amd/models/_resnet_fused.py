@@ -15,7 +15,8 @@ backward (dout)
     dW2 += dh2 (x) a1 ; da1 = dh2 . W2 (+ BN1 sums) ; dh1 = BN1'(da1; h1) ; dW1 += dh1 (x) x
     identity block:   dx = dh1 . W1 + dz3            (residual add fused in the dgrad epilogue)
     downsample block: dhd = BN_d'(dz3; hd); dW_d += dhd (x) x
-                      dx = dh1 . W1 + dhd . W_d      (second dgrad accumulates the first)
+                      dx = dh1 . W1 ; dx += dhd . W_d   (in place, only the parity the strided
+                                                         1x1 reaches is touched)
 
 (A variant that also fused BN1/BN2 + ReLU into the consumer convs' load
 prologues, never materialising a1/a2, measured slower on MI355X: the
@@ -141,8 +142,11 @@ class BottleneckFn(Function):
             if has_down:
                 dhd, _ = bn_bwd(3, dz3, None, hd, cd, False)
                 wgrad(3, dhd, x)
-                dxd = dgrad(3, dhd, list(x.shape))
-                dx = dgrad(0, dh1, list(x.shape), dxd)
+                dx = dgrad(0, dh1, list(x.shape))
+                # downsample branch accumulated in place: a strided 1x1 only reaches one
+                # output parity, the other three are never read or written
+                s, p, d = _conv_conf(convs[3].conv)
+                C.conv_dgrad_acc(dhd, ws[3], dx, s, p, d)
             else:
                 dx = dgrad(0, dh1, list(x.shape), dz3)
         elif has_down:

@@ -504,3 +504,19 @@ def test_s2d_stem_conv(C):
     wr = w16.float().permute(0, 3, 1, 2).requires_grad_(True)
     (gref,) = torch.autograd.grad(F.conv2d(xb, wr, None, 2, 3), wr, dy.float().permute(0, 3, 1, 2))
     assert rel_err(wp.grad, gref.permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,Ci,Co,k,s,p", [(2, 14, 14, 64, 128, 1, 2, 0), (2, 8, 8, 64, 64, 1, 1, 0),
+                                               (2, 14, 14, 32, 64, 3, 2, 1)])
+def test_conv_dgrad_acc_inplace(C, N, H, W, Ci, Co, k, s, p):
+    """dx += dgrad(dy, w) in place (strided: untouched parities keep their values)."""
+    torch.manual_seed(22)
+    x = torch.randn(N, Ci, H, W, device=dev, requires_grad=True)
+    w = bf(torch.randn(Co, k, k, Ci, device=dev) / math.sqrt(k * k * Ci))
+    y = F.conv2d(x, w.permute(0, 3, 1, 2).float(), None, s, p)
+    dy = bf(torch.randn_like(y))
+    (ref,) = torch.autograd.grad(y, x, dy.float())
+    base = bf(torch.randn(N, H, W, Ci, device=dev))
+    dx = base.clone()
+    C.conv_dgrad_acc(dy.permute(0, 2, 3, 1).contiguous(), w, dx, [s, s], [p, p], [1, 1])
+    assert rel_err(dx, base.float() + ref.permute(0, 2, 3, 1)) < 1e-2
