@@ -499,7 +499,8 @@ bool dgrad_as_fwd() {
 std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape,
                                     std::vector<int64_t> stride, std::vector<int64_t> pad, std::vector<int64_t> dil,
                                     const c10::optional<Tensor>& residual, const c10::optional<Tensor>& bn_x,
-                                    const c10::optional<Tensor>& bn_coef, const Tensor* acc_into = nullptr) {
+                                    const c10::optional<Tensor>& bn_coef, const Tensor* acc_into = nullptr,
+                                    const c10::optional<Tensor>& bn_mask = c10::nullopt) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(w); CHECK_CONTIG(dy); CHECK_CONTIG(w);
   // acc_into: dx += dgrad in place (the epilogue reads each element as its residual
   // right before overwriting it); parities no tap reaches are left untouched.
@@ -525,6 +526,12 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
     TORCH_CHECK(bn_coef->numel() == 4 * g.C, "conv_dgrad: bn_coef must be [4][C]");
     a.st_x = bp(*bn_x);
     a.st_coef = fp(*bn_coef);
+    if (bn_mask.has_value() && bn_mask->defined()) {
+      // BN + residual + ReLU: mask from the saved block output, dx stored already masked
+      CHECK_BF16((*bn_mask)); CHECK_CONTIG((*bn_mask));
+      TORCH_CHECK(bn_mask->sizes() == dx.sizes(), "conv_dgrad: bn_mask must have dx's shape");
+      a.st_mask = bp(*bn_mask);
+    }
   }
   Tensor part;
   auto tiles_of = [&](int64_t M, int64_t K) { const Cfg c = pick_cfg(M, g.C, K, false); return (M + c.bm - 1) / c.bm; };
@@ -727,8 +734,10 @@ Tensor bn_coef(const Tensor& stats, int64_t M, const c10::optional<Tensor>& gamm
 // Backward of y = relu(BN(x)) given the (sum dz, sum dz*(x-mean)) partials
 // [2][C][nb] produced by the dgrad epilogue that computed dy; the ReLU mask is
 // recomputed from x and the forward coefficients.  dgamma/dbeta accumulate.
+// relu_mask=false: dy is already dz (masked by its producer, see conv_dgrad_bn's mask).
 Tensor bn_bwd_partials(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& gamma, const Tensor& coef,
-                       const Tensor& partials, const c10::optional<Tensor>& dgamma, const c10::optional<Tensor>& dbeta) {
+                       const Tensor& partials, const c10::optional<Tensor>& dgamma, const c10::optional<Tensor>& dbeta,
+                       bool relu_mask) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_BF16(x);
   TORCH_CHECK(dy.sizes() == x.sizes(), "bn_bwd_partials: dy/x shape mismatch");
   const int64_t C = x.size(-1), M = rows_of(x);
@@ -738,7 +747,8 @@ Tensor bn_bwd_partials(const Tensor& dy, const Tensor& x, const c10::optional<Te
   CHECK_RC(dpe_bn_bwd_finalize(fp(partials), (int)partials.size(2), (int)C, M, fpo(gamma), fp(coef), fpom(dgamma),
                                fpom(dbeta), fp(bcoef), st), "bn_bwd_finalize");
   Tensor dx = at::empty_like(x);
-  CHECK_RC(dpe_bn_bwd_apply(bp(dy), nullptr, bp(x), fp(bcoef), bpm(dx), nullptr, M, (int)C, fp(coef), st), "bn_bwd_apply");
+  CHECK_RC(dpe_bn_bwd_apply(bp(dy), nullptr, bp(x), fp(bcoef), bpm(dx), nullptr, M, (int)C, relu_mask ? fp(coef) : nullptr, st),
+           "bn_bwd_apply");
   return dx;
 }
 
@@ -1004,15 +1014,18 @@ void register_ops(pybind11::module& m) {
         py::arg("dil"), "dx += data grad of conv(w) in place (parities without taps untouched)");
   m.def("conv_dgrad_bn", [](const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape, std::vector<int64_t> stride,
                             std::vector<int64_t> pad, std::vector<int64_t> dil, const c10::optional<Tensor>& residual,
-                            const c10::optional<Tensor>& bn_x, const c10::optional<Tensor>& bn_coef) {
-          return conv_dgrad_impl(dy, w, xshape, stride, pad, dil, residual, bn_x, bn_coef);
+                            const c10::optional<Tensor>& bn_x, const c10::optional<Tensor>& bn_coef,
+                            const c10::optional<Tensor>& bn_mask) {
+          return conv_dgrad_impl(dy, w, xshape, stride, pad, dil, residual, bn_x, bn_coef, nullptr, bn_mask);
         }, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"),
         py::arg("pad"), py::arg("dil"), py::arg("residual") = py::none(), py::arg("bn_x") = py::none(),
-        py::arg("bn_coef") = py::none());
+        py::arg("bn_coef") = py::none(), py::arg("bn_mask") = py::none(),
+        "data grad; with bn_x/bn_coef also the BN-backward partials of the BN+ReLU that produced the conv input; "
+        "with bn_mask (BN + residual + ReLU) the mask is bn_mask > 0 and dx is stored masked");
   m.def("bn_coef", &bn_coef, py::arg("stats"), py::arg("M"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("momentum"), py::arg("eps"));
   m.def("bn_bwd_partials", &bn_bwd_partials, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("coef"),
-        py::arg("partials"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
+        py::arg("partials"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none(), py::arg("relu_mask") = true);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), py::arg("residual") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),

@@ -516,7 +516,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
       if (p.col_stats) {
         float f[8];
         unpack8(v, f);
-        if constexpr (BNB) {  // (sum dz, sum dz*(x - mean)), dz = f * relu'(x*scale + shift)
+        if constexpr (BNB) {  // (sum dz, sum dz*(x - mean)), dz = f * relu'(...)
           float xv[8];
           if (vec) {
             unpack8(ld16(p.st_x + orow * p.ldc + n), xv);
@@ -524,11 +524,28 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) xv[e] = (n + e < p.N) ? bf2f(p.st_x[orow * p.ldc + n + e]) : 0.f;
           }
+          if (p.st_mask) {  // relu'(y) from the saved post-residual output; store dz itself
+            float yv[8];
+            if (vec) {
+              unpack8(ld16(p.st_mask + orow * p.ldc + n), yv);
+            } else {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float dz = fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? f[e] : 0.f;
-            s[e] += dz;
-            ss[e] += dz * (xv[e] - bmu[e]);
+              for (int e = 0; e < 8; ++e) yv[e] = (n + e < p.N) ? bf2f(p.st_mask[orow * p.ldc + n + e]) : 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              f[e] = yv[e] > 0.f ? f[e] : 0.f;
+              s[e] += f[e];
+              ss[e] += f[e] * (xv[e] - bmu[e]);
+            }
+            v = pack8(f);
+          } else {  // relu'(x*scale + shift), recomputed from the pre-BN input
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float dz = fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? f[e] : 0.f;
+              s[e] += dz;
+              ss[e] += dz * (xv[e] - bmu[e]);
+            }
           }
         } else {
 #pragma unroll

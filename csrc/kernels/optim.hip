@@ -28,69 +28,120 @@ struct TensorDesc {
 // Per group, 12 floats: lr, beta1/momentum, beta2/dampening, eps, weight_decay,
 // flags(bitfield: 1 nesterov, 2 maximize, 4 decoupled wd), grad_scale, pad...
 constexpr int HP = 12;
-constexpr int CHUNK = 65536;
+// 16K elements per block: 256 lanes x 4 (one 16-B access per operand) x 16
+// iterations.  Small enough that a 25M-parameter model spreads over ~1.6k
+// blocks (>6 per CU, so the streaming loads of several waves overlap), large
+// enough that the per-block descriptor fetch is noise.
+constexpr int CHUNK = 16384;
+
+// Per-element update rules (shared by the 16-B vector body and the scalar tail).
+struct AdamRule {
+  float lr, b1, b2, eps, wd, step_size, bc2_sqrt;
+  bool maximize, decoupled;
+  float gscale;
+  DPE_DEVICE AdamRule(const float* h, float step) {
+    lr = h[0]; b1 = h[1]; b2 = h[2]; eps = h[3]; wd = h[4];
+    const int flags = (int)h[5];
+    gscale = h[6];
+    maximize = flags & 2; decoupled = flags & 4;
+    step_size = lr / (1.f - powf(b1, step));
+    bc2_sqrt = sqrtf(1.f - powf(b2, step));
+  }
+  DPE_DEVICE void operator()(float& p, float g, float& m, float& v) const {
+    g *= gscale;
+    if (maximize) g = -g;
+    if (wd != 0.f) {
+      if (decoupled) p *= (1.f - lr * wd);
+      else g += wd * p;
+    }
+    m = m + (1.f - b1) * (g - m);  // lerp, as torch
+    v = b2 * v + (1.f - b2) * g * g;
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    p -= step_size * (m / denom);
+  }
+};
+
+struct SgdRule {
+  float lr, mom, damp, wd, gscale;
+  bool nesterov, maximize, first;
+  DPE_DEVICE SgdRule(const float* h, float step) {
+    lr = h[0]; mom = h[1]; damp = h[2]; wd = h[4];
+    const int flags = (int)h[5];
+    gscale = h[6];
+    nesterov = flags & 1; maximize = flags & 2;
+    first = step <= 1.f;
+  }
+  DPE_DEVICE void operator()(float& p, float g, float& b, float&) const {
+    g *= gscale;
+    if (wd != 0.f) g += wd * p;
+    if (mom != 0.f) {
+      b = first ? g : mom * b + (1.f - damp) * g;
+      g = nesterov ? g + mom * b : b;
+    }
+    p = maximize ? p + lr * g : p - lr * g;
+  }
+};
+
+// One (tensor, chunk) per block.  When every operand of the tensor is 16-B
+// aligned (8-B for the bf16 shadow) -- always the case for parameters and for
+// bucket-view gradients of 4-multiple sizes -- each lane moves 4 elements per
+// operand per iteration with dwordx4 loads/stores; otherwise (or for the
+// ragged tail) one element.  `s2` is only touched by rules that use it.
+template <class Rule, bool TWO_STATES>
+DPE_DEVICE void optim_chunk(const TensorDesc& d, const Rule& rule, int chunk) {
+  const int64_t beg = (int64_t)chunk * CHUNK;
+  const int64_t end = min(d.n, beg + CHUNK);
+  const bool has_s1 = d.s1 != nullptr;
+  const uintptr_t align = (uintptr_t)d.p | (uintptr_t)d.g | (uintptr_t)d.s1 | (TWO_STATES ? (uintptr_t)d.s2 : 0);
+  const bool vec = (align & 15) == 0 && ((uintptr_t)d.shadow & 7) == 0;
+  int64_t i = beg;
+  if (vec) {
+    const int64_t vend = beg + ((end - beg) & ~(int64_t)1023);
+    for (int64_t j = beg + threadIdx.x * 4; j < vend; j += 1024) {
+      f32x4 p = *(const f32x4*)(d.p + j);
+      const f32x4 g = *(const f32x4*)(d.g + j);
+      f32x4 m = has_s1 ? *(const f32x4*)(d.s1 + j) : f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 v = TWO_STATES ? *(const f32x4*)(d.s2 + j) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float pe = p[e], me = m[e], ve = v[e];
+        rule(pe, g[e], me, ve);
+        p[e] = pe; m[e] = me; v[e] = ve;
+      }
+      *(f32x4*)(d.p + j) = p;
+      if (has_s1) *(f32x4*)(d.s1 + j) = m;
+      if (TWO_STATES) *(f32x4*)(d.s2 + j) = v;
+      if (d.shadow) {
+        u32x2 sh;
+        sh[0] = pack_bf2(p[0], p[1]);
+        sh[1] = pack_bf2(p[2], p[3]);
+        *(u32x2*)(d.shadow + j) = sh;
+      }
+    }
+    i = vend;
+  }
+  for (int64_t j = i + threadIdx.x; j < end; j += 256) {
+    float p = d.p[j], m = has_s1 ? d.s1[j] : 0.f, v = TWO_STATES ? d.s2[j] : 0.f;
+    rule(p, d.g[j], m, v);
+    d.p[j] = p;
+    if (has_s1) d.s1[j] = m;
+    if (TWO_STATES) d.s2[j] = v;
+    if (d.shadow) d.shadow[j] = f2bf(p);
+  }
+}
 
 __global__ __launch_bounds__(256) void adam_kernel(const TensorDesc* __restrict__ td, const int2* __restrict__ chunks,
                                                    const float* __restrict__ hp, const float* __restrict__ steps) {
   const int2 ck = chunks[blockIdx.x];
   const TensorDesc d = td[ck.x];
-  const float* h = hp + d.group * HP;
-  const float lr = h[0], b1 = h[1], b2 = h[2], eps = h[3], wd = h[4];
-  const int flags = (int)h[5];
-  const float gscale = h[6];
-  const float step = steps[d.step_idx];
-  const float bc1 = 1.f - powf(b1, step);
-  const float bc2 = 1.f - powf(b2, step);
-  const float step_size = lr / bc1;
-  const float bc2_sqrt = sqrtf(bc2);
-  const bool maximize = flags & 2, decoupled = flags & 4;
-  const int64_t beg = (int64_t)ck.y * CHUNK;
-  const int64_t end = min(d.n, beg + CHUNK);
-  for (int64_t i = beg + threadIdx.x; i < end; i += 256) {
-    float g = d.g[i] * gscale;
-    if (maximize) g = -g;
-    float p = d.p[i];
-    if (wd != 0.f) {
-      if (decoupled) p *= (1.f - lr * wd);
-      else g += wd * p;
-    }
-    float m = d.s1[i], v = d.s2[i];
-    m = m + (1.f - b1) * (g - m);  // lerp, as torch
-    v = b2 * v + (1.f - b2) * g * g;
-    d.s1[i] = m;
-    d.s2[i] = v;
-    const float denom = sqrtf(v) / bc2_sqrt + eps;
-    p -= step_size * (m / denom);
-    d.p[i] = p;
-    if (d.shadow) d.shadow[i] = f2bf(p);
-  }
+  optim_chunk<AdamRule, true>(d, AdamRule(hp + d.group * HP, steps[d.step_idx]), ck.y);
 }
 
 __global__ __launch_bounds__(256) void sgd_kernel(const TensorDesc* __restrict__ td, const int2* __restrict__ chunks,
                                                   const float* __restrict__ hp, const float* __restrict__ steps) {
   const int2 ck = chunks[blockIdx.x];
   const TensorDesc d = td[ck.x];
-  const float* h = hp + d.group * HP;
-  const float lr = h[0], mom = h[1], damp = h[2], wd = h[4];
-  const int flags = (int)h[5];
-  const float gscale = h[6];
-  const bool nesterov = flags & 1, maximize = flags & 2;
-  const bool first = steps[d.step_idx] <= 1.f;
-  const int64_t beg = (int64_t)ck.y * CHUNK;
-  const int64_t end = min(d.n, beg + CHUNK);
-  for (int64_t i = beg + threadIdx.x; i < end; i += 256) {
-    float g = d.g[i] * gscale;
-    float p = d.p[i];
-    if (wd != 0.f) g += wd * p;
-    if (mom != 0.f) {
-      float b = first ? g : mom * d.s1[i] + (1.f - damp) * g;
-      d.s1[i] = b;
-      g = nesterov ? g + mom * b : b;
-    }
-    p = maximize ? p + lr * g : p - lr * g;
-    d.p[i] = p;
-    if (d.shadow) d.shadow[i] = f2bf(p);
-  }
+  optim_chunk<SgdRule, false>(d, SgdRule(hp + d.group * HP, steps[d.step_idx]), ck.y);
 }
 
 }  // namespace dpe

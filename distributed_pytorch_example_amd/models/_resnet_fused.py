@@ -18,6 +18,19 @@ backward (dout)
                       dx = dh1 . W1 ; dx += dhd . W_d   (in place, only the parity the strided
                                                          1x1 reaches is touched)
 
+Cross-block fusion of BN3's backward (DPE_BN3_CHAIN=1, default): block i's
+output ``out_i`` is consumed only by block i+1.  When block i+1 is an identity
+block, the epilogue of its first data-grad (dx = dh1 . W1 + dz3) also applies
+block i's ReLU mask (out_i > 0, i.e. relu'(BN3_i(h3_i) + idn_i)), stores the
+masked dz3_i directly, and emits BN3_i's backward partials (sum dz, sum
+dz*(h3_i - mean)).  Block i's BN3 backward is then ONE elementwise pass
+(dh3 = a*dz3 + b*h3 + c) instead of a reduce pass over (dout, out, h3) plus an
+apply pass that re-reads all three and writes dz3: three fewer full passes
+over the block's widest tensor.  The hand-off is a ``_BN3Link`` object filled
+by block i's forward and consumed by block i+1; if the gradient block i
+receives is not the tensor that epilogue produced, block i falls back to the
+standalone path (masking an already-masked gradient again is idempotent).
+
 (A variant that also fused BN1/BN2 + ReLU into the consumer convs' load
 prologues, never materialising a1/a2, measured slower on MI355X: the
 transform sits on the loaders' critical path and the inner BN tensors carry
@@ -40,6 +53,20 @@ from ..ops._state import grad_done, grad_sink, note_use, shadow
 
 # DPE_BN_EPI=0: inner BN backward through the standalone reduce kernel (A/B reference)
 _EPI_BNB = os.environ.get("DPE_BN_EPI", "1") != "0"
+# DPE_BN3_CHAIN=0: every block's BN3 backward through the standalone reduce + apply
+_BN3_CHAIN = _EPI_BNB and os.environ.get("DPE_BN3_CHAIN", "1") != "0"
+
+
+class _BN3Link:
+    """Block i's (h3, BN3 coefficients) handed to block i+1, and block i+1's
+    fused-epilogue result (BN3_i partials, identity of the masked dz3_i)
+    handed back to block i's backward."""
+
+    __slots__ = ("h3", "coef", "part", "dz_ptr", "dz_shape")
+
+    def __init__(self):
+        self.h3 = self.coef = self.part = None
+        self.dz_ptr, self.dz_shape = 0, None
 
 
 def _conv_conf(conv):
@@ -48,7 +75,7 @@ def _conv_conf(conv):
 
 class BottleneckFn(Function):
     @staticmethod
-    def forward(ctx, x, block, *params):
+    def forward(ctx, x, block, link_in, link_out, *params):
         C = ext()
         convs = [block.c1, block.c2, block.c3] + ([block.down] if block.down is not None else [])
         ws = [shadow(cb.conv.weight) for cb in convs]
@@ -70,6 +97,12 @@ class BottleneckFn(Function):
         h2, a2, c2 = convbn(1, a1, True)
         h3, out, c3 = convbn(2, a2, True, idn)
         ctx.save_for_backward(x, h1, a1, h2, a2, h3, out, hd, c1, c2, c3, cd)
+        # previous block's BN3 is fused into this block's first data grad (identity blocks only:
+        # a downsample block's dx is completed by a second, strided kernel)
+        ctx.link_in = link_in if (link_in is not None and block.down is None and link_in.h3 is not None) else None
+        ctx.link_out = link_out
+        if link_out is not None:
+            link_out.h3, link_out.coef = h3, c3
         ctx.block = block
         ctx.convs = convs
         ctx.ws = ws
@@ -131,7 +164,18 @@ class BottleneckFn(Function):
             bn_done(bn, gb, gd, bb, bd)
             return dh
 
-        dh3, dz3 = bn_bwd(2, dout, out, h3, c3, True)
+        lk = ctx.link_out
+        if lk is not None and lk.part is not None and lk.dz_ptr == dout.data_ptr() and lk.dz_shape == tuple(dout.shape):
+            # the next block's dgrad epilogue already produced dz3 = dout*relu'(out) and BN3's partials
+            dz3 = dout
+            bn, gb, gd, bb, bd = bn_sinks(2)
+            dh3 = C.bn_bwd_partials(dz3, h3, bn.weight.detach(), c3, lk.part, gb, bb, relu_mask=False)
+            bn_done(bn, gb, gd, bb, bd)
+            lk.part = None
+        else:
+            dh3, dz3 = bn_bwd(2, dout, out, h3, c3, True)
+        if lk is not None:
+            lk.h3 = lk.coef = None
         wgrad(2, dh3, a2)
         dh2 = dgrad_bnb(2, dh3, 1, a2, h2, c2)
         wgrad(1, dh2, a1)
@@ -147,17 +191,27 @@ class BottleneckFn(Function):
                 # output parity, the other three are never read or written
                 s, p, d = _conv_conf(convs[3].conv)
                 C.conv_dgrad_acc(dhd, ws[3], dx, s, p, d)
+            elif ctx.link_in is not None:
+                li = ctx.link_in
+                s, p, d = _conv_conf(convs[0].conv)
+                dx, part = C.conv_dgrad_bn(dh1, ws[0], list(x.shape), s, p, d, dz3, li.h3, li.coef, x)
+                li.part, li.dz_ptr, li.dz_shape = part, dx.data_ptr(), tuple(dx.shape)
             else:
                 dx = dgrad(0, dh1, list(x.shape), dz3)
         elif has_down:
             dhd, _ = bn_bwd(3, dz3, None, hd, cd, False)
             wgrad(3, dhd, x)
         pgrads = [grads.get(id(p)) for p in ctx.block._fused_params]
-        return (dx, None, *pgrads)
+        return (dx, None, None, None, *pgrads)
 
 
-def bottleneck_forward(block, x):
+def bottleneck_forward(block, x, link_in=None, chain=False):
+    """Fused block forward.  ``chain=True`` (the ResNet's own block loop, where
+    this block's output feeds only the next block) returns ``(out, link)`` for
+    the next block's ``link_in``."""
     params = block._fused_params
     nbt = [cb.bn.num_batches_tracked for cb in [block.c1, block.c2, block.c3] + ([block.down] if block.down is not None else [])]
     torch._foreach_add_(nbt, 1)
-    return BottleneckFn.apply(x, block, *params)
+    link_out = _BN3Link() if (chain and _BN3_CHAIN) else None
+    out = BottleneckFn.apply(x, block, link_in if _BN3_CHAIN else None, link_out, *params)
+    return (out, link_out) if chain else out

@@ -54,10 +54,19 @@ class Bottleneck(nn.Module):
         self.fused = True
 
     def forward(self, x):
+        return self.forward_chained(x, None, chain=False)
+
+    def forward_chained(self, x, link=None, chain=True):
+        """``chain=True``: returns (out, link); the link lets the next block's
+        backward fuse this block's BN3 backward (``_resnet_fused``)."""
         if x.is_cuda and self.training and self.fused:
             from ._resnet_fused import bottleneck_forward
 
-            return bottleneck_forward(self, x)
+            return bottleneck_forward(self, x, link, chain)
+        out = self._forward_per_op(x)
+        return (out, None) if chain else out
+
+    def _forward_per_op(self, x):
         idn = self.down(x, relu=False) if self.down is not None else x
         h = self.c1(x)
         h = self.c2(h)
@@ -102,7 +111,9 @@ class ResNet(nn.Module):
                 x = Fx.to_nhwc_input(x, self.in_pad)
             h = self.stem(x)
         h = Fx.max_pool2d_nhwc(h, 3, 2, 1)
-        h = self.blocks(h)
+        link = None
+        for blk in self.blocks:  # each block's output feeds only the next block
+            h, link = blk.forward_chained(h, link)
         h = Fx.global_avg_pool_nhwc(h)
         return self.fc(h)
 

@@ -2,6 +2,8 @@
 """Per-shape timing of the ResNet-50 convolutions (batch B): our gfx950
 implicit-GEMM kernels vs MIOpen (torch channels_last bf16) for fwd / dgrad /
 wgrad.  Random non-zero data; CUDA-event timing, median of N reps."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import argparse
 import json
 import statistics

@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
 """Run ONE conv pass shape repeatedly (for rocprofv3 PMC collection)."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import sys, torch
 from distributed_pytorch_example_amd.ops import ext
 C = ext()

@@ -1,4 +1,6 @@
 # bf16-vs-fp32 gradient agreement as a function of batch size (noise should shrink ~1/sqrt(rows))
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import copy, torch
 from distributed_pytorch_example_amd.models import get_model
 from distributed_pytorch_example_amd.ops import functional as Fx
