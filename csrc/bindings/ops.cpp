@@ -30,6 +30,14 @@ int dpe_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, c
                      uint16_t* dz_out, int64_t M, int C, const float* mcoef, hipStream_t st);
 int dpe_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int k, int s,
                     int p, hipStream_t st);
+int dpe_bn_apply2(const uint16_t* x, const float* coef, const uint16_t* x2, const float* coef2, uint16_t* y, int64_t M, int C,
+                  int relu, hipStream_t st);
+int dpe_bnrelu_maxpool_fwd(const uint16_t* h, const float* coef, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH,
+                           int OW, int k, int s, int p, hipStream_t st);
+int dpe_maxpool_bn_bwd_reduce(const uint16_t* dy, const uint8_t* idx, const uint16_t* x, const float* coef, int N, int H, int W,
+                              int C, int OH, int OW, int k, int s, int p, int nb, float* part, hipStream_t st);
+int dpe_maxpool_bn_bwd_apply(const uint16_t* dy, const uint8_t* idx, const uint16_t* x, const float* coef, const float* bcoef,
+                             uint16_t* dx, int N, int H, int W, int C, int OH, int OW, int k, int s, int p, hipStream_t st);
 int dpe_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int OH, int OW, int k,
                     int s, int p, hipStream_t st);
 int dpe_gavgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st);
@@ -773,6 +781,58 @@ Tensor maxpool_bwd(const Tensor& dy, const Tensor& idx, std::vector<int64_t> xsh
   return dx;
 }
 
+// y = act(BN(x; coef) + BN(x2; coef2)) in one pass (bottleneck output with a BN'd downsample branch)
+Tensor bn_apply2(const Tensor& x, const Tensor& coef, const Tensor& x2, const Tensor& coef2, bool relu) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(x2); CHECK_CONTIG(x2); CHECK_F32(coef); CHECK_F32(coef2);
+  TORCH_CHECK(x.sizes() == x2.sizes(), "bn_apply2: x/x2 shape mismatch");
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(C % 8 == 0 && coef.numel() == 4 * C && coef2.numel() == 4 * C, "bn_apply2: coef must be [4][C], C % 8 == 0");
+  Tensor y = at::empty_like(x);
+  CHECK_RC(dpe_bn_apply2(bp(x), fp(coef), bp(x2), fp(coef2), bpm(y), rows_of(x), (int)C, relu ? 1 : 0, cur_stream()),
+           "bn_apply2");
+  return y;
+}
+
+// Stem fusion: maxpool(relu(BN(h))) with BN coefficients `coef` [4][C] (bn_coef);
+// the BN+ReLU output is never materialised.  Returns (pooled, argmax bytes).
+std::vector<Tensor> bnrelu_maxpool_fwd(const Tensor& h, const Tensor& coef, int64_t k, int64_t s, int64_t p) {
+  CHECK_GPU(h); CHECK_BF16(h); CHECK_CONTIG(h); CHECK_F32(coef);
+  const int64_t N = h.size(0), H = h.size(1), W = h.size(2), C = h.size(3);
+  TORCH_CHECK(coef.numel() == 4 * C, "bnrelu_maxpool_fwd: coef must be [4][C]");
+  const int64_t OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
+  Tensor y = at::empty({N, OH, OW, C}, h.options());
+  Tensor idx = at::empty({N, OH, OW, C}, h.options().dtype(at::kByte));
+  CHECK_RC(dpe_bnrelu_maxpool_fwd(bp(h), fp(coef), bpm(y), (uint8_t*)idx.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)OH,
+                                  (int)OW, (int)k, (int)s, (int)p, cur_stream()), "bnrelu_maxpool_fwd");
+  return {y, idx};
+}
+
+// Backward of the fused stem: dh = BN'(relu'(h) * maxpool'(dy)); dgamma/dbeta accumulate.
+Tensor maxpool_bn_bwd(const Tensor& dy, const Tensor& idx, const Tensor& h, const c10::optional<Tensor>& gamma,
+                      const Tensor& coef, const c10::optional<Tensor>& dgamma, const c10::optional<Tensor>& dbeta, int64_t k,
+                      int64_t s, int64_t p) {
+  CHECK_GPU(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(h); CHECK_CONTIG(h); CHECK_F32(coef);
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.sizes() == dy.sizes(), "maxpool_bn_bwd: idx must be uint8 of dy's shape");
+  const int64_t N = h.size(0), H = h.size(1), W = h.size(2), C = h.size(3);
+  TORCH_CHECK(dy.size(0) == N && dy.size(3) == C, "maxpool_bn_bwd: dy/h shape mismatch");
+  const int64_t M = N * H * W;
+  hipStream_t st = cur_stream();
+  auto fo = h.options().dtype(at::kFloat);
+  const int nb = dpe_bn_stats_nblocks(M, (int)C);
+  Tensor part = at::empty({2, C, nb}, fo);
+  CHECK_RC(dpe_maxpool_bn_bwd_reduce(bp(dy), (const uint8_t*)idx.data_ptr(), bp(h), fp(coef), (int)N, (int)H, (int)W, (int)C,
+                                     (int)dy.size(1), (int)dy.size(2), (int)k, (int)s, (int)p, nb, fp(part), st),
+           "maxpool_bn_bwd_reduce");
+  Tensor bcoef = at::empty({3, C}, fo);
+  CHECK_RC(dpe_bn_bwd_finalize(fp(part), nb, (int)C, M, fpo(gamma), fp(coef), fpom(dgamma), fpom(dbeta), fp(bcoef), st),
+           "bn_bwd_finalize");
+  Tensor dh = at::empty_like(h);
+  CHECK_RC(dpe_maxpool_bn_bwd_apply(bp(dy), (const uint8_t*)idx.data_ptr(), bp(h), fp(coef), fp(bcoef), bpm(dh), (int)N,
+                                    (int)H, (int)W, (int)C, (int)dy.size(1), (int)dy.size(2), (int)k, (int)s, (int)p, st),
+           "maxpool_bn_bwd_apply");
+  return dh;
+}
+
 Tensor gavgpool_fwd(const Tensor& x) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x);
   const int64_t N = x.size(0), C = x.size(-1), HW = x.numel() / (N * C);
@@ -1024,6 +1084,10 @@ void register_ops(pybind11::module& m) {
         "with bn_mask (BN + residual + ReLU) the mask is bn_mask > 0 and dx is stored masked");
   m.def("bn_coef", &bn_coef, py::arg("stats"), py::arg("M"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("momentum"), py::arg("eps"));
+  m.def("bn_apply2", &bn_apply2, py::arg("x"), py::arg("coef"), py::arg("x2"), py::arg("coef2"), py::arg("relu"));
+  m.def("bnrelu_maxpool_fwd", &bnrelu_maxpool_fwd, py::arg("h"), py::arg("coef"), py::arg("k"), py::arg("s"), py::arg("p"));
+  m.def("maxpool_bn_bwd", &maxpool_bn_bwd, py::arg("dy"), py::arg("idx"), py::arg("h"), py::arg("gamma"), py::arg("coef"),
+        py::arg("dgamma"), py::arg("dbeta"), py::arg("k"), py::arg("s"), py::arg("p"));
   m.def("bn_bwd_partials", &bn_bwd_partials, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("coef"),
         py::arg("partials"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none(), py::arg("relu_mask") = true);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"), py::arg("pad"),

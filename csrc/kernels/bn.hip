@@ -135,6 +135,29 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const uint16_t* __restri
   }
 }
 
+// y = act(x*scale + shift + x2*scale2 + shift2): a bottleneck's BN3 output plus its
+// BN'd downsample branch in one pass (the downsample BN output is never stored).
+__global__ __launch_bounds__(BN_T) void bn_apply2_kernel(const uint16_t* __restrict__ x, const float* __restrict__ coef,
+                                                         const uint16_t* __restrict__ x2, const float* __restrict__ coef2,
+                                                         uint16_t* __restrict__ y, int64_t nchunks, int C, int relu) {
+  const int CPR = C >> 3;
+  for (int64_t i = blockIdx.x * (int64_t)BN_T + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * BN_T) {
+    const int c8 = (int)(i % CPR) * 8;
+    float f[8], g[8];
+    unpack8(*(const u32x4*)(x + i * 8), f);
+    unpack8(*(const u32x4*)(x2 + i * 8), g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      // the residual is rounded to bf16 first, as when it is materialised
+      const float r = bf2f(f2bf(fmaf(g[e], coef2[c8 + e], coef2[C + c8 + e])));
+      float v = fmaf(f[e], coef[c8 + e], coef[C + c8 + e]) + r;
+      if (relu) v = fmaxf(v, 0.f);
+      f[e] = v;
+    }
+    *(u32x4*)(y + i * 8) = pack8(f);
+  }
+}
+
 // partial sums of dz and dz*(x-mean), dz = dy * (y > 0 if relu)
 __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
                                                              const uint16_t* __restrict__ x, const float* __restrict__ coef,
@@ -271,6 +294,13 @@ extern "C" int dpe_bn_apply(const uint16_t* x, const uint16_t* res, uint16_t* y,
                             int relu, hipStream_t st) {
   const int64_t nch = M * C / 8;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, res, y, nch, C, coef, relu);
+  return 0;
+}
+
+extern "C" int dpe_bn_apply2(const uint16_t* x, const float* coef, const uint16_t* x2, const float* coef2, uint16_t* y,
+                             int64_t M, int C, int relu, hipStream_t st) {
+  const int64_t nch = M * C / 8;
+  hipLaunchKernelGGL(bn_apply2_kernel, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, coef, x2, coef2, y, nch, C, relu);
   return 0;
 }
 

@@ -4,9 +4,13 @@
 
 namespace dpe {
 
+// coef != nullptr: the input is the PRE-BatchNorm stem output h and each tap is
+// relu(h*scale + shift) rounded to bf16 exactly as a materialised BN output
+// would be -- the BN+ReLU tensor is never written (stem fusion).
+template <bool BNRELU>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                           uint8_t* __restrict__ idx, int N, int H, int W, int C, int OH,
-                                                          int OW, int k, int s, int p) {
+                                                          int OW, int k, int s, int p, const float* __restrict__ coef) {
   const int CPR = C >> 3;
   const int64_t total = (int64_t)N * OH * OW * CPR;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
@@ -15,6 +19,11 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
     const int ow = (int)(t % OW); t /= OW;
     const int oh = (int)(t % OH);
     const int n = (int)(t / OH);
+    float sc[8], sh[8];
+    if constexpr (BNRELU) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sc[e] = coef[c8 + e]; sh[e] = coef[C + c8 + e]; }
+    }
     float best[8];
     uint8_t bi[8];
 #pragma unroll
@@ -27,6 +36,10 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
         if ((unsigned)iw >= (unsigned)W) continue;
         float f[8];
         unpack8(*(const u32x4*)(x + (((int64_t)n * H + ih) * W + iw) * C + c8), f);
+        if constexpr (BNRELU) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = bf2f(f2bf(fmaxf(fmaf(f[e], sc[e], sh[e]), 0.f)));
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (f[e] > best[e]) { best[e] = f[e]; bi[e] = (uint8_t)(r * k + q); }
@@ -37,6 +50,34 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
     pk[0] = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
     pk[1] = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
     *(u32x2*)(idx + i * 8) = pk;
+  }
+}
+
+// d(pool input)[n,h,w,c8..c8+7]: sum of dy over the windows containing (h, w) whose argmax it is
+DPE_DEVICE void pool_grad8(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ idx, int n, int h, int w, int c8,
+                           int C, int OH, int OW, int k, int s, int p, float* acc) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  // oh*s - p <= h <= oh*s - p + k - 1
+  const int oh_lo = max(0, (h + p - k + s) / s), oh_hi = min(OH - 1, (h + p) / s);
+  const int ow_lo = max(0, (w + p - k + s) / s), ow_hi = min(OW - 1, (w + p) / s);
+  for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+    const int r = h - (oh * s - p);
+    if (r < 0 || r >= k) continue;
+    for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+      const int q = w - (ow * s - p);
+      if (q < 0 || q >= k) continue;
+      const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c8;
+      const u32x2 pk = *(const u32x2*)(idx + o);
+      float g[8];
+      unpack8(*(const u32x4*)(dy + o), g);
+      const uint8_t want = (uint8_t)(r * k + q);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint8_t b = (uint8_t)((pk[e >> 2] >> ((e & 3) * 8)) & 0xff);
+        if (b == want) acc[e] += g[e];
+      }
+    }
   }
 }
 
@@ -53,30 +94,86 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __rest
     const int h = (int)(t % H);
     const int n = (int)(t / H);
     float acc[8];
+    pool_grad8(dy, idx, n, h, w, c8, C, OH, OW, k, s, p, acc);
+    *(u32x4*)(dx + i * 8) = pack8(acc);
+  }
+}
+
+// ---- stem backward: maxpool gather + BN(+ReLU) backward without materialising d(BN output)
+// reduce: per-block partials [2][C][nb] of (sum dz, sum dz*(x - mean)), dz = gather * [x*scale+shift > 0]
+__global__ __launch_bounds__(256) void maxpool_bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy,
+                                                                    const uint8_t* __restrict__ idx,
+                                                                    const uint16_t* __restrict__ x,
+                                                                    const float* __restrict__ coef, int N, int H, int W,
+                                                                    int C, int OH, int OW, int k, int s, int p,
+                                                                    int64_t rows_per_block, float* __restrict__ part) {
+  const int CPR = C >> 3;
+  const int tid = threadIdx.x;
+  const int RPI = 256 / CPR;
+  const int c = tid % CPR, r = tid / CPR;
+  const int64_t M = (int64_t)N * H * W;
+  const int64_t rb = blockIdx.x * rows_per_block;
+  const int64_t re = min(M, rb + rows_per_block);
+  float sm[8], sq[8], mean[8], sc[8], sh[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-    // oh*s - p <= h <= oh*s - p + k - 1
-    const int oh_lo = max(0, (h + p - k + s) / s), oh_hi = min(OH - 1, (h + p) / s);
-    const int ow_lo = max(0, (w + p - k + s) / s), ow_hi = min(OW - 1, (w + p) / s);
-    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-      const int r = h - (oh * s - p);
-      if (r < 0 || r >= k) continue;
-      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        const int q = w - (ow * s - p);
-        if (q < 0 || q >= k) continue;
-        const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c8;
-        const u32x2 pk = *(const u32x2*)(idx + o);
-        float g[8];
-        unpack8(*(const u32x4*)(dy + o), g);
-        const uint8_t want = (uint8_t)(r * k + q);
+  for (int e = 0; e < 8; ++e) {
+    sm[e] = 0.f; sq[e] = 0.f;
+    sc[e] = coef[c * 8 + e]; sh[e] = coef[C + c * 8 + e]; mean[e] = coef[2 * C + c * 8 + e];
+  }
+  if (r < RPI) {
+    for (int64_t row = rb + r; row < re; row += RPI) {
+      const int w = (int)(row % W);
+      const int64_t t = row / W;
+      const int h = (int)(t % H), n = (int)(t / H);
+      float d[8], xv[8];
+      pool_grad8(dy, idx, n, h, w, c * 8, C, OH, OW, k, s, p, d);
+      unpack8(*(const u32x4*)(x + row * C + c * 8), xv);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const uint8_t b = (uint8_t)((pk[e >> 2] >> ((e & 3) * 8)) & 0xff);
-          if (b == want) acc[e] += g[e];
-        }
+      for (int e = 0; e < 8; ++e) {
+        const float dz = fmaf(xv[e], sc[e], sh[e]) > 0.f ? d[e] : 0.f;
+        sm[e] += dz;
+        sq[e] += dz * (xv[e] - mean[e]);
       }
     }
-    *(u32x4*)(dx + i * 8) = pack8(acc);
+  }
+  __shared__ float red[2][256][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][tid][e] = sm[e]; red[1][tid][e] = sq[e]; }
+  __syncthreads();
+  for (int ch = tid; ch < C; ch += 256) {
+    const int cc = ch >> 3, e = ch & 7;
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < RPI; ++rr) { a += red[0][rr * CPR + cc][e]; b += red[1][rr * CPR + cc][e]; }
+    part[(int64_t)ch * gridDim.x + blockIdx.x] = a;
+    part[(int64_t)(C + ch) * gridDim.x + blockIdx.x] = b;
+  }
+}
+
+// apply: dx = a*dz + b*x + c   (bcoef [3][C] from bn_bwd_finalize)
+__global__ __launch_bounds__(256) void maxpool_bn_bwd_apply_kernel(const uint16_t* __restrict__ dy,
+                                                                   const uint8_t* __restrict__ idx,
+                                                                   const uint16_t* __restrict__ x,
+                                                                   const float* __restrict__ coef,
+                                                                   const float* __restrict__ bcoef,
+                                                                   uint16_t* __restrict__ dx, int N, int H, int W, int C,
+                                                                   int OH, int OW, int k, int s, int p) {
+  const int CPR = C >> 3;
+  const int64_t total = (int64_t)N * H * W * CPR;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c8 = (int)(i % CPR) * 8;
+    int64_t t = i / CPR;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float d[8], xv[8], o[8];
+    pool_grad8(dy, idx, n, h, w, c8, C, OH, OW, k, s, p, d);
+    unpack8(*(const u32x4*)(x + i * 8), xv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float dz = fmaf(xv[e], coef[c8 + e], coef[C + c8 + e]) > 0.f ? d[e] : 0.f;
+      o[e] = bcoef[c8 + e] * dz + bcoef[C + c8 + e] * xv[e] + bcoef[2 * C + c8 + e];
+    }
+    *(u32x4*)(dx + i * 8) = pack8(o);
   }
 }
 
@@ -132,8 +229,36 @@ static int gs(int64_t n) {
 extern "C" int dpe_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH, int OW,
                                int k, int s, int p, hipStream_t st) {
   if (C % 8 || k * k > 255) return -1;
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(gs((int64_t)N * OH * OW * C / 8)), dim3(256), 0, st, x, y, idx, N, H, W, C,
-                     OH, OW, k, s, p);
+  hipLaunchKernelGGL(maxpool_fwd_kernel<false>, dim3(gs((int64_t)N * OH * OW * C / 8)), dim3(256), 0, st, x, y, idx, N, H, W,
+                     C, OH, OW, k, s, p, nullptr);
+  return 0;
+}
+
+extern "C" int dpe_bnrelu_maxpool_fwd(const uint16_t* h, const float* coef, uint16_t* y, uint8_t* idx, int N, int H, int W,
+                                      int C, int OH, int OW, int k, int s, int p, hipStream_t st) {
+  if (C % 8 || k * k > 255) return -1;
+  hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3(gs((int64_t)N * OH * OW * C / 8)), dim3(256), 0, st, h, y, idx, N, H, W,
+                     C, OH, OW, k, s, p, coef);
+  return 0;
+}
+
+extern "C" int dpe_maxpool_bn_bwd_reduce(const uint16_t* dy, const uint8_t* idx, const uint16_t* x, const float* coef, int N,
+                                         int H, int W, int C, int OH, int OW, int k, int s, int p, int nb, float* part,
+                                         hipStream_t st) {
+  if (C % 8 || C / 8 > 256) return -1;
+  const int64_t M = (int64_t)N * H * W;
+  const int64_t rpb = (M + nb - 1) / nb;
+  hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, st, dy, idx, x, coef, N, H, W, C, OH, OW, k, s, p,
+                     rpb, part);
+  return 0;
+}
+
+extern "C" int dpe_maxpool_bn_bwd_apply(const uint16_t* dy, const uint8_t* idx, const uint16_t* x, const float* coef,
+                                        const float* bcoef, uint16_t* dx, int N, int H, int W, int C, int OH, int OW, int k,
+                                        int s, int p, hipStream_t st) {
+  if (C % 8) return -1;
+  hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel, dim3(gs((int64_t)N * H * W * C / 8)), dim3(256), 0, st, dy, idx, x, coef,
+                     bcoef, dx, N, H, W, C, OH, OW, k, s, p);
   return 0;
 }
 

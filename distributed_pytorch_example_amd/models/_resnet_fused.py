@@ -3,10 +3,11 @@
 One autograd node per block instead of ~12 per-op nodes:
 
 forward  (x NHWC bf16)
-    [hd = conv_d(x)  -> idn = BN_d(hd)]                          (downsample blocks)
+    [hd = conv_d(x)]                                             (downsample blocks)
     h1 = conv1(x)  -> a1 = relu(BN1(h1))      BN statistics come from the conv epilogue
     h2 = conv2(a1) -> a2 = relu(BN2(h2))
-    h3 = conv3(a2) -> out = relu(BN3(h3) + idn)
+    h3 = conv3(a2) -> out = relu(BN3(h3) + idn)    idn = x, or BN_d(hd) computed inside
+                                                   the same pass (never stored)
 backward (dout)
     dh3, dz3 = BN3'(dout; out, h3)            dz3 = dout*relu'(out) is also d(idn)
     dW3 += dh3 (x) a2 ;  da2 = dh3 . W3       the dgrad epilogue also emits BN2's backward
@@ -89,13 +90,26 @@ class BottleneckFn(Function):
                                      bn.momentum, bn.eps, relu, residual, st)
             return h, y, coef
 
+        def conv_coef(i, inp):
+            cb = convs[i]
+            s, p, d = _conv_conf(cb.conv)
+            h, st = C.conv_fwd(inp, ws[i], s, p, d, True, None)
+            bn = cb.bn
+            M = h.numel() // h.shape[-1]
+            return h, C.bn_coef(st, M, bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var, bn.momentum,
+                                bn.eps)
+
         if block.down is not None:
-            hd, idn, cd = convbn(3, x, False)
+            hd, cd = conv_coef(3, x)  # BN_d is applied inside BN3's pass (bn_apply2)
         else:
-            hd, idn, cd = None, x, None
+            hd, cd = None, None
         h1, a1, c1 = convbn(0, x, True)
         h2, a2, c2 = convbn(1, a1, True)
-        h3, out, c3 = convbn(2, a2, True, idn)
+        if block.down is not None:
+            h3, c3 = conv_coef(2, a2)
+            out = C.bn_apply2(h3, c3, hd, cd, True)
+        else:
+            h3, out, c3 = convbn(2, a2, True, x)
         ctx.save_for_backward(x, h1, a1, h2, a2, h3, out, hd, c1, c2, c3, cd)
         # previous block's BN3 is fused into this block's first data grad (identity blocks only:
         # a downsample block's dx is completed by a second, strided kernel)

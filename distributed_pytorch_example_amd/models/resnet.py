@@ -9,7 +9,10 @@ Execution is MI355X-native:
   (sum, sum^2) in its GEMM epilogue, so the BN statistics pass is skipped;
 * BN apply fuses ReLU and the residual add (one pass per BN);
 * the 7x7/s2 stem runs as a 4x4/s1 conv over a space-to-depth packed input
-  ([N,112,112,16]: 35% fewer MFMA k-steps than an 8-channel-padded 7x7).
+  ([N,112,112,16]: 35% fewer MFMA k-steps than an 8-channel-padded 7x7);
+  its BN + ReLU are applied inside the max-pool (never materialised);
+* each block's BN3 backward is fused into the next block's data-grad
+  epilogue (``_resnet_fused``).
 """
 from __future__ import annotations
 
@@ -79,6 +82,8 @@ class ResNet(nn.Module):
         self.in_pad = in_pad
         # GPU: 7x7/s2 stem as a 4x4/s1 conv over a space-to-depth input (DPE_S2D_STEM=0: NHWC-8 stem)
         self.s2d_stem = in_chans <= 4 and os.environ.get("DPE_S2D_STEM", "1") != "0"
+        # GPU training: stem BN + ReLU fused into the max-pool (DPE_FUSED_STEM=0: separate passes)
+        self.fused_stem = os.environ.get("DPE_FUSED_STEM", "1") != "0"
         self.stem = ConvBN(in_chans, 64, 7, 2, 3)
         blocks = []
         inplanes = 64
@@ -101,16 +106,20 @@ class ResNet(nn.Module):
                 x = x[..., :4].reshape(n, hh // 2, 2, ww // 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(
                     n, hh // 2, ww // 2, 16)
             bn = self.stem.bn
-            if bn.training:
+            if bn.training and self.fused_stem:
+                # BN statistics from the conv epilogue; BN + ReLU applied inside the max-pool
                 y, st = Fx.stem_conv_s2d(x, self.stem.conv.weight, want_stats=True)
+                h = Fx.stem_bn_relu_maxpool(y, bn, st, 3, 2, 1)
             else:
-                y, st = Fx.stem_conv_s2d(x, self.stem.conv.weight), None
-            h = bn(y, relu=True, stats=st)
+                if bn.training:
+                    y, st = Fx.stem_conv_s2d(x, self.stem.conv.weight, want_stats=True)
+                else:
+                    y, st = Fx.stem_conv_s2d(x, self.stem.conv.weight), None
+                h = Fx.max_pool2d_nhwc(bn(y, relu=True, stats=st), 3, 2, 1)
         else:
             if x.dim() == 4 and x.shape[1] != self.in_pad and x.shape[-1] != self.in_pad:
                 x = Fx.to_nhwc_input(x, self.in_pad)
-            h = self.stem(x)
-        h = Fx.max_pool2d_nhwc(h, 3, 2, 1)
+            h = Fx.max_pool2d_nhwc(self.stem(x), 3, 2, 1)
         link = None
         for blk in self.blocks:  # each block's output feeds only the next block
             h, link = blk.forward_chained(h, link)

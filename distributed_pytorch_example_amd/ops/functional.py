@@ -399,6 +399,43 @@ def batch_norm_nhwc(x, gamma, beta, running_mean, running_var, training: bool, m
                              residual.contiguous() if residual is not None else None)
 
 
+class _StemBNReluPoolFn(Function):
+    """maxpool(relu(BN(h))) for the ResNet stem with training-mode BN whose
+    statistics came from the conv epilogue: the BN+ReLU output (the largest
+    activation of the network) is never written or re-read; the backward
+    gathers the pooled gradient per element inside the BN-backward passes."""
+
+    @staticmethod
+    def forward(ctx, h, gamma, beta, rmean, rvar, momentum, eps, stats, k, s, p):
+        C = ext()
+        M = h.numel() // h.shape[-1]
+        coef = C.bn_coef(stats, M, gamma.detach(), beta.detach(), rmean, rvar, momentum, eps)
+        y, idx = C.bnrelu_maxpool_fwd(h, coef, k, s, p)
+        ctx.save_for_backward(h, idx, coef)
+        ctx.gamma, ctx.beta, ctx.conf = gamma, beta, (k, s, p)
+        note_use(gamma)
+        note_use(beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, idx, coef = ctx.saved_tensors
+        gbuf, gdirect = grad_sink(ctx.gamma)
+        bbuf, bdirect = grad_sink(ctx.beta)
+        dh = ext().maxpool_bn_bwd(dy.contiguous(), idx, h, ctx.gamma.detach(), coef, gbuf, bbuf, *ctx.conf)
+        grad_done(ctx.gamma, gdirect)
+        grad_done(ctx.beta, bdirect)
+        return (dh, None if gdirect else gbuf, None if bdirect else bbuf) + (None,) * 8
+
+
+def stem_bn_relu_maxpool(h, bn, stats, kernel_size=3, stride=2, padding=1):
+    """max_pool2d(relu(bn(h))) in training mode from conv-epilogue statistics (GPU)."""
+    if bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    return _StemBNReluPoolFn.apply(h.contiguous(), bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps,
+                                   stats, kernel_size, stride, padding)
+
+
 # ================================================================== pooling
 class _MaxPoolFn(Function):
     @staticmethod

@@ -93,12 +93,25 @@ def _w_buffers(rank, world, port, q):
     torch.manual_seed(rank + 11)
     out = ddp(torch.randn(2, 3, 32, 32))
     out.sum().backward()
-    # forward 2 broadcasts rank 0's running stats before running
-    ddp(torch.randn(2, 3, 32, 32))
+    # ranks' running stats differ after a train forward on different data
+    rm = m.stem.bn.running_mean.clone()
+    dist.broadcast(rm, 0)
+    assert rank == 0 or not torch.equal(rm, m.stem.bn.running_mean)
+    # forward 2 (eval: no stats update) broadcasts rank 0's running stats before running
+    m.eval()
+    with torch.no_grad():
+        ddp(torch.randn(2, 3, 32, 32))
+    n = 0
     for b in m.buffers():
         if b.is_floating_point():
             ref = b.clone()
             dist.broadcast(ref, 0)
+            assert torch.equal(b, ref)
+            n += 1
+    assert n > 0
+    # all floating buffers live in ONE flat tensor: one broadcast per forward, no cat/copy kernels
+    assert len(ddp._flat_bufs) == 1
+    assert m.stem.bn.running_mean.untyped_storage().data_ptr() == ddp._flat_bufs[0].untyped_storage().data_ptr()
     q.put(("ok", rank))
     dist.destroy_process_group()
 

@@ -506,6 +506,43 @@ def test_s2d_stem_conv(C):
     assert rel_err(wp.grad, gref.permute(0, 2, 3, 1)) < 1e-2
 
 
+def test_stem_bn_relu_maxpool_fused(C):
+    """maxpool(relu(BN(h))) with the BN output never materialised (fwd, running stats,
+    and the pooled-gradient gather inside the BN backward) vs fp32 torch autograd."""
+    from distributed_pytorch_example_amd.ops import functional as Fx
+    from distributed_pytorch_example_amd.ops.layers import BatchNorm2d
+
+    torch.manual_seed(23)
+    N, H, W, Cc = 4, 30, 30, 64  # odd pooled border (30 -> 15)
+    h = bf(torch.randn(N, H, W, Cc, device=dev) * 2 + 0.3)
+    bn = BatchNorm2d(Cc, device=dev)
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(Cc, device=dev) + 0.5)
+        bn.bias.copy_(torch.randn(Cc, device=dev) * 0.2)
+    hf = h.float().reshape(-1, Cc)
+    st = torch.stack([hf.sum(0), (hf * hf).sum(0)]).unsqueeze(-1).contiguous()  # [2][C][1] partials
+    hh = h.clone().requires_grad_(True)
+    y = Fx.stem_bn_relu_maxpool(hh, bn, st, 3, 2, 1)
+    g = torch.nn.Parameter(bn.weight.detach().clone())
+    b = torch.nn.Parameter(bn.bias.detach().clone())
+    rm, rv = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
+    xr = h.float().permute(0, 3, 1, 2).requires_grad_(True)
+    a = F.relu(F.batch_norm(xr, rm, rv, g, b, True, 0.1, 1e-5))
+    ref = F.max_pool2d(a.to(torch.bfloat16).float(), 3, 2, 1)
+    assert y.shape == (N, 15, 15, Cc)
+    assert rel_err(y, ref.permute(0, 2, 3, 1)) < 1e-2
+    assert rel_err(bn.running_mean, rm) < 1e-4 and rel_err(bn.running_var, rv) < 1e-4
+    dy = bf(torch.randn_like(y))
+    y.backward(dy)
+    # backward through the bf16-rounded activation (straight-through), so the reference's
+    # argmax ties are the ones the kernel saw
+    a_r = a + (a.to(torch.bfloat16).float() - a).detach()
+    ref2 = F.max_pool2d(a_r, 3, 2, 1)
+    ref2.backward(dy.float().permute(0, 3, 1, 2))
+    assert rel_err(hh.grad, xr.grad.permute(0, 2, 3, 1)) < 2e-2
+    assert rel_err(bn.weight.grad, g.grad) < 1e-2 and rel_err(bn.bias.grad, b.grad) < 1e-2
+
+
 @pytest.mark.parametrize("N,H,W,Ci,Co,k,s,p", [(2, 14, 14, 64, 128, 1, 2, 0), (2, 8, 8, 64, 64, 1, 1, 0),
                                                (2, 14, 14, 32, 64, 3, 2, 1)])
 def test_conv_dgrad_acc_inplace(C, N, H, W, Ci, Co, k, s, p):
