@@ -818,7 +818,8 @@ Tensor maxpool_bn_bwd(const Tensor& dy, const Tensor& idx, const Tensor& h, cons
   const int64_t M = N * H * W;
   hipStream_t st = cur_stream();
   auto fo = h.options().dtype(at::kFloat);
-  const int nb = dpe_bn_stats_nblocks(M, (int)C);
+  // the gather makes each row latency-heavy: ~16 rows per thread-row-phase, up to 8192 partial blocks
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(8192, M / 512));
   Tensor part = at::empty({2, C, nb}, fo);
   CHECK_RC(dpe_maxpool_bn_bwd_reduce(bp(dy), (const uint8_t*)idx.data_ptr(), bp(h), fp(coef), (int)N, (int)H, (int)W, (int)C,
                                      (int)dy.size(1), (int)dy.size(2), (int)k, (int)s, (int)p, nb, fp(part), st),

@@ -110,16 +110,17 @@ __global__ void bn_eval_coeff_kernel(int C, const float* gamma, const float* bet
 }
 
 // y = act(x*scale + shift [+ res]); grid-stride over 16-B chunks.
+template <typename I>
 __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                         uint16_t* __restrict__ y, int64_t nchunks, int C,
                                                         const float* __restrict__ coef, int relu) {
   const int CPR = C >> 3;
-  for (int64_t i = blockIdx.x * (int64_t)BN_T + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * BN_T) {
-    const int c8 = (int)(i % CPR) * 8;
+  for (I i = (I)blockIdx.x * BN_T + threadIdx.x; i < (I)nchunks; i += (I)gridDim.x * BN_T) {
+    const int c8 = (int)(i % (I)CPR) * 8;
     float f[8];
-    unpack8(*(const u32x4*)(x + i * 8), f);
+    unpack8(*(const u32x4*)(x + (size_t)i * 8), f);
     float g[8];
-    if (res) unpack8(*(const u32x4*)(res + i * 8), g);
+    if (res) unpack8(*(const u32x4*)(res + (size_t)i * 8), g);
     const f32x4 sc0 = *(const f32x4*)(coef + c8), sc1 = *(const f32x4*)(coef + c8 + 4);
     const f32x4 sh0 = *(const f32x4*)(coef + C + c8), sh1 = *(const f32x4*)(coef + C + c8 + 4);
 #pragma unroll
@@ -131,21 +132,22 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const uint16_t* __restri
       if (relu) v = fmaxf(v, 0.f);
       f[e] = v;
     }
-    *(u32x4*)(y + i * 8) = pack8(f);
+    *(u32x4*)(y + (size_t)i * 8) = pack8(f);
   }
 }
 
 // y = act(x*scale + shift + x2*scale2 + shift2): a bottleneck's BN3 output plus its
 // BN'd downsample branch in one pass (the downsample BN output is never stored).
+template <typename I>
 __global__ __launch_bounds__(BN_T) void bn_apply2_kernel(const uint16_t* __restrict__ x, const float* __restrict__ coef,
                                                          const uint16_t* __restrict__ x2, const float* __restrict__ coef2,
                                                          uint16_t* __restrict__ y, int64_t nchunks, int C, int relu) {
   const int CPR = C >> 3;
-  for (int64_t i = blockIdx.x * (int64_t)BN_T + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * BN_T) {
-    const int c8 = (int)(i % CPR) * 8;
+  for (I i = (I)blockIdx.x * BN_T + threadIdx.x; i < (I)nchunks; i += (I)gridDim.x * BN_T) {
+    const int c8 = (int)(i % (I)CPR) * 8;
     float f[8], g[8];
-    unpack8(*(const u32x4*)(x + i * 8), f);
-    unpack8(*(const u32x4*)(x2 + i * 8), g);
+    unpack8(*(const u32x4*)(x + (size_t)i * 8), f);
+    unpack8(*(const u32x4*)(x2 + (size_t)i * 8), g);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       // the residual is rounded to bf16 first, as when it is materialised
@@ -154,7 +156,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply2_kernel(const uint16_t* __restr
       if (relu) v = fmaxf(v, 0.f);
       f[e] = v;
     }
-    *(u32x4*)(y + i * 8) = pack8(f);
+    *(u32x4*)(y + (size_t)i * 8) = pack8(f);
   }
 }
 
@@ -225,30 +227,31 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nb, i
 // ReLU mask: from y (y > 0) when y is given, else from the pre-BN input and the
 // forward coefficients (x*scale + shift > 0) when mcoef is given (the BN output
 // was never materialised: it was applied in the consumer's load prologue).
+template <typename I>
 __global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
                                                             const uint16_t* __restrict__ x, const float* __restrict__ bcoef,
                                                             uint16_t* __restrict__ dx, uint16_t* __restrict__ dz_out,
                                                             int64_t nchunks, int C, const float* __restrict__ mcoef) {
   const int CPR = C >> 3;
-  for (int64_t i = blockIdx.x * (int64_t)BN_T + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * BN_T) {
-    const int c8 = (int)(i % CPR) * 8;
+  for (I i = (I)blockIdx.x * BN_T + threadIdx.x; i < (I)nchunks; i += (I)gridDim.x * BN_T) {
+    const int c8 = (int)(i % (I)CPR) * 8;
     float d[8], xv[8];
-    unpack8(*(const u32x4*)(dy + i * 8), d);
-    unpack8(*(const u32x4*)(x + i * 8), xv);
+    unpack8(*(const u32x4*)(dy + (size_t)i * 8), d);
+    unpack8(*(const u32x4*)(x + (size_t)i * 8), xv);
     if (y) {
       float yv[8];
-      unpack8(*(const u32x4*)(y + i * 8), yv);
+      unpack8(*(const u32x4*)(y + (size_t)i * 8), yv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
     } else if (mcoef) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) d[e] = fmaf(xv[e], mcoef[c8 + e], mcoef[C + c8 + e]) > 0.f ? d[e] : 0.f;
     }
-    if (dz_out) *(u32x4*)(dz_out + i * 8) = pack8(d);
+    if (dz_out) *(u32x4*)(dz_out + (size_t)i * 8) = pack8(d);
     float o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = bcoef[c8 + e] * d[e] + bcoef[C + c8 + e] * xv[e] + bcoef[2 * C + c8 + e];
-    *(u32x4*)(dx + i * 8) = pack8(o);
+    *(u32x4*)(dx + (size_t)i * 8) = pack8(o);
   }
 }
 
@@ -293,14 +296,20 @@ extern "C" int dpe_bn_eval_coeff(int C, const float* gamma, const float* beta, c
 extern "C" int dpe_bn_apply(const uint16_t* x, const uint16_t* res, uint16_t* y, int64_t M, int C, const float* coef,
                             int relu, hipStream_t st) {
   const int64_t nch = M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, res, y, nch, C, coef, relu);
+  if (nch < (1ll << 31))
+    hipLaunchKernelGGL(bn_apply_kernel<uint32_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, res, y, nch, C, coef, relu);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<int64_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, res, y, nch, C, coef, relu);
   return 0;
 }
 
 extern "C" int dpe_bn_apply2(const uint16_t* x, const float* coef, const uint16_t* x2, const float* coef2, uint16_t* y,
                              int64_t M, int C, int relu, hipStream_t st) {
   const int64_t nch = M * C / 8;
-  hipLaunchKernelGGL(bn_apply2_kernel, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, coef, x2, coef2, y, nch, C, relu);
+  if (nch < (1ll << 31))
+    hipLaunchKernelGGL(bn_apply2_kernel<uint32_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, coef, x2, coef2, y, nch, C, relu);
+  else
+    hipLaunchKernelGGL(bn_apply2_kernel<int64_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, coef, x2, coef2, y, nch, C, relu);
   return 0;
 }
 
@@ -322,7 +331,11 @@ extern "C" int dpe_bn_bwd_finalize(const float* part, int nb, int C, int64_t M, 
 extern "C" int dpe_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* bcoef, uint16_t* dx,
                                 uint16_t* dz_out, int64_t M, int C, const float* mcoef, hipStream_t st) {
   const int64_t nch = M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(nch)), dim3(BN_T), 0, st, dy, y, x, bcoef, dx, dz_out, nch, C,
-                     mcoef);
+  if (nch < (1ll << 31))
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<uint32_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, dy, y, x, bcoef, dx, dz_out, nch,
+                       C, mcoef);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<int64_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, dy, y, x, bcoef, dx, dz_out, nch,
+                       C, mcoef);
   return 0;
 }

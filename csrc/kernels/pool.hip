@@ -99,21 +99,47 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __rest
   }
 }
 
-// ---- stem backward: maxpool gather + BN(+ReLU) backward without materialising d(BN output)
+// ---- stem backward: maxpool gather + BN(+ReLU) backward without materialising d(BN output).
+// 32-bit index math throughout (the stem tensor has < 2^31 chunks; 64-bit div/mod by a
+// runtime divisor is a ~100-instruction software sequence per element).
+DPE_DEVICE void pool_grad8_32(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ idx, int n, int h, int w, int c8,
+                              int C, int OH, int OW, int k, int s, int p, float* acc) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  const int oh_lo = max(0, (h + p - k + s) / s), oh_hi = min(OH - 1, (h + p) / s);
+  const int ow_lo = max(0, (w + p - k + s) / s), ow_hi = min(OW - 1, (w + p) / s);
+  for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+    const int r = h - (oh * s - p);
+    for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+      const int q = w - (ow * s - p);
+      const uint32_t o = ((uint32_t)(n * OH + oh) * OW + ow) * C + c8;
+      const u32x2 pk = *(const u32x2*)(idx + o);
+      float g[8];
+      unpack8(*(const u32x4*)(dy + o), g);
+      const uint32_t want = (uint32_t)(r * k + q);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t b = (pk[e >> 2] >> ((e & 3) * 8)) & 0xffu;
+        acc[e] += (b == want) ? g[e] : 0.f;
+      }
+    }
+  }
+}
+
 // reduce: per-block partials [2][C][nb] of (sum dz, sum dz*(x - mean)), dz = gather * [x*scale+shift > 0]
 __global__ __launch_bounds__(256) void maxpool_bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy,
                                                                     const uint8_t* __restrict__ idx,
                                                                     const uint16_t* __restrict__ x,
                                                                     const float* __restrict__ coef, int N, int H, int W,
                                                                     int C, int OH, int OW, int k, int s, int p,
-                                                                    int64_t rows_per_block, float* __restrict__ part) {
+                                                                    int rows_per_block, float* __restrict__ part) {
   const int CPR = C >> 3;
   const int tid = threadIdx.x;
   const int RPI = 256 / CPR;
   const int c = tid % CPR, r = tid / CPR;
-  const int64_t M = (int64_t)N * H * W;
-  const int64_t rb = blockIdx.x * rows_per_block;
-  const int64_t re = min(M, rb + rows_per_block);
+  const int M = N * H * W;
+  const int rb = blockIdx.x * rows_per_block;
+  const int re = min(M, rb + rows_per_block);
   float sm[8], sq[8], mean[8], sc[8], sh[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -121,13 +147,12 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_reduce_kernel(const uint16
     sc[e] = coef[c * 8 + e]; sh[e] = coef[C + c * 8 + e]; mean[e] = coef[2 * C + c * 8 + e];
   }
   if (r < RPI) {
-    for (int64_t row = rb + r; row < re; row += RPI) {
-      const int w = (int)(row % W);
-      const int64_t t = row / W;
-      const int h = (int)(t % H), n = (int)(t / H);
+    for (int row = rb + r; row < re; row += RPI) {
+      const int w = row % W, t = row / W;
+      const int h = t % H, n = t / H;
       float d[8], xv[8];
-      pool_grad8(dy, idx, n, h, w, c * 8, C, OH, OW, k, s, p, d);
-      unpack8(*(const u32x4*)(x + row * C + c * 8), xv);
+      unpack8(*(const u32x4*)(x + (size_t)row * C + c * 8), xv);
+      pool_grad8_32(dy, idx, n, h, w, c * 8, C, OH, OW, k, s, p, d);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float dz = fmaf(xv[e], sc[e], sh[e]) > 0.f ? d[e] : 0.f;
@@ -149,7 +174,7 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_reduce_kernel(const uint16
   }
 }
 
-// apply: dx = a*dz + b*x + c   (bcoef [3][C] from bn_bwd_finalize)
+// apply: dx = a*dz + b*x + c   (bcoef [3][C] from bn_bwd_finalize); one (pixel, 8 channels) per thread
 __global__ __launch_bounds__(256) void maxpool_bn_bwd_apply_kernel(const uint16_t* __restrict__ dy,
                                                                    const uint8_t* __restrict__ idx,
                                                                    const uint16_t* __restrict__ x,
@@ -158,22 +183,22 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_apply_kernel(const uint16_
                                                                    uint16_t* __restrict__ dx, int N, int H, int W, int C,
                                                                    int OH, int OW, int k, int s, int p) {
   const int CPR = C >> 3;
-  const int64_t total = (int64_t)N * H * W * CPR;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int c8 = (int)(i % CPR) * 8;
-    int64_t t = i / CPR;
-    const int w = (int)(t % W); t /= W;
-    const int h = (int)(t % H);
-    const int n = (int)(t / H);
+  const int total = N * H * W * CPR;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int c8 = (i % CPR) * 8;
+    int t = i / CPR;
+    const int w = t % W; t /= W;
+    const int h = t % H;
+    const int n = t / H;
     float d[8], xv[8], o[8];
-    pool_grad8(dy, idx, n, h, w, c8, C, OH, OW, k, s, p, d);
-    unpack8(*(const u32x4*)(x + i * 8), xv);
+    unpack8(*(const u32x4*)(x + (size_t)i * 8), xv);
+    pool_grad8_32(dy, idx, n, h, w, c8, C, OH, OW, k, s, p, d);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float dz = fmaf(xv[e], coef[c8 + e], coef[C + c8 + e]) > 0.f ? d[e] : 0.f;
       o[e] = bcoef[c8 + e] * dz + bcoef[C + c8 + e] * xv[e] + bcoef[2 * C + c8 + e];
     }
-    *(u32x4*)(dx + i * 8) = pack8(o);
+    *(u32x4*)(dx + (size_t)i * 8) = pack8(o);
   }
 }
 
@@ -245,9 +270,9 @@ extern "C" int dpe_bnrelu_maxpool_fwd(const uint16_t* h, const float* coef, uint
 extern "C" int dpe_maxpool_bn_bwd_reduce(const uint16_t* dy, const uint8_t* idx, const uint16_t* x, const float* coef, int N,
                                          int H, int W, int C, int OH, int OW, int k, int s, int p, int nb, float* part,
                                          hipStream_t st) {
-  if (C % 8 || C / 8 > 256) return -1;
+  if (C % 8 || C / 8 > 256 || (int64_t)N * H * W * C / 8 >= (1ll << 31)) return -1;
   const int64_t M = (int64_t)N * H * W;
-  const int64_t rpb = (M + nb - 1) / nb;
+  const int rpb = (int)((M + nb - 1) / nb);
   hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, st, dy, idx, x, coef, N, H, W, C, OH, OW, k, s, p,
                      rpb, part);
   return 0;
@@ -256,7 +281,7 @@ extern "C" int dpe_maxpool_bn_bwd_reduce(const uint16_t* dy, const uint8_t* idx,
 extern "C" int dpe_maxpool_bn_bwd_apply(const uint16_t* dy, const uint8_t* idx, const uint16_t* x, const float* coef,
                                         const float* bcoef, uint16_t* dx, int N, int H, int W, int C, int OH, int OW, int k,
                                         int s, int p, hipStream_t st) {
-  if (C % 8) return -1;
+  if (C % 8 || (int64_t)N * H * W * C / 8 >= (1ll << 31)) return -1;
   hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel, dim3(gs((int64_t)N * H * W * C / 8)), dim3(256), 0, st, dy, idx, x, coef,
                      bcoef, dx, N, H, W, C, OH, OW, k, s, p);
   return 0;
