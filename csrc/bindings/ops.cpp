@@ -1052,8 +1052,7 @@ Tensor attn_bwd(const Tensor& qkv, const Tensor& out, const Tensor& dout, const 
   const int64_t B = qkv.size(0), T = qkv.size(1), D = qkv.size(-1);
   Tensor dqkv = at::empty_like(qkv);
   Tensor delta = at::empty({B, H, T}, qkv.options().dtype(at::kFloat));
-  Tensor dq = at::zeros({B, T, H, D}, qkv.options().dtype(at::kFloat));
-  CHECK_RC(dpe_attn_bwd(bp(qkv), bp(out), bp(dout), fp(lse), fp(delta), fp(dq), bpm(dqkv), (int)B, (int)T, (int)H, (int)D,
+  CHECK_RC(dpe_attn_bwd(bp(qkv), bp(out), bp(dout), fp(lse), fp(delta), nullptr, bpm(dqkv), (int)B, (int)T, (int)H, (int)D,
                         (float)scale, causal, cur_stream()), "attn_bwd");
   return dqkv;
 }

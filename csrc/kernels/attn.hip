@@ -13,15 +13,16 @@
 //   next MFMA's operand").  K/V tiles are register-prefetched one tile ahead
 //   into double-buffered, XOR-swizzled LDS.  Heaviest (latest) query tiles are
 //   scheduled first.  Saves lse2 = m + log2(l) (log2 units, scale folded).
-// Backward (one workgroup = 64 keys, 4 waves x 16 keys; loops over query tiles):
+// Backward = two kernels after D = rowsum(dO*O):
+//   dK/dV (one workgroup = 64 keys, 4 waves x 16 keys; loops over query tiles):
 //   key-on-the-lane: S = Q.K^T and dP = dO.V^T have the key on the lane, so
 //   their accumulators ARE the B operands of dV^T += dO^T.P and
-//   dK^T += Q^T.dS (permuted-k trick again, Q/dO read transposed from LDS).
-//   dS crosses LDS once (as a [key][q] image written with 8-B stores, read
-//   transposed) for dQ = dS.K, summed over key tiles with fp32 atomics shaped
-//   as full 256-B rows.  The next query tile's Q/dO/lse/delta are prefetched
-//   into registers during the current tile's MFMAs; two barriers per tile.
-//   D = rowsum(dO*O) is precomputed.
+//   dK^T += Q^T.dS (permuted-k trick again, Q/dO read transposed from LDS,
+//   double-buffered, one barrier per tile).
+//   dQ (one workgroup = 64 queries; loops over key tiles): the forward's
+//   query-on-lane structure recomputing S and dP; dQ^T += K^T.dS^T.  Two
+//   extra MFMA passes replace the fp32 dQ atomics across key tiles (which ran
+//   at the chip's ~1.3 TB/s atomic rate: ~210 MB per layer).
 #include "common.h"
 
 namespace dpe {
@@ -223,21 +224,16 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const uint16_t* __restr
   }
 }
 
+// dK / dV: one workgroup = 64 keys of one (b, h), 4 waves x 16 keys, looping over the
+// query tiles at or after the key tile.  The query tile's Q / dO images are double-
+// buffered in LDS (register-prefetched one tile ahead): one barrier per tile.
 __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dout,
                                                        const float* __restrict__ lse2, const float* __restrict__ delta,
-                                                       float* __restrict__ dq_acc, uint16_t* __restrict__ dqkv, int B,
-                                                       int T, int H, float sl2, float scale) {
-  // LDS: Qk Qm dOk dOm Km dS^T (8 KB each) | dQ staging (16 KB) | lse, delta (512 B)
-  __shared__ __attribute__((aligned(16))) char smem[6 * 8192 + 16384 + 512];
-  char* Qk = smem;
-  char* Qm = smem + 8192;
-  char* Ok = smem + 2 * 8192;
-  char* Om = smem + 3 * 8192;
-  char* Km = smem + 4 * 8192;
-  char* dSt = smem + 5 * 8192;
-  float* stg = (float*)(smem + 6 * 8192);
-  float* sl = (float*)(smem + 6 * 8192 + 16384);
-  float* sd = sl + 64;
+                                                       uint16_t* __restrict__ dqkv, int B, int T, int H, float sl2,
+                                                       float scale) {
+  // per buffer: Qk Qm dOk dOm (8 KB each) + lse, delta (512 B)
+  constexpr int BUF = 4 * 8192 + 512;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
   const int nk = T / AKV, BH = B * H;
   const int kt = (int)(blockIdx.x / BH);  // heaviest key tiles (most query tiles) first
@@ -257,12 +253,6 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
     kf[kk] = __builtin_bit_cast(bf16x8, *(const u32x4*)(kb + (int64_t)mykey * RS + 32 * kk + 8 * g));
     vf[kk] = __builtin_bit_cast(bf16x8, *(const u32x4*)(vb + (int64_t)mykey * RS + 32 * kk + 8 * g));
   }
-  // block's K tile as an [key][d] image for dQ = dS . K (B operand, k = key, read transposed)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = tid + 256 * i, key = c >> 3, dc = c & 7;
-    *(u32x4*)(Km + mnimg(key, dc)) = *(const u32x4*)(kb + (int64_t)(kt * AKV + key) * RS + dc * 8);
-  }
   // Q / dO / lse / delta of a query tile: global -> registers (prefetched one tile ahead) -> LDS
   u32x4 qv[2], ov[2];
   float lv = 0.f;
@@ -276,27 +266,36 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
     if (tid < 64) lv = lse2[(int64_t)bh * T + qt * AQ + tid];
     else if (tid < 128) lv = delta[(int64_t)bh * T + qt * AQ + tid - 64];
   };
-  auto stash = [&]() {
+  auto stash = [&](int buf) {
+    char* base = smem + buf * BUF;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = tid + 256 * i, q = c >> 3, dc = c & 7;
-      *(u32x4*)(Qk + (dc >> 2) * 4096 + kimg(q, dc & 3)) = qv[i];
-      *(u32x4*)(Qm + pimg(q, dc)) = qv[i];
-      *(u32x4*)(Ok + (dc >> 2) * 4096 + kimg(q, dc & 3)) = ov[i];
-      *(u32x4*)(Om + pimg(q, dc)) = ov[i];
+      *(u32x4*)(base + (dc >> 2) * 4096 + kimg(q, dc & 3)) = qv[i];
+      *(u32x4*)(base + 8192 + pimg(q, dc)) = qv[i];
+      *(u32x4*)(base + 2 * 8192 + (dc >> 2) * 4096 + kimg(q, dc & 3)) = ov[i];
+      *(u32x4*)(base + 3 * 8192 + pimg(q, dc)) = ov[i];
     }
-    if (tid < 128) sl[tid] = lv;  // sl[0..63] = lse, sd = sl + 64: delta
+    if (tid < 128) ((float*)(base + 4 * 8192))[tid] = lv;  // [0,64) lse, [64,128) delta
   };
   fetch(kt);
-  stash();
+  stash(0);
   f32x4 dk[4], dv[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
   __syncthreads();
 
+  int cur = 0;
   for (int qt = kt; qt < nk; ++qt) {
     const bool more = qt + 1 < nk;
     if (more) fetch(qt + 1);  // in flight during this tile's MFMAs
+    const char* base = smem + cur * BUF;
+    const char* Qk = base;
+    const char* Qm = base + 8192;
+    const char* Ok = base + 2 * 8192;
+    const char* Om = base + 3 * 8192;
+    const float* sl = (const float*)(base + 4 * 8192);
+    const float* sd = sl + 64;
     // S[q][key], dP[q][key]: lane = key, rows q = 16mt + 4g + e
     f32x4 ps[4], dp[4];
 #pragma unroll
@@ -329,35 +328,9 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
       dk[d] = MFMA(trfrag<true>(Qm, 0, 16 * d), s0, dk[d]);
       dk[d] = MFMA(trfrag<true>(Qm, 32, 16 * d), s1, dk[d]);
     }
-    // dS^T -> LDS as a [key][q] image: each lane owns 4 consecutive q of its key -> 8-B stores
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      u32x2 pk;
-      pk[0] = pack_bf2(dp[mt][0], dp[mt][1]);
-      pk[1] = pack_bf2(dp[mt][2], dp[mt][3]);
-      *(u32x2*)(dSt + mnimg(16 * w + li, 2 * mt + (g >> 1)) + (g & 1) * 8) = pk;
-    }
-    __syncthreads();  // dS^T complete; every wave is done with this tile's Q/dO/lse/delta
-    if (more) stash();
-    // dQ tile rows 16w..16w+15 : D[q][d] (lane = d, rows q = 4g + e);  A = dS (read transposed from dS^T)
-    f32x4 dqa[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      dqa[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        dqa[d] = MFMA(trfrag<false>(dSt, 32 * kk, 16 * w), trfrag<false>(Km, 32 * kk, 16 * d), dqa[d]);
-    }
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) stg[(16 * w + 4 * g + e) * 64 + 16 * d + li] = dqa[d][e] * scale;
-    __syncthreads();  // staging complete; next tile's Q/dO images complete
-    // add whole 256-B rows atomically (full-rate atomic shape)
-    for (int r = w; r < 64; r += 4) {
-      float* dst = dq_acc + ((int64_t)(b * T + qt * AQ + r) * H + h) * AD;
-      atomicAdd(dst + lane, stg[r * 64 + lane]);
-    }
+    if (more) stash(cur ^ 1);  // the other buffer was last read before the previous barrier
+    __syncthreads();
+    cur ^= 1;
   }
   // dK, dV (bf16) -> dqkv[b, key, 1|2, h, :]
   uint16_t* dkb = dqkv + (int64_t)b * T * RS + (int64_t)mykey * RS + H * AD + (int64_t)h * AD;
@@ -374,17 +347,108 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
   }
 }
 
-// dq (fp32 [B,T,H,64]) -> dqkv[:, :, 0] (bf16)
-__global__ __launch_bounds__(256) void attn_dq_store_kernel(const float* __restrict__ dq, uint16_t* __restrict__ dqkv, int B,
-                                                            int T, int H) {
-  const int64_t n8 = (int64_t)B * T * H * AD / 8;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
-    const int64_t e = i * 8;
-    const int64_t bt = e / (H * AD);
-    const int64_t rem = e % (H * AD);
-    const f32x4 a = *(const f32x4*)(dq + e), c = *(const f32x4*)(dq + e + 4);
-    float f[8] = {a[0], a[1], a[2], a[3], c[0], c[1], c[2], c[3]};
-    *(u32x4*)(dqkv + bt * 3 * H * AD + rem) = pack8(f);
+// dQ: the forward's structure with the query on the lane (one workgroup = 64 queries,
+// 4 waves x 16 queries, looping over key tiles <= the query tile).  S^T = K.Q^T and
+// dP^T = V.dO^T are recomputed (A = K / V images, B = the wave's Q / dO in registers);
+// P = exp2(S*sl2 - lse2) and dS = P (dP - delta) are lane-local (one query per lane);
+// dQ^T += K^T . dS^T takes dS^T straight from the accumulators (permuted key order,
+// K read transposed like V in the forward).  dQ is written once, in bf16, into
+// dqkv[:, :, 0] -- no fp32 atomics across key tiles, no conversion pass.
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dout,
+                                                          const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                          uint16_t* __restrict__ dqkv, int B, int T, int H, float sl2,
+                                                          float scale) {
+  // per buffer: K (two d-halves, K-contig) 8K | V (same) 8K | K permuted-row image 8K
+  constexpr int KI = 0, VI = 2 * AKV * 64, KP = 4 * AKV * 64, STG = KP + AKV * 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int nq = T / AQ, BH = B * H;
+  const int qt = nq - 1 - (int)(blockIdx.x / BH);  // heaviest query tiles first
+  const int bh = blockIdx.x % BH, b = bh / H, h = bh % H;
+  const int64_t RS = 3LL * H * AD;
+  const int64_t ORS = (int64_t)H * AD;
+  const uint16_t* qb = qkv + (int64_t)b * T * RS + (int64_t)h * AD;
+  const uint16_t* kb = qb + H * AD;
+  const uint16_t* vb = qb + 2 * H * AD;
+  const int myq = qt * AQ + 16 * w + li;
+
+  bf16x8 qf[2], of[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    qf[kk] = __builtin_bit_cast(bf16x8, *(const u32x4*)(qb + (int64_t)myq * RS + 32 * kk + 8 * g));
+    of[kk] = __builtin_bit_cast(bf16x8, *(const u32x4*)(dout + ((int64_t)b * T + myq) * ORS + (int64_t)h * AD + 32 * kk + 8 * g));
+  }
+  const float lq = lse2[(int64_t)bh * T + myq];
+  const float dq_delta = delta[(int64_t)bh * T + myq];
+
+  u32x4 rk[2], rv[2];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, key = c >> 3, dc = c & 7;
+      const int64_t off = (int64_t)(kt * AKV + key) * RS + dc * 8;
+      rk[i] = *(const u32x4*)(kb + off);
+      rv[i] = *(const u32x4*)(vb + off);
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* st = smem + buf * STG;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, key = c >> 3, dc = c & 7;
+      *(u32x4*)(st + KI + (dc >> 2) * (AKV * 64) + kimg(key, dc & 3)) = rk[i];
+      *(u32x4*)(st + VI + (dc >> 2) * (AKV * 64) + kimg(key, dc & 3)) = rv[i];
+      *(u32x4*)(st + KP + pimg(key, dc)) = rk[i];
+    }
+  };
+
+  f32x4 acc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt <= qt; ++kt) {
+    const bool more = kt < qt;
+    if (more) gload(kt + 1);
+    const char* st = smem + cur * STG;
+    f32x4 sc[4], dp[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[nt] = sc[nt];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        sc[nt] = MFMA(kfrag64(st + KI + kk * (AKV * 64), 16 * nt), qf[kk], sc[nt]);
+        dp[nt] = MFMA(kfrag64(st + VI + kk * (AKV * 64), 16 * nt), of[kk], dp[nt]);
+      }
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float p = exp2f(sc[nt][e] * sl2 - lq);
+        if (kt == qt && kt * AKV + 16 * nt + 4 * g + e > myq) p = 0.f;
+        dp[nt][e] = p * (dp[nt][e] - dq_delta);  // dS^T (unscaled)
+      }
+    const bf16x8 d0 = pack_frag(dp[0], dp[1]), d1 = pack_frag(dp[2], dp[3]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      acc[d] = MFMA(trfrag<true>(st + KP, 0, 16 * d), d0, acc[d]);
+      acc[d] = MFMA(trfrag<true>(st + KP, 32, 16 * d), d1, acc[d]);
+    }
+    if (more) lstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+  uint16_t* o = dqkv + ((int64_t)b * T + myq) * RS + (int64_t)h * AD;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    u32x2 pk;
+    pk[0] = pack_bf2(acc[d][0] * scale, acc[d][1] * scale);
+    pk[1] = pack_bf2(acc[d][2] * scale, acc[d][3] * scale);
+    *(u32x2*)(o + 16 * d + 4 * g) = pk;
   }
 }
 
@@ -403,13 +467,14 @@ extern "C" int dpe_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int 
 extern "C" int dpe_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
                             float* dq_acc, uint16_t* dqkv, int B, int T, int H, int D, float scale, int causal,
                             hipStream_t st) {
+  (void)dq_acc;  // dQ is no longer accumulated with atomics (attn_bwd_dq_kernel)
   if (D != AD || T % AQ != 0 || !causal) return -1;
   const float sl2 = scale * 1.4426950408889634f;
   const int64_t rows = (int64_t)B * T * H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, st, out, dout, delta, B, T, H);
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3(B * H * (T / AKV)), dim3(256), 0, st, qkv, dout, lse, delta, dq_acc, dqkv, B, T,
-                     H, sl2, scale);
-  int64_t g = rows * AD / 8 / 256 + 1;
-  hipLaunchKernelGGL(attn_dq_store_kernel, dim3((unsigned)(g > 8192 ? 8192 : g)), dim3(256), 0, st, dq_acc, dqkv, B, T, H);
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(B * H * (T / AKV)), dim3(256), 0, st, qkv, dout, lse, delta, dqkv, B, T, H, sl2,
+                     scale);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(B * H * (T / AQ)), dim3(256), 0, st, qkv, dout, lse, delta, dqkv, B, T, H, sl2,
+                     scale);
   return 0;
 }
