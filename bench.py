@@ -162,7 +162,8 @@ def main():
     if rank == 0:
         line = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-                "vs_baseline": None, "dtype": "bf16", "data": "synthetic (device-resident, random)",
+                "vs_baseline": None, "dtype": "bf16" if dev.type == "cuda" else "fp32",
+                "data": "synthetic (device-resident, random)",
                 "config": cfg, "loss": float(loss.item())}
         line.update(extra)
         print(json.dumps(line), flush=True)
