@@ -159,11 +159,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
 }
 
 // Column-parallel reduction of the [nb][2][D] partials: block = 64 columns x
-// 4 waves splitting the nb rows (coalesced 256-B row reads), blockIdx.y picks
-// dw (0) or db (1).  Replaces a serial per-column loop (1.7 ms/step on GPT-2).
-__global__ __launch_bounds__(256) void ln_bwd_finalize_kernel(const float* __restrict__ part, int nb, int D,
-                                                              float* __restrict__ dw, float* __restrict__ db) {
-  __shared__ float red[4][64];
+// 16 waves splitting the nb rows (coalesced 256-B row reads, 4 independent
+// accumulators per lane), blockIdx.y picks dw (0) or db (1).
+constexpr int LNF_W = 16;
+__global__ __launch_bounds__(64 * LNF_W) void ln_bwd_finalize_kernel(const float* __restrict__ part, int nb, int D,
+                                                                     float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float red[LNF_W][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int which = blockIdx.y;
   const int col = blockIdx.x * 64 + lane;
@@ -171,18 +172,20 @@ __global__ __launch_bounds__(256) void ln_bwd_finalize_kernel(const float* __res
   if (col < D) {
     const float* src = part + (int64_t)which * D + col;
     int k = wid;
-    for (; k + 12 < nb; k += 16) {
+    for (; k + 3 * LNF_W < nb; k += 4 * LNF_W) {
       a0 += src[(int64_t)k * 2 * D];
-      a1 += src[(int64_t)(k + 4) * 2 * D];
-      a2 += src[(int64_t)(k + 8) * 2 * D];
-      a3 += src[(int64_t)(k + 12) * 2 * D];
+      a1 += src[(int64_t)(k + LNF_W) * 2 * D];
+      a2 += src[(int64_t)(k + 2 * LNF_W) * 2 * D];
+      a3 += src[(int64_t)(k + 3 * LNF_W) * 2 * D];
     }
-    for (; k < nb; k += 4) a0 += src[(int64_t)k * 2 * D];
+    for (; k < nb; k += LNF_W) a0 += src[(int64_t)k * 2 * D];
   }
   red[wid][lane] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (wid == 0 && col < D) {
-    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < LNF_W; ++w) t += red[w][lane];
     if (which == 0) dw[col] += t;
     else if (db) db[col] += t;
   }
@@ -212,18 +215,25 @@ extern "C" int dpe_layernorm_fwd(const void* x, int x_bf16, const float* w, cons
   return -1;
 }
 
+// Partial-sum blocks of the LN backward: ~2 rows per wave (4 waves per block) up to
+// 1024 blocks -- 16 waves per CU on the GPT-2 shape (8192 rows); with 8 rows per
+// wave (256 blocks) the row-serial wave ran latency-bound at ~2.7 TB/s.
+extern "C" int dpe_layernorm_bwd_nblocks(int64_t rows) {
+  const int64_t nb = (rows + 7) / 8;
+  return (int)(nb < 1 ? 1 : (nb > 1024 ? 1024 : nb));
+}
+
 extern "C" int dpe_layernorm_bwd(const uint16_t* dy, const void* x, int x_bf16, const float* w, const float* mean,
                                  const float* rstd, void* dx, int dx_acc, const float* res_in, uint16_t* dx_bf16, float* dw,
                                  float* db, float* part, int64_t rows, int D, hipStream_t st) {
   if (D % 8 || D > 2048) return -1;
-  const int nb = (int)(rows < 16384 ? (rows + 31) / 32 : 512);
-  const int nbc = nb > 512 ? 512 : nb;
+  const int nbc = dpe_layernorm_bwd_nblocks(rows);
   if (x_bf16)
     hipLaunchKernelGGL((ln_bwd_kernel<true>), dim3(nbc), dim3(256), 0, st, dy, x, w, mean, rstd, dx, dx_acc, res_in, dx_bf16,
                        part, rows, D);
   else
     hipLaunchKernelGGL((ln_bwd_kernel<false>), dim3(nbc), dim3(256), 0, st, dy, x, w, mean, rstd, dx, dx_acc, res_in, dx_bf16,
                        part, rows, D);
-  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 63) / 64, db ? 2 : 1), dim3(256), 0, st, part, nbc, D, dw, db);
+  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 63) / 64, db ? 2 : 1), dim3(64 * LNF_W), 0, st, part, nbc, D, dw, db);
   return 0;
 }
