@@ -10,7 +10,10 @@ backward with bucketed RCCL all-reduce overlapped on a side stream, fused SGD
 (momentum 0.9, wd 5e-5) update of fp32 masters + bf16 shadows.  Synthetic,
 device-resident ImageNet-shaped batches (3x224x224, generated directly in the
 model's NHWC-bf16 input format, several distinct batches cycled), random-init
-weights.  Weak scaling: --batch-size images per GPU.
+weights.  Weak scaling: --batch-size images per GPU (default 512, the per-GPU
+batch BASELINE.json names for ResNet-50 (config 5); measured on one MI355X:
+256 -> 9.2k, 512 -> 10.0k, 1024 -> 10.7k img/s; stock PyTorch-ROCm 6.3k / 6.7k
+at 256 / 512).
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -35,7 +38,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "gpt2", "simplenet"])
-    ap.add_argument("--batch-size", type=int, default=None, help="per-GPU batch (resnet50: 256, gpt2: 8 seqs)")
+    ap.add_argument("--batch-size", type=int, default=None,
+                    help="per-GPU batch (resnet50: 512 = BASELINE config 5's per-GPU batch, sized for 288 GB HBM; "
+                         "gpt2: 8 seqs)")
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--first-bucket-mb", type=float, default=1.0)
@@ -65,7 +70,7 @@ def main():
     torch.manual_seed(1234 + rank)
 
     if args.model == "resnet50":
-        bs = args.batch_size or 256
+        bs = args.batch_size or 512
         model = get_model("resnet50").to(dev)
         opt_name, lr = args.optimizer or "sgd", args.lr or 0.1
         wd = 5e-5

@@ -7,6 +7,7 @@ as bench.py; prints one JSON line.  This is the bar our framework must beat.
 """
 import argparse
 import json
+import sys
 import os
 import time
 
@@ -127,8 +128,21 @@ def main():
         opt.step()
         return loss
 
+    # MIOpen's exhaustive find (cudnn.benchmark) can run for minutes at large batch:
+    # keep a heartbeat on stderr so a watchdog does not take the run for hung
+    import threading
+
+    done = threading.Event()
+
+    def beat():
+        while not done.wait(30):
+            print(f"[stock] warming up (MIOpen find)... rank {rank}", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
     for i in range(args.warmup):
         step(i)
+        print(f"[stock] warmup step {i + 1}/{args.warmup}", file=sys.stderr, flush=True)
+    done.set()
     torch.cuda.synchronize(); dist.barrier(); torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
