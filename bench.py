@@ -48,7 +48,11 @@ def parse():
     ap.add_argument("--optimizer", default=None)
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--graph", type=int, default=0, help="capture the step in a hipGraph (1) or run eagerly (0)")
-    ap.add_argument("--bucket-timing", action="store_true")
+    ap.add_argument("--bucket-timing", action="store_true",
+                    help="after the timed steps, one instrumented step: per-bucket all-reduce time and its overlap "
+                         "with backward (HIP events on the RCCL stream), reported under 'buckets'")
+    ap.add_argument("--force-comm", action="store_true",
+                    help="run the RCCL bucket all-reduces even at world size 1 (reducer/overlap mechanics check)")
     ap.add_argument("--nbatches", type=int, default=4, help="distinct synthetic batches cycled")
     return ap.parse_args()
 
@@ -120,7 +124,7 @@ def main():
         num_classes = 10
 
     fused_loss = args.model == "gpt2"
-    ddp = DDP(model, bucket_cap_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb)
+    ddp = DDP(model, bucket_cap_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb, force_comm=args.force_comm)
     opt = build_optimizer(opt_name, model.parameters(), lr=lr, weight_decay=wd)
 
     def step(i):
@@ -162,8 +166,22 @@ def main():
     ms = 1000.0 * dt / args.steps
     value = samples_per_step * world * args.steps / dt
     extra = {}
-    if args.bucket_timing and hasattr(ddp, "bucket_timings"):
-        extra["buckets"] = ddp.num_buckets()
+    if args.bucket_timing:
+        # one extra (untimed) step with per-bucket HIP events on the comm stream
+        ddp.enable_timing(True)
+        step(args.warmup + args.steps)
+        _sync(dev)
+        tim = ddp.bucket_timings()
+        sizes = ddp.bucket_bytes()
+        rows, comm, hidden = [], 0.0, 0.0
+        for b, ms, rel in tim:
+            # rel = start of this bucket's all-reduce relative to the end of backward (negative: overlapped)
+            ov = min(max(-rel, 0.0), ms)
+            comm += ms
+            hidden += ov
+            rows.append({"bucket": b, "bytes": sizes[b], "allreduce_ms": round(ms, 4), "start_vs_bwd_end_ms": round(rel, 4)})
+        extra["buckets"] = {"count": ddp.num_buckets(), "per_bucket": rows, "comm_ms": round(comm, 4),
+                            "overlap_pct": round(100.0 * hidden / comm, 1) if comm > 0 else None}
     if rank == 0:
         line = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",

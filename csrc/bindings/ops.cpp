@@ -31,7 +31,9 @@ int dpe_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, c
 int dpe_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int k, int s,
                     int p, hipStream_t st);
 int dpe_bn_apply2(const uint16_t* x, const float* coef, const uint16_t* x2, const float* coef2, uint16_t* y, int64_t M, int C,
-                  int relu, hipStream_t st);
+                  int relu, uint8_t* mbits, hipStream_t st);
+int dpe_bn_apply_m(const uint16_t* x, const uint16_t* res, uint16_t* y, int64_t M, int C, const float* coef, int relu,
+                   uint8_t* mbits, hipStream_t st);
 int dpe_bnrelu_maxpool_fwd(const uint16_t* h, const float* coef, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH,
                            int OW, int k, int s, int p, hipStream_t st);
 int dpe_maxpool_bn_bwd_reduce(const uint16_t* dy, const uint8_t* idx, const uint16_t* x, const float* coef, int N, int H, int W,
@@ -536,10 +538,12 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
     a.st_x = bp(*bn_x);
     a.st_coef = fp(*bn_coef);
     if (bn_mask.has_value() && bn_mask->defined()) {
-      // BN + residual + ReLU: mask from the saved block output, dx stored already masked
-      CHECK_BF16((*bn_mask)); CHECK_CONTIG((*bn_mask));
-      TORCH_CHECK(bn_mask->sizes() == dx.sizes(), "conv_dgrad: bn_mask must have dx's shape");
-      a.st_mask = bp(*bn_mask);
+      // BN + residual + ReLU: ReLU-mask bits of the saved block output (bn_apply want_mask),
+      // dx stored already masked
+      CHECK_CONTIG((*bn_mask));
+      TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() * 8 == dx.numel() && g.C % 8 == 0,
+                  "conv_dgrad: bn_mask must be uint8 mask bits [N,H,W,C/8] of dx's shape");
+      a.st_mask = (const uint8_t*)bn_mask->data_ptr();
     }
   }
   Tensor part;
@@ -782,16 +786,38 @@ Tensor maxpool_bwd(const Tensor& dy, const Tensor& idx, std::vector<int64_t> xsh
   return dx;
 }
 
-// y = act(BN(x; coef) + BN(x2; coef2)) in one pass (bottleneck output with a BN'd downsample branch)
-Tensor bn_apply2(const Tensor& x, const Tensor& coef, const Tensor& x2, const Tensor& coef2, bool relu) {
-  CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(x2); CHECK_CONTIG(x2); CHECK_F32(coef); CHECK_F32(coef2);
-  TORCH_CHECK(x.sizes() == x2.sizes(), "bn_apply2: x/x2 shape mismatch");
+// y = act(BN(x; coef) + r), r = residual (bf16) or, with residual_coef, BN(residual; residual_coef)
+// computed in the same pass (bottleneck output with a BN'd downsample branch).
+// want_mask: also the ReLU-mask bits of y, uint8 [.., C/8] (bit e of byte j = y[.., 8j+e] > 0).
+std::vector<Tensor> bn_apply(const Tensor& x, const Tensor& coef, const c10::optional<Tensor>& residual,
+                             const c10::optional<Tensor>& residual_coef, bool relu, bool want_mask) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_F32(coef);
   const int64_t C = x.size(-1);
-  TORCH_CHECK(C % 8 == 0 && coef.numel() == 4 * C && coef2.numel() == 4 * C, "bn_apply2: coef must be [4][C], C % 8 == 0");
+  TORCH_CHECK(C % 8 == 0 && coef.numel() == 4 * C, "bn_apply: coef must be [4][C], C % 8 == 0");
+  const bool has_res = residual.has_value() && residual->defined();
+  if (has_res) {
+    CHECK_BF16((*residual)); CHECK_CONTIG((*residual));
+    TORCH_CHECK(residual->sizes() == x.sizes(), "bn_apply: residual shape mismatch");
+  }
   Tensor y = at::empty_like(x);
-  CHECK_RC(dpe_bn_apply2(bp(x), fp(coef), bp(x2), fp(coef2), bpm(y), rows_of(x), (int)C, relu ? 1 : 0, cur_stream()),
-           "bn_apply2");
-  return y;
+  Tensor bits;
+  if (want_mask) {
+    auto sz = x.sizes().vec();
+    sz.back() = C / 8;
+    bits = at::empty(sz, x.options().dtype(at::kByte));
+  }
+  uint8_t* mb = want_mask ? (uint8_t*)bits.data_ptr() : nullptr;
+  if (residual_coef.has_value() && residual_coef->defined()) {
+    TORCH_CHECK(has_res, "bn_apply: residual_coef needs a residual");
+    CHECK_F32((*residual_coef));
+    TORCH_CHECK(residual_coef->numel() == 4 * C, "bn_apply: residual_coef must be [4][C]");
+    CHECK_RC(dpe_bn_apply2(bp(x), fp(coef), bp(*residual), fp(*residual_coef), bpm(y), rows_of(x), (int)C, relu ? 1 : 0, mb,
+                           cur_stream()), "bn_apply2");
+  } else {
+    CHECK_RC(dpe_bn_apply_m(bp(x), has_res ? bp(*residual) : nullptr, bpm(y), rows_of(x), (int)C, fp(coef), relu ? 1 : 0, mb,
+                            cur_stream()), "bn_apply");
+  }
+  return {y, bits};
 }
 
 // Stem fusion: maxpool(relu(BN(h))) with BN coefficients `coef` [4][C] (bn_coef);
@@ -1085,7 +1111,8 @@ void register_ops(pybind11::module& m) {
         "with bn_mask (BN + residual + ReLU) the mask is bn_mask > 0 and dx is stored masked");
   m.def("bn_coef", &bn_coef, py::arg("stats"), py::arg("M"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("momentum"), py::arg("eps"));
-  m.def("bn_apply2", &bn_apply2, py::arg("x"), py::arg("coef"), py::arg("x2"), py::arg("coef2"), py::arg("relu"));
+  m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("coef"), py::arg("residual") = py::none(),
+        py::arg("residual_coef") = py::none(), py::arg("relu") = true, py::arg("want_mask") = false);
   m.def("bnrelu_maxpool_fwd", &bnrelu_maxpool_fwd, py::arg("h"), py::arg("coef"), py::arg("k"), py::arg("s"), py::arg("p"));
   m.def("maxpool_bn_bwd", &maxpool_bn_bwd, py::arg("dy"), py::arg("idx"), py::arg("h"), py::arg("gamma"), py::arg("coef"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("k"), py::arg("s"), py::arg("p"));

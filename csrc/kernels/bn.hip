@@ -18,6 +18,18 @@ namespace dpe {
 
 constexpr int BN_T = 256;
 
+// ReLU-mask bits of 8 packed bf16 outputs: bit e = (y[e] > 0), i.e. sign clear and nonzero
+DPE_DEVICE uint8_t mask_byte(const u32x4& pk) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t lo = pk[j] & 0xffffu, hi = pk[j] >> 16;
+    b |= (uint32_t)(lo != 0 && !(lo & 0x8000u)) << (2 * j);
+    b |= (uint32_t)(hi != 0 && !(hi & 0x8000u)) << (2 * j + 1);
+  }
+  return (uint8_t)b;
+}
+
 // Thread layout for a [rows][C] pass: chunk c = tid % CPR (8 channels), row phase tid / CPR.
 __global__ __launch_bounds__(BN_T) void bn_stats_partial_kernel(const uint16_t* __restrict__ x, int64_t M, int C,
                                                                 int64_t rows_per_block, float* __restrict__ part) {
@@ -113,7 +125,8 @@ __global__ void bn_eval_coeff_kernel(int C, const float* gamma, const float* bet
 template <typename I>
 __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                         uint16_t* __restrict__ y, int64_t nchunks, int C,
-                                                        const float* __restrict__ coef, int relu) {
+                                                        const float* __restrict__ coef, int relu,
+                                                        uint8_t* __restrict__ mbits) {
   const int CPR = C >> 3;
   for (I i = (I)blockIdx.x * BN_T + threadIdx.x; i < (I)nchunks; i += (I)gridDim.x * BN_T) {
     const int c8 = (int)(i % (I)CPR) * 8;
@@ -132,7 +145,9 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const uint16_t* __restri
       if (relu) v = fmaxf(v, 0.f);
       f[e] = v;
     }
-    *(u32x4*)(y + (size_t)i * 8) = pack8(f);
+    const u32x4 pk = pack8(f);
+    *(u32x4*)(y + (size_t)i * 8) = pk;
+    if (mbits) mbits[i] = mask_byte(pk);
   }
 }
 
@@ -141,7 +156,8 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const uint16_t* __restri
 template <typename I>
 __global__ __launch_bounds__(BN_T) void bn_apply2_kernel(const uint16_t* __restrict__ x, const float* __restrict__ coef,
                                                          const uint16_t* __restrict__ x2, const float* __restrict__ coef2,
-                                                         uint16_t* __restrict__ y, int64_t nchunks, int C, int relu) {
+                                                         uint16_t* __restrict__ y, int64_t nchunks, int C, int relu,
+                                                         uint8_t* __restrict__ mbits) {
   const int CPR = C >> 3;
   for (I i = (I)blockIdx.x * BN_T + threadIdx.x; i < (I)nchunks; i += (I)gridDim.x * BN_T) {
     const int c8 = (int)(i % (I)CPR) * 8;
@@ -156,7 +172,9 @@ __global__ __launch_bounds__(BN_T) void bn_apply2_kernel(const uint16_t* __restr
       if (relu) v = fmaxf(v, 0.f);
       f[e] = v;
     }
-    *(u32x4*)(y + (size_t)i * 8) = pack8(f);
+    const u32x4 pk = pack8(f);
+    *(u32x4*)(y + (size_t)i * 8) = pk;
+    if (mbits) mbits[i] = mask_byte(pk);
   }
 }
 
@@ -293,23 +311,32 @@ extern "C" int dpe_bn_eval_coeff(int C, const float* gamma, const float* beta, c
   return 0;
 }
 
-extern "C" int dpe_bn_apply(const uint16_t* x, const uint16_t* res, uint16_t* y, int64_t M, int C, const float* coef,
-                            int relu, hipStream_t st) {
+extern "C" int dpe_bn_apply_m(const uint16_t* x, const uint16_t* res, uint16_t* y, int64_t M, int C, const float* coef,
+                              int relu, uint8_t* mbits, hipStream_t st) {
   const int64_t nch = M * C / 8;
   if (nch < (1ll << 31))
-    hipLaunchKernelGGL(bn_apply_kernel<uint32_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, res, y, nch, C, coef, relu);
+    hipLaunchKernelGGL(bn_apply_kernel<uint32_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, res, y, nch, C, coef, relu,
+                       mbits);
   else
-    hipLaunchKernelGGL(bn_apply_kernel<int64_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, res, y, nch, C, coef, relu);
+    hipLaunchKernelGGL(bn_apply_kernel<int64_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, res, y, nch, C, coef, relu,
+                       mbits);
   return 0;
 }
 
+extern "C" int dpe_bn_apply(const uint16_t* x, const uint16_t* res, uint16_t* y, int64_t M, int C, const float* coef,
+                            int relu, hipStream_t st) {
+  return dpe_bn_apply_m(x, res, y, M, C, coef, relu, nullptr, st);
+}
+
 extern "C" int dpe_bn_apply2(const uint16_t* x, const float* coef, const uint16_t* x2, const float* coef2, uint16_t* y,
-                             int64_t M, int C, int relu, hipStream_t st) {
+                             int64_t M, int C, int relu, uint8_t* mbits, hipStream_t st) {
   const int64_t nch = M * C / 8;
   if (nch < (1ll << 31))
-    hipLaunchKernelGGL(bn_apply2_kernel<uint32_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, coef, x2, coef2, y, nch, C, relu);
+    hipLaunchKernelGGL(bn_apply2_kernel<uint32_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, coef, x2, coef2, y, nch, C, relu,
+                       mbits);
   else
-    hipLaunchKernelGGL(bn_apply2_kernel<int64_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, coef, x2, coef2, y, nch, C, relu);
+    hipLaunchKernelGGL(bn_apply2_kernel<int64_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, coef, x2, coef2, y, nch, C, relu,
+                       mbits);
   return 0;
 }
 

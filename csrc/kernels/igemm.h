@@ -54,9 +54,10 @@ struct IgemmArgs {
                              //                  x = st_x, [scale|shift|mean|invstd] = st_coef  (BN+ReLU backward)
   const uint16_t* st_x;      // [M][ldc] bf16 pre-BN input (row indexing as C, incl. phase remap)  (EPI_BF16_BNB)
   const float* st_coef;      // [4][N]                                                            (EPI_BF16_BNB)
-  const uint16_t* st_mask;   // EPI_BF16_BNB variant for a BN whose ReLU follows a residual add
-                             //   (y = relu(BN(x) + idn)): the ReLU mask is st_mask > 0 (the saved y,
-                             //   row indexing as C) and the STORED value is the masked dz, not v
+  const uint8_t* st_mask;    // EPI_BF16_BNB variant for a BN whose ReLU follows a residual add
+                             //   (y = relu(BN(x) + idn)): ReLU-mask BITS of the saved y, one byte per
+                             //   8 columns ([M][ldc/8], bit e = column 8j+e, written by bn_apply), and
+                             //   the STORED value is the masked dz, not v
   int stats_ld;              // partial columns per channel (0 -> tilesM of this launch)
   int stats_off;             // first partial column written by this launch (phase-decomposed dgrad)
   int M, N, K;

@@ -524,17 +524,11 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) xv[e] = (n + e < p.N) ? bf2f(p.st_x[orow * p.ldc + n + e]) : 0.f;
           }
-          if (p.st_mask) {  // relu'(y) from the saved post-residual output; store dz itself
-            float yv[8];
-            if (vec) {
-              unpack8(ld16(p.st_mask + orow * p.ldc + n), yv);
-            } else {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) yv[e] = (n + e < p.N) ? bf2f(p.st_mask[orow * p.ldc + n + e]) : 0.f;
-            }
+          if (p.st_mask) {  // relu'(y) from the saved post-residual output's mask bits; store dz itself
+            const uint32_t mb = p.st_mask[(orow * p.ldc + n) >> 3];
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              f[e] = yv[e] > 0.f ? f[e] : 0.f;
+              f[e] = ((mb >> e) & 1u) ? f[e] : 0.f;
               s[e] += f[e];
               ss[e] += f[e] * (xv[e] - bmu[e]);
             }

@@ -202,6 +202,122 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_apply_kernel(const uint16_
   }
 }
 
+// ---- quad form for the ResNet stem pool (k = 3, s = 2, p = 1, even H, W; OH = H/2, OW = W/2):
+// a thread owns the 2x2 input quad (2i.., 2j..) x 8 channels, which only windows (i|i+1, j|j+1)
+// reach -- 4 (dy, argmax) loads serve 4 pixels (instead of 9 for 4 pixels one by one), no loops.
+//   pixel (0,0): w00 tap 4 | (0,1): w00 5, w01 3 | (1,0): w00 7, w10 1 | (1,1): w00 8, w01 6, w10 2, w11 0
+DPE_DEVICE void pool_grad_quad(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ idx, int n, int i, int j, int c8,
+                               int C, int OH, int OW, float (*d)[8]) {
+  float g[4][8];
+  uint32_t b[4][2];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const int oi = i + (w >> 1), oj = j + (w & 1);
+    const bool v = oi < OH && oj < OW;
+    const size_t o = ((size_t)(n * OH + min(oi, OH - 1)) * OW + min(oj, OW - 1)) * C + c8;
+    const u32x2 pk = *(const u32x2*)(idx + o);
+    unpack8(*(const u32x4*)(dy + o), g[w]);
+    b[w][0] = v ? pk[0] : 0xffffffffu;  // 0xff never matches a tap
+    b[w][1] = v ? pk[1] : 0xffffffffu;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t t0 = (b[0][e >> 2] >> ((e & 3) * 8)) & 0xffu, t1 = (b[1][e >> 2] >> ((e & 3) * 8)) & 0xffu;
+    const uint32_t t2 = (b[2][e >> 2] >> ((e & 3) * 8)) & 0xffu, t3 = (b[3][e >> 2] >> ((e & 3) * 8)) & 0xffu;
+    d[0][e] = t0 == 4u ? g[0][e] : 0.f;
+    d[1][e] = (t0 == 5u ? g[0][e] : 0.f) + (t1 == 3u ? g[1][e] : 0.f);
+    d[2][e] = (t0 == 7u ? g[0][e] : 0.f) + (t2 == 1u ? g[2][e] : 0.f);
+    d[3][e] = (t0 == 8u ? g[0][e] : 0.f) + (t1 == 6u ? g[1][e] : 0.f) + (t2 == 2u ? g[2][e] : 0.f) +
+              (t3 == 0u ? g[3][e] : 0.f);
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bn_bwd_reduce_quad_kernel(const uint16_t* __restrict__ dy,
+                                                                         const uint8_t* __restrict__ idx,
+                                                                         const uint16_t* __restrict__ x,
+                                                                         const float* __restrict__ coef, int N, int H,
+                                                                         int W, int C, int quads_per_block,
+                                                                         float* __restrict__ part) {
+  const int CPR = C >> 3;
+  const int tid = threadIdx.x;
+  const int QPI = 256 / CPR;
+  const int c = tid % CPR, r = tid / CPR;
+  const int OH = H >> 1, OW = W >> 1;
+  const int Q = N * OH * OW;
+  const int qb = blockIdx.x * quads_per_block;
+  const int qe = min(Q, qb + quads_per_block);
+  float sm[8], sq[8], mean[8], sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sm[e] = 0.f; sq[e] = 0.f;
+    sc[e] = coef[c * 8 + e]; sh[e] = coef[C + c * 8 + e]; mean[e] = coef[2 * C + c * 8 + e];
+  }
+  if (r < QPI) {
+    for (int qd = qb + r; qd < qe; qd += QPI) {
+      const int j = qd % OW, t = qd / OW;
+      const int i = t % OH, n = t / OH;
+      float d[4][8];
+      pool_grad_quad(dy, idx, n, i, j, c * 8, C, OH, OW, d);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const size_t row = ((size_t)n * H + 2 * i + (u >> 1)) * W + 2 * j + (u & 1);
+        float xv[8];
+        unpack8(*(const u32x4*)(x + row * C + c * 8), xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dz = fmaf(xv[e], sc[e], sh[e]) > 0.f ? d[u][e] : 0.f;
+          sm[e] += dz;
+          sq[e] += dz * (xv[e] - mean[e]);
+        }
+      }
+    }
+  }
+  __shared__ float red[2][256][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][tid][e] = sm[e]; red[1][tid][e] = sq[e]; }
+  __syncthreads();
+  for (int ch = tid; ch < C; ch += 256) {
+    const int cc = ch >> 3, e = ch & 7;
+    float a = 0.f, b2 = 0.f;
+    for (int rr = 0; rr < QPI; ++rr) { a += red[0][rr * CPR + cc][e]; b2 += red[1][rr * CPR + cc][e]; }
+    part[(int64_t)ch * gridDim.x + blockIdx.x] = a;
+    part[(int64_t)(C + ch) * gridDim.x + blockIdx.x] = b2;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bn_bwd_apply_quad_kernel(const uint16_t* __restrict__ dy,
+                                                                        const uint8_t* __restrict__ idx,
+                                                                        const uint16_t* __restrict__ x,
+                                                                        const float* __restrict__ coef,
+                                                                        const float* __restrict__ bcoef,
+                                                                        uint16_t* __restrict__ dx, int N, int H, int W,
+                                                                        int C) {
+  const int CPR = C >> 3;
+  const int OH = H >> 1, OW = W >> 1;
+  const int total = N * OH * OW * CPR;
+  for (int it = blockIdx.x * 256 + threadIdx.x; it < total; it += gridDim.x * 256) {
+    const int c8 = (it % CPR) * 8;
+    int t = it / CPR;
+    const int j = t % OW; t /= OW;
+    const int i = t % OH;
+    const int n = t / OH;
+    float d[4][8];
+    pool_grad_quad(dy, idx, n, i, j, c8, C, OH, OW, d);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t off = (((size_t)n * H + 2 * i + (u >> 1)) * W + 2 * j + (u & 1)) * C + c8;
+      float xv[8], o[8];
+      unpack8(*(const u32x4*)(x + off), xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dz = fmaf(xv[e], coef[c8 + e], coef[C + c8 + e]) > 0.f ? d[u][e] : 0.f;
+        o[e] = bcoef[c8 + e] * dz + bcoef[C + c8 + e] * xv[e] + bcoef[2 * C + c8 + e];
+      }
+      *(u32x4*)(dx + off) = pack8(o);
+    }
+  }
+}
+
 // global average pool: x [N][HW][C] -> y [N][C] (bf16); one thread per (n, 8 channels)
 __global__ __launch_bounds__(256) void gavgpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int N,
                                                            int HW, int C) {
@@ -272,6 +388,12 @@ extern "C" int dpe_maxpool_bn_bwd_reduce(const uint16_t* dy, const uint8_t* idx,
                                          hipStream_t st) {
   if (C % 8 || C / 8 > 256 || (int64_t)N * H * W * C / 8 >= (1ll << 31)) return -1;
   const int64_t M = (int64_t)N * H * W;
+  if (k == 3 && s == 2 && p == 1 && H % 2 == 0 && W % 2 == 0 && OH == H / 2 && OW == W / 2) {
+    const int64_t Q = M / 4;
+    const int qpb = (int)((Q + nb - 1) / nb);
+    hipLaunchKernelGGL(maxpool_bn_bwd_reduce_quad_kernel, dim3(nb), dim3(256), 0, st, dy, idx, x, coef, N, H, W, C, qpb, part);
+    return 0;
+  }
   const int rpb = (int)((M + nb - 1) / nb);
   hipLaunchKernelGGL(maxpool_bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, st, dy, idx, x, coef, N, H, W, C, OH, OW, k, s, p,
                      rpb, part);
@@ -282,6 +404,11 @@ extern "C" int dpe_maxpool_bn_bwd_apply(const uint16_t* dy, const uint8_t* idx, 
                                         const float* bcoef, uint16_t* dx, int N, int H, int W, int C, int OH, int OW, int k,
                                         int s, int p, hipStream_t st) {
   if (C % 8 || (int64_t)N * H * W * C / 8 >= (1ll << 31)) return -1;
+  if (k == 3 && s == 2 && p == 1 && H % 2 == 0 && W % 2 == 0 && OH == H / 2 && OW == W / 2) {
+    hipLaunchKernelGGL(maxpool_bn_bwd_apply_quad_kernel, dim3(gs((int64_t)N * OH * OW * C / 8)), dim3(256), 0, st, dy, idx, x,
+                       coef, bcoef, dx, N, H, W, C);
+    return 0;
+  }
   hipLaunchKernelGGL(maxpool_bn_bwd_apply_kernel, dim3(gs((int64_t)N * H * W * C / 8)), dim3(256), 0, st, dy, idx, x, coef,
                      bcoef, dx, N, H, W, C, OH, OW, k, s, p);
   return 0;

@@ -22,8 +22,9 @@ backward (dout)
 Cross-block fusion of BN3's backward (DPE_BN3_CHAIN=1, default): block i's
 output ``out_i`` is consumed only by block i+1.  When block i+1 is an identity
 block, the epilogue of its first data-grad (dx = dh1 . W1 + dz3) also applies
-block i's ReLU mask (out_i > 0, i.e. relu'(BN3_i(h3_i) + idn_i)), stores the
-masked dz3_i directly, and emits BN3_i's backward partials (sum dz, sum
+block i's ReLU mask (out_i > 0, i.e. relu'(BN3_i(h3_i) + idn_i); read as the
+bit mask that block i's BN3 apply wrote beside out_i -- 1/16 of out_i's
+bytes), stores the masked dz3_i directly, and emits BN3_i's backward partials (sum dz, sum
 dz*(h3_i - mean)).  Block i's BN3 backward is then ONE elementwise pass
 (dh3 = a*dz3 + b*h3 + c) instead of a reduce pass over (dout, out, h3) plus an
 apply pass that re-reads all three and writes dz3: three fewer full passes
@@ -63,10 +64,10 @@ class _BN3Link:
     fused-epilogue result (BN3_i partials, identity of the masked dz3_i)
     handed back to block i's backward."""
 
-    __slots__ = ("h3", "coef", "part", "dz_ptr", "dz_shape")
+    __slots__ = ("h3", "coef", "mask", "part", "dz_ptr", "dz_shape")
 
     def __init__(self):
-        self.h3 = self.coef = self.part = None
+        self.h3 = self.coef = self.mask = self.part = None
         self.dz_ptr, self.dz_shape = 0, None
 
 
@@ -100,23 +101,26 @@ class BottleneckFn(Function):
                                 bn.eps)
 
         if block.down is not None:
-            hd, cd = conv_coef(3, x)  # BN_d is applied inside BN3's pass (bn_apply2)
+            hd, cd = conv_coef(3, x)  # BN_d is applied inside BN3's pass (bn_apply with residual_coef)
         else:
             hd, cd = None, None
         h1, a1, c1 = convbn(0, x, True)
         h2, a2, c2 = convbn(1, a1, True)
+        # the next block's fused data-grad epilogue reads this output's ReLU mask as bits
+        want_bits = link_out is not None
+        h3, c3 = conv_coef(2, a2)
         if block.down is not None:
-            h3, c3 = conv_coef(2, a2)
-            out = C.bn_apply2(h3, c3, hd, cd, True)
+            out, bits = C.bn_apply(h3, c3, hd, cd, True, want_bits)
         else:
-            h3, out, c3 = convbn(2, a2, True, x)
+            out, bits = C.bn_apply(h3, c3, x, None, True, want_bits)
         ctx.save_for_backward(x, h1, a1, h2, a2, h3, out, hd, c1, c2, c3, cd)
         # previous block's BN3 is fused into this block's first data grad (identity blocks only:
         # a downsample block's dx is completed by a second, strided kernel)
-        ctx.link_in = link_in if (link_in is not None and block.down is None and link_in.h3 is not None) else None
+        ctx.link_in = (link_in if (link_in is not None and block.down is None and link_in.h3 is not None
+                                   and link_in.mask is not None) else None)
         ctx.link_out = link_out
         if link_out is not None:
-            link_out.h3, link_out.coef = h3, c3
+            link_out.h3, link_out.coef, link_out.mask = h3, c3, bits
         ctx.block = block
         ctx.convs = convs
         ctx.ws = ws
@@ -189,7 +193,7 @@ class BottleneckFn(Function):
         else:
             dh3, dz3 = bn_bwd(2, dout, out, h3, c3, True)
         if lk is not None:
-            lk.h3 = lk.coef = None
+            lk.h3 = lk.coef = lk.mask = None
         wgrad(2, dh3, a2)
         dh2 = dgrad_bnb(2, dh3, 1, a2, h2, c2)
         wgrad(1, dh2, a1)
@@ -208,7 +212,7 @@ class BottleneckFn(Function):
             elif ctx.link_in is not None:
                 li = ctx.link_in
                 s, p, d = _conv_conf(convs[0].conv)
-                dx, part = C.conv_dgrad_bn(dh1, ws[0], list(x.shape), s, p, d, dz3, li.h3, li.coef, x)
+                dx, part = C.conv_dgrad_bn(dh1, ws[0], list(x.shape), s, p, d, dz3, li.h3, li.coef, li.mask)
                 li.part, li.dz_ptr, li.dz_shape = part, dx.data_ptr(), tuple(dx.shape)
             else:
                 dx = dgrad(0, dh1, list(x.shape), dz3)

@@ -482,6 +482,39 @@ def test_dgrad_bn_backward_partials(C, N, H, W, Ci, Co, k, s, p):
     assert rel_err(dh, dh_ref) < 2e-2 and rel_err(dg1, dg2) < 1e-3 and rel_err(db1, db2) < 1e-3
 
 
+def test_bn_apply_mask_bits_and_residual_relu_dgrad(C):
+    """bn_apply's ReLU-mask bits, and the dgrad epilogue variant that masks dx with them
+    (BN + residual + ReLU backward: dx stored as dz, BN partials of dz)."""
+    torch.manual_seed(14)
+    N, H, W, Ci, Co = 2, 14, 14, 64, 128
+    h = bf(torch.randn(N, H, W, Ci, device=dev))
+    coef = _bn_coef(C, Ci)
+    res = bf(torch.randn(N, H, W, Ci, device=dev))
+    y, bits = C.bn_apply(h, coef, res, None, True, True)
+    yref = torch.relu(h.float() * coef[0] + coef[1] + res.float())
+    assert rel_err(y, yref) < 1e-2
+    want = (y.float() > 0).reshape(-1, 8).to(torch.int32)
+    packed = (want << torch.arange(8, device=dev, dtype=torch.int32)).sum(-1).to(torch.uint8)
+    assert bits.shape == (N, H, W, Ci // 8) and torch.equal(bits.reshape(-1), packed)
+    # downsample form: residual BN'd in the same pass
+    coef2 = _bn_coef(C, Ci)
+    y2, _ = C.bn_apply(h, coef, res, coef2, True, False)
+    r2 = (res.float() * coef2[0] + coef2[1]).to(torch.bfloat16).float()
+    assert rel_err(y2, torch.relu(h.float() * coef[0] + coef[1] + r2)) < 1e-2
+    # 1x1 data grad + residual, masked by the bits, with partials over (dz, dz*(h - mean))
+    w = bf(torch.randn(Co, 1, 1, Ci, device=dev) / math.sqrt(Ci))
+    dy = bf(torch.randn(N, H, W, Co, device=dev))
+    dres = bf(torch.randn(N, H, W, Ci, device=dev))
+    dx, part = C.conv_dgrad_bn(dy, w, [N, H, W, Ci], [1, 1], [0, 0], [1, 1], dres, h, coef, bits)
+    full = C.conv_dgrad(dy, w, [N, H, W, Ci], [1, 1], [0, 0], [1, 1], dres).float()
+    dz = torch.where(y.float() > 0, full, torch.zeros_like(full))
+    assert rel_err(dx, dz) < 1e-2
+    tot = part.sum(-1)
+    dzf, hf = dz.reshape(-1, Ci), h.float().reshape(-1, Ci)
+    assert rel_err(tot[0], dzf.sum(0)) < 1e-2
+    assert rel_err(tot[1], (dzf * (hf - coef[2])).sum(0)) < 1e-2
+
+
 def test_s2d_stem_conv(C):
     """Space-to-depth packing + 4x4/s1 stem conv (fwd, BN stats, weight grad) == 7x7/s2/p3 conv."""
     from distributed_pytorch_example_amd.ops import functional as Fx
@@ -506,14 +539,16 @@ def test_s2d_stem_conv(C):
     assert rel_err(wp.grad, gref.permute(0, 2, 3, 1)) < 1e-2
 
 
-def test_stem_bn_relu_maxpool_fused(C):
+@pytest.mark.parametrize("H", [30, 29])
+def test_stem_bn_relu_maxpool_fused(C, H):
     """maxpool(relu(BN(h))) with the BN output never materialised (fwd, running stats,
-    and the pooled-gradient gather inside the BN backward) vs fp32 torch autograd."""
+    and the pooled-gradient gather inside the BN backward) vs fp32 torch autograd.
+    H even: quad-form backward kernels; H odd: the general gather."""
     from distributed_pytorch_example_amd.ops import functional as Fx
     from distributed_pytorch_example_amd.ops.layers import BatchNorm2d
 
     torch.manual_seed(23)
-    N, H, W, Cc = 4, 30, 30, 64  # odd pooled border (30 -> 15)
+    N, W, Cc = 4, H, 64  # odd pooled border (30 -> 15)
     h = bf(torch.randn(N, H, W, Cc, device=dev) * 2 + 0.3)
     bn = BatchNorm2d(Cc, device=dev)
     with torch.no_grad():
@@ -529,7 +564,7 @@ def test_stem_bn_relu_maxpool_fused(C):
     xr = h.float().permute(0, 3, 1, 2).requires_grad_(True)
     a = F.relu(F.batch_norm(xr, rm, rv, g, b, True, 0.1, 1e-5))
     ref = F.max_pool2d(a.to(torch.bfloat16).float(), 3, 2, 1)
-    assert y.shape == (N, 15, 15, Cc)
+    assert y.shape == (N, (H + 1) // 2, (W + 1) // 2, Cc)
     assert rel_err(y, ref.permute(0, 2, 3, 1)) < 1e-2
     assert rel_err(bn.running_mean, rm) < 1e-4 and rel_err(bn.running_var, rv) < 1e-4
     dy = bf(torch.randn_like(y))
