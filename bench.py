@@ -174,12 +174,13 @@ def main():
         tim = ddp.bucket_timings()
         sizes = ddp.bucket_bytes()
         rows, comm, hidden = [], 0.0, 0.0
-        for b, ms, rel in tim:
+        for b, ar_ms, rel in tim:
             # rel = start of this bucket's all-reduce relative to the end of backward (negative: overlapped)
-            ov = min(max(-rel, 0.0), ms)
-            comm += ms
+            ov = min(max(-rel, 0.0), ar_ms)
+            comm += ar_ms
             hidden += ov
-            rows.append({"bucket": b, "bytes": sizes[b], "allreduce_ms": round(ms, 4), "start_vs_bwd_end_ms": round(rel, 4)})
+            rows.append({"bucket": b, "bytes": sizes[b], "allreduce_ms": round(ar_ms, 4),
+                         "start_vs_bwd_end_ms": round(rel, 4)})
         extra["buckets"] = {"count": ddp.num_buckets(), "per_bucket": rows, "comm_ms": round(comm, 4),
                             "overlap_pct": round(100.0 * hidden / comm, 1) if comm > 0 else None}
     if rank == 0:
