@@ -487,28 +487,14 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
         bmu[e] = p.st_coef[2 * p.N + ch];
       }
     }
-    for (int rr = r0; rr < BM; rr += RPP) {
-      const int m = m0 + rr;
-      if (m >= p.M) break;
-      u32x4 v = *(const u32x4*)(smem + rr * CROW + c * 16);
-      int64_t orow = m;
-      if (p.g.remap) {  // phase dgrad: virtual row (n, hh, ww) -> real dX pixel
-        // remap 1: dgrad-form geometry (virtual output = H x W); 2: forward-form (OH x OW)
-        const int VW = p.g.remap == 2 ? p.g.OW : p.g.W, VH = p.g.remap == 2 ? p.g.OH : p.g.H;
-        const int ww = m % VW, t = m / VW, hh = t % VH, nn = t / VH;
-        orow = ((int64_t)nn * p.g.Hr + p.g.oa + p.g.psh * hh) * p.g.Wr + p.g.ob + p.g.psw * ww;
-      }
-      uint16_t* dst = C + orow * p.ldc + n;
+    // Per-row finish: residual add, BN-backward partials / ReLU-mask (BNB) or BN-forward
+    // partials, store.  Operands arrive pre-loaded (rv / xv / mb) so the fast path can
+    // issue the loads of several rows before the first use.
+    auto finish_row = [&](u32x4 v, const u32x4& rv, const u32x4& xv_raw, uint32_t mb, uint16_t* dst, bool vec_row) {
       if (p.residual) {
         float f[8], g[8];
         unpack8(v, f);
-        const uint16_t* src = p.residual + orow * p.ldc + n;
-        if (vec) {
-          unpack8(ld16(src), g);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) g[e] = (n + e < p.N) ? bf2f(src[e]) : 0.f;
-        }
+        unpack8(rv, g);
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] += g[e];
         v = pack8(f);
@@ -518,14 +504,8 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
         unpack8(v, f);
         if constexpr (BNB) {  // (sum dz, sum dz*(x - mean)), dz = f * relu'(...)
           float xv[8];
-          if (vec) {
-            unpack8(ld16(p.st_x + orow * p.ldc + n), xv);
-          } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) xv[e] = (n + e < p.N) ? bf2f(p.st_x[orow * p.ldc + n + e]) : 0.f;
-          }
+          unpack8(xv_raw, xv);
           if (p.st_mask) {  // relu'(y) from the saved post-residual output's mask bits; store dz itself
-            const uint32_t mb = p.st_mask[(orow * p.ldc + n) >> 3];
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               f[e] = ((mb >> e) & 1u) ? f[e] : 0.f;
@@ -546,13 +526,69 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
           for (int e = 0; e < 8; ++e) { s[e] += f[e]; ss[e] += f[e] * f[e]; }
         }
       }
-      if (vec) {
+      if (vec_row) {
         *(u32x4*)dst = v;
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           if (n + e < p.N) dst[e] = (uint16_t)((e & 1) ? (v[e >> 1] >> 16) : (v[e >> 1] & 0xffff));
         }
+      }
+    };
+    constexpr int RPI = BM / RPP;                 // rows per thread: 2, 4 or 8
+    constexpr int G = RPI < 4 ? RPI : 4;          // rows whose operand loads are issued together
+    const u32x4 z4 = zero16();
+    if (vec && !p.g.remap && m0 + BM <= p.M) {
+      // full tile, contiguous rows: G rows' residual / pre-BN / mask loads in flight at once
+#pragma unroll
+      for (int u0 = 0; u0 < RPI; u0 += G) {
+        u32x4 tv[G], rv[G], xv[G];
+        uint32_t mb[G];
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+          const int rr = r0 + (u0 + q) * RPP;
+          const int64_t off = (int64_t)(m0 + rr) * p.ldc + n;
+          tv[q] = *(const u32x4*)(smem + rr * CROW + c * 16);
+          rv[q] = p.residual ? ld16(p.residual + off) : z4;
+          xv[q] = (BNB && p.col_stats) ? ld16(p.st_x + off) : z4;
+          mb[q] = (BNB && p.st_mask) ? (uint32_t)p.st_mask[off >> 3] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+          const int rr = r0 + (u0 + q) * RPP;
+          finish_row(tv[q], rv[q], xv[q], mb[q], C + (int64_t)(m0 + rr) * p.ldc + n, true);
+        }
+      }
+    } else {
+      for (int rr = r0; rr < BM; rr += RPP) {
+        const int m = m0 + rr;
+        if (m >= p.M) break;
+        const u32x4 v = *(const u32x4*)(smem + rr * CROW + c * 16);
+        int64_t orow = m;
+        if (p.g.remap) {  // phase dgrad: virtual row (n, hh, ww) -> real dX pixel
+          // remap 1: dgrad-form geometry (virtual output = H x W); 2: forward-form (OH x OW)
+          const int VW = p.g.remap == 2 ? p.g.OW : p.g.W, VH = p.g.remap == 2 ? p.g.OH : p.g.H;
+          const int ww = m % VW, t = m / VW, hh = t % VH, nn = t / VH;
+          orow = ((int64_t)nn * p.g.Hr + p.g.oa + p.g.psh * hh) * p.g.Wr + p.g.ob + p.g.psw * ww;
+        }
+        const int64_t off = orow * p.ldc + n;
+        u32x4 rv = z4, xv = z4;
+        uint32_t mb = 0;
+        if (vec) {
+          if (p.residual) rv = ld16(p.residual + off);
+          if (BNB && p.col_stats) xv = ld16(p.st_x + off);
+        } else {
+          float g[8], xf[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            g[e] = (p.residual && n + e < p.N) ? bf2f(p.residual[off + e]) : 0.f;
+            xf[e] = (BNB && p.col_stats && n + e < p.N) ? bf2f(p.st_x[off + e]) : 0.f;
+          }
+          rv = pack8(g);
+          xv = pack8(xf);
+        }
+        if (BNB && p.st_mask) mb = p.st_mask[off >> 3];
+        finish_row(v, rv, xv, mb, C + off, vec);
       }
     }
     if (p.col_stats) {
