@@ -121,33 +121,64 @@ __global__ void bn_eval_coeff_kernel(int C, const float* gamma, const float* bet
   out[3 * C + ch] = invstd;
 }
 
-// y = act(x*scale + shift [+ res]); grid-stride over 16-B chunks.
+// Elementwise BN passes: grid-stride over 16-B chunks, BN_U chunks per thread per
+// iteration with all of their loads issued before the first use (one chunk in
+// flight per thread left these passes latency-bound), per-channel coefficients
+// hoisted out of the loop (the stride is a multiple of C/8 whenever C/8 divides BN_T).
+constexpr int BN_U = 4;
+
+template <int NCOEF>
+struct Coef8 {
+  float v[NCOEF][8];
+  DPE_DEVICE void load(const float* __restrict__ base, int C, int c8) {
+#pragma unroll
+    for (int k = 0; k < NCOEF; ++k) {
+      const f32x4 a = *(const f32x4*)(base + k * C + c8), b = *(const f32x4*)(base + k * C + c8 + 4);
+      v[k][0] = a[0]; v[k][1] = a[1]; v[k][2] = a[2]; v[k][3] = a[3];
+      v[k][4] = b[0]; v[k][5] = b[1]; v[k][6] = b[2]; v[k][7] = b[3];
+    }
+  }
+};
+
+// y = act(x*scale + shift [+ res])
 template <typename I>
 __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                         uint16_t* __restrict__ y, int64_t nchunks, int C,
                                                         const float* __restrict__ coef, int relu,
                                                         uint8_t* __restrict__ mbits) {
   const int CPR = C >> 3;
-  for (I i = (I)blockIdx.x * BN_T + threadIdx.x; i < (I)nchunks; i += (I)gridDim.x * BN_T) {
-    const int c8 = (int)(i % (I)CPR) * 8;
-    float f[8];
-    unpack8(*(const u32x4*)(x + (size_t)i * 8), f);
-    float g[8];
-    if (res) unpack8(*(const u32x4*)(res + (size_t)i * 8), g);
-    const f32x4 sc0 = *(const f32x4*)(coef + c8), sc1 = *(const f32x4*)(coef + c8 + 4);
-    const f32x4 sh0 = *(const f32x4*)(coef + C + c8), sh1 = *(const f32x4*)(coef + C + c8 + 4);
+  const I n = (I)nchunks, stride = (I)gridDim.x * BN_T;
+  const I first = (I)blockIdx.x * BN_T + threadIdx.x;
+  const bool hoist = (BN_T % CPR) == 0;
+  Coef8<2> cf;
+  if (hoist) cf.load(coef, C, (int)(first % (I)CPR) * 8);
+  for (I i0 = first; i0 < n; i0 += stride * BN_U) {
+    u32x4 xr[BN_U], rr[BN_U];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float sc = e < 4 ? sc0[e] : sc1[e - 4];
-      const float sh = e < 4 ? sh0[e] : sh1[e - 4];
-      float v = f[e] * sc + sh;
-      if (res) v += g[e];
-      if (relu) v = fmaxf(v, 0.f);
-      f[e] = v;
+    for (int u = 0; u < BN_U; ++u) {
+      const I i = min(i0 + (I)u * stride, n - 1);
+      xr[u] = *(const u32x4*)(x + (size_t)i * 8);
+      if (res) rr[u] = *(const u32x4*)(res + (size_t)i * 8);
     }
-    const u32x4 pk = pack8(f);
-    *(u32x4*)(y + (size_t)i * 8) = pk;
-    if (mbits) mbits[i] = mask_byte(pk);
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const I i = i0 + (I)u * stride;
+      if (i >= n) break;
+      if (!hoist) cf.load(coef, C, (int)(i % (I)CPR) * 8);
+      float f[8], g[8];
+      unpack8(xr[u], f);
+      if (res) unpack8(rr[u], g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v = fmaf(f[e], cf.v[0][e], cf.v[1][e]);
+        if (res) v += g[e];
+        if (relu) v = fmaxf(v, 0.f);
+        f[e] = v;
+      }
+      const u32x4 pk = pack8(f);
+      *(u32x4*)(y + (size_t)i * 8) = pk;
+      if (mbits) mbits[i] = mask_byte(pk);
+    }
   }
 }
 
@@ -159,22 +190,45 @@ __global__ __launch_bounds__(BN_T) void bn_apply2_kernel(const uint16_t* __restr
                                                          uint16_t* __restrict__ y, int64_t nchunks, int C, int relu,
                                                          uint8_t* __restrict__ mbits) {
   const int CPR = C >> 3;
-  for (I i = (I)blockIdx.x * BN_T + threadIdx.x; i < (I)nchunks; i += (I)gridDim.x * BN_T) {
-    const int c8 = (int)(i % (I)CPR) * 8;
-    float f[8], g[8];
-    unpack8(*(const u32x4*)(x + (size_t)i * 8), f);
-    unpack8(*(const u32x4*)(x2 + (size_t)i * 8), g);
+  const I n = (I)nchunks, stride = (I)gridDim.x * BN_T;
+  const I first = (I)blockIdx.x * BN_T + threadIdx.x;
+  const bool hoist = (BN_T % CPR) == 0;
+  Coef8<2> cf, cf2;
+  if (hoist) {
+    cf.load(coef, C, (int)(first % (I)CPR) * 8);
+    cf2.load(coef2, C, (int)(first % (I)CPR) * 8);
+  }
+  for (I i0 = first; i0 < n; i0 += stride * BN_U) {
+    u32x4 xr[BN_U], x2r[BN_U];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      // the residual is rounded to bf16 first, as when it is materialised
-      const float r = bf2f(f2bf(fmaf(g[e], coef2[c8 + e], coef2[C + c8 + e])));
-      float v = fmaf(f[e], coef[c8 + e], coef[C + c8 + e]) + r;
-      if (relu) v = fmaxf(v, 0.f);
-      f[e] = v;
+    for (int u = 0; u < BN_U; ++u) {
+      const I i = min(i0 + (I)u * stride, n - 1);
+      xr[u] = *(const u32x4*)(x + (size_t)i * 8);
+      x2r[u] = *(const u32x4*)(x2 + (size_t)i * 8);
     }
-    const u32x4 pk = pack8(f);
-    *(u32x4*)(y + (size_t)i * 8) = pk;
-    if (mbits) mbits[i] = mask_byte(pk);
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const I i = i0 + (I)u * stride;
+      if (i >= n) break;
+      if (!hoist) {
+        cf.load(coef, C, (int)(i % (I)CPR) * 8);
+        cf2.load(coef2, C, (int)(i % (I)CPR) * 8);
+      }
+      float f[8], g[8];
+      unpack8(xr[u], f);
+      unpack8(x2r[u], g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        // the residual is rounded to bf16 first, as when it is materialised
+        const float r = bf2f(f2bf(fmaf(g[e], cf2.v[0][e], cf2.v[1][e])));
+        float v = fmaf(f[e], cf.v[0][e], cf.v[1][e]) + r;
+        if (relu) v = fmaxf(v, 0.f);
+        f[e] = v;
+      }
+      const u32x4 pk = pack8(f);
+      *(u32x4*)(y + (size_t)i * 8) = pk;
+      if (mbits) mbits[i] = mask_byte(pk);
+    }
   }
 }
 
@@ -251,25 +305,50 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const uint16_t* __re
                                                             uint16_t* __restrict__ dx, uint16_t* __restrict__ dz_out,
                                                             int64_t nchunks, int C, const float* __restrict__ mcoef) {
   const int CPR = C >> 3;
-  for (I i = (I)blockIdx.x * BN_T + threadIdx.x; i < (I)nchunks; i += (I)gridDim.x * BN_T) {
-    const int c8 = (int)(i % (I)CPR) * 8;
-    float d[8], xv[8];
-    unpack8(*(const u32x4*)(dy + (size_t)i * 8), d);
-    unpack8(*(const u32x4*)(x + (size_t)i * 8), xv);
-    if (y) {
-      float yv[8];
-      unpack8(*(const u32x4*)(y + (size_t)i * 8), yv);
+  const I n = (I)nchunks, stride = (I)gridDim.x * BN_T;
+  const I first = (I)blockIdx.x * BN_T + threadIdx.x;
+  const bool hoist = (BN_T % CPR) == 0;
+  Coef8<3> bc;
+  Coef8<2> mc;
+  if (hoist) {
+    bc.load(bcoef, C, (int)(first % (I)CPR) * 8);
+    if (mcoef) mc.load(mcoef, C, (int)(first % (I)CPR) * 8);
+  }
+  for (I i0 = first; i0 < n; i0 += stride * BN_U) {
+    u32x4 dr[BN_U], xr[BN_U], yr[BN_U];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
-    } else if (mcoef) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) d[e] = fmaf(xv[e], mcoef[c8 + e], mcoef[C + c8 + e]) > 0.f ? d[e] : 0.f;
+    for (int u = 0; u < BN_U; ++u) {
+      const I i = min(i0 + (I)u * stride, n - 1);
+      dr[u] = *(const u32x4*)(dy + (size_t)i * 8);
+      xr[u] = *(const u32x4*)(x + (size_t)i * 8);
+      if (y) yr[u] = *(const u32x4*)(y + (size_t)i * 8);
     }
-    if (dz_out) *(u32x4*)(dz_out + (size_t)i * 8) = pack8(d);
-    float o[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = bcoef[c8 + e] * d[e] + bcoef[C + c8 + e] * xv[e] + bcoef[2 * C + c8 + e];
-    *(u32x4*)(dx + (size_t)i * 8) = pack8(o);
+    for (int u = 0; u < BN_U; ++u) {
+      const I i = i0 + (I)u * stride;
+      if (i >= n) break;
+      if (!hoist) {
+        bc.load(bcoef, C, (int)(i % (I)CPR) * 8);
+        if (mcoef) mc.load(mcoef, C, (int)(i % (I)CPR) * 8);
+      }
+      float d[8], xv[8];
+      unpack8(dr[u], d);
+      unpack8(xr[u], xv);
+      if (y) {
+        float yv[8];
+        unpack8(yr[u], yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+      } else if (mcoef) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = fmaf(xv[e], mc.v[0][e], mc.v[1][e]) > 0.f ? d[e] : 0.f;
+      }
+      if (dz_out) *(u32x4*)(dz_out + (size_t)i * 8) = pack8(d);
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = fmaf(bc.v[0][e], d[e], fmaf(bc.v[1][e], xv[e], bc.v[2][e]));
+      *(u32x4*)(dx + (size_t)i * 8) = pack8(o);
+    }
   }
 }
 
