@@ -64,32 +64,46 @@ __global__ __launch_bounds__(BN_T) void bn_stats_partial_kernel(const uint16_t* 
   }
 }
 
-// Sum channel ch's nb partials (layout [2][C][nb]) with the whole 256-thread
-// block (the conv-epilogue partials number M/BM -- thousands for the early
-// layers -- so one wave per channel was latency-bound); fp64 accumulation.
+// Sum channel ch's nb partials (layout [2][C][nb]) with the whole NTHR-thread
+// block (the conv-epilogue partials number M/BM -- 12,544 per channel for the
+// first stage at batch 512 -- so a narrow block was latency-bound): four
+// independent fp64 accumulator pairs per thread keep 8 loads in flight.
 // Result valid in thread 0.
+template <int NTHR>
 DPE_DEVICE void block_sum2(const float* __restrict__ part, int nb, int C, int ch, double& s, double& q) {
-  __shared__ double red[2][4];
+  constexpr int NW = NTHR / 64;
+  __shared__ double red[2][NW];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  double a = 0.0, b = 0.0;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
   const float* ps = part + (int64_t)ch * nb;
   const float* pq = part + (int64_t)(C + ch) * nb;
-  for (int i = threadIdx.x; i < nb; i += 256) { a += ps[i]; b += pq[i]; }
+  int i = threadIdx.x;
+  for (; i + 3 * NTHR < nb; i += 4 * NTHR) {
+    const float x0 = ps[i], x1 = ps[i + NTHR], x2 = ps[i + 2 * NTHR], x3 = ps[i + 3 * NTHR];
+    const float y0 = pq[i], y1 = pq[i + NTHR], y2 = pq[i + 2 * NTHR], y3 = pq[i + 3 * NTHR];
+    a0 += x0; a1 += x1; a2 += x2; a3 += x3;
+    b0 += y0; b1 += y1; b2 += y2; b3 += y3;
+  }
+  for (; i < nb; i += NTHR) { a0 += ps[i]; b0 += pq[i]; }
+  double a = (a0 + a1) + (a2 + a3), b = (b0 + b1) + (b2 + b3);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
   if (lane == 0) { red[0][wid] = a; red[1][wid] = b; }
   __syncthreads();
-  s = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-  q = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  s = 0.0; q = 0.0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) { s += red[0][w]; q += red[1][w]; }
 }
 
 // out: [4][C] = scale, shift, mean, invstd
-__global__ void bn_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M, const float* __restrict__ gamma,
-                                   const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
-                                   float momentum, float eps, float* __restrict__ out) {
+template <int NTHR>
+__global__ __launch_bounds__(NTHR) void bn_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M,
+                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                           float* __restrict__ rmean, float* __restrict__ rvar,
+                                                           float momentum, float eps, float* __restrict__ out) {
   const int ch = blockIdx.x;
   double s, q;
-  block_sum2(part, nb, C, ch, s, q);
+  block_sum2<NTHR>(part, nb, C, ch, s, q);
   if (threadIdx.x != 0) return;
   const double mean = s / (double)M;
   double var = q / (double)M - mean * mean;
@@ -275,12 +289,14 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const uint16_t* __r
 }
 
 // bcoef: [3][C] = a, b, c  for dx = a*dz + b*x + c ; dgamma/dbeta accumulated (+=) into fp32 grads
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M, const float* __restrict__ gamma,
-                                       const float* __restrict__ coef, float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                       float* __restrict__ bcoef) {
+template <int NTHR>
+__global__ __launch_bounds__(NTHR) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nb, int C, int64_t M,
+                                                               const float* __restrict__ gamma, const float* __restrict__ coef,
+                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                               float* __restrict__ bcoef) {
   const int ch = blockIdx.x;
   double s, q;
-  block_sum2(part, nb, C, ch, s, q);
+  block_sum2<NTHR>(part, nb, C, ch, s, q);
   if (threadIdx.x != 0) return;
   const float mean = coef[2 * C + ch], invstd = coef[3 * C + ch];
   const float g = gamma ? gamma[ch] : 1.f;
@@ -379,7 +395,12 @@ extern "C" int dpe_bn_stats(const uint16_t* x, int64_t M, int C, int nb, float* 
 
 extern "C" int dpe_bn_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* beta,
                                float* rmean, float* rvar, float momentum, float eps, float* coef, hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, part, nb, C, M, gamma, beta, rmean, rvar,
+  if (nb > 2048) {
+    hipLaunchKernelGGL(bn_finalize_kernel<1024>, dim3(C), dim3(1024), 0, st, part, nb, C, M, gamma, beta, rmean, rvar,
+                       momentum, eps, coef);
+    return 0;
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel<256>, dim3(C), dim3(256), 0, st, part, nb, C, M, gamma, beta, rmean, rvar,
                      momentum, eps, coef);
   return 0;
 }
@@ -429,7 +450,12 @@ extern "C" int dpe_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const ui
 
 extern "C" int dpe_bn_bwd_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* coef,
                                    float* dgamma, float* dbeta, float* bcoef, hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, nb, C, M, gamma, coef, dgamma,
+  if (nb > 2048) {
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<1024>, dim3(C), dim3(1024), 0, st, part, nb, C, M, gamma, coef, dgamma, dbeta,
+                       bcoef);
+    return 0;
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<256>, dim3(C), dim3(256), 0, st, part, nb, C, M, gamma, coef, dgamma,
                      dbeta, bcoef);
   return 0;
 }
