@@ -113,7 +113,11 @@ Cfg pick_cfg(int64_t M, int64_t N, int64_t K, bool allow_split) {
     c.bn = N <= 64 ? 64 : 128;
     const int64_t t = tiles(c.bm, c.bn);
     const int64_t ksteps = (K + 31) / 32;
-    int64_t splits = std::max<int64_t>(1, std::min<int64_t>((512 + t - 1) / t, ksteps / 8));
+    static const int64_t target_blocks = [] {
+      const char* e = getenv("DPE_WGRAD_BLOCKS");
+      return (int64_t)(e ? std::max(64, atoi(e)) : 512);
+    }();
+    int64_t splits = std::max<int64_t>(1, std::min<int64_t>((target_blocks + t - 1) / t, ksteps / 8));
     const int64_t kps = (ksteps + splits - 1) / splits;
     c.k_split = (int)(kps * 32);
     c.splits = (int)((ksteps + kps - 1) / kps);
