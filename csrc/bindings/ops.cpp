@@ -4,6 +4,7 @@
 // HIP stream, so the ops compose with the caching allocator and hipGraph
 // capture (no host sync, no hipMalloc inside).
 #include <torch/extension.h>
+#include <cstring>
 #include <map>
 #include <string>
 #include <c10/hip/HIPStream.h>
@@ -192,10 +193,56 @@ bool try_gemm256(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_sp
 
 // conv_*: the 128-tile kernel measured faster than the 256-tile one on every
 // ResNet-50 1x1 shape (small K / N), so convolutions opt out of it unless forced.
+// DPE_IGEMM_DMA=0: forward-form convolutions stay on the register-staged kernel (A/B reference)
+bool igemm_dma_on() {
+  static const bool on = [] { const char* e = getenv("DPE_IGEMM_DMA"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
+// Tile of the LDS-DMA conv kernel: 0 auto, 1 128-tile (pick_cfg), 2 256x128, 3 256x256
+// (8 waves; only where pick_cfg chose a 128-row tile, so BN partial layouts never change).
+// DPE_DMA_TILE=128|256x128|256x256 or set_conv_tile().
+int g_dma_tile = -1;
+int dma_tile_mode() {
+  if (g_dma_tile < 0) {
+    const char* e = getenv("DPE_DMA_TILE");
+    g_dma_tile = !e ? 0 : !strcmp(e, "128") ? 1 : !strcmp(e, "256x128") ? 2 : !strcmp(e, "256x256") ? 3 : 0;
+  }
+  return g_dma_tile;
+}
+
+void dma_tile(const dpe::IgemmArgs& a, int aload, int bload, int& bm, int& bn) {
+  if (bm != 128 || bload != dpe::B_DENSE_K) return;
+  int mode = dma_tile_mode();
+  if (mode == 0) {
+    // measured (scripts/bench_convs.py, batch 512): 256x128 wins on 3x3 convs with K >= 576 and
+    // on K >= 1024; 256x256 (one block per CU) loses on most ResNet-50 shapes
+    const bool taps = aload == dpe::A_CONV_FWD && a.g.R * a.g.S > 1;
+    mode = (a.K >= 1024 || (taps && a.K >= 576)) ? 2 : 1;
+  }
+  if (mode == 3 && a.N > 128) { bm = 256; bn = 256; }
+  else if (mode >= 2 && a.N > 64) { bm = 256; bn = 128; }
+}
+
 void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_split, bool conv = false) {
   if ((!conv || g_g256_override == 1 || g256_mode() == 2) && try_gemm256(a, aload, bload, epi, allow_split)) return;
   Cfg c = pick_cfg(a.M, a.N, a.K, allow_split && epi == dpe::EPI_ATOMIC_F32);
   a.k_split = c.k_split;
+  // LDS-DMA kernel where it measured faster: im2col A (3x3 / strided), dense 1x1 A at K >= 512,
+  // B K-contiguous (the N-contiguous B of 1x1 data grads measured 5-10 % slower on it)
+  const bool dma_role = bload == dpe::B_DENSE_K && (aload == dpe::A_CONV_FWD || (aload == dpe::A_DENSE_K && a.K >= 512));
+  if (conv && c.splits == 1 && dma_role && igemm_dma_on()) {
+    // convolutions whose A is an im2col / dense K-contiguous operand: LDS-DMA kernel
+    // (same tile shape, so BatchNorm partial layouts are unchanged)
+    int bm = c.bm, bn = c.bn;
+    dma_tile(a, aload, bload, bm, bn);
+    const int rc = dpe_igemm_dma_launch(&a, bm, bn, aload, bload, epi, cur_stream());
+    if (rc == 0) {
+      const hipError_t e = hipGetLastError();
+      TORCH_CHECK(e == hipSuccess, "igemm_dma launch failed: ", hipGetErrorString(e));
+      return;
+    }
+  }
   const int rc = dpe_igemm_launch(&a, c.bm, c.bn, aload, bload, epi, c.splits, cur_stream());
   const hipError_t e = hipGetLastError();
   TORCH_CHECK(e == hipSuccess, "igemm launch failed: ", hipGetErrorString(e));
@@ -1169,6 +1216,8 @@ void register_ops(pybind11::module& m) {
     return v;
   });
   m.def("set_gemm256_mode", [](int64_t mode) { g_g256_mode = (int)mode; }, "0 auto, 1 off, 2 force (when supported)");
+  m.def("set_conv_tile", [](int64_t mode) { g_dma_tile = (int)mode; },
+        "LDS-DMA conv tile: 0 auto, 1 128-tile, 2 256x128, 3 256x256 (8 waves)");
   m.def("pick_gemm_cfg", [](int64_t M, int64_t N, int64_t K, bool split) {
     auto c = pick_cfg(M, N, K, split);
     return std::make_tuple(c.bm, c.bn, c.splits, c.k_split);

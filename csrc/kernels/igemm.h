@@ -77,3 +77,8 @@ extern "C" int dpe_igemm_launch(const dpe::IgemmArgs* args, int bm, int bn, int 
 // 256x256x64 LDS-DMA / 8-phase GEMM (gemm256.hip) for large dense shapes.
 // a_k / b_k: operand K-contiguous (1) or M/N-contiguous (0); K % 64 == 0.
 extern "C" int dpe_gemm256_launch(const dpe::IgemmArgs* args, int a_k, int b_k, int epi, int splits, hipStream_t stream);
+
+// LDS-DMA implicit-GEMM (igemm.hip) for forward-form convolutions and dense K-contiguous A
+// (B K- or N-contiguous; EPI_BF16 / EPI_BF16_BNB, no split-K).  -1: outside its envelope.
+extern "C" int dpe_igemm_dma_launch(const dpe::IgemmArgs* args, int bm, int bn, int aload, int bload, int epi,
+                                    hipStream_t stream);

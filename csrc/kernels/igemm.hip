@@ -294,6 +294,204 @@ DPE_DEVICE float act_fn(float x, int act) {
   return x;
 }
 
+// Shared bf16 epilogue (EPI_BF16 / EPI_BF16_BNB) of the implicit-GEMM kernels: stage the
+// tile through LDS, then coalesced 16-B row stores with residual add and BatchNorm partials.
+// acc[RM][RN] is one wave's (16 RM) x (16 RN) sub-tile at (wm, wn); NTH threads.  BatchNorm
+// partials are always per 128-row (64 for BM = 64) sub-tile, so the partial layout does not
+// depend on which kernel / tile ran: column (tm * NSUB + sub) of [2][N][stats_ld].
+template <int BM, int BN, int RM, int RN, int NTH, int EPI>
+DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* smem, int m0, int n0, int tm, int wm,
+                              int wn) {
+  constexpr int CROW = BN * 2 + 16;
+  constexpr int NW = NTH / 64;
+  constexpr int SUBM = BM < 128 ? BM : 128, NSUB = BM / SUBM;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lm = lane & 15, ln4 = (lane >> 4) * 4;
+  const int tilesSub = (p.M + SUBM - 1) / SUBM;
+  constexpr bool BNB = (EPI == EPI_BF16_BNB);
+  // Stage bf16 tile in LDS (row stride CROW), then coalesced 16-B stores.
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    const int ml = wm + 16 * i + lm;
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int nl = wn + 16 * j + ln4;
+      const int n = n0 + nl;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float b = (p.bias && n + e < p.N) ? p.bias[n + e] : 0.f;
+        v[e] = act_fn(p.alpha * acc[i][j][e] + b, p.act);
+      }
+      u32x2 pk;
+      pk[0] = pack_bf2(v[0], v[1]);
+      pk[1] = pack_bf2(v[2], v[3]);
+      *(u32x2*)(smem + ml * CROW + nl * 2) = pk;
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8, RPP = NTH / CPR;
+  static_assert(SUBM % RPP == 0, "row passes must tile a stats sub-tile");
+  const int c = tid % CPR, r0 = tid / CPR;
+  const int n = n0 + c * 8;
+  uint16_t* C = (uint16_t*)p.C;
+  const bool vec = ((p.ldc & 7) == 0) && (n + 8 <= p.N);
+  float s[8], ss[8];
+  float bsc[8], bsh[8], bmu[8];  // BN forward coefficients of this thread's 8 columns (EPI_BF16_BNB)
+  if constexpr (BNB) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int ch = min(n + e, p.N - 1);
+      bsc[e] = p.st_coef[ch];
+      bsh[e] = p.st_coef[p.N + ch];
+      bmu[e] = p.st_coef[2 * p.N + ch];
+    }
+  }
+  // Per-row finish: residual add, BN-backward partials / ReLU-mask (BNB) or BN-forward
+  // partials, store.  Operands arrive pre-loaded (rv / xv / mb) so the fast path can
+  // issue the loads of several rows before the first use.
+  auto finish_row = [&](u32x4 v, const u32x4& rv, const u32x4& xv_raw, uint32_t mb, uint16_t* dst, bool vec_row) {
+    if (p.residual) {
+      float f[8], g[8];
+      unpack8(v, f);
+      unpack8(rv, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] += g[e];
+      v = pack8(f);
+    }
+    if (p.col_stats) {
+      float f[8];
+      unpack8(v, f);
+      if constexpr (BNB) {  // (sum dz, sum dz*(x - mean)), dz = f * relu'(...)
+        float xv[8];
+        unpack8(xv_raw, xv);
+        if (p.st_mask) {  // relu'(y) from the saved post-residual output's mask bits; store dz itself
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            f[e] = ((mb >> e) & 1u) ? f[e] : 0.f;
+            s[e] += f[e];
+            ss[e] += f[e] * (xv[e] - bmu[e]);
+          }
+          v = pack8(f);
+        } else {  // relu'(x*scale + shift), recomputed from the pre-BN input
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float dz = fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? f[e] : 0.f;
+            s[e] += dz;
+            ss[e] += dz * (xv[e] - bmu[e]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { s[e] += f[e]; ss[e] += f[e] * f[e]; }
+      }
+    }
+    if (vec_row) {
+      *(u32x4*)dst = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (n + e < p.N) dst[e] = (uint16_t)((e & 1) ? (v[e >> 1] >> 16) : (v[e >> 1] & 0xffff));
+      }
+    }
+  };
+  constexpr int RPS = SUBM / RPP;               // rows per thread per stats sub-tile
+  constexpr int G = RPS < 4 ? RPS : 4;          // rows whose operand loads are issued together
+  const u32x4 z4 = zero16();
+  const bool fast = vec && !p.g.remap && m0 + BM <= p.M;
+#pragma unroll
+  for (int sub = 0; sub < NSUB; ++sub) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
+    const int rb = sub * SUBM;
+    if (fast) {
+      // full tile, contiguous rows: G rows' residual / pre-BN / mask loads in flight at once
+#pragma unroll
+      for (int u0 = 0; u0 < RPS; u0 += G) {
+        u32x4 tv[G], rv[G], xv[G];
+        uint32_t mb[G];
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+          const int rr = rb + r0 + (u0 + q) * RPP;
+          const int64_t off = (int64_t)(m0 + rr) * p.ldc + n;
+          tv[q] = *(const u32x4*)(smem + rr * CROW + c * 16);
+          rv[q] = p.residual ? ld16(p.residual + off) : z4;
+          xv[q] = (BNB && p.col_stats) ? ld16(p.st_x + off) : z4;
+          mb[q] = (BNB && p.st_mask) ? (uint32_t)p.st_mask[off >> 3] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+          const int rr = rb + r0 + (u0 + q) * RPP;
+          finish_row(tv[q], rv[q], xv[q], mb[q], C + (int64_t)(m0 + rr) * p.ldc + n, true);
+        }
+      }
+    } else {
+      for (int rr = rb + r0; rr < rb + SUBM; rr += RPP) {
+        const int m = m0 + rr;
+        if (m >= p.M) break;
+        const u32x4 v = *(const u32x4*)(smem + rr * CROW + c * 16);
+        int64_t orow = m;
+        if (p.g.remap) {  // phase dgrad: virtual row (n, hh, ww) -> real dX pixel
+          // remap 1: dgrad-form geometry (virtual output = H x W); 2: forward-form (OH x OW)
+          const int VW = p.g.remap == 2 ? p.g.OW : p.g.W, VH = p.g.remap == 2 ? p.g.OH : p.g.H;
+          const int ww = m % VW, t = m / VW, hh = t % VH, nn = t / VH;
+          orow = ((int64_t)nn * p.g.Hr + p.g.oa + p.g.psh * hh) * p.g.Wr + p.g.ob + p.g.psw * ww;
+        }
+        const int64_t off = orow * p.ldc + n;
+        u32x4 rv = z4, xv = z4;
+        uint32_t mb = 0;
+        if (vec) {
+          if (p.residual) rv = ld16(p.residual + off);
+          if (BNB && p.col_stats) xv = ld16(p.st_x + off);
+        } else {
+          float g[8], xf[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            g[e] = (p.residual && n + e < p.N) ? bf2f(p.residual[off + e]) : 0.f;
+            xf[e] = (BNB && p.col_stats && n + e < p.N) ? bf2f(p.st_x[off + e]) : 0.f;
+          }
+          rv = pack8(g);
+          xv = pack8(xf);
+        }
+        if (BNB && p.st_mask) mb = p.st_mask[off >> 3];
+        finish_row(v, rv, xv, mb, C + off, vec);
+      }
+    }
+    if (p.col_stats) {
+      // reduce over threads sharing column chunk c: lanes c + CPR*t within a wave, then NW waves via LDS
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+#pragma unroll
+        for (int o = CPR; o < 64; o <<= 1) {
+          s[e] += __shfl_xor(s[e], o, 64);
+          ss[e] += __shfl_xor(ss[e], o, 64);
+        }
+      }
+      float* red = (float*)(smem + BM * CROW);  // [2][NW][BN]
+      if (sub > 0) __syncthreads();             // previous sub-tile's readers are done
+      if (lane < CPR) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          red[wid * BN + c * 8 + e] = s[e];
+          red[NW * BN + wid * BN + c * 8 + e] = ss[e];
+        }
+      }
+      __syncthreads();
+      // per-(M sub-tile) partials, layout [2][N][stats_ld]: no atomics, deterministic;
+      // the BatchNorm finalize reduces the partials of each channel.
+      const int col = tm * NSUB + sub;
+      if (tid < BN && n0 + tid < p.N && col < tilesSub) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) { a += red[w * BN + tid]; b += red[NW * BN + w * BN + tid]; }
+        const int sld = p.stats_ld ? p.stats_ld : tilesSub;
+        p.col_stats[(int64_t)(n0 + tid) * sld + p.stats_off + col] = a;
+        p.col_stats[(int64_t)(p.N + n0 + tid) * sld + p.stats_off + col] = b;
+      }
+    }
+  }
+}
+
 // -------------------------------------------------------------------- kernel
 template <int BM, int BN, int AL, int BL, int EPI>
 __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
@@ -447,181 +645,193 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
     }
     return;
   } else {
-    constexpr bool BNB = (EPI == EPI_BF16_BNB);
-    // Stage bf16 tile in LDS (row stride CROW), then coalesced 16-B stores.
+    epilogue_bf16<BM, BN, RM, RN, NT, EPI>(p, acc, smem, m0, n0, tm, wm, wn);
+  }
+}
+
+// ------------------------------------------------- LDS-DMA conv / GEMM kernel
+// Forward-form convolutions (and 1x1 / dense K-contiguous A) with operands
+// streamed straight into LDS by buffer_load ... lds (no VGPR staging, no
+// ds_write), a 3-stage ring (two K-steps of loads in flight behind the MFMAs)
+// and one barrier per K-step.  Address work per K-step is scalar: with
+// C % 32 == 0 a 32-wide K-step lies inside one filter tap, so the tap's byte
+// offset goes in soffset, every lane keeps one 32-bit row offset (voffset) for
+// the whole loop, and padding / tails come from a per-row tap-validity mask
+// that swaps the offset for an out-of-range one (the buffer unit returns 0).
+//
+// B is [N][K] (BL == B_DENSE_K, K-image, ds_read_b128) or [K][N]
+// (BL == B_DENSE_N, MN-image, ds_read_b64_tr_b16).  Shared epilogue.
+typedef __attribute__((address_space(3))) void lds_void_t;
+constexpr uint32_t DMA_OOB = 0x80000000u;  // voffset past every buffer's num_records (< 2^31 bytes)
+constexpr int DSTAGES = 3;
+
+DPE_DEVICE __amdgpu_buffer_rsrc_t dma_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+DPE_DEVICE void dma16(__amdgpu_buffer_rsrc_t r, char* wave_dst, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)wave_dst, 16, voff, soff, 0, 0);
+}
+
+template <int N>
+DPE_DEVICE void wait_vm() {
+  static_assert(N >= 0 && N <= 6, "vmcnt");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+}
+
+// WGM x WGN waves, each owning a (BM/WGM) x (BN/WGN) sub-tile; 128x128 (2x2 waves),
+// 256x128 (4x2) and 256x256 (2x4).  Bigger tiles cut the L2->LDS bytes per FLOP, which
+// bounds the 128-tile kernel (16 KiB per 256 MFMA-cycles per block).
+template <int BM, int BN, int WGM, int WGN, int BL, int EPI>
+__global__ __launch_bounds__(64 * WGM * WGN, (BM == 256 && BN == 128) ? 4 : 1) void igemm_dma_kernel(IgemmArgs p, int a_dense) {
+  constexpr int NTH = 64 * WGM * WGN, NW = WGM * WGN;
+  constexpr bool BKc = (BL == B_DENSE_K);
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int CROW = BN * 2 + 16;
+  constexpr int LDS_MAIN = DSTAGES * STAGE;
+  constexpr int LDS_C = BM * CROW + 2 * NW * BN * 4;
+  constexpr int LDS = LDS_MAIN > LDS_C ? LDS_MAIN : LDS_C;
+  constexpr int RM = BM / WGM / 16, RN = BN / WGN / 16;
+  constexpr int PA = BM / (16 * NW), PB = BN / (16 * NW);  // 1-KiB DMA pieces per wave per stage
+  static_assert(PA >= 1 && PB >= 1 && PA * 16 * NW == BM && PB * 16 * NW == BN, "DMA piece split");
+  static_assert(BKc || BN <= 128, "MN image supports 64/128 columns");
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tilesN = (p.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = bid / tilesN, tn = bid % tilesN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int wm = (wid / WGN) * (BM / WGM), wn = (wid % WGN) * (BN / WGN);
+  const ConvGeom& g = p.g;
+  const int C = a_dense ? p.K : g.C;  // channels per tap (the whole K for dense A)
+
+  // ---- A rows: per-piece row offset + tap-validity mask (bit t = tap t in range)
+  uint32_t aoff[PA], amask[PA];
 #pragma unroll
-    for (int i = 0; i < RM; ++i) {
-      const int ml = wm + 16 * i + lm;
-#pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        const int nl = wn + 16 * j + ln4;
-        const int n = n0 + nl;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float b = (p.bias && n + e < p.N) ? p.bias[n + e] : 0.f;
-          v[e] = act_fn(p.alpha * acc[i][j][e] + b, p.act);
-        }
-        u32x2 pk;
-        pk[0] = pack_bf2(v[0], v[1]);
-        pk[1] = pack_bf2(v[2], v[3]);
-        *(u32x2*)(smem + ml * CROW + nl * 2) = pk;
-      }
-    }
-    __syncthreads();
-    constexpr int CPR = BN / 8, RPP = NT / CPR;
-    const int c = tid % CPR, r0 = tid / CPR;
-    const int n = n0 + c * 8;
-    uint16_t* C = (uint16_t*)p.C;
-    const bool vec = ((p.ldc & 7) == 0) && (n + 8 <= p.N);
-    float s[8], ss[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
-    float bsc[8], bsh[8], bmu[8];  // BN forward coefficients of this thread's 8 columns (EPI_BF16_BNB)
-    if constexpr (BNB) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int ch = min(n + e, p.N - 1);
-        bsc[e] = p.st_coef[ch];
-        bsh[e] = p.st_coef[p.N + ch];
-        bmu[e] = p.st_coef[2 * p.N + ch];
-      }
-    }
-    // Per-row finish: residual add, BN-backward partials / ReLU-mask (BNB) or BN-forward
-    // partials, store.  Operands arrive pre-loaded (rv / xv / mb) so the fast path can
-    // issue the loads of several rows before the first use.
-    auto finish_row = [&](u32x4 v, const u32x4& rv, const u32x4& xv_raw, uint32_t mb, uint16_t* dst, bool vec_row) {
-      if (p.residual) {
-        float f[8], g[8];
-        unpack8(v, f);
-        unpack8(rv, g);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] += g[e];
-        v = pack8(f);
-      }
-      if (p.col_stats) {
-        float f[8];
-        unpack8(v, f);
-        if constexpr (BNB) {  // (sum dz, sum dz*(x - mean)), dz = f * relu'(...)
-          float xv[8];
-          unpack8(xv_raw, xv);
-          if (p.st_mask) {  // relu'(y) from the saved post-residual output's mask bits; store dz itself
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              f[e] = ((mb >> e) & 1u) ? f[e] : 0.f;
-              s[e] += f[e];
-              ss[e] += f[e] * (xv[e] - bmu[e]);
-            }
-            v = pack8(f);
-          } else {  // relu'(x*scale + shift), recomputed from the pre-BN input
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float dz = fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? f[e] : 0.f;
-              s[e] += dz;
-              ss[e] += dz * (xv[e] - bmu[e]);
-            }
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) { s[e] += f[e]; ss[e] += f[e] * f[e]; }
-        }
-      }
-      if (vec_row) {
-        *(u32x4*)dst = v;
+  for (int i = 0; i < PA; ++i) {
+    const int row = (wid * PA + i) * 16 + (lane >> 2);
+    const int lc = (lane & 3) ^ ((0x78 >> (((row >> 2) & 3) << 1)) & 3);  // kimg swizzle (inverse = itself)
+    const int m = m0 + row;
+    uint32_t mask = 0u, off = 0u;
+    if (m < p.M) {
+      if (a_dense) {
+        off = (uint32_t)m * (uint32_t)p.lda * 2u;
+        mask = 1u;
       } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          if (n + e < p.N) dst[e] = (uint16_t)((e & 1) ? (v[e >> 1] >> 16) : (v[e >> 1] & 0xffff));
-        }
-      }
-    };
-    constexpr int RPI = BM / RPP;                 // rows per thread: 2, 4 or 8
-    constexpr int G = RPI < 4 ? RPI : 4;          // rows whose operand loads are issued together
-    const u32x4 z4 = zero16();
-    if (vec && !p.g.remap && m0 + BM <= p.M) {
-      // full tile, contiguous rows: G rows' residual / pre-BN / mask loads in flight at once
-#pragma unroll
-      for (int u0 = 0; u0 < RPI; u0 += G) {
-        u32x4 tv[G], rv[G], xv[G];
-        uint32_t mb[G];
-#pragma unroll
-        for (int q = 0; q < G; ++q) {
-          const int rr = r0 + (u0 + q) * RPP;
-          const int64_t off = (int64_t)(m0 + rr) * p.ldc + n;
-          tv[q] = *(const u32x4*)(smem + rr * CROW + c * 16);
-          rv[q] = p.residual ? ld16(p.residual + off) : z4;
-          xv[q] = (BNB && p.col_stats) ? ld16(p.st_x + off) : z4;
-          mb[q] = (BNB && p.st_mask) ? (uint32_t)p.st_mask[off >> 3] : 0u;
-        }
-#pragma unroll
-        for (int q = 0; q < G; ++q) {
-          const int rr = r0 + (u0 + q) * RPP;
-          finish_row(tv[q], rv[q], xv[q], mb[q], C + (int64_t)(m0 + rr) * p.ldc + n, true);
-        }
-      }
-    } else {
-      for (int rr = r0; rr < BM; rr += RPP) {
-        const int m = m0 + rr;
-        if (m >= p.M) break;
-        const u32x4 v = *(const u32x4*)(smem + rr * CROW + c * 16);
-        int64_t orow = m;
-        if (p.g.remap) {  // phase dgrad: virtual row (n, hh, ww) -> real dX pixel
-          // remap 1: dgrad-form geometry (virtual output = H x W); 2: forward-form (OH x OW)
-          const int VW = p.g.remap == 2 ? p.g.OW : p.g.W, VH = p.g.remap == 2 ? p.g.OH : p.g.H;
-          const int ww = m % VW, t = m / VW, hh = t % VH, nn = t / VH;
-          orow = ((int64_t)nn * p.g.Hr + p.g.oa + p.g.psh * hh) * p.g.Wr + p.g.ob + p.g.psw * ww;
-        }
-        const int64_t off = orow * p.ldc + n;
-        u32x4 rv = z4, xv = z4;
-        uint32_t mb = 0;
-        if (vec) {
-          if (p.residual) rv = ld16(p.residual + off);
-          if (BNB && p.col_stats) xv = ld16(p.st_x + off);
-        } else {
-          float g[8], xf[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            g[e] = (p.residual && n + e < p.N) ? bf2f(p.residual[off + e]) : 0.f;
-            xf[e] = (BNB && p.col_stats && n + e < p.N) ? bf2f(p.st_x[off + e]) : 0.f;
+        const int ow = m % g.OW, t = m / g.OW, oh = t % g.OH, n = t / g.OH;
+        const int ih0 = oh * g.sh - g.ph, iw0 = ow * g.sw - g.pw;
+        off = (uint32_t)((((int64_t)n * g.H + oh * g.sh) * g.W + ow * g.sw) * g.C) * 2u;
+        for (int r = 0; r < g.R; ++r) {
+          const bool vr = (unsigned)(ih0 + r * g.dh) < (unsigned)g.H;
+          for (int s = 0; s < g.S; ++s) {
+            const bool vs = (unsigned)(iw0 + s * g.dw) < (unsigned)g.W;
+            if (vr && vs) mask |= 1u << (r * g.S + s);
           }
-          rv = pack8(g);
-          xv = pack8(xf);
         }
-        if (BNB && p.st_mask) mb = p.st_mask[off >> 3];
-        finish_row(v, rv, xv, mb, C + off, vec);
       }
     }
-    if (p.col_stats) {
-      // reduce over threads sharing column chunk c: lanes c + CPR*t within a wave, then 4 waves via LDS
+    aoff[i] = off + lc * 16;
+    amask[i] = mask;
+  }
+  // A's buffer starts (ph*W + pw)*C elements before x so that every in-range tap offset is >= 0
+  const int64_t apre = a_dense ? 0 : ((int64_t)g.ph * g.W + g.pw) * g.C;
+  const int64_t abytes = a_dense ? (int64_t)p.M * p.lda * 2 : ((int64_t)g.N * g.H * g.W * g.C + apre) * 2;
+  const __amdgpu_buffer_rsrc_t ar = dma_rsrc(p.A - apre, (uint32_t)abytes);
+
+  // ---- B: per-piece offsets, fixed for the loop (validity never changes along K)
+  uint32_t boff[PB];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-#pragma unroll
-        for (int o = CPR; o < 64; o <<= 1) {
-          s[e] += __shfl_xor(s[e], o, 64);
-          ss[e] += __shfl_xor(ss[e], o, 64);
-        }
-      }
-      float* red = (float*)(smem + BM * CROW);  // [2][4 waves][BN]
-      if (lane < CPR) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          red[wid * BN + c * 8 + e] = s[e];
-          red[4 * BN + wid * BN + c * 8 + e] = ss[e];
-        }
-      }
-      __syncthreads();
-      // per-(M-tile) partials, layout [2][N][tilesM]: no atomics, deterministic;
-      // the BatchNorm finalize reduces the tilesM partials of each channel.
-      if (tid < BN && n0 + tid < p.N) {
-        float a = 0.f, b = 0.f;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) { a += red[w * BN + tid]; b += red[4 * BN + w * BN + tid]; }
-        const int sld = p.stats_ld ? p.stats_ld : tilesM;
-        p.col_stats[(int64_t)(n0 + tid) * sld + p.stats_off + tm] = a;
-        p.col_stats[(int64_t)(p.N + n0 + tid) * sld + p.stats_off + tm] = b;
-      }
+  for (int i = 0; i < PB; ++i) {
+    const int pc = wid * PB + i;
+    if constexpr (BKc) {
+      const int row = pc * 16 + (lane >> 2);
+      const int lc = (lane & 3) ^ ((0x78 >> (((row >> 2) & 3) << 1)) & 3);
+      const int n = n0 + row;
+      boff[i] = n < p.N ? (uint32_t)(n * p.ldb + lc * 8) * 2u : DMA_OOB;
+    } else {
+      constexpr int CPR = BN / 8, KR = 64 / CPR;  // chunks per k-row, k-rows per piece
+      const int krow = pc * KR + lane / CPR, ph_ = lane % CPR;
+      int h;
+      if constexpr (BN == 128) h = ((krow & 3) | (((krow >> 3) & 1) << 2)) << 1;
+      else h = (((krow >> 1) & 1) | (((krow >> 3) & 1) << 1)) << 1;
+      const int n = n0 + (ph_ ^ h) * 8;
+      boff[i] = n < p.N ? (uint32_t)(krow * p.ldb + n) * 2u : DMA_OOB;
     }
   }
+  const int64_t bbytes = BKc ? (int64_t)p.N * p.ldb * 2 : (int64_t)p.K * p.ldb * 2;
+  const __amdgpu_buffer_rsrc_t br = dma_rsrc(p.B, (uint32_t)bbytes);
+  const uint32_t bstep = BKc ? 64u : (uint32_t)p.ldb * 64u;  // bytes per K-step
+
+  // ---- scalar K-walk state of the NEXT stage to issue
+  int tap = 0, ci = 0, ts = 0;          // tap index, channel offset in tap, tap column s
+  uint32_t tapoff = 0, kbo = 0;         // tap byte offset into A, K-step byte offset into B
+  const uint32_t s_step = (uint32_t)g.dw * g.C * 2u, r_step = (uint32_t)g.dh * g.W * g.C * 2u;
+  const int nt = p.K / BK;
+
+  auto issue = [&](int buf) {
+    char* st = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const uint32_t v = ((amask[i] >> tap) & 1u) ? aoff[i] : DMA_OOB;
+      dma16(ar, st + (wid * PA + i) * 1024, v, tapoff + ci * 2);
+    }
+#pragma unroll
+    for (int i = 0; i < PB; ++i) dma16(br, st + A_BYTES + (wid * PB + i) * 1024, boff[i], kbo);
+    kbo += bstep;
+    ci += BK;
+    if (ci >= C) {
+      ci = 0;
+      ++tap;
+      if (++ts == (a_dense ? 1 : g.S)) {
+        ts = 0;
+        tapoff += r_step - (uint32_t)(g.S - 1) * s_step;
+      } else {
+        tapoff += s_step;
+      }
+    }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nt > 0) issue(0);
+  if (nt > 1) issue(1);
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) wait_vm<PA + PB>(); else wait_vm<0>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < nt) issue((t + 2) % DSTAGES);
+    const char* As = smem + (t % DSTAGES) * STAGE;
+    const char* Bs = As + A_BYTES;
+    bf16x8 af[RM], bfr[RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) af[i] = kfrag(As, wm + 16 * i);
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      if constexpr (BKc) bfr[j] = kfrag(Bs, wn + 16 * j);
+      else bfr[j] = mnfrag<BN>(Bs, wn + 16 * j);
+    }
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+  }
+  __syncthreads();
+  if (p.alpha_ptr) p.alpha *= *p.alpha_ptr;
+  epilogue_bf16<BM, BN, RM, RN, NTH, EPI>(p, acc, smem, m0, n0, tm, wm, wn);
 }
 
 template <int BM, int BN, int AL, int BL, int EPI>
@@ -668,5 +878,48 @@ extern "C" int dpe_igemm_launch(const IgemmArgs* args, int bm, int bn, int aload
   DPE_CASE(A_CONV_FWD, B_DENSE_K, EPI_BF16_BNB)
   DPE_CASE(A_DENSE_M, B_CONV_WGRAD, EPI_ATOMIC_F32)
 #undef DPE_CASE
+  return -1;
+}
+
+// LDS-DMA kernel for forward-form convolutions / dense K-contiguous A.  Returns -1
+// when the problem is outside its envelope (the caller then uses dpe_igemm_launch).
+extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int aload, int bload, int epi,
+                                    hipStream_t st) {
+  const IgemmArgs& a = *args;
+  if (a.M <= 0 || a.N <= 0) return 0;
+  if (aload != A_DENSE_K && aload != A_CONV_FWD) return -1;
+  if (bload != B_DENSE_K && bload != B_DENSE_N) return -1;
+  if (epi != EPI_BF16 && epi != EPI_BF16_BNB) return -1;
+  if (a.K <= 0 || a.K % 32 || a.k_split < a.K) return -1;
+  const bool dense = aload == A_DENSE_K;
+  const ConvGeom& g = a.g;
+  if (!dense && (g.C % 32 || g.R * g.S > 32 || g.R * g.S * g.C != a.K)) return -1;
+  if (a.ldb % 8 || (bload == B_DENSE_N && a.N % 8) || (dense && a.lda % 8)) return -1;
+  const int64_t lim = (1ll << 31) - 4096;
+  const int64_t abytes = dense ? (int64_t)a.M * a.lda * 2
+                               : ((int64_t)g.N * g.H * g.W * g.C + ((int64_t)g.ph * g.W + g.pw) * g.C) * 2;
+  const int64_t bbytes = bload == B_DENSE_K ? (int64_t)a.N * a.ldb * 2 : (int64_t)a.K * a.ldb * 2;
+  if (abytes >= lim || bbytes >= lim) return -1;
+  const int tiles = ((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+  const int dn = dense ? 1 : 0;
+#define DPE_DMA(BM_, BN_, WGM_, WGN_, BL_, EP_)                                                             \
+  if (bm == BM_ && bn == BN_ && bload == BL_ && epi == EP_) {                                               \
+    hipLaunchKernelGGL((igemm_dma_kernel<BM_, BN_, WGM_, WGN_, BL_, EP_>), dim3(tiles), dim3(64 * WGM_ * WGN_), \
+                       0, st, a, dn);                                                                       \
+    return 0;                                                                                               \
+  }
+#define DPE_DMA_T(BL_, EP_) \
+  DPE_DMA(128, 128, 2, 2, BL_, EP_) DPE_DMA(128, 64, 2, 2, BL_, EP_) DPE_DMA(64, 128, 2, 2, BL_, EP_) DPE_DMA(64, 64, 2, 2, BL_, EP_)
+  DPE_DMA_T(B_DENSE_K, EPI_BF16)
+  DPE_DMA_T(B_DENSE_K, EPI_BF16_BNB)
+  DPE_DMA_T(B_DENSE_N, EPI_BF16)
+  DPE_DMA_T(B_DENSE_N, EPI_BF16_BNB)
+  // 8-wave big tiles (B K-contiguous)
+  DPE_DMA(256, 128, 4, 2, B_DENSE_K, EPI_BF16)
+  DPE_DMA(256, 128, 4, 2, B_DENSE_K, EPI_BF16_BNB)
+  DPE_DMA(256, 256, 2, 4, B_DENSE_K, EPI_BF16)
+  DPE_DMA(256, 256, 2, 4, B_DENSE_K, EPI_BF16_BNB)
+#undef DPE_DMA_T
+#undef DPE_DMA
   return -1;
 }

@@ -83,6 +83,12 @@ CONV_CASES = [
     (1, 9, 9, 32, 48, 3, 2, 1),
     (2, 10, 10, 16, 32, 5, 1, 2),    # stride-1 data grad as a forward conv (pad R-1-p)
     (2, 9, 9, 64, 64, 3, 1, 0),
+    # ResNet-50 shapes at small batch (LDS-DMA kernel: M / N tails, 3-stage ring, strided 1x1)
+    (2, 56, 56, 64, 256, 1, 1, 0),
+    (2, 28, 28, 128, 128, 3, 1, 1),
+    (2, 56, 56, 256, 512, 1, 2, 0),
+    (5, 7, 7, 512, 512, 3, 1, 1),
+    (3, 14, 14, 96, 200, 3, 1, 1),
 ]
 
 
@@ -592,3 +598,39 @@ def test_conv_dgrad_acc_inplace(C, N, H, W, Ci, Co, k, s, p):
     dx = base.clone()
     C.conv_dgrad_acc(dy.permute(0, 2, 3, 1).contiguous(), w, dx, [s, s], [p, p], [1, 1])
     assert rel_err(dx, base.float() + ref.permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("N,H,W,Ci,Co,k,s,p", [(2, 14, 14, 64, 256, 3, 1, 1), (3, 7, 7, 128, 384, 3, 1, 1),
+                                               (2, 28, 28, 128, 128, 3, 2, 1), (2, 14, 14, 256, 512, 1, 1, 0),
+                                               (2, 14, 14, 96, 200, 3, 1, 1)])
+def test_conv_tiles_lds_dma(C, mode, N, H, W, Ci, Co, k, s, p):
+    """LDS-DMA conv kernel at every tile (128, 256x128, 256x256 8-wave): forward output + BN
+    statistics partials (128-row sub-tiles), and the forward-form data grad with BN partials."""
+    torch.manual_seed(31)
+    C.set_conv_tile(mode)
+    try:
+        x = bf(torch.randn(N, H, W, Ci, device=dev))
+        w = bf(torch.randn(Co, k, k, Ci, device=dev) / math.sqrt(k * k * Ci))
+        ref = _conv_ref(x, w, s, p)
+        y, stats = C.conv_fwd(x, w, [s, s], [p, p], [1, 1], True, None)
+        assert rel_err(y, ref) < 1e-2
+        yf = y.float().reshape(-1, Co)
+        tot = stats.sum(-1)
+        assert rel_err(tot[0], yf.sum(0)) < 1e-3 and rel_err(tot[1], (yf * yf).sum(0)) < 1e-3
+        # data grad (stride-1 / phase forward form) with BN-backward partials
+        h = bf(torch.randn(N, H, W, Ci, device=dev))
+        coef = _bn_coef(C, Ci)
+        OH = (H + 2 * p - k) // s + 1
+        dy = bf(torch.randn(N, OH, OH, Co, device=dev))
+        xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+        yr = F.conv2d(xr, w.permute(0, 3, 1, 2).float(), None, s, p)
+        (gx,) = torch.autograd.grad(yr, xr, dy.float().permute(0, 3, 1, 2))
+        da, part = C.conv_dgrad_bn(dy, w, [N, H, W, Ci], [s, s], [p, p], [1, 1], None, h, coef)
+        assert rel_err(da, gx.permute(0, 2, 3, 1)) < 1e-2
+        df, hf = da.float().reshape(-1, Ci), h.float().reshape(-1, Ci)
+        dz = torch.where(hf * coef[0] + coef[1] > 0, df, torch.zeros_like(df))
+        tp = part.sum(-1)
+        assert rel_err(tp[0], dz.sum(0)) < 1e-3 and rel_err(tp[1], (dz * (hf - coef[2])).sum(0)) < 1e-3
+    finally:
+        C.set_conv_tile(0)
