@@ -163,6 +163,12 @@ void Communicator::abort() {
   }
 }
 
+// ------------------------------------------------ weight-grad side streams
+// Per-device stream that the model's backward writes some gradients on
+// (ops/_state.py run_on_aux); bucket all-reduces wait for it as well.
+static hipStream_t g_aux_streams[64] = {};
+hipStream_t aux_stream(int device) { return (device >= 0 && device < 64) ? g_aux_streams[device] : nullptr; }
+
 // ------------------------------------------------------------------ Reducer
 Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params, int64_t nparams,
                  std::shared_ptr<Communicator> comm, bool timing, bool force, bool comm_bf16, bool sync_debug)
@@ -184,10 +190,12 @@ Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_
   seen_.assign(nparams, 0);
   const unsigned flags = timing_ ? hipEventDefault : hipEventDisableTiming;
   ev_ready_.resize(buckets_.size());
+  ev_aux_.resize(buckets_.size());
   ev_start_.resize(buckets_.size());
   ev_end_.resize(buckets_.size());
   for (size_t b = 0; b < buckets_.size(); ++b) {
     HIP_CHECK(hipEventCreateWithFlags(&ev_ready_[b], hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_aux_[b], hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_start_[b], flags));
     HIP_CHECK(hipEventCreateWithFlags(&ev_end_[b], flags));
     if (comm_) c10::hip::HIPCachingAllocator::recordStream(buckets_[b].storage().data_ptr(), comm_->comm_stream());
@@ -203,7 +211,7 @@ Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_
 }
 
 Reducer::~Reducer() {
-  for (auto* v : {&ev_ready_, &ev_start_, &ev_end_})
+  for (auto* v : {&ev_ready_, &ev_aux_, &ev_start_, &ev_end_})
     for (auto e : *v) (void)hipEventDestroy(e);
   (void)hipEventDestroy(ev_bwd_end_);
   (void)hipEventDestroy(ev_done_);
@@ -227,6 +235,13 @@ void Reducer::launch(int64_t b) {
   hipStream_t cs = comm_->comm_stream().stream();
   HIP_CHECK(hipEventRecord(ev_ready_[b], cur));
   HIP_CHECK(hipStreamWaitEvent(cs, ev_ready_[b], 0));
+  // gradients written on the weight-grad side stream (set_aux_stream) are covered too
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  if (hipStream_t aux = aux_stream(dev)) {
+    HIP_CHECK(hipEventRecord(ev_aux_[b], aux));
+    HIP_CHECK(hipStreamWaitEvent(cs, ev_aux_[b], 0));
+  }
   if (timing_) HIP_CHECK(hipEventRecord(ev_start_[b], cs));
   auto& t = buckets_[b];
   if (comm_bf16_) {
@@ -287,6 +302,10 @@ std::vector<std::tuple<int64_t, double, double>> Reducer::last_timings() {
 void register_comm(pybind11::module& m) {
   namespace py = pybind11;
   m.def("rccl_unique_id", []() { return py::bytes(Communicator::unique_id()); });
+  m.def("set_aux_stream", [](int device, uint64_t stream) {
+    TORCH_CHECK(device >= 0 && device < 64, "set_aux_stream: bad device");
+    g_aux_streams[device] = (hipStream_t)(uintptr_t)stream;
+  }, "register the weight-grad side stream of a device (bucket all-reduces wait for it)");
   m.def("rccl_version", []() {
     int v = 0;
     ncclGetVersion(&v);

@@ -101,10 +101,13 @@ class Reducer {
   bool comm_bf16_, sync_debug_;
   std::vector<at::Tensor> staging_;  // bf16 copies of the buckets (comm_bf16)
   std::vector<int64_t> launch_order_;
-  std::vector<hipEvent_t> ev_ready_, ev_start_, ev_end_;
+  std::vector<hipEvent_t> ev_ready_, ev_aux_, ev_start_, ev_end_;
   hipEvent_t ev_bwd_end_ = nullptr, ev_done_ = nullptr, ev_step_begin_ = nullptr;
   bool step_open_ = false;
 };
+
+// weight-grad side stream registered for a device (nullptr: none)
+hipStream_t aux_stream(int device);
 
 void register_comm(pybind11::module& m);
 

@@ -51,7 +51,7 @@ import torch
 from torch.autograd import Function
 
 from ..ops._ext import ext
-from ..ops._state import grad_done, grad_sink, note_use, shadow
+from ..ops._state import grad_done, grad_sink, note_use, run_on_aux, shadow
 
 # DPE_BN_EPI=0: inner BN backward through the standalone reduce kernel (A/B reference)
 _EPI_BNB = os.environ.get("DPE_BN_EPI", "1") != "0"
@@ -161,7 +161,10 @@ class BottleneckFn(Function):
             w = convs[i].conv.weight
             s, p, d = _conv_conf(convs[i].conv)
             buf, direct = grad_sink(w)
-            C.conv_wgrad(dy, inp, buf, s, p, d, 1.0)
+            if direct:  # bucket view: on the weight-grad side stream (the reducers wait for it)
+                run_on_aux(dy.device, lambda: C.conv_wgrad(dy, inp, buf, s, p, d, 1.0), dy, inp)
+            else:
+                C.conv_wgrad(dy, inp, buf, s, p, d, 1.0)
             grad_done(w, direct)
             grads[id(w)] = None if direct else buf
 

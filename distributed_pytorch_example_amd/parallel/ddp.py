@@ -57,6 +57,7 @@ from . import dist as pdist
 from . import hooks as _hooks
 from .buckets import assign_buckets
 from ..utils.logging import get_logger
+from ..ops._state import aux_wait as _aux_wait
 
 log = get_logger(__name__)
 
@@ -96,6 +97,8 @@ class _PyReducer:
     def _launch(self, b):
         self.order.append(b)
         t = self.buckets[b]
+        if t.is_cuda:
+            _aux_wait(t.device)  # weight grads written on the side stream
         if self.hook is not None:
             gb = _hooks.GradBucket(b, t, [self.params[i] for i in self.bucket_params[b]], b == len(self.buckets) - 1)
             self.works.append((b, self.hook(self.state, gb)))
