@@ -199,6 +199,15 @@ bool igemm_dma_on() {
   return on;
 }
 
+bool wgrad_dma_on() {
+  static const bool on = [] { const char* e = getenv("DPE_WGRAD_DMA"); return !(e && e[0] == '0'); }();
+  return on;
+}
+bool wgrad_dma_dense() {
+  static const bool on = [] { const char* e = getenv("DPE_WGRAD_DMA"); return e && e[0] == '2'; }();
+  return on;
+}
+
 // Tile of the LDS-DMA conv kernel: 0 auto, 1 128-tile (pick_cfg), 2 256x128, 3 256x256
 // (8 waves; only where pick_cfg chose a 128-row tile, so BN partial layouts never change).
 // DPE_DMA_TILE=128|256x128|256x256 or set_conv_tile().
@@ -228,6 +237,18 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
   if ((!conv || g_g256_override == 1 || g256_mode() == 2) && try_gemm256(a, aload, bload, epi, allow_split)) return;
   Cfg c = pick_cfg(a.M, a.N, a.K, allow_split && epi == dpe::EPI_ATOMIC_F32);
   a.k_split = c.k_split;
+  // weight grads over an im2col B (3x3 / strided; split-K fp32 atomics): LDS-DMA kernel, measured 1.3-1.5x
+  // faster (scripts/bench_convs.py); on the dense 1x1 ones it measured 10-15 % slower, so those stay
+  // register-staged (DPE_WGRAD_DMA=0: all register-staged, 2: dense 1x1 too)
+  if (conv && epi == dpe::EPI_ATOMIC_F32 && aload == dpe::A_DENSE_M && igemm_dma_on() && wgrad_dma_on() &&
+      (bload == dpe::B_CONV_WGRAD || (bload == dpe::B_DENSE_N && wgrad_dma_dense()))) {
+    const int rc = dpe_igemm_wgrad_dma_launch(&a, c.bm, c.bn, bload, c.splits, cur_stream());
+    if (rc == 0) {
+      const hipError_t e = hipGetLastError();
+      TORCH_CHECK(e == hipSuccess, "igemm_wgrad_dma launch failed: ", hipGetErrorString(e));
+      return;
+    }
+  }
   // LDS-DMA kernel where it measured faster: im2col A (3x3 / strided), dense 1x1 A at K >= 512,
   // B K-contiguous (the N-contiguous B of 1x1 data grads measured 5-10 % slower on it)
   const bool dma_role = bload == dpe::B_DENSE_K && (aload == dpe::A_CONV_FWD || (aload == dpe::A_DENSE_K && a.K >= 512));

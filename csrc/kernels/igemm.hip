@@ -492,6 +492,47 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* sm
   }
 }
 
+// Split-K / accumulate epilogue (EPI_ATOMIC_F32) of the 2x2-wave kernels: stage the fp32 tile
+// through LDS, half the rows at a time (the two wave-rows take turns), then add it with
+// atomics shaped as whole contiguous row segments: every wave-instruction covers 64
+// consecutive floats (256 B) of one row -- the full-rate atomic shape (MI355X_MICROARCH
+// "Global float atomics"); a 16-rows x 4-dwords shape runs ~17x slower.
+template <int BM, int BN, int LDS>
+DPE_DEVICE void epilogue_atomic_f32(const IgemmArgs& p, f32x4 (&acc)[BM / 32][BN / 32], char* smem, int m0, int n0,
+                                    int wn) {
+  constexpr int RM = BM / 32, RN = BN / 32;
+  constexpr int HR = BM / 2;          // rows per half
+  constexpr int FROW = BN + 4;        // fp32 row stride (pad: conflict-free b128 writes)
+  static_assert(HR * FROW * 4 <= LDS, "atomic staging must fit the main-loop LDS");
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lm = lane & 15, ln4 = (lane >> 4) * 4;
+  float* C = (float*)p.C;
+  float* st = (float*)smem;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    if ((wid >> 1) == half) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int ml = 16 * i + lm;  // row within this half
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          const int nl = wn + 16 * j + ln4;
+          *(f32x4*)(st + ml * FROW + nl) = acc[i][j] * p.alpha;
+        }
+      }
+    }
+    __syncthreads();
+    constexpr int SEG = 64;                   // floats per wave-instruction
+    constexpr int SEGS_PER_ROW = BN / SEG;    // 1 or 2
+    for (int s = wid; s < HR * SEGS_PER_ROW; s += 4) {
+      const int r = s / SEGS_PER_ROW, c = (s % SEGS_PER_ROW) * SEG + lane;
+      const int m = m0 + half * HR + r, n = n0 + c;
+      if (m < p.M && n < p.N) atomicAdd(C + (int64_t)m * p.ldc + n, st[r * FROW + c]);
+    }
+    __syncthreads();
+  }
+}
+
 // -------------------------------------------------------------------- kernel
 template <int BM, int BN, int AL, int BL, int EPI>
 __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
@@ -584,39 +625,7 @@ __global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
   if (p.alpha_ptr) p.alpha *= *p.alpha_ptr;
   const int lm = lane & 15, ln4 = (lane >> 4) * 4;
   if constexpr (EPI == EPI_ATOMIC_F32) {
-    // Stage the fp32 tile through LDS, half the rows at a time (the two
-    // wave-rows take turns), then add it with atomics shaped as whole
-    // contiguous row segments: every wave-instruction covers 64 consecutive
-    // floats (256 B) of one row -- the full-rate atomic shape (MI355X_MICROARCH
-    // "Global float atomics"); a 16-rows x 4-dwords shape runs ~17x slower.
-    constexpr int HR = BM / 2;          // rows per half
-    constexpr int FROW = BN + 4;        // fp32 row stride (pad: conflict-free b128 writes)
-    static_assert(HR * FROW * 4 <= LDS, "atomic staging must fit the main-loop LDS");
-    float* C = (float*)p.C;
-    float* st = (float*)smem;
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      if ((wid >> 1) == half) {
-#pragma unroll
-        for (int i = 0; i < RM; ++i) {
-          const int ml = 16 * i + lm;  // row within this half
-#pragma unroll
-          for (int j = 0; j < RN; ++j) {
-            const int nl = wn + 16 * j + ln4;
-            *(f32x4*)(st + ml * FROW + nl) = acc[i][j] * p.alpha;
-          }
-        }
-      }
-      __syncthreads();
-      constexpr int SEG = 64;                   // floats per wave-instruction
-      constexpr int SEGS_PER_ROW = BN / SEG;    // 1 or 2
-      for (int s = wid; s < HR * SEGS_PER_ROW; s += 4) {
-        const int r = s / SEGS_PER_ROW, c = (s % SEGS_PER_ROW) * SEG + lane;
-        const int m = m0 + half * HR + r, n = n0 + c;
-        if (m < p.M && n < p.N) atomicAdd(C + (int64_t)m * p.ldc + n, st[r * FROW + c]);
-      }
-      __syncthreads();
-    }
+    epilogue_atomic_f32<BM, BN, LDS>(p, acc, smem, m0, n0, wn);
     return;
   } else if constexpr (EPI == EPI_F32) {
     float* C = (float*)p.C;
@@ -834,6 +843,151 @@ __global__ __launch_bounds__(64 * WGM * WGN, (BM == 256 && BN == 128) ? 4 : 1) v
   epilogue_bf16<BM, BN, RM, RN, NTH, EPI>(p, acc, smem, m0, n0, tm, wm, wn);
 }
 
+// ------------------------------------------- LDS-DMA weight-grad (split-K) kernel
+// dW[m = co][n] += sum_k dy[k][m] * B[k][n], k = output pixel: both operands are
+// M/N-contiguous ([32][COLS] images, ds_read_b64_tr_b16 fragments) streamed by
+// buffer_load ... lds into the same 3-stage ring as igemm_dma_kernel.  B is x
+// itself (1x1 stride-1, B_DENSE_N) or the im2col of x (B_CONV_WGRAD): every
+// lane's 8-column chunk is one (tap, channel-run) for the whole loop, and the
+// pixel row it reads advances 32 pixels per K-step through an incremental
+// (oh, ow, byte offset) walk -- no divisions in the loop, padding via the
+// out-of-range offset.  fp32 atomic epilogue (split-K).
+template <int COLS>
+DPE_DEVICE int mn_swz(int k) {
+  if constexpr (COLS == 128) return ((k & 3) | (((k >> 3) & 1) << 2)) << 1;
+  else return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1;
+}
+
+template <int BM, int BN, int BL>
+__global__ __launch_bounds__(NT) void igemm_wgrad_dma_kernel(IgemmArgs p) {
+  constexpr bool CONV = (BL == B_CONV_WGRAD);
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int LDS = DSTAGES * STAGE;
+  constexpr int RM = BM / 32, RN = BN / 32;
+  constexpr int PA = BM / 64, PB = BN / 64;  // 1-KiB pieces per wave per stage (4 waves)
+  constexpr int ACPR = BM / 8, AKR = 64 / ACPR, BCPR = BN / 8, BKR = 64 / BCPR;
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tilesN = (p.N + BN - 1) / BN, tilesM = (p.M + BM - 1) / BM;
+  const int ntile = tilesM * tilesN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid % ntile, split = bid / ntile;
+  const int m0 = (tile / tilesN) * BM, n0 = (tile % tilesN) * BN;
+  const int kb = split * p.k_split;
+  const int ke = min(p.K, kb + p.k_split);
+  const int nt = (ke - kb) / BK;
+  const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN / 2);
+  const ConvGeom& g = p.g;
+
+  // ---- A = dy [K][lda]: fixed per-lane offsets, scalar K-step offset
+  uint32_t aoff[PA];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    const int krow = (wid * PA + i) * AKR + lane / ACPR;
+    const int m = m0 + ((lane % ACPR) ^ mn_swz<BM>(krow)) * 8;
+    aoff[i] = m < p.M ? (uint32_t)(((int64_t)(kb + krow) * p.lda + m) * 2) : DMA_OOB;
+  }
+  const __amdgpu_buffer_rsrc_t ar = dma_rsrc(p.A, (uint32_t)((int64_t)p.K * p.lda * 2));
+  const uint32_t astep = (uint32_t)p.lda * 64u;
+
+  // ---- B
+  uint32_t boff[PB];                      // dense: fixed offsets; conv: tap byte offset of the chunk
+  int oh[PB], ow[PB], tr[PB], ts[PB];     // conv: pixel walk + tap displacement
+  uint32_t roff[PB];                      // conv: byte offset of pixel (img, oh*sh, ow*sw)
+  int64_t bpre = 0, bbytes;
+  const uint32_t bstep = (uint32_t)p.ldb * 64u;
+  if constexpr (CONV) {
+    bpre = ((int64_t)g.ph * g.W + g.pw) * g.C;
+    bbytes = ((int64_t)g.N * g.H * g.W * g.C + bpre) * 2;
+  } else {
+    bbytes = (int64_t)p.K * p.ldb * 2;
+  }
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int krow = (wid * PB + i) * BKR + lane / BCPR;
+    const int gc = n0 + ((lane % BCPR) ^ mn_swz<BN>(krow)) * 8;
+    if constexpr (CONV) {
+      const bool vc = gc < p.N;
+      const int gcc = vc ? gc : 0;
+      const int ci = gcc % g.C, t = gcc / g.C;
+      const int ss = t % g.S, rr = t / g.S;
+      tr[i] = vc ? rr * g.dh - g.ph : -(1 << 28);  // invalid column: never in range
+      ts[i] = ss * g.dw - g.pw;
+      boff[i] = (uint32_t)((((int64_t)rr * g.dh * g.W + ss * g.dw) * g.C + ci) * 2);
+      const int px = kb + krow;
+      ow[i] = px % g.OW;
+      const int q = px / g.OW;
+      oh[i] = q % g.OH;
+      const int img = q / g.OH;
+      roff[i] = (uint32_t)((((int64_t)img * g.H + oh[i] * g.sh) * g.W + ow[i] * g.sw) * g.C * 2);
+    } else {
+      boff[i] = gc < p.N ? (uint32_t)(((int64_t)(kb + krow) * p.ldb + gc) * 2) : DMA_OOB;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t br = dma_rsrc(p.B - bpre, (uint32_t)bbytes);
+  // per-step pixel advance of 32 = wa rows + wb columns (host guarantees wa + 1 <= OH)
+  const int wa = CONV ? BK / g.OW : 0, wb = CONV ? BK % g.OW : 0;
+  const uint32_t rs_ow = (uint32_t)g.sw * g.C * 2u, rs_oh = (uint32_t)g.sh * g.W * g.C * 2u;
+  const uint32_t rs_img = (uint32_t)g.H * g.W * g.C * 2u;
+  const uint32_t d_step = (uint32_t)wa * rs_oh + (uint32_t)wb * rs_ow;
+  const uint32_t d_ow = rs_oh - (uint32_t)g.OW * rs_ow, d_oh = rs_img - (uint32_t)g.OH * rs_oh;
+
+  uint32_t kso = 0;  // A / dense-B K-step byte offset of the next stage to issue
+  auto issue = [&](int buf) {
+    char* st = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) dma16(ar, st + (wid * PA + i) * 1024, aoff[i], kso * astep);
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      if constexpr (CONV) {
+        const bool v = (unsigned)(oh[i] * g.sh + tr[i]) < (unsigned)g.H && (unsigned)(ow[i] * g.sw + ts[i]) < (unsigned)g.W;
+        dma16(br, st + A_BYTES + (wid * PB + i) * 1024, v ? roff[i] + boff[i] : DMA_OOB, 0u);
+        // advance this lane's pixel by BK
+        ow[i] += wb; oh[i] += wa; roff[i] += d_step;
+        if (ow[i] >= g.OW) { ow[i] -= g.OW; oh[i] += 1; roff[i] += d_ow; }
+        if (oh[i] >= g.OH) { oh[i] -= g.OH; roff[i] += d_oh; }
+      } else {
+        dma16(br, st + A_BYTES + (wid * PB + i) * 1024, boff[i], kso * bstep);
+      }
+    }
+    ++kso;
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nt > 0) issue(0);
+  if (nt > 1) issue(1);
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) wait_vm<PA + PB>(); else wait_vm<0>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < nt) issue((t + 2) % DSTAGES);
+    const char* As = smem + (t % DSTAGES) * STAGE;
+    const char* Bs = As + A_BYTES;
+    bf16x8 af[RM], bfr[RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) af[i] = mnfrag<BM>(As, wm + 16 * i);
+#pragma unroll
+    for (int j = 0; j < RN; ++j) bfr[j] = mnfrag<BN>(Bs, wn + 16 * j);
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+  }
+  __syncthreads();
+  if (p.alpha_ptr) p.alpha *= *p.alpha_ptr;
+  epilogue_atomic_f32<BM, BN, LDS>(p, acc, smem, m0, n0, wn);
+}
+
 template <int BM, int BN, int AL, int BL, int EPI>
 static void launch_t(const IgemmArgs& a, int splits, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
@@ -921,5 +1075,37 @@ extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int a
   DPE_DMA(256, 256, 2, 4, B_DENSE_K, EPI_BF16_BNB)
 #undef DPE_DMA_T
 #undef DPE_DMA
+  return -1;
+}
+
+// LDS-DMA weight-grad kernel (A = dy M-contiguous; B = x or im2col(x) N-contiguous;
+// EPI_ATOMIC_F32, split-K).  -1: outside its envelope (caller uses dpe_igemm_launch).
+extern "C" int dpe_igemm_wgrad_dma_launch(const IgemmArgs* args, int bm, int bn, int bload, int splits, hipStream_t st) {
+  const IgemmArgs& a = *args;
+  if (a.M <= 0 || a.N <= 0) return 0;
+  if (bload != B_DENSE_N && bload != B_CONV_WGRAD) return -1;
+  if (a.K <= 0 || a.K % 32 || a.k_split % 32 || a.M % 8 || a.N % 8 || a.lda % 8 || a.ldb % 8) return -1;
+  const int64_t lim = (1ll << 31) - 4096;
+  if ((int64_t)a.K * a.lda * 2 >= lim) return -1;
+  const ConvGeom& g = a.g;
+  if (bload == B_CONV_WGRAD) {
+    if (g.C % 8 || (int64_t)g.N * g.OH * g.OW != a.K || g.R * g.S * g.C != a.N) return -1;
+    if (32 / g.OW + 1 > g.OH) return -1;  // pixel walk: at most one image wrap per K-step
+    if (((int64_t)g.N * g.H * g.W * g.C + ((int64_t)g.ph * g.W + g.pw) * g.C) * 2 >= lim) return -1;
+  } else if ((int64_t)a.K * a.ldb * 2 >= lim) {
+    return -1;
+  }
+  if (splits < 1) splits = 1;
+  const int tiles = ((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+#define DPE_WG(BM_, BN_, BL_)                                                                            \
+  if (bm == BM_ && bn == BN_ && bload == BL_) {                                                           \
+    hipLaunchKernelGGL((igemm_wgrad_dma_kernel<BM_, BN_, BL_>), dim3(tiles * splits), dim3(NT), 0, st, a); \
+    return 0;                                                                                           \
+  }
+#define DPE_WG_T(BL_) DPE_WG(128, 128, BL_) DPE_WG(128, 64, BL_) DPE_WG(64, 128, BL_) DPE_WG(64, 64, BL_)
+  DPE_WG_T(B_DENSE_N)
+  DPE_WG_T(B_CONV_WGRAD)
+#undef DPE_WG_T
+#undef DPE_WG
   return -1;
 }

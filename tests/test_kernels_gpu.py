@@ -634,3 +634,22 @@ def test_conv_tiles_lds_dma(C, mode, N, H, W, Ci, Co, k, s, p):
         assert rel_err(tp[0], dz.sum(0)) < 1e-3 and rel_err(tp[1], (dz * (hf - coef[2])).sum(0)) < 1e-3
     finally:
         C.set_conv_tile(0)
+
+
+@pytest.mark.parametrize("N,H,W,Ci,Co,k,s,p", [(8, 14, 14, 64, 64, 3, 1, 1), (32, 7, 7, 128, 200, 3, 1, 1),
+                                               (8, 28, 28, 96, 128, 3, 2, 1), (4, 56, 56, 64, 256, 1, 1, 0),
+                                               (8, 28, 28, 256, 512, 1, 2, 0), (32, 7, 7, 512, 512, 3, 1, 1)])
+def test_conv_wgrad_lds_dma(C, N, H, W, Ci, Co, k, s, p):
+    """LDS-DMA weight-grad kernel (pixel count % 32 == 0): im2col pixel walk across image
+    boundaries (OW = 7 / 14 / 28), taps spanning a column tile (C = 64 / 96), split-K, M / N
+    tails, strided 1x1; accumulates into an existing gradient."""
+    torch.manual_seed(7)
+    x = bf(torch.randn(N, H, W, Ci, device=dev))
+    w = torch.randn(Co, Ci, k, k, device=dev, requires_grad=True)
+    y = F.conv2d(x.permute(0, 3, 1, 2).float(), w, None, s, p)
+    dy = bf(torch.randn_like(y))
+    (ref,) = torch.autograd.grad(y, w, dy.float())
+    dw0 = torch.randn(Co, k, k, Ci, device=dev)
+    dw = dw0.clone()
+    C.conv_wgrad(dy.permute(0, 2, 3, 1).contiguous(), x, dw, [s, s], [p, p], [1, 1], 1.0)
+    assert rel_err(dw - dw0, ref.permute(0, 2, 3, 1)) < 1e-3
