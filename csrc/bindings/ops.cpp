@@ -203,6 +203,16 @@ bool wgrad_dma_on() {
   static const bool on = [] { const char* e = getenv("DPE_WGRAD_DMA"); return !(e && e[0] == '0'); }();
   return on;
 }
+int g_wgrad_wide = [] { const char* e = getenv("DPE_WGRAD_WIDE"); return !(e && e[0] == '0'); }();  // 64x256 wgrad tile
+
+// LDS ring depth of the 4-wave (<= 128x128) DMA tiles: 2 (default: one K-step of loads in flight but
+// 2/3 of the LDS, so 4 instead of 3 blocks per CU -- measured ~10 % faster on 3x3 weight grads, neutral
+// on forward convs) or 3 (two K-steps in flight).  DPE_DMA_STAGES=2|3.  8-wave tiles keep 3.
+int dma_stages(int bm, int bn) {
+  static const int st = [] { const char* e = getenv("DPE_DMA_STAGES"); return (e && e[0] == '3') ? 3 : 2; }();
+  return (bm <= 128 && bn <= 128) ? st : 3;
+}
+
 bool wgrad_dma_dense() {
   static const bool on = [] { const char* e = getenv("DPE_WGRAD_DMA"); return e && e[0] == '2'; }();
   return on;
@@ -223,10 +233,14 @@ int dma_tile_mode() {
 void dma_tile(const dpe::IgemmArgs& a, int aload, int bload, int& bm, int& bn) {
   if (bm != 128 || bload != dpe::B_DENSE_K) return;
   int mode = dma_tile_mode();
+  const bool taps = aload == dpe::A_CONV_FWD && a.g.R * a.g.S > 1;
+  if (a.N <= 64) {  // N = 64: 256x64 only when forced (measured 240 -> 282 us on 64->64 3x3 at 56x56:
+    if (mode >= 2) { bm = 256; bn = 64; }  // 61 KiB LDS halves the blocks per CU)
+    return;
+  }
   if (mode == 0) {
     // measured (scripts/bench_convs.py, batch 512): 256x128 wins on 3x3 convs with K >= 576 and
     // on K >= 1024; 256x256 (one block per CU) loses on most ResNet-50 shapes
-    const bool taps = aload == dpe::A_CONV_FWD && a.g.R * a.g.S > 1;
     mode = (a.K >= 1024 || (taps && a.K >= 576)) ? 2 : 1;
   }
   if (mode == 3 && a.N > 128) { bm = 256; bn = 256; }
@@ -242,7 +256,20 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
   // register-staged (DPE_WGRAD_DMA=0: all register-staged, 2: dense 1x1 too)
   if (conv && epi == dpe::EPI_ATOMIC_F32 && aload == dpe::A_DENSE_M && igemm_dma_on() && wgrad_dma_on() &&
       (bload == dpe::B_CONV_WGRAD || (bload == dpe::B_DENSE_N && wgrad_dma_dense()))) {
-    const int rc = dpe_igemm_wgrad_dma_launch(&a, c.bm, c.bn, bload, c.splits, cur_stream());
+    int bm = c.bm, bn = c.bn, splits = c.splits;
+    if (c.bm == 64 && bload == dpe::B_CONV_WGRAD && a.N >= 256 && g_wgrad_wide && (a.g.C <= 16 || g_wgrad_wide > 1)) {
+      // Cout = 64 with few channels per tap (the stem): 64x256 tile (4 waves across N), split-K
+      // re-derived for its tile count.  Measured: stem 1167 -> 783 us; 64->64 3x3 388 -> 512 us
+      // (2 instead of 4 blocks per CU), so C > 16 keeps 64x128 unless forced (set_wgrad_wide(2)).
+      bn = 256;
+      const int64_t t = (int64_t)((a.N + 255) / 256), ksteps = (a.K + 31) / 32;
+      const int64_t sp = std::max<int64_t>(1, std::min<int64_t>((512 + t - 1) / t, ksteps / 8));
+      const int64_t kps = (ksteps + sp - 1) / sp;
+      a.k_split = (int)(kps * 32);
+      splits = (int)((ksteps + kps - 1) / kps);
+    }
+    const int rc = dpe_igemm_wgrad_dma_launch(&a, bm, bn, bload, splits, dma_stages(bm, bn), cur_stream());
+    a.k_split = c.k_split;  // (register-staged fallback uses pick_cfg's split)
     if (rc == 0) {
       const hipError_t e = hipGetLastError();
       TORCH_CHECK(e == hipSuccess, "igemm_wgrad_dma launch failed: ", hipGetErrorString(e));
@@ -257,7 +284,7 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
     // (same tile shape, so BatchNorm partial layouts are unchanged)
     int bm = c.bm, bn = c.bn;
     dma_tile(a, aload, bload, bm, bn);
-    const int rc = dpe_igemm_dma_launch(&a, bm, bn, aload, bload, epi, cur_stream());
+    const int rc = dpe_igemm_dma_launch(&a, bm, bn, aload, bload, epi, dma_stages(bm, bn), cur_stream());
     if (rc == 0) {
       const hipError_t e = hipGetLastError();
       TORCH_CHECK(e == hipSuccess, "igemm_dma launch failed: ", hipGetErrorString(e));
@@ -1237,6 +1264,8 @@ void register_ops(pybind11::module& m) {
     return v;
   });
   m.def("set_gemm256_mode", [](int64_t mode) { g_g256_mode = (int)mode; }, "0 auto, 1 off, 2 force (when supported)");
+  m.def("set_wgrad_wide", [](int64_t v) { g_wgrad_wide = (int)v; },
+        "64x256 tile for Cout = 64 weight grads: 0 off, 1 when C <= 16 (default), 2 always");
   m.def("set_conv_tile", [](int64_t mode) { g_dma_tile = (int)mode; },
         "LDS-DMA conv tile: 0 auto, 1 128-tile, 2 256x128, 3 256x256 (8 waves)");
   m.def("pick_gemm_cfg", [](int64_t M, int64_t N, int64_t K, bool split) {

@@ -79,11 +79,12 @@ extern "C" int dpe_igemm_launch(const dpe::IgemmArgs* args, int bm, int bn, int 
 extern "C" int dpe_gemm256_launch(const dpe::IgemmArgs* args, int a_k, int b_k, int epi, int splits, hipStream_t stream);
 
 // LDS-DMA implicit-GEMM (igemm.hip) for forward-form convolutions and dense K-contiguous A
-// (B K- or N-contiguous; EPI_BF16 / EPI_BF16_BNB, no split-K).  -1: outside its envelope.
+// (B K- or N-contiguous; EPI_BF16 / EPI_BF16_BNB, no split-K); stages: 2 or 3 (LDS ring depth;
+// 2 only for the 2x2-wave tiles).  -1: outside its envelope.
 extern "C" int dpe_igemm_dma_launch(const dpe::IgemmArgs* args, int bm, int bn, int aload, int bload, int epi,
-                                    hipStream_t stream);
+                                    int stages, hipStream_t stream);
 
 // LDS-DMA weight-grad kernel (igemm.hip): A = dy (A_DENSE_M), B = x (B_DENSE_N) or its im2col
 // (B_CONV_WGRAD), EPI_ATOMIC_F32 with split-K.  -1: outside its envelope.
 extern "C" int dpe_igemm_wgrad_dma_launch(const dpe::IgemmArgs* args, int bm, int bn, int bload, int splits,
-                                          hipStream_t stream);
+                                          int stages, hipStream_t stream);

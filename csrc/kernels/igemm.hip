@@ -42,10 +42,12 @@ DPE_DEVICE int kimg_off(int row, int chunk) {
 template <int COLS>
 DPE_DEVICE int mnimg_off(int k, int chunk) {
   int h;
-  if constexpr (COLS == 128) {
+  if constexpr (COLS == 128 || COLS == 256) {
+    // rows are whole multiples of the 256-B bank window, so the 128-column swizzle
+    // (xor < 16 stays inside the row's first 16-chunk window) serves 256 columns too
     h = ((k & 3) | (((k >> 3) & 1) << 2)) << 1;
   } else {
-    static_assert(COLS == 64, "mn image supports 64/128 columns");
+    static_assert(COLS == 64, "mn image supports 64/128/256 columns");
     h = (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1;
   }
   return k * (COLS * 2) + ((chunk ^ h) << 4);
@@ -497,23 +499,23 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* sm
 // atomics shaped as whole contiguous row segments: every wave-instruction covers 64
 // consecutive floats (256 B) of one row -- the full-rate atomic shape (MI355X_MICROARCH
 // "Global float atomics"); a 16-rows x 4-dwords shape runs ~17x slower.
-template <int BM, int BN, int LDS>
-DPE_DEVICE void epilogue_atomic_f32(const IgemmArgs& p, f32x4 (&acc)[BM / 32][BN / 32], char* smem, int m0, int n0,
-                                    int wn) {
-  constexpr int RM = BM / 32, RN = BN / 32;
-  constexpr int HR = BM / 2;          // rows per half
+template <int BM, int BN, int LDS, int WGM = 2, int WGN = 2>
+DPE_DEVICE void epilogue_atomic_f32(const IgemmArgs& p, f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16], char* smem, int m0,
+                                    int n0, int wn) {
+  constexpr int RM = BM / WGM / 16, RN = BN / WGN / 16, NW = WGM * WGN;
+  constexpr int HR = BM / WGM;        // rows per pass (one wave-row at a time)
   constexpr int FROW = BN + 4;        // fp32 row stride (pad: conflict-free b128 writes)
-  static_assert(HR * FROW * 4 <= LDS, "atomic staging must fit the main-loop LDS");
+  static_assert(HR * FROW * 4 <= LDS, "atomic staging must fit the kernel's LDS");
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lm = lane & 15, ln4 = (lane >> 4) * 4;
   float* C = (float*)p.C;
   float* st = (float*)smem;
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    if ((wid >> 1) == half) {
+  for (int half = 0; half < WGM; ++half) {
+    if ((wid / WGN) == half) {
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
-        const int ml = 16 * i + lm;  // row within this half
+        const int ml = 16 * i + lm;  // row within this pass
 #pragma unroll
         for (int j = 0; j < RN; ++j) {
           const int nl = wn + 16 * j + ln4;
@@ -523,8 +525,8 @@ DPE_DEVICE void epilogue_atomic_f32(const IgemmArgs& p, f32x4 (&acc)[BM / 32][BN
     }
     __syncthreads();
     constexpr int SEG = 64;                   // floats per wave-instruction
-    constexpr int SEGS_PER_ROW = BN / SEG;    // 1 or 2
-    for (int s = wid; s < HR * SEGS_PER_ROW; s += 4) {
+    constexpr int SEGS_PER_ROW = BN / SEG;    // 1, 2 or 4
+    for (int s = wid; s < HR * SEGS_PER_ROW; s += NW) {
       const int r = s / SEGS_PER_ROW, c = (s % SEGS_PER_ROW) * SEG + lane;
       const int m = m0 + half * HR + r, n = n0 + c;
       if (m < p.M && n < p.N) atomicAdd(C + (int64_t)m * p.ldc + n, st[r * FROW + c]);
@@ -696,14 +698,14 @@ DPE_DEVICE void wait_vm() {
 // WGM x WGN waves, each owning a (BM/WGM) x (BN/WGN) sub-tile; 128x128 (2x2 waves),
 // 256x128 (4x2) and 256x256 (2x4).  Bigger tiles cut the L2->LDS bytes per FLOP, which
 // bounds the 128-tile kernel (16 KiB per 256 MFMA-cycles per block).
-template <int BM, int BN, int WGM, int WGN, int BL, int EPI>
+template <int BM, int BN, int WGM, int WGN, int BL, int EPI, int NS = DSTAGES>
 __global__ __launch_bounds__(64 * WGM * WGN, (BM == 256 && BN == 128) ? 4 : 1) void igemm_dma_kernel(IgemmArgs p, int a_dense) {
   constexpr int NTH = 64 * WGM * WGN, NW = WGM * WGN;
   constexpr bool BKc = (BL == B_DENSE_K);
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int CROW = BN * 2 + 16;
-  constexpr int LDS_MAIN = DSTAGES * STAGE;
+  constexpr int LDS_MAIN = NS * STAGE;
   constexpr int LDS_C = BM * CROW + 2 * NW * BN * 4;
   constexpr int LDS = LDS_MAIN > LDS_C ? LDS_MAIN : LDS_C;
   constexpr int RM = BM / WGM / 16, RN = BN / WGN / 16;
@@ -814,15 +816,17 @@ __global__ __launch_bounds__(64 * WGM * WGN, (BM == 256 && BN == 128) ? 4 : 1) v
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // NS-stage ring: stages t+1 .. t+NS-2 stay in flight while stage t is consumed
+  static_assert(NS == 2 || NS == 3, "2- or 3-stage ring");
   if (nt > 0) issue(0);
-  if (nt > 1) issue(1);
+  if (NS == 3 && nt > 1) issue(1);
   for (int t = 0; t < nt; ++t) {
-    if (t + 1 < nt) wait_vm<PA + PB>(); else wait_vm<0>();
+    if (NS == 3 && t + 1 < nt) wait_vm<PA + PB>(); else wait_vm<0>();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 2 < nt) issue((t + 2) % DSTAGES);
-    const char* As = smem + (t % DSTAGES) * STAGE;
+    if (t + NS - 1 < nt) issue((t + NS - 1) % NS);
+    const char* As = smem + (t % NS) * STAGE;
     const char* Bs = As + A_BYTES;
     bf16x8 af[RM], bfr[RN];
 #pragma unroll
@@ -854,17 +858,19 @@ __global__ __launch_bounds__(64 * WGM * WGN, (BM == 256 && BN == 128) ? 4 : 1) v
 // out-of-range offset.  fp32 atomic epilogue (split-K).
 template <int COLS>
 DPE_DEVICE int mn_swz(int k) {
-  if constexpr (COLS == 128) return ((k & 3) | (((k >> 3) & 1) << 2)) << 1;
+  if constexpr (COLS >= 128) return ((k & 3) | (((k >> 3) & 1) << 2)) << 1;
   else return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1;
 }
 
-template <int BM, int BN, int BL>
+template <int BM, int BN, int BL, int WGM = 2, int WGN = 2, int NS = DSTAGES>
 __global__ __launch_bounds__(NT) void igemm_wgrad_dma_kernel(IgemmArgs p) {
+  static_assert(WGM * WGN == 4, "4 waves");
   constexpr bool CONV = (BL == B_CONV_WGRAD);
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int LDS = DSTAGES * STAGE;
-  constexpr int RM = BM / 32, RN = BN / 32;
+  constexpr int LDS_MAIN = NS * STAGE, LDS_ST = (BM / WGM) * (BN + 4) * 4;
+  constexpr int LDS = LDS_MAIN > LDS_ST ? LDS_MAIN : LDS_ST;
+  constexpr int RM = BM / WGM / 16, RN = BN / WGN / 16;
   constexpr int PA = BM / 64, PB = BN / 64;  // 1-KiB pieces per wave per stage (4 waves)
   constexpr int ACPR = BM / 8, AKR = 64 / ACPR, BCPR = BN / 8, BKR = 64 / BCPR;
   __shared__ __attribute__((aligned(16))) char smem[LDS];
@@ -879,7 +885,7 @@ __global__ __launch_bounds__(NT) void igemm_wgrad_dma_kernel(IgemmArgs p) {
   const int kb = split * p.k_split;
   const int ke = min(p.K, kb + p.k_split);
   const int nt = (ke - kb) / BK;
-  const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN / 2);
+  const int wm = (wid / WGN) * (BM / WGM), wn = (wid % WGN) * (BN / WGN);
   const ConvGeom& g = p.g;
 
   // ---- A = dy [K][lda]: fixed per-lane offsets, scalar K-step offset
@@ -962,15 +968,17 @@ __global__ __launch_bounds__(NT) void igemm_wgrad_dma_kernel(IgemmArgs p) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // NS-stage ring: stages t+1 .. t+NS-2 stay in flight while stage t is consumed
+  static_assert(NS == 2 || NS == 3, "2- or 3-stage ring");
   if (nt > 0) issue(0);
-  if (nt > 1) issue(1);
+  if (NS == 3 && nt > 1) issue(1);
   for (int t = 0; t < nt; ++t) {
-    if (t + 1 < nt) wait_vm<PA + PB>(); else wait_vm<0>();
+    if (NS == 3 && t + 1 < nt) wait_vm<PA + PB>(); else wait_vm<0>();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 2 < nt) issue((t + 2) % DSTAGES);
-    const char* As = smem + (t % DSTAGES) * STAGE;
+    if (t + NS - 1 < nt) issue((t + NS - 1) % NS);
+    const char* As = smem + (t % NS) * STAGE;
     const char* Bs = As + A_BYTES;
     bf16x8 af[RM], bfr[RN];
 #pragma unroll
@@ -985,7 +993,7 @@ __global__ __launch_bounds__(NT) void igemm_wgrad_dma_kernel(IgemmArgs p) {
   }
   __syncthreads();
   if (p.alpha_ptr) p.alpha *= *p.alpha_ptr;
-  epilogue_atomic_f32<BM, BN, LDS>(p, acc, smem, m0, n0, wn);
+  epilogue_atomic_f32<BM, BN, LDS, WGM, WGN>(p, acc, smem, m0, n0, wn);
 }
 
 template <int BM, int BN, int AL, int BL, int EPI>
@@ -1038,7 +1046,7 @@ extern "C" int dpe_igemm_launch(const IgemmArgs* args, int bm, int bn, int aload
 // LDS-DMA kernel for forward-form convolutions / dense K-contiguous A.  Returns -1
 // when the problem is outside its envelope (the caller then uses dpe_igemm_launch).
 extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int aload, int bload, int epi,
-                                    hipStream_t st) {
+                                    int stages, hipStream_t st) {
   const IgemmArgs& a = *args;
   if (a.M <= 0 || a.N <= 0) return 0;
   if (aload != A_DENSE_K && aload != A_CONV_FWD) return -1;
@@ -1058,8 +1066,12 @@ extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int a
   const int dn = dense ? 1 : 0;
 #define DPE_DMA(BM_, BN_, WGM_, WGN_, BL_, EP_)                                                             \
   if (bm == BM_ && bn == BN_ && bload == BL_ && epi == EP_) {                                               \
-    hipLaunchKernelGGL((igemm_dma_kernel<BM_, BN_, WGM_, WGN_, BL_, EP_>), dim3(tiles), dim3(64 * WGM_ * WGN_), \
-                       0, st, a, dn);                                                                       \
+    if (stages == 2)                                                                                        \
+      hipLaunchKernelGGL((igemm_dma_kernel<BM_, BN_, WGM_, WGN_, BL_, EP_, 2>), dim3(tiles),                 \
+                         dim3(64 * WGM_ * WGN_), 0, st, a, dn);                                             \
+    else                                                                                                    \
+      hipLaunchKernelGGL((igemm_dma_kernel<BM_, BN_, WGM_, WGN_, BL_, EP_>), dim3(tiles),                    \
+                         dim3(64 * WGM_ * WGN_), 0, st, a, dn);                                             \
     return 0;                                                                                               \
   }
 #define DPE_DMA_T(BL_, EP_) \
@@ -1073,6 +1085,9 @@ extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int a
   DPE_DMA(256, 128, 4, 2, B_DENSE_K, EPI_BF16_BNB)
   DPE_DMA(256, 256, 2, 4, B_DENSE_K, EPI_BF16)
   DPE_DMA(256, 256, 2, 4, B_DENSE_K, EPI_BF16_BNB)
+  // 4-wave 256x64 (4x1 waves) for the N = 64 layers
+  DPE_DMA(256, 64, 4, 1, B_DENSE_K, EPI_BF16)
+  DPE_DMA(256, 64, 4, 1, B_DENSE_K, EPI_BF16_BNB)
 #undef DPE_DMA_T
 #undef DPE_DMA
   return -1;
@@ -1080,7 +1095,8 @@ extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int a
 
 // LDS-DMA weight-grad kernel (A = dy M-contiguous; B = x or im2col(x) N-contiguous;
 // EPI_ATOMIC_F32, split-K).  -1: outside its envelope (caller uses dpe_igemm_launch).
-extern "C" int dpe_igemm_wgrad_dma_launch(const IgemmArgs* args, int bm, int bn, int bload, int splits, hipStream_t st) {
+extern "C" int dpe_igemm_wgrad_dma_launch(const IgemmArgs* args, int bm, int bn, int bload, int splits, int stages,
+                                          hipStream_t st) {
   const IgemmArgs& a = *args;
   if (a.M <= 0 || a.N <= 0) return 0;
   if (bload != B_DENSE_N && bload != B_CONV_WGRAD) return -1;
@@ -1097,14 +1113,22 @@ extern "C" int dpe_igemm_wgrad_dma_launch(const IgemmArgs* args, int bm, int bn,
   }
   if (splits < 1) splits = 1;
   const int tiles = ((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
-#define DPE_WG(BM_, BN_, BL_)                                                                            \
-  if (bm == BM_ && bn == BN_ && bload == BL_) {                                                           \
-    hipLaunchKernelGGL((igemm_wgrad_dma_kernel<BM_, BN_, BL_>), dim3(tiles * splits), dim3(NT), 0, st, a); \
-    return 0;                                                                                           \
+#define DPE_WG(BM_, BN_, BL_)                                                                                \
+  if (bm == BM_ && bn == BN_ && bload == BL_) {                                                               \
+    if (stages == 2)                                                                                          \
+      hipLaunchKernelGGL((igemm_wgrad_dma_kernel<BM_, BN_, BL_, 2, 2, 2>), dim3(tiles * splits), dim3(NT), 0, st, a); \
+    else                                                                                                      \
+      hipLaunchKernelGGL((igemm_wgrad_dma_kernel<BM_, BN_, BL_>), dim3(tiles * splits), dim3(NT), 0, st, a);     \
+    return 0;                                                                                                 \
   }
 #define DPE_WG_T(BL_) DPE_WG(128, 128, BL_) DPE_WG(128, 64, BL_) DPE_WG(64, 128, BL_) DPE_WG(64, 64, BL_)
   DPE_WG_T(B_DENSE_N)
   DPE_WG_T(B_CONV_WGRAD)
+  // Cout = 64 layers: one 64-row wave band, 4 waves across 256 columns
+  if (bm == 64 && bn == 256 && bload == B_CONV_WGRAD) {
+    hipLaunchKernelGGL((igemm_wgrad_dma_kernel<64, 256, B_CONV_WGRAD, 1, 4>), dim3(tiles * splits), dim3(NT), 0, st, a);
+    return 0;
+  }
 #undef DPE_WG_T
 #undef DPE_WG
   return -1;

@@ -603,7 +603,8 @@ def test_conv_dgrad_acc_inplace(C, N, H, W, Ci, Co, k, s, p):
 @pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("N,H,W,Ci,Co,k,s,p", [(2, 14, 14, 64, 256, 3, 1, 1), (3, 7, 7, 128, 384, 3, 1, 1),
                                                (2, 28, 28, 128, 128, 3, 2, 1), (2, 14, 14, 256, 512, 1, 1, 0),
-                                               (2, 14, 14, 96, 200, 3, 1, 1)])
+                                               (2, 14, 14, 96, 200, 3, 1, 1), (2, 28, 28, 64, 64, 3, 1, 1),
+                                               (3, 14, 14, 64, 40, 3, 1, 1)])
 def test_conv_tiles_lds_dma(C, mode, N, H, W, Ci, Co, k, s, p):
     """LDS-DMA conv kernel at every tile (128, 256x128, 256x256 8-wave): forward output + BN
     statistics partials (128-row sub-tiles), and the forward-form data grad with BN partials."""
@@ -638,7 +639,8 @@ def test_conv_tiles_lds_dma(C, mode, N, H, W, Ci, Co, k, s, p):
 
 @pytest.mark.parametrize("N,H,W,Ci,Co,k,s,p", [(8, 14, 14, 64, 64, 3, 1, 1), (32, 7, 7, 128, 200, 3, 1, 1),
                                                (8, 28, 28, 96, 128, 3, 2, 1), (4, 56, 56, 64, 256, 1, 1, 0),
-                                               (8, 28, 28, 256, 512, 1, 2, 0), (32, 7, 7, 512, 512, 3, 1, 1)])
+                                               (8, 28, 28, 256, 512, 1, 2, 0), (32, 7, 7, 512, 512, 3, 1, 1),
+                                               (16, 14, 14, 64, 48, 3, 1, 1), (8, 28, 28, 32, 64, 3, 1, 1)])
 def test_conv_wgrad_lds_dma(C, N, H, W, Ci, Co, k, s, p):
     """LDS-DMA weight-grad kernel (pixel count % 32 == 0): im2col pixel walk across image
     boundaries (OW = 7 / 14 / 28), taps spanning a column tile (C = 64 / 96), split-K, M / N
@@ -650,6 +652,11 @@ def test_conv_wgrad_lds_dma(C, N, H, W, Ci, Co, k, s, p):
     dy = bf(torch.randn_like(y))
     (ref,) = torch.autograd.grad(y, w, dy.float())
     dw0 = torch.randn(Co, k, k, Ci, device=dev)
-    dw = dw0.clone()
-    C.conv_wgrad(dy.permute(0, 2, 3, 1).contiguous(), x, dw, [s, s], [p, p], [1, 1], 1.0)
-    assert rel_err(dw - dw0, ref.permute(0, 2, 3, 1)) < 1e-3
+    for wide in (1, 2):  # 2: the 64x256 tile also for C > 16
+        C.set_wgrad_wide(wide)
+        try:
+            dw = dw0.clone()
+            C.conv_wgrad(dy.permute(0, 2, 3, 1).contiguous(), x, dw, [s, s], [p, p], [1, 1], 1.0)
+        finally:
+            C.set_wgrad_wide(1)
+        assert rel_err(dw - dw0, ref.permute(0, 2, 3, 1)) < 1e-3
