@@ -276,9 +276,16 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
       return;
     }
   }
-  // LDS-DMA kernel where it measured faster: im2col A (3x3 / strided), dense 1x1 A at K >= 512,
-  // B K-contiguous (the N-contiguous B of 1x1 data grads measured 5-10 % slower on it)
-  const bool dma_role = bload == dpe::B_DENSE_K && (aload == dpe::A_CONV_FWD || (aload == dpe::A_DENSE_K && a.K >= 512));
+  // LDS-DMA kernel where it measured faster (2-stage ring, batch 512, profiles/convs_bs512_*):
+  //   im2col A (3x3 / strided), K-contiguous B: always;
+  //   dense 1x1 forward (A_DENSE_K x B_DENSE_K): unless K and N are both 64 (store-bound);
+  //   1x1 data grads (A_DENSE_K x B_DENSE_N): for 128 <= N <= 512 (8-27 % faster; N = 64 and
+  //   N >= 1024 measured 2-10 % slower).  DPE_DMA_ALL=1: every forward-form role.
+  static const bool dma_all = [] { const char* e = getenv("DPE_DMA_ALL"); return e && e[0] == '1'; }();
+  bool dma_role = false;
+  if (aload == dpe::A_CONV_FWD) dma_role = bload == dpe::B_DENSE_K || dma_all;
+  else if (aload == dpe::A_DENSE_K && bload == dpe::B_DENSE_K) dma_role = dma_all || a.K >= 128 || a.N >= 256;
+  else if (aload == dpe::A_DENSE_K && bload == dpe::B_DENSE_N) dma_role = dma_all || (a.N >= 128 && a.N <= 512);
   if (conv && c.splits == 1 && dma_role && igemm_dma_on()) {
     // convolutions whose A is an im2col / dense K-contiguous operand: LDS-DMA kernel
     // (same tile shape, so BatchNorm partial layouts are unchanged)
