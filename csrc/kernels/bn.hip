@@ -12,6 +12,7 @@
 // When a GEMM epilogue already accumulated the column (sum, sumsq) for this
 // BN (igemm col_stats), `finalize` is called with nb = 1 on that buffer and
 // the stats pass is skipped entirely.
+#include <cstdlib>
 #include "common.h"
 
 namespace dpe {
@@ -141,6 +142,20 @@ __global__ void bn_eval_coeff_kernel(int C, const float* gamma, const float* bet
 // hoisted out of the loop (the stride is a multiple of C/8 whenever C/8 divides BN_T).
 constexpr int BN_U = 4;
 
+// Streaming (non-temporal) 16-B load for operands not re-read soon (the pre-BN input saved for
+// backward, the incoming gradient): keeps the caches for the output, which the next conv reads.
+template <bool NTL>
+DPE_DEVICE u32x4 ld_stream(const uint16_t* p) {
+  if constexpr (NTL) return __builtin_nontemporal_load((const u32x4*)p);
+  else return *(const u32x4*)p;
+}
+// Default on: in the ResNet-50 step it measured 45.5 -> 45.0 ms/step (two A/B pairs); in isolation
+// it is shape-dependent (scripts/bench_bn.py).  DPE_BN_NT=0 disables.
+static bool bn_nt_loads() {
+  static const bool on = [] { const char* e = getenv("DPE_BN_NT"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 template <int NCOEF>
 struct Coef8 {
   float v[NCOEF][8];
@@ -155,7 +170,7 @@ struct Coef8 {
 };
 
 // y = act(x*scale + shift [+ res])
-template <typename I>
+template <typename I, bool NTL = false>
 __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                         uint16_t* __restrict__ y, int64_t nchunks, int C,
                                                         const float* __restrict__ coef, int relu,
@@ -171,8 +186,8 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const uint16_t* __restri
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       const I i = min(i0 + (I)u * stride, n - 1);
-      xr[u] = *(const u32x4*)(x + (size_t)i * 8);
-      if (res) rr[u] = *(const u32x4*)(res + (size_t)i * 8);
+      xr[u] = ld_stream<NTL>(x + (size_t)i * 8);
+      if (res) rr[u] = ld_stream<NTL>(res + (size_t)i * 8);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
@@ -315,7 +330,7 @@ __global__ __launch_bounds__(NTHR) void bn_bwd_finalize_kernel(const float* __re
 // ReLU mask: from y (y > 0) when y is given, else from the pre-BN input and the
 // forward coefficients (x*scale + shift > 0) when mcoef is given (the BN output
 // was never materialised: it was applied in the consumer's load prologue).
-template <typename I>
+template <typename I, bool NTL = false>
 __global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
                                                             const uint16_t* __restrict__ x, const float* __restrict__ bcoef,
                                                             uint16_t* __restrict__ dx, uint16_t* __restrict__ dz_out,
@@ -335,9 +350,9 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const uint16_t* __re
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       const I i = min(i0 + (I)u * stride, n - 1);
-      dr[u] = *(const u32x4*)(dy + (size_t)i * 8);
-      xr[u] = *(const u32x4*)(x + (size_t)i * 8);
-      if (y) yr[u] = *(const u32x4*)(y + (size_t)i * 8);
+      dr[u] = ld_stream<NTL>(dy + (size_t)i * 8);
+      xr[u] = ld_stream<NTL>(x + (size_t)i * 8);
+      if (y) yr[u] = ld_stream<NTL>(y + (size_t)i * 8);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
@@ -415,8 +430,12 @@ extern "C" int dpe_bn_apply_m(const uint16_t* x, const uint16_t* res, uint16_t* 
                               int relu, uint8_t* mbits, hipStream_t st) {
   const int64_t nch = M * C / 8;
   if (nch < (1ll << 31))
-    hipLaunchKernelGGL(bn_apply_kernel<uint32_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, res, y, nch, C, coef, relu,
-                       mbits);
+    if (bn_nt_loads())
+      hipLaunchKernelGGL((bn_apply_kernel<uint32_t, true>), dim3(grid_for(nch)), dim3(BN_T), 0, st, x, res, y, nch, C, coef,
+                         relu, mbits);
+    else
+      hipLaunchKernelGGL(bn_apply_kernel<uint32_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, res, y, nch, C, coef, relu,
+                         mbits);
   else
     hipLaunchKernelGGL(bn_apply_kernel<int64_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, x, res, y, nch, C, coef, relu,
                        mbits);
@@ -463,7 +482,10 @@ extern "C" int dpe_bn_bwd_finalize(const float* part, int nb, int C, int64_t M, 
 extern "C" int dpe_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* bcoef, uint16_t* dx,
                                 uint16_t* dz_out, int64_t M, int C, const float* mcoef, hipStream_t st) {
   const int64_t nch = M * C / 8;
-  if (nch < (1ll << 31))
+  if (nch < (1ll << 31) && bn_nt_loads())
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<uint32_t, true>), dim3(grid_for(nch)), dim3(BN_T), 0, st, dy, y, x, bcoef, dx,
+                       dz_out, nch, C, mcoef);
+  else if (nch < (1ll << 31))
     hipLaunchKernelGGL(bn_bwd_apply_kernel<uint32_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, dy, y, x, bcoef, dx, dz_out, nch,
                        C, mcoef);
   else
