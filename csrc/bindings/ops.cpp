@@ -629,7 +629,13 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
   a.A = bp(dy); a.B = bp(w); a.C = dx.data_ptr();
   a.M = g.N * g.H * g.W; a.N = g.C; a.K = g.R * g.S * g.K;
   a.lda = g.K; a.ldb = g.C; a.ldc = g.C;
-  if (residual.has_value() && residual->defined()) { CHECK_BF16((*residual)); CHECK_CONTIG((*residual)); a.residual = bp(*residual); }
+  if (residual.has_value() && residual->defined()) {
+    CHECK_BF16((*residual)); CHECK_CONTIG((*residual));
+    a.residual = bp(*residual);
+    // the data-grad residual (a block's dz3 pass-through) is at its last use
+    static const bool nt = [] { const char* e = getenv("DPE_EPI_NT"); return !(e && e[0] == '0'); }();
+    a.res_nt = nt ? 1 : 0;
+  }
   if (acc_into) {
     TORCH_CHECK(!a.residual && !(bn_x.has_value() && bn_x->defined()), "conv_dgrad_acc: no residual / BN with accumulate");
     CHECK_BF16(dx); CHECK_CONTIG(dx);

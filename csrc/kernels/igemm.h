@@ -58,6 +58,7 @@ struct IgemmArgs {
                              //   (y = relu(BN(x) + idn)): ReLU-mask BITS of the saved y, one byte per
                              //   8 columns ([M][ldc/8], bit e = column 8j+e, written by bn_apply), and
                              //   the STORED value is the masked dz, not v
+  int res_nt;                // residual is at its last use: stream it (non-temporal loads)
   int stats_ld;              // partial columns per channel (0 -> tilesM of this launch)
   int stats_off;             // first partial column written by this launch (phase-decomposed dgrad)
   int M, N, K;

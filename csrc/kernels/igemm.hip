@@ -417,7 +417,9 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* sm
           const int rr = rb + r0 + (u0 + q) * RPP;
           const int64_t off = (int64_t)(m0 + rr) * p.ldc + n;
           tv[q] = *(const u32x4*)(smem + rr * CROW + c * 16);
-          rv[q] = p.residual ? ld16(p.residual + off) : z4;
+          rv[q] = p.residual ? (p.res_nt ? __builtin_nontemporal_load((const u32x4*)(p.residual + off))
+                                         : ld16(p.residual + off))
+                             : z4;
           xv[q] = (BNB && p.col_stats) ? ld16(p.st_x + off) : z4;
           mb[q] = (BNB && p.st_mask) ? (uint32_t)p.st_mask[off >> 3] : 0u;
         }
