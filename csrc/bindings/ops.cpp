@@ -23,11 +23,11 @@ int dpe_bn_eval_coeff(int C, const float* gamma, const float* beta, const float*
                       float* coef, hipStream_t st);
 int dpe_bn_apply(const uint16_t* x, const uint16_t* res, uint16_t* y, int64_t M, int C, const float* coef, int relu,
                  hipStream_t st);
-int dpe_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* coef, int64_t M, int C, int nb,
+int dpe_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint8_t* ybits, const uint16_t* x, const float* coef, int64_t M, int C, int nb,
                       float* part, hipStream_t st);
 int dpe_bn_bwd_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* coef, float* dgamma,
                         float* dbeta, float* bcoef, hipStream_t st);
-int dpe_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* bcoef, uint16_t* dx,
+int dpe_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint8_t* ybits, const uint16_t* x, const float* bcoef, uint16_t* dx,
                      uint16_t* dz_out, int64_t M, int C, const float* mcoef, hipStream_t st);
 int dpe_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int k, int s,
                     int p, hipStream_t st);
@@ -822,22 +822,31 @@ Tensor bn_fwd_eval(const Tensor& x, const c10::optional<Tensor>& gamma, const c1
 // returns (dx, dz or empty); dgamma/dbeta accumulated (+=) if given
 std::vector<Tensor> bn_bwd(const Tensor& dy, const c10::optional<Tensor>& y, const Tensor& x,
                            const c10::optional<Tensor>& gamma, const Tensor& coef, const c10::optional<Tensor>& dgamma,
-                           const c10::optional<Tensor>& dbeta, bool want_dz) {
+                           const c10::optional<Tensor>& dbeta, bool want_dz, const c10::optional<Tensor>& y_bits) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x);
   const int64_t C = x.size(-1), M = rows_of(x);
   const uint16_t* yp = (y.has_value() && y->defined()) ? bp(*y) : nullptr;
+  const uint8_t* yb = nullptr;
+  if (y_bits.has_value() && y_bits->defined()) {
+    // ReLU mask as bn_apply's bits (1/16 of y's bytes): y itself is not read
+    CHECK_CONTIG((*y_bits));
+    TORCH_CHECK(y_bits->scalar_type() == at::kByte && y_bits->numel() * 8 == x.numel() && C % 8 == 0,
+                "bn_bwd: y_bits must be uint8 mask bits [.., C/8] of x's shape");
+    yb = (const uint8_t*)y_bits->data_ptr();
+    yp = nullptr;
+  }
   hipStream_t st = cur_stream();
   auto fo = x.options().dtype(at::kFloat);
   const int nb = dpe_bn_stats_nblocks(M, (int)C);
   Tensor part = at::empty({nb, 2, C}, fo);
-  CHECK_RC(dpe_bn_bwd_reduce(bp(dy), yp, bp(x), fp(coef), M, (int)C, nb, fp(part), st), "bn_bwd_reduce");
+  CHECK_RC(dpe_bn_bwd_reduce(bp(dy), yp, yb, bp(x), fp(coef), M, (int)C, nb, fp(part), st), "bn_bwd_reduce");
   Tensor bcoef = at::empty({3, C}, fo);
   CHECK_RC(dpe_bn_bwd_finalize(fp(part), nb, (int)C, M, fpo(gamma), fp(coef), fpom(dgamma), fpom(dbeta), fp(bcoef), st),
            "bn_bwd_finalize");
   Tensor dx = at::empty_like(x);
   Tensor dz;
   if (want_dz) dz = at::empty_like(x);
-  CHECK_RC(dpe_bn_bwd_apply(bp(dy), yp, bp(x), fp(bcoef), bpm(dx), want_dz ? bpm(dz) : nullptr, M, (int)C, nullptr, st),
+  CHECK_RC(dpe_bn_bwd_apply(bp(dy), yp, yb, bp(x), fp(bcoef), bpm(dx), want_dz ? bpm(dz) : nullptr, M, (int)C, nullptr, st),
            "bn_bwd_apply");
   return {dx, dz};
 }
@@ -872,7 +881,7 @@ Tensor bn_bwd_partials(const Tensor& dy, const Tensor& x, const c10::optional<Te
   CHECK_RC(dpe_bn_bwd_finalize(fp(partials), (int)partials.size(2), (int)C, M, fpo(gamma), fp(coef), fpom(dgamma),
                                fpom(dbeta), fp(bcoef), st), "bn_bwd_finalize");
   Tensor dx = at::empty_like(x);
-  CHECK_RC(dpe_bn_bwd_apply(bp(dy), nullptr, bp(x), fp(bcoef), bpm(dx), nullptr, M, (int)C, relu_mask ? fp(coef) : nullptr, st),
+  CHECK_RC(dpe_bn_bwd_apply(bp(dy), nullptr, nullptr, bp(x), fp(bcoef), bpm(dx), nullptr, M, (int)C, relu_mask ? fp(coef) : nullptr, st),
            "bn_bwd_apply");
   return dx;
 }
@@ -1239,7 +1248,7 @@ void register_ops(pybind11::module& m) {
   m.def("bn_fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),
         py::arg("eps"), py::arg("relu"), py::arg("residual") = py::none());
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("coef"), py::arg("dgamma"),
-        py::arg("dbeta"), py::arg("want_dz") = false);
+        py::arg("dbeta"), py::arg("want_dz") = false, py::arg("y_bits") = py::none());
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("gavgpool_fwd", &gavgpool_fwd);

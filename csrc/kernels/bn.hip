@@ -262,7 +262,9 @@ __global__ __launch_bounds__(BN_T) void bn_apply2_kernel(const uint16_t* __restr
 }
 
 // partial sums of dz and dz*(x-mean), dz = dy * (y > 0 if relu)
+// ybits: the ReLU mask as bits of y (one byte per 8 columns, bn_apply's want_mask) instead of y itself
 __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+                                                             const uint8_t* __restrict__ ybits,
                                                              const uint16_t* __restrict__ x, const float* __restrict__ coef,
                                                              int64_t M, int C, int64_t rows_per_block, float* __restrict__ part) {
   const int CPR = C >> 3;
@@ -280,7 +282,11 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const uint16_t* __r
       float d[8], xv[8];
       unpack8(*(const u32x4*)(dy + off), d);
       unpack8(*(const u32x4*)(x + off), xv);
-      if (y) {
+      if (ybits) {
+        const uint32_t mb = ybits[off >> 3];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = ((mb >> e) & 1u) ? d[e] : 0.f;
+      } else if (y) {
         float yv[8];
         unpack8(*(const u32x4*)(y + off), yv);
 #pragma unroll
@@ -332,6 +338,7 @@ __global__ __launch_bounds__(NTHR) void bn_bwd_finalize_kernel(const float* __re
 // was never materialised: it was applied in the consumer's load prologue).
 template <typename I, bool NTL = false>
 __global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+                                                            const uint8_t* __restrict__ ybits,
                                                             const uint16_t* __restrict__ x, const float* __restrict__ bcoef,
                                                             uint16_t* __restrict__ dx, uint16_t* __restrict__ dz_out,
                                                             int64_t nchunks, int C, const float* __restrict__ mcoef) {
@@ -365,7 +372,11 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const uint16_t* __re
       float d[8], xv[8];
       unpack8(dr[u], d);
       unpack8(xr[u], xv);
-      if (y) {
+      if (ybits) {
+        const uint32_t mb = ybits[i];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = ((mb >> e) & 1u) ? d[e] : 0.f;
+      } else if (y) {
         float yv[8];
         unpack8(yr[u], yv);
 #pragma unroll
@@ -459,11 +470,11 @@ extern "C" int dpe_bn_apply2(const uint16_t* x, const float* coef, const uint16_
   return 0;
 }
 
-extern "C" int dpe_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* coef, int64_t M,
-                                 int C, int nb, float* part, hipStream_t st) {
+extern "C" int dpe_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint8_t* ybits, const uint16_t* x,
+                                 const float* coef, int64_t M, int C, int nb, float* part, hipStream_t st) {
   if (C % 8 || C / 8 > BN_T) return -1;
   const int64_t rpb = (M + nb - 1) / nb;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(BN_T), 0, st, dy, y, x, coef, M, C, rpb, part);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(BN_T), 0, st, dy, y, ybits, x, coef, M, C, rpb, part);
   return 0;
 }
 
@@ -479,17 +490,18 @@ extern "C" int dpe_bn_bwd_finalize(const float* part, int nb, int C, int64_t M, 
   return 0;
 }
 
-extern "C" int dpe_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* bcoef, uint16_t* dx,
-                                uint16_t* dz_out, int64_t M, int C, const float* mcoef, hipStream_t st) {
+extern "C" int dpe_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint8_t* ybits, const uint16_t* x,
+                                const float* bcoef, uint16_t* dx, uint16_t* dz_out, int64_t M, int C, const float* mcoef,
+                                hipStream_t st) {
   const int64_t nch = M * C / 8;
   if (nch < (1ll << 31) && bn_nt_loads())
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<uint32_t, true>), dim3(grid_for(nch)), dim3(BN_T), 0, st, dy, y, x, bcoef, dx,
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<uint32_t, true>), dim3(grid_for(nch)), dim3(BN_T), 0, st, dy, y, ybits, x, bcoef, dx,
                        dz_out, nch, C, mcoef);
   else if (nch < (1ll << 31))
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<uint32_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, dy, y, x, bcoef, dx, dz_out, nch,
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<uint32_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, dy, y, ybits, x, bcoef, dx, dz_out, nch,
                        C, mcoef);
   else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<int64_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, dy, y, x, bcoef, dx, dz_out, nch,
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<int64_t>, dim3(grid_for(nch)), dim3(BN_T), 0, st, dy, y, ybits, x, bcoef, dx, dz_out, nch,
                        C, mcoef);
   return 0;
 }

@@ -107,7 +107,7 @@ class BottleneckFn(Function):
         h1, a1, c1 = convbn(0, x, True)
         h2, a2, c2 = convbn(1, a1, True)
         # the next block's fused data-grad epilogue reads this output's ReLU mask as bits
-        want_bits = link_out is not None
+        want_bits = True  # 1/16 of out: read by the next block's fused epilogue or by this block's BN3 backward
         h3, c3 = conv_coef(2, a2)
         if block.down is not None:
             out, bits = C.bn_apply(h3, c3, hd, cd, True, want_bits)
@@ -119,6 +119,7 @@ class BottleneckFn(Function):
         ctx.link_in = (link_in if (link_in is not None and block.down is None and link_in.h3 is not None
                                    and link_in.mask is not None) else None)
         ctx.link_out = link_out
+        ctx.bits = bits  # ReLU mask of out as bits: the standalone BN3 backward reads these, not out
         if link_out is not None:
             link_out.h3, link_out.coef, link_out.mask = h3, c3, bits
         ctx.block = block
@@ -151,9 +152,9 @@ class BottleneckFn(Function):
             grads[id(bn.weight)] = None if gd else gb
             grads[id(bn.bias)] = None if bd else bb
 
-        def bn_bwd(i, dy, y, h, coef, want_dz):
+        def bn_bwd(i, dy, y, h, coef, want_dz, y_bits=None):
             bn, gb, gd, bb, bd = bn_sinks(i)
-            dh, dz = C.bn_bwd(dy, y, h, bn.weight.detach(), coef, gb, bb, want_dz)
+            dh, dz = C.bn_bwd(dy, y, h, bn.weight.detach(), coef, gb, bb, want_dz, y_bits)
             bn_done(bn, gb, gd, bb, bd)
             return dh, dz
 
@@ -194,7 +195,8 @@ class BottleneckFn(Function):
             bn_done(bn, gb, gd, bb, bd)
             lk.part = None
         else:
-            dh3, dz3 = bn_bwd(2, dout, out, h3, c3, True)
+            dh3, dz3 = bn_bwd(2, dout, out, h3, c3, True, ctx.bits)
+        ctx.bits = None
         if lk is not None:
             lk.h3 = lk.coef = lk.mask = None
         wgrad(2, dh3, a2)

@@ -660,3 +660,24 @@ def test_conv_wgrad_lds_dma(C, N, H, W, Ci, Co, k, s, p):
         finally:
             C.set_wgrad_wide(1)
         assert rel_err(dw - dw0, ref.permute(0, 2, 3, 1)) < 1e-3
+
+
+def test_bn_bwd_with_mask_bits_matches_y(C):
+    """BN+ReLU backward (reduce + apply, dz written) with the ReLU mask read as bn_apply's bits
+    instead of the saved output y: identical results."""
+    torch.manual_seed(17)
+    N, H, W, Ci = 4, 14, 14, 256
+    h = bf(torch.randn(N, H, W, Ci, device=dev))
+    coef = _bn_coef(C, Ci)
+    res = bf(torch.randn(N, H, W, Ci, device=dev))
+    y, bits = C.bn_apply(h, coef, res, None, True, True)
+    dy = bf(torch.randn(N, H, W, Ci, device=dev))
+    gamma = torch.rand(Ci, device=dev) + 0.5
+    outs = []
+    for use_bits in (False, True):
+        dg, db = torch.zeros(Ci, device=dev), torch.zeros(Ci, device=dev)
+        dx, dz = C.bn_bwd(dy, y, h, gamma, coef, dg, db, True, bits if use_bits else None)
+        outs.append((dx, dz, dg, db))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert torch.equal(outs[0][1], torch.where(y > 0, dy, torch.zeros_like(dy)))
