@@ -617,7 +617,8 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
                                     std::vector<int64_t> stride, std::vector<int64_t> pad, std::vector<int64_t> dil,
                                     const c10::optional<Tensor>& residual, const c10::optional<Tensor>& bn_x,
                                     const c10::optional<Tensor>& bn_coef, const Tensor* acc_into = nullptr,
-                                    const c10::optional<Tensor>& bn_mask = c10::nullopt) {
+                                    const c10::optional<Tensor>& bn_mask = c10::nullopt,
+                                    const c10::optional<Tensor>& residual_mask = c10::nullopt) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(w); CHECK_CONTIG(dy); CHECK_CONTIG(w);
   // acc_into: dx += dgrad in place (the epilogue reads each element as its residual
   // right before overwriting it); parities no tap reaches are left untouched.
@@ -635,6 +636,14 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
     // the data-grad residual (a block's dz3 pass-through) is at its last use
     static const bool nt = [] { const char* e = getenv("DPE_EPI_NT"); return !(e && e[0] == '0'); }();
     a.res_nt = nt ? 1 : 0;
+    if (residual_mask.has_value() && residual_mask->defined()) {
+      // residual = dy of a BN + residual + ReLU output: masked by that output's bits in the epilogue
+      CHECK_CONTIG((*residual_mask));
+      TORCH_CHECK(residual_mask->scalar_type() == at::kByte && residual_mask->numel() * 8 == residual->numel() &&
+                      residual->size(-1) % 8 == 0,
+                  "conv_dgrad: residual_mask must be uint8 mask bits [.., C/8] of the residual");
+      a.res_mask = (const uint8_t*)residual_mask->data_ptr();
+    }
   }
   if (acc_into) {
     TORCH_CHECK(!a.residual && !(bn_x.has_value() && bn_x->defined()), "conv_dgrad_acc: no residual / BN with accumulate");
@@ -754,8 +763,10 @@ void conv_dgrad_acc(const Tensor& dy, const Tensor& w, Tensor& dx, std::vector<i
 }
 
 Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape, std::vector<int64_t> stride,
-                  std::vector<int64_t> pad, std::vector<int64_t> dil, const c10::optional<Tensor>& residual) {
-  return conv_dgrad_impl(dy, w, xshape, stride, pad, dil, residual, c10::nullopt, c10::nullopt)[0];
+                  std::vector<int64_t> pad, std::vector<int64_t> dil, const c10::optional<Tensor>& residual,
+                  const c10::optional<Tensor>& residual_mask) {
+  return conv_dgrad_impl(dy, w, xshape, stride, pad, dil, residual, c10::nullopt, c10::nullopt, nullptr, c10::nullopt,
+                         residual_mask)[0];
 }
 
 // dw [K,R,S,C] fp32 (+)= alpha * dy^T (x) im2col(x)
@@ -1223,11 +1234,11 @@ void register_ops(pybind11::module& m) {
   m.def("conv_dgrad_bn", [](const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape, std::vector<int64_t> stride,
                             std::vector<int64_t> pad, std::vector<int64_t> dil, const c10::optional<Tensor>& residual,
                             const c10::optional<Tensor>& bn_x, const c10::optional<Tensor>& bn_coef,
-                            const c10::optional<Tensor>& bn_mask) {
-          return conv_dgrad_impl(dy, w, xshape, stride, pad, dil, residual, bn_x, bn_coef, nullptr, bn_mask);
+                            const c10::optional<Tensor>& bn_mask, const c10::optional<Tensor>& residual_mask) {
+          return conv_dgrad_impl(dy, w, xshape, stride, pad, dil, residual, bn_x, bn_coef, nullptr, bn_mask, residual_mask);
         }, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"),
         py::arg("pad"), py::arg("dil"), py::arg("residual") = py::none(), py::arg("bn_x") = py::none(),
-        py::arg("bn_coef") = py::none(), py::arg("bn_mask") = py::none(),
+        py::arg("bn_coef") = py::none(), py::arg("bn_mask") = py::none(), py::arg("residual_mask") = py::none(),
         "data grad; with bn_x/bn_coef also the BN-backward partials of the BN+ReLU that produced the conv input; "
         "with bn_mask (BN + residual + ReLU) the mask is bn_mask > 0 and dx is stored masked");
   m.def("bn_coef", &bn_coef, py::arg("stats"), py::arg("M"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
@@ -1240,7 +1251,7 @@ void register_ops(pybind11::module& m) {
   m.def("bn_bwd_partials", &bn_bwd_partials, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("coef"),
         py::arg("partials"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none(), py::arg("relu_mask") = true);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"), py::arg("pad"),
-        py::arg("dil"), py::arg("residual") = py::none());
+        py::arg("dil"), py::arg("residual") = py::none(), py::arg("residual_mask") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), py::arg("alpha") = 1.0);
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),

@@ -352,11 +352,16 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* sm
   // Per-row finish: residual add, BN-backward partials / ReLU-mask (BNB) or BN-forward
   // partials, store.  Operands arrive pre-loaded (rv / xv / mb) so the fast path can
   // issue the loads of several rows before the first use.
-  auto finish_row = [&](u32x4 v, const u32x4& rv, const u32x4& xv_raw, uint32_t mb, uint16_t* dst, bool vec_row) {
+  auto finish_row = [&](u32x4 v, const u32x4& rv, const u32x4& xv_raw, uint32_t mb, uint32_t rmb, uint16_t* dst,
+                        bool vec_row) {
     if (p.residual) {
       float f[8], g[8];
       unpack8(v, f);
       unpack8(rv, g);
+      if (p.res_mask) {  // residual = dy * relu'(y) from y's mask bits (dz never materialised)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = ((rmb >> e) & 1u) ? g[e] : 0.f;
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) f[e] += g[e];
       v = pack8(f);
@@ -411,7 +416,7 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* sm
 #pragma unroll
       for (int u0 = 0; u0 < RPS; u0 += G) {
         u32x4 tv[G], rv[G], xv[G];
-        uint32_t mb[G];
+        uint32_t mb[G], rmb[G];
 #pragma unroll
         for (int q = 0; q < G; ++q) {
           const int rr = rb + r0 + (u0 + q) * RPP;
@@ -422,11 +427,12 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* sm
                              : z4;
           xv[q] = (BNB && p.col_stats) ? ld16(p.st_x + off) : z4;
           mb[q] = (BNB && p.st_mask) ? (uint32_t)p.st_mask[off >> 3] : 0u;
+          rmb[q] = p.res_mask ? (uint32_t)p.res_mask[off >> 3] : 0u;
         }
 #pragma unroll
         for (int q = 0; q < G; ++q) {
           const int rr = rb + r0 + (u0 + q) * RPP;
-          finish_row(tv[q], rv[q], xv[q], mb[q], C + (int64_t)(m0 + rr) * p.ldc + n, true);
+          finish_row(tv[q], rv[q], xv[q], mb[q], rmb[q], C + (int64_t)(m0 + rr) * p.ldc + n, true);
         }
       }
     } else {
@@ -458,7 +464,8 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* sm
           xv = pack8(xf);
         }
         if (BNB && p.st_mask) mb = p.st_mask[off >> 3];
-        finish_row(v, rv, xv, mb, C + off, vec);
+        const uint32_t rmb = p.res_mask ? (uint32_t)p.res_mask[off >> 3] : 0u;
+        finish_row(v, rv, xv, mb, rmb, C + off, vec);
       }
     }
     if (p.col_stats) {

@@ -139,6 +139,7 @@ class BottleneckFn(Function):
         has_down = len(convs) == 4
         dout = dout.contiguous()
         grads = {}
+        res_mask = None  # set when dz3 is represented as (dout, ReLU bits of out)
 
         def bn_sinks(i):
             bn = convs[i].bn
@@ -194,6 +195,11 @@ class BottleneckFn(Function):
             dh3 = C.bn_bwd_partials(dz3, h3, bn.weight.detach(), c3, lk.part, gb, bb, relu_mask=False)
             bn_done(bn, gb, gd, bb, bd)
             lk.part = None
+        elif ctx.bits is not None and not has_down:
+            # dz3 = dout * relu'(out) is only this block's residual gradient: the data-grad
+            # epilogue masks dout with the bits itself, so dz3 is never written
+            dh3, _ = bn_bwd(2, dout, out, h3, c3, False, ctx.bits)
+            dz3, res_mask = dout, ctx.bits
         else:
             dh3, dz3 = bn_bwd(2, dout, out, h3, c3, True, ctx.bits)
         ctx.bits = None
@@ -217,10 +223,11 @@ class BottleneckFn(Function):
             elif ctx.link_in is not None:
                 li = ctx.link_in
                 s, p, d = _conv_conf(convs[0].conv)
-                dx, part = C.conv_dgrad_bn(dh1, ws[0], list(x.shape), s, p, d, dz3, li.h3, li.coef, li.mask)
+                dx, part = C.conv_dgrad_bn(dh1, ws[0], list(x.shape), s, p, d, dz3, li.h3, li.coef, li.mask, res_mask)
                 li.part, li.dz_ptr, li.dz_shape = part, dx.data_ptr(), tuple(dx.shape)
             else:
-                dx = dgrad(0, dh1, list(x.shape), dz3)
+                s, p, d = _conv_conf(convs[0].conv)
+                dx = C.conv_dgrad(dh1, ws[0], list(x.shape), s, p, d, dz3, res_mask)
         elif has_down:
             dhd, _ = bn_bwd(3, dz3, None, hd, cd, False)
             wgrad(3, dhd, x)

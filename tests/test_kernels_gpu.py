@@ -681,3 +681,28 @@ def test_bn_bwd_with_mask_bits_matches_y(C):
     for a, b in zip(*outs):
         assert torch.equal(a, b)
     assert torch.equal(outs[0][1], torch.where(y > 0, dy, torch.zeros_like(dy)))
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_dgrad_residual_masked_by_bits(C, k):
+    """Data grad + residual where the residual is dy of a BN+residual+ReLU output, masked in the
+    epilogue by that output's bits (plain and BN-partials epilogues) == adding the masked residual."""
+    torch.manual_seed(19)
+    N, H, W, Ci, Co = 4, 14, 14, 128, 64
+    w = bf(torch.randn(Co, k, k, Ci, device=dev) / math.sqrt(k * k * Ci))
+    dy = bf(torch.randn(N, H, W, Co, device=dev))
+    h = bf(torch.randn(N, H, W, Ci, device=dev))
+    coef = _bn_coef(C, Ci)
+    y, bits = C.bn_apply(h, coef, bf(torch.randn(N, H, W, Ci, device=dev)), None, True, True)
+    dout = bf(torch.randn(N, H, W, Ci, device=dev))
+    dz = torch.where(y > 0, dout, torch.zeros_like(dout))
+    p = k // 2
+    ref = C.conv_dgrad(dy, w, [N, H, W, Ci], [1, 1], [p, p], [1, 1], dz)
+    got = C.conv_dgrad(dy, w, [N, H, W, Ci], [1, 1], [p, p], [1, 1], dout, bits)
+    assert torch.equal(got, ref)
+    h0 = bf(torch.randn(N, H, W, Ci, device=dev))
+    c0 = _bn_coef(C, Ci)
+    _, bits0 = C.bn_apply(h0, c0, h, None, True, True)
+    r1, p1 = C.conv_dgrad_bn(dy, w, [N, H, W, Ci], [1, 1], [p, p], [1, 1], dz, h0, c0, bits0)
+    r2, p2 = C.conv_dgrad_bn(dy, w, [N, H, W, Ci], [1, 1], [p, p], [1, 1], dout, h0, c0, bits0, bits)
+    assert torch.equal(r1, r2) and torch.equal(p1, p2)
