@@ -25,6 +25,8 @@ int dpe_bn_apply(const uint16_t* x, const uint16_t* res, uint16_t* y, int64_t M,
                  hipStream_t st);
 int dpe_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const uint8_t* ybits, const uint16_t* x, const float* coef, int64_t M, int C, int nb,
                       float* part, hipStream_t st);
+int dpe_bn_bwd_reduce_apply(const uint16_t* dz, const uint16_t* x, const float* coef, const uint16_t* ax, const float* abcoef,
+                            uint16_t* adx, int64_t M, int C, int nb, float* part, hipStream_t st);
 int dpe_bn_bwd_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* coef, float* dgamma,
                         float* dbeta, float* bcoef, hipStream_t st);
 int dpe_bn_bwd_apply(const uint16_t* dy, const uint16_t* y, const uint8_t* ybits, const uint16_t* x, const float* bcoef, uint16_t* dx,
@@ -897,6 +899,36 @@ Tensor bn_bwd_partials(const Tensor& dy, const Tensor& x, const c10::optional<Te
   return dx;
 }
 
+// Two BatchNorms fed by the same dz (a downsample bottleneck: BN3 and BN_d both see dz3):
+// BN3's backward from its epilogue partials, BN_d's reduce fused into BN3's apply pass
+// (dz read once for both), then BN_d's apply.  Returns (dx, dx2).
+std::vector<Tensor> bn_bwd_dual(const Tensor& dz, const Tensor& x, const c10::optional<Tensor>& gamma, const Tensor& coef,
+                                const Tensor& partials, const c10::optional<Tensor>& dgamma,
+                                const c10::optional<Tensor>& dbeta, const Tensor& x2, const c10::optional<Tensor>& gamma2,
+                                const Tensor& coef2, const c10::optional<Tensor>& dgamma2, const c10::optional<Tensor>& dbeta2) {
+  CHECK_GPU(dz); CHECK_BF16(dz); CHECK_CONTIG(dz); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(x2); CHECK_CONTIG(x2);
+  TORCH_CHECK(dz.sizes() == x.sizes() && dz.sizes() == x2.sizes(), "bn_bwd_dual: dz / x / x2 shape mismatch");
+  const int64_t C = x.size(-1), M = rows_of(x);
+  TORCH_CHECK(partials.dim() == 3 && partials.size(0) == 2 && partials.size(1) == C, "partials must be [2][C][nb]");
+  hipStream_t st = cur_stream();
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor bcoef = at::empty({3, C}, fo);
+  CHECK_RC(dpe_bn_bwd_finalize(fp(partials), (int)partials.size(2), (int)C, M, fpo(gamma), fp(coef), fpom(dgamma),
+                               fpom(dbeta), fp(bcoef), st), "bn_bwd_finalize");
+  const int nb = dpe_bn_stats_nblocks(M, (int)C);
+  Tensor part2 = at::empty({2, C, nb}, fo);
+  Tensor dx = at::empty_like(x);
+  CHECK_RC(dpe_bn_bwd_reduce_apply(bp(dz), bp(x2), fp(coef2), bp(x), fp(bcoef), bpm(dx), M, (int)C, nb, fp(part2), st),
+           "bn_bwd_reduce_apply");
+  Tensor bcoef2 = at::empty({3, C}, fo);
+  CHECK_RC(dpe_bn_bwd_finalize(fp(part2), nb, (int)C, M, fpo(gamma2), fp(coef2), fpom(dgamma2), fpom(dbeta2), fp(bcoef2), st),
+           "bn_bwd_finalize");
+  Tensor dx2 = at::empty_like(x2);
+  CHECK_RC(dpe_bn_bwd_apply(bp(dz), nullptr, nullptr, bp(x2), fp(bcoef2), bpm(dx2), nullptr, M, (int)C, nullptr, st),
+           "bn_bwd_apply");
+  return {dx, dx2};
+}
+
 // ----------------------------------------------------------------- pooling
 std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x);
@@ -1258,6 +1290,9 @@ void register_ops(pybind11::module& m) {
         py::arg("momentum"), py::arg("eps"), py::arg("relu"), py::arg("residual") = py::none(), py::arg("stats") = py::none());
   m.def("bn_fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),
         py::arg("eps"), py::arg("relu"), py::arg("residual") = py::none());
+  m.def("bn_bwd_dual", &bn_bwd_dual, py::arg("dz"), py::arg("x"), py::arg("gamma"), py::arg("coef"), py::arg("partials"),
+        py::arg("dgamma"), py::arg("dbeta"), py::arg("x2"), py::arg("gamma2"), py::arg("coef2"), py::arg("dgamma2"),
+        py::arg("dbeta2"), "backward of two BatchNorms fed by one dz (BN3 + downsample BN): dz read once for both");
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("coef"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("want_dz") = false, py::arg("y_bits") = py::none());
   m.def("maxpool_fwd", &maxpool_fwd);

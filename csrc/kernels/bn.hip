@@ -263,10 +263,15 @@ __global__ __launch_bounds__(BN_T) void bn_apply2_kernel(const uint16_t* __restr
 
 // partial sums of dz and dz*(x-mean), dz = dy * (y > 0 if relu)
 // ybits: the ReLU mask as bits of y (one byte per 8 columns, bn_apply's want_mask) instead of y itself
+// With adx: the same pass also applies ANOTHER BatchNorm's backward to the same dz,
+// adx = a*dz + b*ax + c (abcoef [3][C]) -- a bottleneck's BN3 apply fused with its
+// downsample BN's reduce (both are functions of dz3): dz3 is read once.
 __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
                                                              const uint8_t* __restrict__ ybits,
                                                              const uint16_t* __restrict__ x, const float* __restrict__ coef,
-                                                             int64_t M, int C, int64_t rows_per_block, float* __restrict__ part) {
+                                                             int64_t M, int C, int64_t rows_per_block, float* __restrict__ part,
+                                                             const uint16_t* __restrict__ ax, const float* __restrict__ abcoef,
+                                                             uint16_t* __restrict__ adx) {
   const int CPR = C >> 3;
   const int tid = threadIdx.x;
   const int RPI = BN_T / CPR;
@@ -276,12 +281,21 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const uint16_t* __r
   float s[8], q[8], mean[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s[e] = 0.f; q[e] = 0.f; mean[e] = coef[2 * C + c * 8 + e]; }
+  Coef8<3> ac;
+  if (adx) ac.load(abcoef, C, c * 8);
   if (r < RPI) {
     for (int64_t row = rb + r; row < re; row += RPI) {
       const int64_t off = row * C + c * 8;
       float d[8], xv[8];
       unpack8(*(const u32x4*)(dy + off), d);
       unpack8(*(const u32x4*)(x + off), xv);
+      if (adx) {
+        float av[8], o[8];
+        unpack8(*(const u32x4*)(ax + off), av);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = fmaf(ac.v[0][e], d[e], fmaf(ac.v[1][e], av[e], ac.v[2][e]));
+        *(u32x4*)(adx + off) = pack8(o);
+      }
       if (ybits) {
         const uint32_t mb = ybits[off >> 3];
 #pragma unroll
@@ -474,7 +488,19 @@ extern "C" int dpe_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const ui
                                  const float* coef, int64_t M, int C, int nb, float* part, hipStream_t st) {
   if (C % 8 || C / 8 > BN_T) return -1;
   const int64_t rpb = (M + nb - 1) / nb;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(BN_T), 0, st, dy, y, ybits, x, coef, M, C, rpb, part);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(BN_T), 0, st, dy, y, ybits, x, coef, M, C, rpb, part,
+                     (const uint16_t*)nullptr, (const float*)nullptr, (uint16_t*)nullptr);
+  return 0;
+}
+
+// reduce (dz, x; coef) for one BatchNorm + apply adx = a*dz + b*ax + c for another, one pass
+extern "C" int dpe_bn_bwd_reduce_apply(const uint16_t* dz, const uint16_t* x, const float* coef, const uint16_t* ax,
+                                       const float* abcoef, uint16_t* adx, int64_t M, int C, int nb, float* part,
+                                       hipStream_t st) {
+  if (C % 8 || C / 8 > BN_T) return -1;
+  const int64_t rpb = (M + nb - 1) / nb;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(BN_T), 0, st, dz, (const uint16_t*)nullptr,
+                     (const uint8_t*)nullptr, x, coef, M, C, rpb, part, ax, abcoef, adx);
   return 0;
 }
 

@@ -57,6 +57,8 @@ from ..ops._state import grad_done, grad_sink, note_use, run_on_aux, shadow
 _EPI_BNB = os.environ.get("DPE_BN_EPI", "1") != "0"
 # DPE_BN3_CHAIN=0: every block's BN3 backward through the standalone reduce + apply
 _BN3_CHAIN = _EPI_BNB and os.environ.get("DPE_BN3_CHAIN", "1") != "0"
+# DPE_BN_DUAL=0: downsample blocks run BN3's and BN_d's backward as separate passes
+_BN_DUAL = os.environ.get("DPE_BN_DUAL", "1") != "0"
 
 
 class _BN3Link:
@@ -140,6 +142,7 @@ class BottleneckFn(Function):
         dout = dout.contiguous()
         grads = {}
         res_mask = None  # set when dz3 is represented as (dout, ReLU bits of out)
+        dhd = None  # downsample BN's dL/dhd, when computed together with BN3's (bn_bwd_dual)
 
         def bn_sinks(i):
             bn = convs[i].bn
@@ -192,7 +195,15 @@ class BottleneckFn(Function):
             # the next block's dgrad epilogue already produced dz3 = dout*relu'(out) and BN3's partials
             dz3 = dout
             bn, gb, gd, bb, bd = bn_sinks(2)
-            dh3 = C.bn_bwd_partials(dz3, h3, bn.weight.detach(), c3, lk.part, gb, bb, relu_mask=False)
+            if has_down and _BN_DUAL:
+                # BN3 and the downsample BN both see dz3: one pass applies BN3's backward and
+                # reduces BN_d's sums, then BN_d's apply (dz3 read twice instead of three times)
+                bnd, gbd, gdd, bbd, bdd = bn_sinks(3)
+                dh3, dhd = C.bn_bwd_dual(dz3, h3, bn.weight.detach(), c3, lk.part, gb, bb, hd, bnd.weight.detach(), cd,
+                                         gbd, bbd)
+                bn_done(bnd, gbd, gdd, bbd, bdd)
+            else:
+                dh3 = C.bn_bwd_partials(dz3, h3, bn.weight.detach(), c3, lk.part, gb, bb, relu_mask=False)
             bn_done(bn, gb, gd, bb, bd)
             lk.part = None
         elif ctx.bits is not None and not has_down:
@@ -213,7 +224,8 @@ class BottleneckFn(Function):
         dx = None
         if ctx.needs_input_grad[0]:
             if has_down:
-                dhd, _ = bn_bwd(3, dz3, None, hd, cd, False)
+                if dhd is None:
+                    dhd, _ = bn_bwd(3, dz3, None, hd, cd, False)
                 wgrad(3, dhd, x)
                 dx = dgrad(0, dh1, list(x.shape))
                 # downsample branch accumulated in place: a strided 1x1 only reaches one
@@ -229,7 +241,8 @@ class BottleneckFn(Function):
                 s, p, d = _conv_conf(convs[0].conv)
                 dx = C.conv_dgrad(dh1, ws[0], list(x.shape), s, p, d, dz3, res_mask)
         elif has_down:
-            dhd, _ = bn_bwd(3, dz3, None, hd, cd, False)
+            if dhd is None:
+                dhd, _ = bn_bwd(3, dz3, None, hd, cd, False)
             wgrad(3, dhd, x)
         pgrads = [grads.get(id(p)) for p in ctx.block._fused_params]
         return (dx, None, None, None, *pgrads)

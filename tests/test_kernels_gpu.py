@@ -706,3 +706,24 @@ def test_dgrad_residual_masked_by_bits(C, k):
     r1, p1 = C.conv_dgrad_bn(dy, w, [N, H, W, Ci], [1, 1], [p, p], [1, 1], dz, h0, c0, bits0)
     r2, p2 = C.conv_dgrad_bn(dy, w, [N, H, W, Ci], [1, 1], [p, p], [1, 1], dout, h0, c0, bits0, bits)
     assert torch.equal(r1, r2) and torch.equal(p1, p2)
+
+
+def test_bn_bwd_dual_matches_two_backwards(C):
+    """bn_bwd_dual (BN3 from epilogue partials + downsample BN, dz read once for both) ==
+    bn_bwd_partials for BN3 and the standalone reduce+apply for BN_d."""
+    torch.manual_seed(23)
+    N, H, W, Ch = 4, 14, 14, 256
+    dz = bf(torch.randn(N, H, W, Ch, device=dev))
+    h3, hd = bf(torch.randn(N, H, W, Ch, device=dev)), bf(torch.randn(N, H, W, Ch, device=dev))
+    c3, cd = _bn_coef(C, Ch), _bn_coef(C, Ch)
+    dzf, h3f = dz.float().reshape(-1, Ch), h3.float().reshape(-1, Ch)
+    part = torch.stack([dzf.sum(0), (dzf * (h3f - c3[2])).sum(0)]).unsqueeze(-1).contiguous()
+    g3, gd = torch.rand(Ch, device=dev) + 0.5, torch.rand(Ch, device=dev) + 0.5
+    z = lambda: torch.zeros(Ch, device=dev)  # noqa: E731
+    a_g3, a_b3, a_gd, a_bd = z(), z(), z(), z()
+    dh3, dhd = C.bn_bwd_dual(dz, h3, g3, c3, part, a_g3, a_b3, hd, gd, cd, a_gd, a_bd)
+    b_g3, b_b3, b_gd, b_bd = z(), z(), z(), z()
+    ref3 = C.bn_bwd_partials(dz, h3, g3, c3, part, b_g3, b_b3, relu_mask=False)
+    refd, _ = C.bn_bwd(dz, None, hd, gd, cd, b_gd, b_bd, False)
+    assert torch.equal(dh3, ref3) and torch.allclose(a_g3, b_g3) and torch.allclose(a_b3, b_b3)
+    assert rel_err(dhd, refd) < 1e-2 and rel_err(a_gd, b_gd) < 1e-4 and rel_err(a_bd, b_bd) < 1e-4
