@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
 
 // D <= 2048: each lane owns at most 4 chunks (32 columns) for the dw/db partials.
 // dy and x of the row are loaded once and kept in registers for both passes.
-template <bool XBF>
+template <bool XBF, int NJ>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict__ dy, const void* __restrict__ x,
                                                      const float* __restrict__ w, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, void* __restrict__ dx, int dx_acc,
@@ -83,18 +83,18 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
                                                      float* __restrict__ part, int64_t rows, int D) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int CH = D >> 3;
-  float pw[4][8], pb[4][8];
+  float pw[NJ][8], pb[NJ][8];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int e = 0; e < 8; ++e) { pw[j][e] = 0.f; pb[j][e] = 0.f; }
   for (int64_t row = blockIdx.x * 4ll + wid; row < rows; row += (int64_t)gridDim.x * 4) {
     const int64_t base = row * D;
     const float mean = mean_in[row], rstd = rstd_in[row];
     float sg = 0.f, sgx = 0.f;
-    float dd[4][8], xh[4][8];
+    float dd[NJ][8], xh[NJ][8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int c = lane + 64 * j;
       if (c < CH) {
         float f[8];
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
     sg = warp_sum(sg) / (float)D;
     sgx = warp_sum(sgx) / (float)D;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int c = lane + 64 * j;
       if (c < CH) {
         float o[8];
@@ -143,18 +143,21 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
     }
   }
   // block-reduce partials over 4 waves
-  __shared__ float red[2][4][2048];
+  // (dynamic LDS sized [2][4][D]: 24 KiB at D = 768 instead of a fixed 64 KiB -> 6 blocks per CU)
+  extern __shared__ float red_dyn[];
+  float* red0 = red_dyn;          // [4][D]
+  float* red1 = red_dyn + 4 * D;  // [4][D]
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     const int c = lane + 64 * j;
     if (c < CH)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { red[0][wid][c * 8 + e] = pw[j][e]; red[1][wid][c * 8 + e] = pb[j][e]; }
+      for (int e = 0; e < 8; ++e) { red0[wid * D + c * 8 + e] = pw[j][e]; red1[wid * D + c * 8 + e] = pb[j][e]; }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < D; i += 256) {
-    part[(int64_t)blockIdx.x * 2 * D + i] = red[0][0][i] + red[0][1][i] + red[0][2][i] + red[0][3][i];
-    part[(int64_t)blockIdx.x * 2 * D + D + i] = red[1][0][i] + red[1][1][i] + red[1][2][i] + red[1][3][i];
+    part[(int64_t)blockIdx.x * 2 * D + i] = red0[i] + red0[D + i] + red0[2 * D + i] + red0[3 * D + i];
+    part[(int64_t)blockIdx.x * 2 * D + D + i] = red1[i] + red1[D + i] + red1[2 * D + i] + red1[3 * D + i];
   }
 }
 
@@ -228,12 +231,16 @@ extern "C" int dpe_layernorm_bwd(const uint16_t* dy, const void* x, int x_bf16, 
                                  float* db, float* part, int64_t rows, int D, hipStream_t st) {
   if (D % 8 || D > 2048) return -1;
   const int nbc = dpe_layernorm_bwd_nblocks(rows);
-  if (x_bf16)
-    hipLaunchKernelGGL((ln_bwd_kernel<true>), dim3(nbc), dim3(256), 0, st, dy, x, w, mean, rstd, dx, dx_acc, res_in, dx_bf16,
-                       part, rows, D);
-  else
-    hipLaunchKernelGGL((ln_bwd_kernel<false>), dim3(nbc), dim3(256), 0, st, dy, x, w, mean, rstd, dx, dx_acc, res_in, dx_bf16,
-                       part, rows, D);
+  const int nj = (D / 8 + 63) / 64;  // 16-B chunks per lane per row
+  const size_t lds = (size_t)2 * 4 * D * sizeof(float);
+#define DPE_LNB(XB, NJ_) \
+  hipLaunchKernelGGL((ln_bwd_kernel<XB, NJ_>), dim3(nbc), dim3(256), lds, st, dy, x, w, mean, rstd, dx, dx_acc, res_in, \
+                     dx_bf16, part, rows, D)
+#define DPE_LNB_J(XB) \
+  if (nj == 1) DPE_LNB(XB, 1); else if (nj == 2) DPE_LNB(XB, 2); else if (nj == 3) DPE_LNB(XB, 3); else DPE_LNB(XB, 4)
+  if (x_bf16) { DPE_LNB_J(true); } else { DPE_LNB_J(false); }
+#undef DPE_LNB_J
+#undef DPE_LNB
   hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 63) / 64, db ? 2 : 1), dim3(64 * LNF_W), 0, st, part, nbc, D, dw, db);
   return 0;
 }
