@@ -237,7 +237,10 @@ void dma_tile(const dpe::IgemmArgs& a, int aload, int bload, int& bm, int& bn) {
   int mode = dma_tile_mode();
   const bool taps = aload == dpe::A_CONV_FWD && a.g.R * a.g.S > 1;
   if (a.N <= 64) {  // N = 64: 256x64 only when forced (measured 240 -> 282 us on 64->64 3x3 at 56x56:
-    if (mode >= 2) { bm = 256; bn = 64; }  // 61 KiB LDS halves the blocks per CU)
+    // 61 KiB LDS halves the blocks per CU) or, with DPE_DMA_W64=1, for short K (the s2d stem, K = 256),
+    // where every 128-row tile re-reading the whole filter is a third of the L2->LDS bytes
+    static const bool w64 = [] { const char* e = getenv("DPE_DMA_W64"); return e && e[0] == '1'; }();
+    if (mode >= 2 || (mode == 0 && w64 && a.K <= 256 && a.M >= (1 << 20))) { bm = 256; bn = 64; }
     return;
   }
   if (mode == 0) {
@@ -249,7 +252,17 @@ void dma_tile(const dpe::IgemmArgs& a, int aload, int bload, int& bm, int& bn) {
   else if (mode >= 2 && a.N > 64) { bm = 256; bn = 128; }
 }
 
+// DPE_EPI_NT_STORE=1: bf16 conv outputs larger than the 256 MiB Infinity Cache are written with
+// non-temporal stores (they are evicted before their consumer reads them anyway)
+bool epi_nt_store() {
+  static const bool on = [] { const char* e = getenv("DPE_EPI_NT_STORE"); return e && e[0] == '1'; }();
+  return on;
+}
+
 void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_split, bool conv = false) {
+  if (conv && (epi == dpe::EPI_BF16 || epi == dpe::EPI_BF16_BNB) && epi_nt_store() &&
+      (int64_t)a.M * a.ldc * 2 > (320ll << 20))
+    a.c_nt = 1;
   if ((!conv || g_g256_override == 1 || g256_mode() == 2) && try_gemm256(a, aload, bload, epi, allow_split)) return;
   Cfg c = pick_cfg(a.M, a.N, a.K, allow_split && epi == dpe::EPI_ATOMIC_F32);
   a.k_split = c.k_split;

@@ -394,7 +394,8 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* sm
       }
     }
     if (vec_row) {
-      *(u32x4*)dst = v;
+      if (p.c_nt) __builtin_nontemporal_store(v, (u32x4*)dst);
+      else *(u32x4*)dst = v;
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -734,7 +735,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, (BM == 256 && BN == 128) ? 4 : 1) v
   const int C = a_dense ? p.K : g.C;  // channels per tap (the whole K for dense A)
 
   // ---- A rows: per-piece row offset + tap-validity mask (bit t = tap t in range)
-  uint32_t aoff[PA], amask[PA];
+  const bool c16 = !a_dense && g.C == 16;
+  uint32_t aoff[PA], amask[PA], adsel[PA];
 #pragma unroll
   for (int i = 0; i < PA; ++i) {
     const int row = (wid * PA + i) * 16 + (lane >> 2);
@@ -758,8 +760,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, (BM == 256 && BN == 128) ? 4 : 1) v
         }
       }
     }
-    aoff[i] = off + lc * 16;
+    // C = 16 (the s2d stem): a 32-wide K-step spans two taps; chunks 0-1 read tap t,
+    // chunks 2-3 tap t+1 (adsel), each at channel offset (lc & 1) * 8
+    aoff[i] = off + (c16 ? (lc & 1) : lc) * 16;
     amask[i] = mask;
+    adsel[i] = c16 ? (lc >> 1) : 0;
   }
   // A's buffer starts (ph*W + pw)*C elements before x so that every in-range tap offset is >= 0
   const int64_t apre = a_dense ? 0 : ((int64_t)g.ph * g.W + g.pw) * g.C;
@@ -796,25 +801,43 @@ __global__ __launch_bounds__(64 * WGM * WGN, (BM == 256 && BN == 128) ? 4 : 1) v
   const uint32_t s_step = (uint32_t)g.dw * g.C * 2u, r_step = (uint32_t)g.dh * g.W * g.C * 2u;
   const int nt = p.K / BK;
 
+  auto next_tap = [&]() {
+    ++tap;
+    if (++ts == (a_dense ? 1 : g.S)) {
+      ts = 0;
+      tapoff += r_step - (uint32_t)(g.S - 1) * s_step;
+    } else {
+      tapoff += s_step;
+    }
+  };
   auto issue = [&](int buf) {
     char* st = smem + buf * STAGE;
+    if (c16) {  // taps (tap, tap + 1): per-lane tap select, offsets in voffset
+      const uint32_t off1 = (ts + 1 == g.S) ? tapoff + r_step - (uint32_t)(g.S - 1) * s_step : tapoff + s_step;
 #pragma unroll
-    for (int i = 0; i < PA; ++i) {
-      const uint32_t v = ((amask[i] >> tap) & 1u) ? aoff[i] : DMA_OOB;
-      dma16(ar, st + (wid * PA + i) * 1024, v, tapoff + ci * 2);
+      for (int i = 0; i < PA; ++i) {
+        const int tl = tap + (int)adsel[i];
+        const uint32_t v = ((amask[i] >> tl) & 1u) ? aoff[i] + (adsel[i] ? off1 : tapoff) : DMA_OOB;
+        dma16(ar, st + (wid * PA + i) * 1024, v, 0u);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < PA; ++i) {
+        const uint32_t v = ((amask[i] >> tap) & 1u) ? aoff[i] : DMA_OOB;
+        dma16(ar, st + (wid * PA + i) * 1024, v, tapoff + ci * 2);
+      }
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) dma16(br, st + A_BYTES + (wid * PB + i) * 1024, boff[i], kbo);
     kbo += bstep;
-    ci += BK;
-    if (ci >= C) {
-      ci = 0;
-      ++tap;
-      if (++ts == (a_dense ? 1 : g.S)) {
-        ts = 0;
-        tapoff += r_step - (uint32_t)(g.S - 1) * s_step;
-      } else {
-        tapoff += s_step;
+    if (c16) {
+      next_tap();
+      next_tap();
+    } else {
+      ci += BK;
+      if (ci >= C) {
+        ci = 0;
+        next_tap();
       }
     }
   };
@@ -1064,7 +1087,7 @@ extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int a
   if (a.K <= 0 || a.K % 32 || a.k_split < a.K) return -1;
   const bool dense = aload == A_DENSE_K;
   const ConvGeom& g = a.g;
-  if (!dense && (g.C % 32 || g.R * g.S > 32 || g.R * g.S * g.C != a.K)) return -1;
+  if (!dense && ((g.C % 32 && !(g.C == 16 && (g.R * g.S) % 2 == 0)) || g.R * g.S > 32 || g.R * g.S * g.C != a.K)) return -1;
   if (a.ldb % 8 || (bload == B_DENSE_N && a.N % 8) || (dense && a.lda % 8)) return -1;
   const int64_t lim = (1ll << 31) - 4096;
   const int64_t abytes = dense ? (int64_t)a.M * a.lda * 2
