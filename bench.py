@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--first-bucket-mb", type=float, default=1.0)
+    ap.add_argument("--last-bucket-mb", type=float, default=2.0,
+                    help="re-split the last-ready bucket (the all-reduce that cannot overlap backward) into <= this")
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--optimizer", default=None)
     ap.add_argument("--lr", type=float, default=None)
@@ -124,7 +126,8 @@ def main():
         num_classes = 10
 
     fused_loss = args.model == "gpt2"
-    ddp = DDP(model, bucket_cap_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb, force_comm=args.force_comm)
+    ddp = DDP(model, bucket_cap_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb, force_comm=args.force_comm,
+              last_bucket_mb=args.last_bucket_mb)
     opt = build_optimizer(opt_name, model.parameters(), lr=lr, weight_decay=wd)
 
     def step(i):

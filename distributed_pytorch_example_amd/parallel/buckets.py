@@ -18,8 +18,30 @@ from typing import List, Sequence
 
 
 def assign_buckets(sizes_bytes: Sequence[int], order: Sequence[int], cap_bytes: int,
-                   first_cap_bytes: int | None = None, keys: Sequence | None = None) -> List[List[int]]:
-    """Return a list of buckets (lists of parameter indices, in ``order``)."""
+                   first_cap_bytes: int | None = None, keys: Sequence | None = None,
+                   last_cap_bytes: int | None = None) -> List[List[int]]:
+    """Return a list of buckets (lists of parameter indices, in ``order``).
+
+    ``last_cap_bytes`` (MI355X addition, not in c10d): the final bucket -- the gradients
+    that become ready last, whose all-reduce is the only one that cannot overlap
+    backward -- is re-split into pieces of at most this many bytes, so all but the
+    last small piece start while the earliest layers are still in backward."""
+    buckets = _assign(sizes_bytes, order, cap_bytes, first_cap_bytes, keys)
+    if last_cap_bytes and len(buckets) > 1:
+        tail, pieces, cur, nbytes = buckets.pop(), [], [], 0
+        for idx in tail:
+            if cur and nbytes + sizes_bytes[idx] > last_cap_bytes:
+                pieces.append(cur)
+                cur, nbytes = [], 0
+            cur.append(idx)
+            nbytes += sizes_bytes[idx]
+        if cur:
+            pieces.append(cur)
+        buckets.extend(pieces)
+    return buckets
+
+
+def _assign(sizes_bytes, order, cap_bytes, first_cap_bytes, keys) -> List[List[int]]:
     if first_cap_bytes is None:
         first_cap_bytes = cap_bytes
     buckets: List[List[int]] = []

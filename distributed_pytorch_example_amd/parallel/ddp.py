@@ -163,7 +163,7 @@ class DistributedDataParallel(nn.Module):
                  find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
                  init_sync: bool = True, timing: bool = False, comm=None, force_comm: bool = False,
                  gradient_compression: Optional[str] = None, rebuild_buckets: bool = True,
-                 debug: Optional[bool] = None):
+                 debug: Optional[bool] = None, last_bucket_mb: Optional[float] = 2.0):
         super().__init__()
         self.module = module
         self.broadcast_buffers = broadcast_buffers
@@ -175,6 +175,9 @@ class DistributedDataParallel(nn.Module):
         cap = int((bucket_cap_mb if bucket_cap_mb is not None else 25.0) * 1024 * 1024)
         first = int(first_bucket_mb * 1024 * 1024) if first_bucket_mb else cap
         self.bucket_cap_bytes, self.first_bucket_bytes = cap, first
+        # the last-ready gradients (the only all-reduce that cannot overlap backward) go in
+        # small buckets: at 8 GPUs only the final <= last_bucket_mb piece is exposed
+        self.last_bucket_bytes = int(last_bucket_mb * 1024 * 1024) if last_bucket_mb else None
         self._comm = comm if comm is not None else pdist.comm()
         self._force = force_comm
         self._timing = timing
@@ -230,7 +233,8 @@ class DistributedDataParallel(nn.Module):
         old = None
         if getattr(self, "buckets", None) is not None:
             old = [p.grad.detach().clone() if p.grad is not None else None for p in self._params]
-        self.bucket_indices = assign_buckets(sizes, order, self.bucket_cap_bytes, self.first_bucket_bytes, keys)
+        self.bucket_indices = assign_buckets(sizes, order, self.bucket_cap_bytes, self.first_bucket_bytes, keys,
+                                             self.last_bucket_bytes)
         self.buckets: List[torch.Tensor] = []
         self._views = {}
         for bidx in self.bucket_indices:
