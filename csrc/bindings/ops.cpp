@@ -212,6 +212,9 @@ int g_wgrad_wide = [] { const char* e = getenv("DPE_WGRAD_WIDE"); return !(e && 
 // on forward convs) or 3 (two K-steps in flight).  DPE_DMA_STAGES=2|3.  8-wave tiles keep 3.
 int dma_stages(int bm, int bn) {
   static const int st = [] { const char* e = getenv("DPE_DMA_STAGES"); return (e && e[0] == '3') ? 3 : 2; }();
+  // DPE_DMA_PF=1: forward DMA kernels use the fragment-prefetch loop (3 buffers, "stages" 4)
+  static const bool pf = [] { const char* e = getenv("DPE_DMA_PF"); return e && e[0] == '1'; }();
+  if (pf && bm <= 128 && bn <= 128) return 4;  // (8-wave tiles: a second fragment set spills at 128 VGPRs)
   return (bm <= 128 && bn <= 128) ? st : 3;
 }
 
@@ -260,6 +263,8 @@ bool epi_nt_store() {
 }
 
 void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_split, bool conv = false) {
+  static const int mfma_prio = [] { const char* e = getenv("DPE_MFMA_PRIO"); return (e && e[0] == '1') ? 1 : 0; }();
+  a.mfma_prio = mfma_prio;
   if (conv && (epi == dpe::EPI_BF16 || epi == dpe::EPI_BF16_BNB) && epi_nt_store() &&
       (int64_t)a.M * a.ldc * 2 > (320ll << 20))
     a.c_nt = 1;
@@ -283,7 +288,7 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
       a.k_split = (int)(kps * 32);
       splits = (int)((ksteps + kps - 1) / kps);
     }
-    const int rc = dpe_igemm_wgrad_dma_launch(&a, bm, bn, bload, splits, dma_stages(bm, bn), cur_stream());
+    const int rc = dpe_igemm_wgrad_dma_launch(&a, bm, bn, bload, splits, std::min(dma_stages(bm, bn), 3), cur_stream());
     a.k_split = c.k_split;  // (register-staged fallback uses pick_cfg's split)
     if (rc == 0) {
       const hipError_t e = hipGetLastError();

@@ -60,6 +60,7 @@ struct IgemmArgs {
                              //   the STORED value is the masked dz, not v
   int res_nt;                // residual is at its last use: stream it (non-temporal loads)
   int c_nt;                  // bf16 output far larger than the Infinity Cache: non-temporal stores
+  int mfma_prio;             // LDS-DMA kernels: s_setprio(1) around each K-step's MFMA cluster
   const uint8_t* res_mask;   // optional ReLU-mask bits ([M][ldc/8]) applied to the residual before the add
                              //   (residual = dy of a BN+residual+ReLU output: dz = dy * relu'(y) on the fly)
   int stats_ld;              // partial columns per channel (0 -> tilesM of this launch)

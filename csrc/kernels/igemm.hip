@@ -695,14 +695,11 @@ DPE_DEVICE void dma16(__amdgpu_buffer_rsrc_t r, char* wave_dst, uint32_t voff, u
 
 template <int N>
 DPE_DEVICE void wait_vm() {
-  static_assert(N >= 0 && N <= 6, "vmcnt");
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  // s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14; expcnt / lgkmcnt left at "no wait")
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+  asm volatile("" ::: "memory");
 }
 
 // WGM x WGN waves, each owning a (BM/WGM) x (BN/WGN) sub-tile; 128x128 (2x2 waves),
@@ -715,7 +712,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (BM == 256 && BN == 128) ? 4 : 1) v
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int CROW = BN * 2 + 16;
-  constexpr int LDS_MAIN = NS * STAGE;
+  constexpr int LDS_MAIN = (NS == 4 ? 3 : NS) * STAGE;
   constexpr int LDS_C = BM * CROW + 2 * NW * BN * 4;
   constexpr int LDS = LDS_MAIN > LDS_C ? LDS_MAIN : LDS_C;
   constexpr int RM = BM / WGM / 16, RN = BN / WGN / 16;
@@ -848,31 +845,73 @@ __global__ __launch_bounds__(64 * WGM * WGN, (BM == 256 && BN == 128) ? 4 : 1) v
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // NS-stage ring: stages t+1 .. t+NS-2 stay in flight while stage t is consumed
-  static_assert(NS == 2 || NS == 3, "2- or 3-stage ring");
-  if (nt > 0) issue(0);
-  if (NS == 3 && nt > 1) issue(1);
-  for (int t = 0; t < nt; ++t) {
-    if (NS == 3 && t + 1 < nt) wait_vm<PA + PB>(); else wait_vm<0>();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (t + NS - 1 < nt) issue((t + NS - 1) % NS);
-    const char* As = smem + (t % NS) * STAGE;
+  auto read_frags = [&](int buf, bf16x8 (&a)[RM], bf16x8 (&b)[RN]) {
+    const char* As = smem + buf * STAGE;
     const char* Bs = As + A_BYTES;
-    bf16x8 af[RM], bfr[RN];
 #pragma unroll
-    for (int i = 0; i < RM; ++i) af[i] = kfrag(As, wm + 16 * i);
+    for (int i = 0; i < RM; ++i) a[i] = kfrag(As, wm + 16 * i);
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
-      if constexpr (BKc) bfr[j] = kfrag(Bs, wn + 16 * j);
-      else bfr[j] = mnfrag<BN>(Bs, wn + 16 * j);
+      if constexpr (BKc) b[j] = kfrag(Bs, wn + 16 * j);
+      else b[j] = mnfrag<BN>(Bs, wn + 16 * j);
     }
+  };
+  auto mfmas = [&](const bf16x8 (&a)[RM], const bf16x8 (&b)[RN]) {
+    if (p.mfma_prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
       for (int j = 0; j < RN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+    if (p.mfma_prio) __builtin_amdgcn_s_setprio(0);
+  };
+  auto barrier = [&]() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  if constexpr (NS == 4) {
+    // 3-buffer ring with fragment double-buffering: the wave reads stage t+1's fragments
+    // while its MFMAs consume stage t (already in registers); DMA runs 3 stages ahead of
+    // the MFMAs (stage t+3 is issued into stage t's buffer, free once every wave's reads
+    // of it retired -- lgkmcnt(0) before the barrier).
+    bf16x8 fa0[RM], fb0[RN], fa1[RM], fb1[RN];
+    if (nt > 0) issue(0);
+    if (nt > 1) issue(1);
+    if (nt > 2) issue(2);
+    if (nt > 2) wait_vm<2 * (PA + PB)>(); else if (nt > 1) wait_vm<PA + PB>(); else wait_vm<0>();
+    barrier();
+    if (nt > 0) read_frags(0, fa0, fb0);
+    auto step = [&](int t, const bf16x8 (&ca)[RM], const bf16x8 (&cb)[RN], bf16x8 (&na)[RM], bf16x8 (&nb)[RN]) {
+      if (t + 1 < nt) {
+        if (t + 2 < nt) wait_vm<PA + PB>(); else wait_vm<0>();  // stage t+1 landed (own DMA)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // own reads of stage t's buffer retired
+        barrier();
+        if (t + 3 < nt) issue((t + 3) % 3);
+        read_frags((t + 1) % 3, na, nb);
+      }
+      mfmas(ca, cb);
+    };
+    int t = 0;
+    for (; t + 1 < nt; t += 2) {
+      step(t, fa0, fb0, fa1, fb1);
+      step(t + 1, fa1, fb1, fa0, fb0);
+    }
+    if (t < nt) step(t, fa0, fb0, fa1, fb1);
+  } else {
+    // NS-stage ring: stages t+1 .. t+NS-2 stay in flight while stage t is consumed
+    static_assert(NS == 2 || NS == 3, "2- or 3-stage ring (4: 3 buffers + fragment prefetch)");
+    if (nt > 0) issue(0);
+    if (NS == 3 && nt > 1) issue(1);
+    for (int t = 0; t < nt; ++t) {
+      if (NS == 3 && t + 1 < nt) wait_vm<PA + PB>(); else wait_vm<0>();
+      barrier();
+      if (t + NS - 1 < nt) issue((t + NS - 1) % NS);
+      bf16x8 af[RM], bfr[RN];
+      read_frags(t % NS, af, bfr);
+      mfmas(af, bfr);
+    }
   }
   __syncthreads();
   if (p.alpha_ptr) p.alpha *= *p.alpha_ptr;
@@ -1017,11 +1056,13 @@ __global__ __launch_bounds__(NT) void igemm_wgrad_dma_kernel(IgemmArgs p) {
     for (int i = 0; i < RM; ++i) af[i] = mnfrag<BM>(As, wm + 16 * i);
 #pragma unroll
     for (int j = 0; j < RN; ++j) bfr[j] = mnfrag<BN>(Bs, wn + 16 * j);
+    if (p.mfma_prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
       for (int j = 0; j < RN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    if (p.mfma_prio) __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();
   if (p.alpha_ptr) p.alpha *= *p.alpha_ptr;
@@ -1100,6 +1141,9 @@ extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int a
   if (bm == BM_ && bn == BN_ && bload == BL_ && epi == EP_) {                                               \
     if (stages == 2)                                                                                        \
       hipLaunchKernelGGL((igemm_dma_kernel<BM_, BN_, WGM_, WGN_, BL_, EP_, 2>), dim3(tiles),                 \
+                         dim3(64 * WGM_ * WGN_), 0, st, a, dn);                                             \
+    else if (stages == 4)                                                                                   \
+      hipLaunchKernelGGL((igemm_dma_kernel<BM_, BN_, WGM_, WGN_, BL_, EP_, 4>), dim3(tiles),                 \
                          dim3(64 * WGM_ * WGN_), 0, st, a, dn);                                             \
     else                                                                                                    \
       hipLaunchKernelGGL((igemm_dma_kernel<BM_, BN_, WGM_, WGN_, BL_, EP_>), dim3(tiles),                    \
