@@ -546,8 +546,11 @@ DPE_DEVICE void epilogue_atomic_f32(const IgemmArgs& p, f32x4 (&acc)[BM / WGM / 
 }
 
 // -------------------------------------------------------------------- kernel
+#ifndef DPE_IGEMM_OCC4
+#define DPE_IGEMM_OCC4 0
+#endif
 template <int BM, int BN, int AL, int BL, int EPI>
-__global__ __launch_bounds__(NT) void igemm_kernel(IgemmArgs p) {
+__global__ __launch_bounds__(NT, DPE_IGEMM_OCC4 ? 4 : 1) void igemm_kernel(IgemmArgs p) {
   constexpr bool AK = IsK<AL>::v;
   constexpr bool BKc = IsBK<BL>::v;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
@@ -705,8 +708,13 @@ DPE_DEVICE void wait_vm() {
 // WGM x WGN waves, each owning a (BM/WGM) x (BN/WGN) sub-tile; 128x128 (2x2 waves),
 // 256x128 (4x2) and 256x256 (2x4).  Bigger tiles cut the L2->LDS bytes per FLOP, which
 // bounds the 128-tile kernel (16 KiB per 256 MFMA-cycles per block).
+#ifndef DPE_DMA_OCC4
+#define DPE_DMA_OCC4 1  // hold the 4-wave tiles to 128 VGPRs: 4 blocks per CU even with the BN epilogue
+                        // (a few epilogue spills; measured 44.2 -> 43.9 ms/step)
+#endif
 template <int BM, int BN, int WGM, int WGN, int BL, int EPI, int NS = DSTAGES>
-__global__ __launch_bounds__(64 * WGM * WGN, (BM == 256 && BN == 128) ? 4 : 1) void igemm_dma_kernel(IgemmArgs p, int a_dense) {
+__global__ __launch_bounds__(64 * WGM * WGN, ((BM == 256 && BN == 128) || (DPE_DMA_OCC4 && WGM * WGN == 4)) ? 4 : 1)
+void igemm_dma_kernel(IgemmArgs p, int a_dense) {
   constexpr int NTH = 64 * WGM * WGN, NW = WGM * WGN;
   constexpr bool BKc = (BL == B_DENSE_K);
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;

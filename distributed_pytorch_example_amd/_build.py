@@ -55,14 +55,28 @@ def _run(cmd):
     return time.time() - t0, p.stdout
 
 
-def build(verbose: bool = True, jobs: int | None = None, force: bool = False) -> str:
+def build_variant(defines, out_name: str, verbose: bool = True) -> str:
+    """Build the extension with extra ``-D`` defines into ``<pkg>/<out_name>`` (own object dir):
+    a compile-time variant for A/B runs, loaded with ``DPE_EXT_SO=<path>``."""
+    global BUILD, OUT
+    saved = BUILD, OUT
+    tag = out_name.replace(".so", "")
+    BUILD, OUT = os.path.join(ROOT, "build", tag), os.path.join(PKG, out_name)
+    try:
+        return build(verbose=verbose, extra_defines=[f"-D{d}" for d in defines])
+    finally:
+        BUILD, OUT = saved
+
+
+def build(verbose: bool = True, jobs: int | None = None, force: bool = False, extra_defines=()) -> str:
     tdir, tinc, tlib = _torch_dirs()
     os.makedirs(BUILD, exist_ok=True)
     hdr = _headers()
     py_inc = sysconfig.get_paths()["include"]
     hip_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     cpp_srcs = sorted(glob.glob(os.path.join(CSRC, "bindings", "*.cpp")) + glob.glob(os.path.join(CSRC, "comm", "*.cpp")))
-    common_defs = ["-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=_C", "-D_GLIBCXX_USE_CXX11_ABI=1"]
+    common_defs = ["-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=_C", "-D_GLIBCXX_USE_CXX11_ABI=1",
+                   *extra_defines]
     jobs = jobs or int(os.environ.get("MAX_JOBS", min(16, os.cpu_count() or 4)))
 
     tasks = []
@@ -75,7 +89,7 @@ def build(verbose: bool = True, jobs: int | None = None, force: bool = False) ->
                           "-ffp-contract=fast", "-munsafe-fp-atomics",
                           # MFMA C/D in arch VGPRs (gfx950 unified file): avoids per-K-step
                           # v_accvgpr_read/write shuffles of the accumulators in the main loops
-                          "-mllvm", "-amdgpu-mfma-vgpr-form",
+                          "-mllvm", "-amdgpu-mfma-vgpr-form", *extra_defines,
                           "-c", src, "-o", obj])
     for src in cpp_srcs:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")

@@ -8,7 +8,9 @@ reference's CPU/gloo configuration and the CPU test suite).
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sys
 
 _C = None
 _err: Exception | None = None
@@ -21,7 +23,14 @@ def _load():
     try:
         import torch  # noqa: F401  (loads torch's HIP/RCCL runtimes first)
 
-        _C = importlib.import_module("distributed_pytorch_example_amd._C")
+        alt = os.environ.get("DPE_EXT_SO")
+        if alt:  # A/B of a compile-time variant (``_build.build_variant``), same module name
+            spec = importlib.util.spec_from_file_location("distributed_pytorch_example_amd._C", alt)
+            _C = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_C)
+            sys.modules["distributed_pytorch_example_amd._C"] = _C
+        else:
+            _C = importlib.import_module("distributed_pytorch_example_amd._C")
     except Exception as e:  # pragma: no cover - exercised only when not built
         if os.environ.get("DPE_AUTOBUILD", "0") == "1":
             from .. import _build
