@@ -118,7 +118,7 @@ def set_wgrad_stream(on: bool) -> bool:
     prev, _WGRAD_STREAM_ON = _WGRAD_STREAM_ON, bool(on)
     return prev
 _aux_streams: dict = {}
-_aux_join_queued = [False]
+_aux_join_gen = [None]  # autograd graph task that already has a join queued
 
 
 def aux_stream(device: torch.device):
@@ -137,7 +137,6 @@ def aux_stream(device: torch.device):
 
 
 def _join_aux():
-    _aux_join_queued[0] = False
     for idx, s in _aux_streams.items():
         torch.cuda.current_stream(idx).wait_stream(s)
 
@@ -156,8 +155,11 @@ def run_on_aux(device: torch.device, fn, *tensors):
     for t in tensors:
         if t is not None:
             t.record_stream(s)
-    if not _aux_join_queued[0]:
-        _aux_join_queued[0] = True
+    # one join per backward pass: keyed on the running graph task (a raised backward
+    # cannot leave a stale "already queued" flag behind)
+    gen = torch._C._current_graph_task_id() if hasattr(torch._C, "_current_graph_task_id") else None
+    if gen is None or gen != _aux_join_gen[0]:
+        _aux_join_gen[0] = gen
         torch.autograd.Variable._execution_engine.queue_callback(_join_aux)
     return out
 
