@@ -50,6 +50,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--optimizer", default=None, choices=[None, "adam", "adamw", "sgd"])
     p.add_argument("--weight-decay", type=float, default=0.0)
     p.add_argument("--bucket-mb", type=float, default=25.0)
+    p.add_argument("--last-bucket-mb", type=float, default=2.0,
+                   help="re-split the last-ready gradient bucket into pieces of at most this size (0: off)")
     p.add_argument("--grad-accum", type=int, default=1)
     p.add_argument("--seed", type=int, default=None, help="seed the synthetic data (reference: unseeded)")
     p.add_argument("--loader", default="auto", choices=["auto", "device", "torch"])
@@ -151,7 +153,7 @@ def main(argv=None):
     logger.info(f"Configuration: epochs={args.epochs}, batch_size={args.batch_size}, lr={args.lr}")
 
     model = get_model(args.model).to(device)
-    model = DDP(model, bucket_cap_mb=args.bucket_mb,
+    model = DDP(model, bucket_cap_mb=args.bucket_mb, last_bucket_mb=args.last_bucket_mb or None,
                 gradient_compression=None if args.gradient_compression == "none" else args.gradient_compression,
                 debug=args.ddp_debug or None)
     if args.roctx:
