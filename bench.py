@@ -24,7 +24,10 @@ import os
 import sys
 import time
 
-import torch
+# RCCL / CUDA-tensor sharing across processes needs dmabuf IPC on this driver
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

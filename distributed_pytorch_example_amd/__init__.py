@@ -7,3 +7,10 @@ RCCL communicator + bucketed reducer overlapped with backward on a side HIP
 stream, and a device-resident data path.
 """
 __version__ = "0.1.0"
+
+import os as _os
+
+# RCCL and cross-process GPU tensor sharing fail on dmabuf-only host drivers
+# (hipIpcGetMemHandle: invalid argument) unless legacy IPC is off; must be set
+# before the HIP runtime initialises.
+_os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
