@@ -218,9 +218,12 @@ int dma_stages(int bm, int bn) {
   return (bm <= 128 && bn <= 128) ? st : 3;
 }
 
+int g_wgrad_dma_force = 0;  // set around linear_wgrad's LDS-DMA arm (dense 1x1 weight grad)
+// linear_wgrad LDS-DMA arm: -1 autotuned, 0 never, 1 always when eligible (tests; A/B via DPE_LWG_DMA)
+int g_lwg_arm = [] { const char* e = getenv("DPE_LWG_DMA"); return e ? atoi(e) : -1; }();
 bool wgrad_dma_dense() {
   static const bool on = [] { const char* e = getenv("DPE_WGRAD_DMA"); return e && e[0] == '2'; }();
-  return on;
+  return on || g_wgrad_dma_force;
 }
 
 // Tile of the LDS-DMA conv kernel: 0 auto, 1 128-tile (pick_cfg), 2 256x128, 3 256x256
@@ -542,6 +545,9 @@ Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const c10::optional<Tenso
 // dw[N,K] (+)= dy[M,N]^T @ x[M,K]   (fp32, atomic split-K; dw must be zeroed or hold an accumulation)
 // dy may be column-padded (row stride ldy >= N, ldy % 8 == 0, pad columns zero): then N need not be a
 // multiple of 8 (vocab-padded LM head: N = 50257, ldy = 50304).
+dpe::ConvGeom geom(const Tensor& x, const Tensor& w, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
+                   int64_t OH, int64_t OW);
+
 void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha, const c10::optional<Tensor>& alpha_t) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(x); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
   const int64_t N = dw.size(0), K = dw.size(1), ldy = dy.size(-1);
@@ -569,7 +575,32 @@ void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha, c
     Tensor tmp;
     auto get_tmp = [&]() -> Tensor& { if (!tmp.defined()) tmp = at::zeros_like(dw); return tmp; };
     const int c = pick_backend(2, N, K, M, a.alpha_ptr ? 2 : 0, [&] { native(get_tmp()); }, [&] { blas(get_tmp()); });
-    if (c == 2) blas(dw);
+    // Third arm: the LDS-DMA split-K weight-grad kernel, reached as a 1x1 conv over a [1, M, 1, K]
+    // image (GPT-2 MLP weight grads: 80 us vs 92 us hipBLASLt, scripts/bench_linear_wgrad.py).
+    auto dma = [&](Tensor& out) {
+      auto b = a;
+      b.g = geom(x2.view({1, M, 1, K}), out.view({N, 1, 1, K}), 1, 1, 0, 0, 1, 1, M, 1);
+      b.C = out.data_ptr();
+      g_wgrad_dma_force = 1;
+      run_igemm(b, dpe::A_DENSE_M, dpe::B_DENSE_N, dpe::EPI_ATOMIC_F32, true, true);
+      g_wgrad_dma_force = 0;
+    };
+    bool use_dma = false;
+    if (ldy == N && !a.alpha_ptr && blas_mode() == 0 && g256_mode() == 0 && igemm_dma_on() && wgrad_dma_on() &&
+        N % 64 == 0 && K % 64 == 0 && M % 64 == 0) {
+      static std::map<std::tuple<int64_t, int64_t, int64_t>, bool> picks;
+      const auto key = std::make_tuple(N, K, M);
+      auto it = picks.find(key);
+      if (it == picks.end() && g_lwg_arm < 0) {
+        auto fd = [&] { dma(get_tmp()); };
+        auto fc = [&] { if (c == 2) blas(get_tmp()); else run_native(c, [&] { native(get_tmp()); }); };
+        const double td = time_ms(fd, 5), tc = time_ms(fc, 5);
+        it = picks.emplace(key, td < 0.97 * tc).first;
+      }
+      use_dma = g_lwg_arm >= 0 ? g_lwg_arm == 1 : it->second;  // (it valid: inserted above when autotuned)
+    }
+    if (use_dma) dma(dw);
+    else if (c == 2) blas(dw);
     else run_native(c, [&] { native(dw); });
   }
 }
@@ -1350,6 +1381,8 @@ void register_ops(pybind11::module& m) {
     return v;
   });
   m.def("set_gemm256_mode", [](int64_t mode) { g_g256_mode = (int)mode; }, "0 auto, 1 off, 2 force (when supported)");
+  m.def("set_linear_wgrad_dma", [](int64_t v) { g_lwg_arm = (int)v; },
+        "linear_wgrad's LDS-DMA weight-grad arm: -1 autotuned (default), 0 off, 1 forced when eligible");
   m.def("set_wgrad_wide", [](int64_t v) { g_wgrad_wide = (int)v; },
         "64x256 tile for Cout = 64 weight grads: 0 off, 1 when C <= 16 (default), 2 always");
   m.def("set_conv_tile", [](int64_t mode) { g_dma_tile = (int)mode; },

@@ -71,6 +71,25 @@ def test_linear_wgrad(C, M, N, K):
     assert rel_err(dw, 1.5 * ref) < 1e-3
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 3072, 768), (2048, 768, 3072), (512, 256, 192)])
+def test_linear_wgrad_lds_dma_arm(C, M, N, K):
+    """linear_wgrad's LDS-DMA split-K arm (a 1x1 conv weight grad), forced on, vs fp32."""
+    torch.manual_seed(3)
+    dy = bf(torch.randn(M, N, device=dev))
+    x = bf(torch.randn(M, K, device=dev))
+    dw = torch.zeros(N, K, device=dev)
+    ref = dy.float().t() @ x.float()
+    C.set_linear_wgrad_dma(1)
+    try:
+        C.linear_wgrad(dy, x, dw, 1.0)
+        torch.cuda.synchronize()
+        assert rel_err(dw, ref) < 1e-3
+        C.linear_wgrad(dy, x, dw, 0.5)
+        assert rel_err(dw, 1.5 * ref) < 1e-3
+    finally:
+        C.set_linear_wgrad_dma(-1)
+
+
 # ------------------------------------------------------------------- conv
 CONV_CASES = [
     # N, H, W, Cin, Cout, k, stride, pad
