@@ -156,6 +156,12 @@ static bool bn_nt_loads() {
   return on;
 }
 
+// BN backward reduce passes with 4 rows in flight per thread (DPE_BN_RED_UNROLL=0: one row)
+static bool bn_red_unroll() {
+  static const bool on = [] { const char* e = getenv("DPE_BN_RED_UNROLL"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 template <int NCOEF>
 struct Coef8 {
   float v[NCOEF][8];
@@ -266,6 +272,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply2_kernel(const uint16_t* __restr
 // With adx: the same pass also applies ANOTHER BatchNorm's backward to the same dz,
 // adx = a*dz + b*ax + c (abcoef [3][C]) -- a bottleneck's BN3 apply fused with its
 // downsample BN's reduce (both are functions of dz3): dz3 is read once.
+template <int U>
 __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
                                                              const uint8_t* __restrict__ ybits,
                                                              const uint16_t* __restrict__ x, const float* __restrict__ coef,
@@ -284,30 +291,52 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const uint16_t* __r
   Coef8<3> ac;
   if (adx) ac.load(abcoef, C, c * 8);
   if (r < RPI) {
-    for (int64_t row = rb + r; row < re; row += RPI) {
-      const int64_t off = row * C + c * 8;
-      float d[8], xv[8];
-      unpack8(*(const u32x4*)(dy + off), d);
-      unpack8(*(const u32x4*)(x + off), xv);
-      if (adx) {
-        float av[8], o[8];
-        unpack8(*(const u32x4*)(ax + off), av);
+    // U rows per thread per iteration, all of their loads issued before the first use
+    // (1024 blocks x 256 threads leave 4 blocks per CU: one row in flight per thread
+    // was latency-bound)
+    for (int64_t row0 = rb + r; row0 < re; row0 += (int64_t)U * RPI) {
+      u32x4 rd[U], rx[U], ra[U], ry[U];
+      uint32_t mbits[U];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = fmaf(ac.v[0][e], d[e], fmaf(ac.v[1][e], av[e], ac.v[2][e]));
-        *(u32x4*)(adx + off) = pack8(o);
-      }
-      if (ybits) {
-        const uint32_t mb = ybits[off >> 3];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) d[e] = ((mb >> e) & 1u) ? d[e] : 0.f;
-      } else if (y) {
-        float yv[8];
-        unpack8(*(const u32x4*)(y + off), yv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+      for (int u = 0; u < U; ++u) {
+        const int64_t row = row0 + (int64_t)u * RPI;
+        if (U == 1 || row < re) {
+          const int64_t off = row * C + c * 8;
+          rd[u] = *(const u32x4*)(dy + off);
+          rx[u] = *(const u32x4*)(x + off);
+          if (adx) ra[u] = *(const u32x4*)(ax + off);
+          if (ybits) mbits[u] = ybits[off >> 3];
+          else if (y) ry[u] = *(const u32x4*)(y + off);
+        }
       }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { s[e] += d[e]; q[e] += d[e] * (xv[e] - mean[e]); }
+      for (int u = 0; u < U; ++u) {
+        const int64_t row = row0 + (int64_t)u * RPI;
+        if (U > 1 && row >= re) break;
+        const int64_t off = row * C + c * 8;
+        float d[8], xv[8];
+        unpack8(rd[u], d);
+        unpack8(rx[u], xv);
+        if (adx) {
+          float av[8], o[8];
+          unpack8(ra[u], av);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = fmaf(ac.v[0][e], d[e], fmaf(ac.v[1][e], av[e], ac.v[2][e]));
+          *(u32x4*)(adx + off) = pack8(o);
+        }
+        if (ybits) {
+          const uint32_t mb = mbits[u];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d[e] = ((mb >> e) & 1u) ? d[e] : 0.f;
+        } else if (y) {
+          float yv[8];
+          unpack8(ry[u], yv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { s[e] += d[e]; q[e] += d[e] * (xv[e] - mean[e]); }
+      }
     }
   }
   __shared__ float red[2][BN_T][8];
@@ -488,8 +517,12 @@ extern "C" int dpe_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const ui
                                  const float* coef, int64_t M, int C, int nb, float* part, hipStream_t st) {
   if (C % 8 || C / 8 > BN_T) return -1;
   const int64_t rpb = (M + nb - 1) / nb;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(BN_T), 0, st, dy, y, ybits, x, coef, M, C, rpb, part,
-                     (const uint16_t*)nullptr, (const float*)nullptr, (uint16_t*)nullptr);
+  if (bn_red_unroll())
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<4>, dim3(nb), dim3(BN_T), 0, st, dy, y, ybits, x, coef, M, C, rpb, part,
+                       (const uint16_t*)nullptr, (const float*)nullptr, (uint16_t*)nullptr);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<1>, dim3(nb), dim3(BN_T), 0, st, dy, y, ybits, x, coef, M, C, rpb, part,
+                       (const uint16_t*)nullptr, (const float*)nullptr, (uint16_t*)nullptr);
   return 0;
 }
 
@@ -499,8 +532,12 @@ extern "C" int dpe_bn_bwd_reduce_apply(const uint16_t* dz, const uint16_t* x, co
                                        hipStream_t st) {
   if (C % 8 || C / 8 > BN_T) return -1;
   const int64_t rpb = (M + nb - 1) / nb;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(BN_T), 0, st, dz, (const uint16_t*)nullptr,
-                     (const uint8_t*)nullptr, x, coef, M, C, rpb, part, ax, abcoef, adx);
+  if (bn_red_unroll())
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<4>, dim3(nb), dim3(BN_T), 0, st, dz, (const uint16_t*)nullptr,
+                       (const uint8_t*)nullptr, x, coef, M, C, rpb, part, ax, abcoef, adx);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<1>, dim3(nb), dim3(BN_T), 0, st, dz, (const uint16_t*)nullptr,
+                       (const uint8_t*)nullptr, x, coef, M, C, rpb, part, ax, abcoef, adx);
   return 0;
 }
 
