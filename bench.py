@@ -52,7 +52,6 @@ def parse():
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--optimizer", default=None)
     ap.add_argument("--lr", type=float, default=None)
-    ap.add_argument("--graph", type=int, default=0, help="capture the step in a hipGraph (1) or run eagerly (0)")
     ap.add_argument("--bucket-timing", action="store_true",
                     help="after the timed steps, one instrumented step: per-bucket all-reduce time and its overlap "
                          "with backward (HIP events on the RCCL stream), reported under 'buckets'")
