@@ -170,6 +170,34 @@ def test_train_e2e_and_resume(tmp_path):
     assert "Epoch 0 completed" in log2 and "Epoch 1 completed" in log2
 
 
+def test_two_simulated_nodes(tmp_path):
+    """Two launcher instances on one host as 2 nodes x 1 process (static rendezvous,
+    --node-rank 0/1, OMP_NUM_THREADS=1 -- SURVEY §4.4 item 2, BASELINE.md §2's
+    unpinned-OMP pitfall): both agents finish and rank 0 logs a 2-process job."""
+    port = str(_port())
+    e = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    procs = []
+    for nr in (0, 1):
+        cmd = [sys.executable, "-m", "distributed_pytorch_example_amd.launch", "--nnodes", "2", "--nproc-per-node", "1",
+               "--node-rank", str(nr), "--master-addr", "127.0.0.1", "--master-port", port,
+               os.path.join(ROOT, "train.py"), "--epochs", "1", "--num-samples", "256",
+               "--checkpoint-dir", str(tmp_path / f"ck{nr}"), "--backend", "gloo"]
+        procs.append(subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=240)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert [p.returncode for p in procs] == [0, 0], outs[0][-1500:] + outs[1][-1500:]
+    assert "Starting distributed training with 2 processes" in outs[0]
+    assert "[Rank 1]" in outs[1]
+    assert os.path.exists(tmp_path / "ck0" / "latest_model.pt")  # only global rank 0 saves
+    assert not os.path.exists(tmp_path / "ck1" / "latest_model.pt")
+
+
 def test_fault_injection_fails_fast(tmp_path):
     r = _launch(["--epochs", "3", "--num-samples", "2048", "--checkpoint-dir", str(tmp_path), "--backend", "gloo"],
                 env={"DPE_FAULT_INJECT": "1:0:3:kill"}, timeout=120)
