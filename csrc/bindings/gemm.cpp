@@ -1,0 +1,183 @@
+// Launch planning for the persistent dense GEMM (csrc/kernels/hgemm.hip).
+//
+// The plan is a pure function of (M, N, K, operand layouts, device CU count):
+// every rank of a DDP job computes the same kernel, tile and K split for the
+// same GEMM without timing anything (no per-rank autotune, no host sync inside
+// a training step).  A small analytic model picks, per shape, the tile
+// (256x256 / 128x256 / 256x128 / 128x128) and the K split:
+//   time = rounds * (unit FLOPs / per-block rate) + fixed prologue/epilogue
+//          + (split > 1) slab traffic + the finalize launch,
+// rounds = ceil(units / (CUs * blocks per CU)).  The per-tile rates are the
+// measured single-shape throughputs of each tile (profiles/hgemm_*), relative
+// to the 256x256 tile.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "../kernels/hgemm.h"
+#include "../kernels/igemm.h"
+#include "gemm_plan.h"
+
+using at::Tensor;
+
+namespace dpe_gemm {
+
+namespace {
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+struct TileCfg { int cfg, bm, bn, bpc; double eff; };
+// eff: per-CU throughput relative to the 256x256 tile with the CU fully occupied
+constexpr TileCfg kTiles[] = {
+    {dpe::HC_256x256, 256, 256, 1, 1.00},
+    {dpe::HC_128x256, 128, 256, 1, 0.70},
+    {dpe::HC_256x128, 256, 128, 1, 0.70},
+    {dpe::HC_128x128, 128, 128, 2, 0.75},
+};
+// per-CU main-loop rate of the 256x256 tile by operand layout (random bf16, 8192^3:
+// NT 1334 / NN 1047 / TN 885 TF on 256 CUs)
+double layout_rate(int ak, int bk) { return ak && bk ? 5.2e12 : (ak ? 4.1e12 : 3.5e12); }
+constexpr double kEpi = 5.0e-11;  // s per output byte per CU: the store tail is issue-bound (~20 GB/s per CU)
+constexpr double kFix = 2.0e-6;   // first prologue + launch
+constexpr double kBw = 4.0e12;    // slab write + finalize read bandwidth
+constexpr double kLaunch = 3.0e-6;
+
+int g_force_cfg = -1, g_force_splits = -1;
+}  // namespace
+
+int num_cus() {
+  static const int n = [] {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceProp_t pr;
+    hipGetDeviceProperties(&pr, dev);
+    return pr.multiProcessorCount > 0 ? pr.multiProcessorCount : 256;
+  }();
+  return n;
+}
+
+bool layout_ok(int cfg, int ak, int bk) {
+  if (ak && bk) return true;
+  if (ak && !bk) return cfg == dpe::HC_256x256 || cfg == dpe::HC_128x256;
+  if (!ak && !bk) return cfg == dpe::HC_256x256;
+  return false;
+}
+
+Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int out_bytes, int force_cfg,
+          int force_splits) {
+  const int ncu = num_cus();
+  const int64_t ktiles = K / 64;
+  Plan best{-1, 1, (int)K, 0, 1e30};
+  if (force_cfg < 0) force_cfg = g_force_cfg;
+  if (force_splits < 0) force_splits = g_force_splits;
+  for (const TileCfg& c : kTiles) {
+    if (force_cfg >= 0 && c.cfg != force_cfg) continue;
+    if (!layout_ok(c.cfg, ak, bk)) continue;
+    const int64_t tiles = ((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
+    const int64_t slots = (int64_t)ncu * c.bpc;
+    const int max_split = allow_split ? 8 : 1;
+    for (int s = 1; s <= max_split; ++s) {
+      if (force_splits > 0 && s != force_splits) continue;
+      const int64_t kt = (ktiles + s - 1) / s;
+      const int64_t se = (ktiles + kt - 1) / kt;  // effective splits (no empty split)
+      if (se != s) continue;
+      if (s > 1 && (kt < 4 || (double)s * M * N * 4 > 2.0e9)) continue;
+      const int64_t units = tiles * s;
+      const int64_t rounds = (units + slots - 1) / slots;
+      const double t_unit = 2.0 * c.bm * c.bn * kt * 64 / (layout_rate(ak, bk) * c.eff / c.bpc) +
+                            kEpi * c.bm * c.bn * (s > 1 ? 4 : out_bytes) * c.bpc;
+      double t = rounds * t_unit + kFix;
+      if (s > 1) t += ((double)s * M * N * 4 * 2 + (double)M * N * out_bytes) / kBw + kLaunch;
+      if (t < best.est_s * 0.995) best = Plan{c.cfg, s, (int)(kt * 64), (int)std::min<int64_t>(units, slots), t};
+    }
+  }
+  return best;
+}
+
+int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_bytes) {
+  TORCH_CHECK(a.K % 64 == 0 && a.K > 0, "hgemm: K must be a positive multiple of 64 (got ", a.K, ")");
+  const Plan pl = plan(a.M, a.N, a.K, ak, bk, allow_split, out_bytes);
+  TORCH_CHECK(pl.cfg >= 0, "hgemm: no tile configuration for M=", a.M, " N=", a.N, " K=", a.K, " layout ", ak, bk);
+  a.splits = pl.splits;
+  a.kps = pl.kps;
+  Tensor ws;
+  if (pl.splits > 1) {
+    ws = at::empty({(int64_t)pl.splits * a.M * a.N}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA));
+    a.ws = (float*)ws.data_ptr();
+    const int rc = dpe_hgemm_launch(&a, pl.cfg, ak, bk, dpe::HE_SLAB, pl.grid, cur_stream());
+    hipError_t e = hipGetLastError();
+    TORCH_CHECK(rc == 0 && e == hipSuccess, "hgemm (split) launch failed rc=", rc, " ", hipGetErrorString(e));
+    const int rf = dpe_hgemm_finalize(&a, epi, cur_stream());
+    e = hipGetLastError();
+    TORCH_CHECK(rf == 0 && e == hipSuccess, "hgemm finalize failed rc=", rf, " ", hipGetErrorString(e));
+    return pl.cfg;
+  }
+  const int rc = dpe_hgemm_launch(&a, pl.cfg, ak, bk, epi, pl.grid, cur_stream());
+  const hipError_t e = hipGetLastError();
+  TORCH_CHECK(rc == 0 && e == hipSuccess, "hgemm launch failed rc=", rc, " ", hipGetErrorString(e));
+  return pl.cfg;
+}
+
+namespace {
+
+// Raw entry for tests and benchmarks: C (M x N, ldc) from A / B with explicit layouts.
+Tensor hgemm_raw(const Tensor& A, const Tensor& B, Tensor C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+                 int64_t ldc, bool ak, bool bk, int64_t epi, int64_t act, const c10::optional<Tensor>& bias,
+                 const c10::optional<Tensor>& residual, const c10::optional<Tensor>& aux_in,
+                 const c10::optional<Tensor>& aux_out, double alpha, int64_t cfg, int64_t splits) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "hgemm: GPU tensors");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "hgemm: bf16 operands");
+  TORCH_CHECK(C.scalar_type() == (epi == dpe::HE_BF16 ? at::kBFloat16 : at::kFloat), "hgemm: output dtype");
+  TORCH_CHECK(A.numel() >= (ak ? M * lda : K * lda) - (ak ? lda - K : lda - M), "hgemm: A too small");
+  TORCH_CHECK(B.numel() >= (bk ? N * ldb : K * ldb) - (bk ? ldb - K : ldb - N), "hgemm: B too small");
+  TORCH_CHECK(C.numel() >= M * ldc - (ldc - N), "hgemm: C too small");
+  dpe::HgemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.A = (const uint16_t*)A.data_ptr(); a.B = (const uint16_t*)B.data_ptr(); a.C = C.data_ptr();
+  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.alpha = (float)alpha; a.act = (int)act;
+  if (bias && bias->defined()) { TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= N); a.bias = (const float*)bias->data_ptr(); }
+  if (residual && residual->defined()) { TORCH_CHECK(residual->scalar_type() == at::kFloat); a.residual_f32 = (const float*)residual->data_ptr(); }
+  if (aux_in && aux_in->defined()) { TORCH_CHECK(aux_in->scalar_type() == at::kBFloat16); a.aux_in = (const uint16_t*)aux_in->data_ptr(); }
+  if (aux_out && aux_out->defined()) { TORCH_CHECK(aux_out->scalar_type() == at::kBFloat16); a.aux_out = (uint16_t*)aux_out->data_ptr(); }
+  TORCH_CHECK(act != dpe::HACT_GELU_BWD || a.aux_in, "hgemm: gelu backward needs aux_in");
+  const int out_bytes = epi == dpe::HE_BF16 ? 2 : 4;
+  const Plan pl = plan(M, N, K, ak, bk, splits != 1, out_bytes, (int)cfg, (int)splits);
+  TORCH_CHECK(pl.cfg >= 0, "hgemm: no configuration (cfg=", cfg, " splits=", splits, ")");
+  a.splits = pl.splits;
+  a.kps = pl.kps;
+  Tensor ws;
+  if (pl.splits > 1) {
+    ws = at::empty({(int64_t)pl.splits * M * N}, A.options().dtype(at::kFloat));
+    a.ws = (float*)ws.data_ptr();
+    int rc = dpe_hgemm_launch(&a, pl.cfg, ak, bk, dpe::HE_SLAB, pl.grid, cur_stream());
+    TORCH_CHECK(rc == 0 && hipGetLastError() == hipSuccess, "hgemm split launch rc=", rc);
+    rc = dpe_hgemm_finalize(&a, (int)epi, cur_stream());
+    TORCH_CHECK(rc == 0 && hipGetLastError() == hipSuccess, "hgemm finalize rc=", rc);
+  } else {
+    const int rc = dpe_hgemm_launch(&a, pl.cfg, ak, bk, (int)epi, pl.grid, cur_stream());
+    TORCH_CHECK(rc == 0 && hipGetLastError() == hipSuccess, "hgemm launch rc=", rc);
+  }
+  return C;
+}
+
+}  // namespace
+
+void register_gemm(pybind11::module& m) {
+  namespace py = pybind11;
+  m.def("hgemm", &hgemm_raw, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("M"), py::arg("N"), py::arg("K"),
+        py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("a_k"), py::arg("b_k"), py::arg("epi") = 0,
+        py::arg("act") = 0, py::arg("bias") = py::none(), py::arg("residual") = py::none(), py::arg("aux_in") = py::none(),
+        py::arg("aux_out") = py::none(), py::arg("alpha") = 1.0, py::arg("cfg") = -1, py::arg("splits") = -1,
+        "persistent MFMA GEMM with explicit layouts (cfg / splits -1: planner's choice)");
+  m.def("hgemm_plan", [](int64_t M, int64_t N, int64_t K, bool ak, bool bk, bool allow_split, int64_t out_bytes) {
+          const Plan p = plan(M, N, K, ak, bk, allow_split, (int)out_bytes);
+          return std::make_tuple(p.cfg, p.splits, p.kps, p.grid, p.est_s * 1e6);
+        }, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("a_k"), py::arg("b_k"), py::arg("allow_split") = true,
+        py::arg("out_bytes") = 2, "the planner's (cfg, splits, k per split, grid, estimated us) for a GEMM");
+  m.def("set_hgemm_force", [](int64_t cfg, int64_t splits) { g_force_cfg = (int)cfg; g_force_splits = (int)splits; },
+        py::arg("cfg") = -1, py::arg("splits") = -1, "pin the planner's tile / split (-1: free); A/B testing only");
+}
+
+}  // namespace dpe_gemm

@@ -1,0 +1,25 @@
+// Deterministic launch planning of the persistent GEMM (bindings/gemm.cpp).
+#pragma once
+#include <stdint.h>
+
+#include "../kernels/hgemm.h"
+
+namespace dpe_gemm {
+
+struct Plan {
+  int cfg;       // dpe::HCfg, -1 if none fits
+  int splits;    // K splits (> 1: fp32 slabs + finalize)
+  int kps;       // K elements per split
+  int grid;      // persistent workgroups
+  double est_s;  // modelled time
+};
+
+int num_cus();
+bool layout_ok(int cfg, int ak, int bk);
+// out_bytes: bytes per output element of the final epilogue (slab traffic estimate)
+Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int out_bytes, int force_cfg = -1,
+          int force_splits = -1);
+// Plans, allocates the split workspace if any and launches; returns the tile configuration used.
+int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_bytes);
+
+}  // namespace dpe_gemm

@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 
 #include "../kernels/igemm.h"
+#include "../kernels/hgemm.h"
+#include "gemm_plan.h"
 
 using at::Tensor;
 
@@ -144,57 +146,6 @@ Cfg pick_cfg(int64_t M, int64_t N, int64_t K, bool allow_split) {
   return c;
 }
 
-// Large dense GEMMs go to the 256-tile LDS-DMA kernel when the shape fills
-// the chip (>= 192 tiles, or split-K for atomic weight-grads).  Mode:
-// 0 auto, 1 never (A/B testing, DPE_GEMM256=0), 2 always when supported.
-int g_g256_mode = -1;
-int g256_mode() {
-  if (g_g256_mode < 0) {
-    const char* e = getenv("DPE_GEMM256");
-    g_g256_mode = (e && e[0] == '0') ? 1 : (e && e[0] == '2') ? 2 : 0;
-  }
-  return g_g256_mode;
-}
-
-int g_g256_override = -1;  // set by the per-shape autotuner: 0 off, 1 force
-
-bool try_gemm256(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_split) {
-  int mode = g256_mode();
-  if (g_g256_override == 0) return false;
-  if (g_g256_override == 1 && mode != 1) mode = 2;
-  if (mode == 1) return false;
-  int ak, bk;
-  if (aload == dpe::A_DENSE_K && bload == dpe::B_DENSE_K) { ak = 1; bk = 1; }
-  else if (aload == dpe::A_DENSE_K && bload == dpe::B_DENSE_N) { ak = 1; bk = 0; }
-  else if (aload == dpe::A_DENSE_M && bload == dpe::B_DENSE_N) { ak = 0; bk = 0; }
-  else return false;
-  if (!ak && epi == dpe::EPI_BF16) return false;
-  if (a.K % 64 || a.K == 0 || a.col_stats || (a.act != 0 && a.act != 2)) return false;
-  if (a.lda % 8 || a.ldb % 8 || (!bk && a.N % 8) || (!ak && a.M % 8)) return false;
-  // 32-bit per-lane source offsets
-  const int64_t abytes = (ak ? (int64_t)a.M * a.lda : (int64_t)a.K * a.lda) * 2;
-  const int64_t bbytes = (bk ? (int64_t)a.N * a.ldb : (int64_t)a.K * a.ldb) * 2;
-  if (abytes >= (1ll << 32) || bbytes >= (1ll << 32)) return false;
-  const int64_t tiles = ((a.M + 255) / 256) * ((int64_t)(a.N + 255) / 256);
-  const int64_t ktiles = a.K / 64;
-  int64_t splits = 1;
-  if (epi == dpe::EPI_ATOMIC_F32 && allow_split) {
-    // fill >= 1.5 waves of 256 CUs, keep >= 8 K-tiles (512) per split
-    splits = std::max<int64_t>(1, std::min<int64_t>((384 + tiles - 1) / tiles, ktiles / 8));
-  }
-  // tile-quantisation waste: the 256x256 tile must be >= 75 % useful
-  if (mode == 0 && ((double)a.M * a.N < 0.75 * 65536.0 * tiles || tiles * splits < 192)) return false;
-  const int64_t kps = (ktiles + splits - 1) / splits;
-  splits = (ktiles + kps - 1) / kps;
-  a.k_split = (int)(kps * 64);
-  const int rc = dpe_gemm256_launch(&a, ak, bk, epi, (int)splits, cur_stream());
-  const hipError_t e = hipGetLastError();
-  TORCH_CHECK(e == hipSuccess, "gemm256 launch failed: ", hipGetErrorString(e));
-  return rc == 0;
-}
-
-// conv_*: the 128-tile kernel measured faster than the 256-tile one on every
-// ResNet-50 1x1 shape (small K / N), so convolutions opt out of it unless forced.
 // DPE_IGEMM_DMA=0: forward-form convolutions stay on the register-staged kernel (A/B reference)
 bool igemm_dma_on() {
   static const bool on = [] { const char* e = getenv("DPE_IGEMM_DMA"); return !(e && e[0] == '0'); }();
@@ -218,12 +169,10 @@ int dma_stages(int bm, int bn) {
   return (bm <= 128 && bn <= 128) ? st : 3;
 }
 
-int g_wgrad_dma_force = 0;  // set around linear_wgrad's LDS-DMA arm (dense 1x1 weight grad)
-// linear_wgrad LDS-DMA arm: -1 autotuned, 0 never, 1 always when eligible (tests; A/B via DPE_LWG_DMA)
-int g_lwg_arm = [] { const char* e = getenv("DPE_LWG_DMA"); return e ? atoi(e) : -1; }();
+// DPE_WGRAD_DMA=2: dense 1x1 weight grads on the LDS-DMA kernel too (measured 10-15 % slower; A/B only)
 bool wgrad_dma_dense() {
   static const bool on = [] { const char* e = getenv("DPE_WGRAD_DMA"); return e && e[0] == '2'; }();
-  return on || g_wgrad_dma_force;
+  return on;
 }
 
 // Tile of the LDS-DMA conv kernel: 0 auto, 1 128-tile (pick_cfg), 2 256x128, 3 256x256
@@ -271,7 +220,6 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
   if (conv && (epi == dpe::EPI_BF16 || epi == dpe::EPI_BF16_BNB) && epi_nt_store() &&
       (int64_t)a.M * a.ldc * 2 > (320ll << 20))
     a.c_nt = 1;
-  if ((!conv || g_g256_override == 1 || g256_mode() == 2) && try_gemm256(a, aload, bload, epi, allow_split)) return;
   Cfg c = pick_cfg(a.M, a.N, a.K, allow_split && epi == dpe::EPI_ATOMIC_F32);
   a.k_split = c.k_split;
   // weight grads over an im2col B (3x3 / strided; split-K fp32 atomics): LDS-DMA kernel, measured 1.3-1.5x
@@ -343,78 +291,25 @@ dpe::IgemmArgs base_args() {
 }
 
 
-// ------------------------------------------------ vendor-library arm (plain GEMMs)
-// A GEMM whose epilogue the library can express exactly (no activation, no
-// fp32 residual stream, no BN statistics) is autotuned once per shape between
-// our MFMA kernels and hipBLASLt (through ATen): both run a few times into
-// scratch outputs, timed with HIP events, and the faster one is cached.
-// DPE_GEMM_BACKEND = auto (default) | native | blas.
-int g_blas_mode = -1;  // 0 auto, 1 native only, 2 blas whenever eligible
-int blas_mode() {
-  if (g_blas_mode < 0) {
-    const char* e = getenv("DPE_GEMM_BACKEND");
-    const std::string v = e ? e : "auto";
-    g_blas_mode = v == "native" ? 1 : v == "blas" ? 2 : 0;
-  }
-  return g_blas_mode;
-}
-std::map<std::tuple<int, int64_t, int64_t, int64_t, int>, int> g_blas_choice;
-
-template <class F>
-double time_ms(F& f, int reps) {
-  hipStream_t st = cur_stream();
-  hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
-  f();  // warm-up (first-call library heuristics, caches)
-  hipEventRecord(e0, st);
-  for (int i = 0; i < reps; ++i) f();
-  hipEventRecord(e1, st);
-  hipEventSynchronize(e1);
-  float ms = 0.f;
-  hipEventElapsedTime(&ms, e0, e1);
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  return ms / reps;
-}
-
-// kind: 0 fwd, 1 dgrad, 2 wgrad, 3 fwd+f32 residual.  Returns 0 = native 128-tile
-// igemm, 1 = native 256-tile LDS-DMA kernel, 2 = library.  native/blas write
-// into a scratch output while being timed.
-template <class FN, class FB>
-int pick_backend(int kind, int64_t M, int64_t N, int64_t K, int flags, FN&& native_into_scratch,
-                 FB&& blas_into_scratch) {
-  const int mode = blas_mode();
-  if (mode == 2) return 2;
-  if (mode == 1 || g256_mode() != 0) return g256_mode() == 2 ? 1 : (g256_mode() == 1 ? 0 : -1);
-  auto key = std::make_tuple(kind, M, N, K, flags);
-  auto it = g_blas_choice.find(key);
-  if (it != g_blas_choice.end()) return it->second;
-  g_g256_override = 0;
-  const double t0 = time_ms(native_into_scratch, 3);
-  g_g256_override = 1;
-  const double t1 = time_ms(native_into_scratch, 3);
-  g_g256_override = -1;
-  const double t2 = time_ms(blas_into_scratch, 3);
-  int best = t1 < t0 ? 1 : 0;
-  const double tn = std::min(t0, t1);
-  if (t2 < 0.97 * tn) best = 2;
-  g_blas_choice[key] = best;
-  return best;
-}
-
-// run the native arm with the autotuner's tile choice (-1 = heuristic)
-template <class F>
-void run_native(int choice, F&& f) {
-  g_g256_override = choice == 0 ? 0 : choice == 1 ? 1 : -1;
-  f();
-  g_g256_override = -1;
-}
-
 // -------------------------------------------------------------- dense GEMMs
-// y[M,N] = act(x[M,K] @ w[N,K]^T + bias) (+ residual)
+// Every Linear GEMM runs on our MFMA kernels: the persistent hgemm kernel
+// (csrc/kernels/hgemm.hip; tile / K split from the deterministic planner in
+// bindings/gemm.cpp, identical on every rank, no timing) whenever the shape is
+// inside its envelope (K % 64, 16-B aligned rows, N % 8 for bf16 outputs), and
+// the 128-tile implicit-GEMM kernel otherwise (SimpleNet's K = 784 input, odd
+// classifier widths).  There is no vendor-library arm.
+dpe::HgemmArgs hargs() {
+  dpe::HgemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.alpha = 1.f;
+  a.splits = 1;
+  return a;
+}
+
+// y[M,N] = act(x[M,K] @ w[N,K]^T + bias) (+ residual);  aux_out (act = GELU): pre-activation v
 Tensor linear_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, int64_t act, bool out_f32,
-                  const c10::optional<Tensor>& residual, const c10::optional<Tensor>& out) {
+                  const c10::optional<Tensor>& residual, const c10::optional<Tensor>& out,
+                  const c10::optional<Tensor>& aux_out) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(w);
   TORCH_CHECK(x.stride(-1) == 1, "x must have unit inner stride");
   const int64_t K = x.size(-1), N = w.size(0);
@@ -432,6 +327,30 @@ Tensor linear_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>&
   } else {
     y = at::empty(sizes, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
   }
+  const bool has_aux = aux_out.has_value() && aux_out->defined();
+  if (has_aux) {
+    TORCH_CHECK(act == dpe::ACT_GELU && !out_f32, "linear: aux_out (pre-activation) is for bf16 GELU outputs");
+    CHECK_BF16((*aux_out)); CHECK_CONTIG((*aux_out));
+    TORCH_CHECK(aux_out->numel() == M * N, "linear: aux_out shape mismatch");
+  }
+  const bool bf16_res = residual.has_value() && residual->defined() && !out_f32;
+  if (K % 64 == 0 && N % 8 == 0 && !bf16_res && (out_f32 ? act == 0 : true)) {
+    auto a = hargs();
+    a.A = bp(x2); a.B = bp(w); a.C = y.data_ptr();
+    a.M = (int)M; a.N = (int)N; a.K = (int)K;
+    a.lda = x2.stride(0); a.ldb = K; a.ldc = N;
+    a.bias = fpo(bias);
+    a.act = (int)act;
+    if (has_aux) a.aux_out = bpm(*aux_out);
+    if (out_f32 && residual.has_value() && residual->defined()) {
+      CHECK_F32((*residual)); CHECK_CONTIG((*residual));
+      TORCH_CHECK(residual->numel() == M * N, "residual shape mismatch");
+      a.residual_f32 = (const float*)residual->data_ptr();
+    }
+    dpe_gemm::run(a, 1, 1, out_f32 ? dpe::HE_F32 : dpe::HE_BF16, true, out_f32 ? 4 : 2);
+    return y;
+  }
+  TORCH_CHECK(!has_aux, "linear: aux_out needs K % 64 == 0 and N % 8 == 0");
   auto a = base_args();
   a.A = bp(x2); a.B = bp(w); a.C = y.data_ptr();
   a.M = (int)M; a.N = (int)N; a.K = (int)K;
@@ -449,55 +368,14 @@ Tensor linear_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>&
       a.residual = bp(*residual);
     }
   }
-  const bool plain = !out_f32 && act == 0 && !a.residual;
-  if (plain) {
-    Tensor y2 = y.view({M, N});
-    Tensor bb = bias.has_value() && bias->defined() ? bias->to(at::kBFloat16) : Tensor();
-    auto blas = [&](Tensor& out) {
-      if (bb.defined()) at::addmm_out(out, bb, x2, w.t());
-      else at::mm_out(out, x2, w.t());
-    };
-    auto native = [&](Tensor& out) {
-      auto b = a;
-      b.C = out.data_ptr();
-      run_igemm(b, dpe::A_DENSE_K, dpe::B_DENSE_K, dpe::EPI_BF16, false);
-    };
-    Tensor tmp;
-    auto get_tmp = [&]() -> Tensor& { if (!tmp.defined()) tmp = at::empty_like(y2); return tmp; };
-    const int c = pick_backend(0, M, N, K, bb.defined(), [&] { native(get_tmp()); }, [&] { blas(get_tmp()); });
-    if (c == 2) blas(y2);
-    else run_native(c, [&] { native(y2); });
-    return y;
-  }
-  if (out_f32 && act == 0 && a.residual_f32) {
-    // x + (x_in @ w^T + b) on the fp32 residual stream: library arm = fp32-out addmm onto the residual
-    Tensor y2 = y.view({M, N});
-    Tensor res2 = residual->view({M, N});
-    auto blas = [&](Tensor& out) {
-      at::addmm_out(out, res2, x2, w.t(), at::kFloat);
-      if (bias.has_value() && bias->defined()) out.add_(*bias);
-    };
-    auto native = [&](Tensor& out) {
-      auto b = a;
-      b.C = out.data_ptr();
-      run_igemm(b, dpe::A_DENSE_K, dpe::B_DENSE_K, dpe::EPI_F32, false);
-    };
-    const bool aliased = y.data_ptr() == residual->data_ptr();
-    Tensor tmp;
-    auto get_tmp = [&]() -> Tensor& { if (!tmp.defined()) tmp = at::empty_like(y2); return tmp; };
-    const int c = aliased ? 0 : pick_backend(3, M, N, K, bias.has_value() && bias->defined(), [&] { native(get_tmp()); },
-                                             [&] { blas(get_tmp()); });
-    if (c == 2) blas(y2);
-    else run_native(c, [&] { native(y2); });
-    return y;
-  }
   run_igemm(a, dpe::A_DENSE_K, dpe::B_DENSE_K, out_f32 ? dpe::EPI_F32 : dpe::EPI_BF16, false);
   return y;
 }
 
-// dx[M,K] = dy[M,N] @ w[N,K]
+// dx[M,K] = dy[M,N] @ w[N,K]  (alpha_t: device scalar; gelu_in: dx *= gelu'(gelu_in), the
+// backward of a GELU whose pre-activation gelu_in [M,K] produced this layer's input)
 Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const c10::optional<Tensor>& residual,
-                    const c10::optional<Tensor>& alpha_t) {
+                    const c10::optional<Tensor>& alpha_t, const c10::optional<Tensor>& gelu_in) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(dy);
   const int64_t N = w.size(0), K = w.size(1);
   TORCH_CHECK(dy.size(-1) == N, "linear_dgrad: shape mismatch");
@@ -506,43 +384,34 @@ Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const c10::optional<Tenso
   auto sizes = dy.sizes().vec();
   sizes.back() = K;
   Tensor dx = at::empty(sizes, dy.options());
+  const bool has_res = residual.has_value() && residual->defined();
+  const bool has_gelu = gelu_in.has_value() && gelu_in->defined();
+  if (has_gelu) {
+    CHECK_BF16((*gelu_in)); CHECK_CONTIG((*gelu_in));
+    TORCH_CHECK(gelu_in->numel() == M * K, "linear_dgrad: gelu_in shape mismatch");
+  }
+  if (N % 64 == 0 && !has_res) {
+    auto a = hargs();
+    a.A = bp(dy); a.B = bp(w); a.C = dx.data_ptr();
+    a.M = (int)M; a.N = (int)K; a.K = (int)N;
+    a.lda = N; a.ldb = K; a.ldc = K;
+    a.alpha_ptr = alpha_ptr_of(alpha_t);
+    if (has_gelu) { a.act = dpe::HACT_GELU_BWD; a.aux_in = bp(*gelu_in); }
+    dpe_gemm::run(a, 1, 0, dpe::HE_BF16, true, 2);
+    return dx;
+  }
+  TORCH_CHECK(!has_gelu, "linear_dgrad: gelu_in needs out_features % 64 == 0 and no residual");
   auto a = base_args();
   a.A = bp(dy); a.B = bp(w); a.C = dx.data_ptr();
   a.M = (int)M; a.N = (int)K; a.K = (int)N;
   a.lda = N; a.ldb = K; a.ldc = K;
-  if (residual.has_value() && residual->defined()) { CHECK_BF16((*residual)); CHECK_CONTIG((*residual)); a.residual = bp(*residual); }
+  if (has_res) { CHECK_BF16((*residual)); CHECK_CONTIG((*residual)); a.residual = bp(*residual); }
   a.alpha_ptr = alpha_ptr_of(alpha_t);
-  {
-    Tensor dy2 = dy.reshape({M, N}), dx2 = dx.view({M, K});
-    Tensor res2 = a.residual ? residual->reshape({M, K}) : Tensor();
-    auto blas = [&](Tensor& out) {
-      if (res2.defined()) at::addmm_out(out, res2, dy2, w);
-      else at::mm_out(out, dy2, w);
-      if (a.alpha_ptr) {
-        TORCH_CHECK(!res2.defined(), "linear_dgrad: alpha_t with residual unsupported on the library arm");
-        out.mul_(*alpha_t);
-      }
-    };
-    auto native = [&](Tensor& out) {
-      auto b = a;
-      b.C = out.data_ptr();
-      run_igemm(b, dpe::A_DENSE_K, dpe::B_DENSE_N, dpe::EPI_BF16, false);
-    };
-    Tensor tmp;
-    auto get_tmp = [&]() -> Tensor& { if (!tmp.defined()) tmp = at::empty_like(dx2); return tmp; };
-    const bool ok = !(a.alpha_ptr && res2.defined());
-    const int c = ok ? pick_backend(1, M, K, N, (res2.defined() ? 1 : 0) | (a.alpha_ptr ? 2 : 0), [&] { native(get_tmp()); },
-                                    [&] { blas(get_tmp()); })
-                     : -1;
-    if (c == 2) blas(dx2);
-    else run_native(c, [&] { native(dx2); });
-    return dx;
-  }
   run_igemm(a, dpe::A_DENSE_K, dpe::B_DENSE_N, dpe::EPI_BF16, false);
   return dx;
 }
 
-// dw[N,K] (+)= dy[M,N]^T @ x[M,K]   (fp32, atomic split-K; dw must be zeroed or hold an accumulation)
+// dw[N,K] (+)= alpha * dy[M,N]^T @ x[M,K]   (fp32 accumulate into dw, e.g. a DDP bucket view).
 // dy may be column-padded (row stride ldy >= N, ldy % 8 == 0, pad columns zero): then N need not be a
 // multiple of 8 (vocab-padded LM head: N = 50257, ldy = 50304).
 dpe::ConvGeom geom(const Tensor& x, const Tensor& w, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
@@ -554,55 +423,25 @@ void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha, c
   TORCH_CHECK(ldy >= N && x.size(-1) == K && dy.numel() / ldy == x.numel() / K, "linear_wgrad: shape mismatch");
   TORCH_CHECK(ldy % 8 == 0 && K % 8 == 0, "linear_wgrad: dy row stride and in_features must be multiples of 8");
   const int64_t M = dy.numel() / ldy;
+  if (M % 64 == 0) {
+    // TN: A = dy^T (M-contiguous, loads may read dy's zero pad columns up to ldy), B = x (N-contiguous)
+    auto a = hargs();
+    a.A = bp(dy); a.B = bp(x); a.C = dw.data_ptr();
+    a.M = (int)N; a.N = (int)K; a.K = (int)M;
+    a.lda = ldy; a.ldb = K; a.ldc = K;
+    a.a_dim = (int)((N + 7) / 8 * 8);
+    a.alpha = (float)alpha;
+    a.alpha_ptr = alpha_ptr_of(alpha_t);
+    dpe_gemm::run(a, 0, 0, dpe::HE_ACC_F32, true, 4);
+    return;
+  }
   auto a = base_args();
   a.A = bp(dy); a.B = bp(x); a.C = dw.data_ptr();
   a.M = (int)N; a.N = (int)K; a.K = (int)M;
   a.lda = ldy; a.ldb = K; a.ldc = K;
   a.alpha = (float)alpha;
   a.alpha_ptr = alpha_ptr_of(alpha_t);
-  {
-    Tensor dyT = dy.reshape({M, ldy}).narrow(1, 0, N).t();
-    Tensor x2 = x.reshape({M, K});
-    auto blas = [&](Tensor& out) {
-      Tensor xs = a.alpha_ptr ? (x2 * *alpha_t).to(at::kBFloat16) : x2;  // device-scalar scale folded into the small operand
-      at::addmm_out(out, out, dyT, xs, at::kFloat, 1.0, alpha);
-    };
-    auto native = [&](Tensor& out) {
-      auto b = a;
-      b.C = out.data_ptr();
-      run_igemm(b, dpe::A_DENSE_M, dpe::B_DENSE_N, dpe::EPI_ATOMIC_F32, true);
-    };
-    Tensor tmp;
-    auto get_tmp = [&]() -> Tensor& { if (!tmp.defined()) tmp = at::zeros_like(dw); return tmp; };
-    const int c = pick_backend(2, N, K, M, a.alpha_ptr ? 2 : 0, [&] { native(get_tmp()); }, [&] { blas(get_tmp()); });
-    // Third arm: the LDS-DMA split-K weight-grad kernel, reached as a 1x1 conv over a [1, M, 1, K]
-    // image (GPT-2 MLP weight grads: 80 us vs 92 us hipBLASLt, scripts/bench_linear_wgrad.py).
-    auto dma = [&](Tensor& out) {
-      auto b = a;
-      b.g = geom(x2.view({1, M, 1, K}), out.view({N, 1, 1, K}), 1, 1, 0, 0, 1, 1, M, 1);
-      b.C = out.data_ptr();
-      g_wgrad_dma_force = 1;
-      run_igemm(b, dpe::A_DENSE_M, dpe::B_DENSE_N, dpe::EPI_ATOMIC_F32, true, true);
-      g_wgrad_dma_force = 0;
-    };
-    bool use_dma = false;
-    if (ldy == N && !a.alpha_ptr && blas_mode() == 0 && g256_mode() == 0 && igemm_dma_on() && wgrad_dma_on() &&
-        N % 64 == 0 && K % 64 == 0 && M % 64 == 0) {
-      static std::map<std::tuple<int64_t, int64_t, int64_t>, bool> picks;
-      const auto key = std::make_tuple(N, K, M);
-      auto it = picks.find(key);
-      if (it == picks.end() && g_lwg_arm < 0) {
-        auto fd = [&] { dma(get_tmp()); };
-        auto fc = [&] { if (c == 2) blas(get_tmp()); else run_native(c, [&] { native(get_tmp()); }); };
-        const double td = time_ms(fd, 5), tc = time_ms(fc, 5);
-        it = picks.emplace(key, td < 0.97 * tc).first;
-      }
-      use_dma = g_lwg_arm >= 0 ? g_lwg_arm == 1 : it->second;  // (it valid: inserted above when autotuned)
-    }
-    if (use_dma) dma(dw);
-    else if (c == 2) blas(dw);
-    else run_native(c, [&] { native(dw); });
-  }
+  run_igemm(a, dpe::A_DENSE_M, dpe::B_DENSE_N, dpe::EPI_ATOMIC_F32, true);
 }
 
 // ------------------------------------------------------------------- conv
@@ -1303,9 +1142,10 @@ void register_ops(pybind11::module& m) {
   namespace py = pybind11;
   using c10::optional;
   m.def("linear_fwd", &linear_fwd, py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("act") = 0,
-        py::arg("out_f32") = false, py::arg("residual") = py::none(), py::arg("out") = py::none());
+        py::arg("out_f32") = false, py::arg("residual") = py::none(), py::arg("out") = py::none(),
+        py::arg("aux_out") = py::none());
   m.def("linear_dgrad", &linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("residual") = py::none(),
-        py::arg("alpha_t") = py::none());
+        py::arg("alpha_t") = py::none(), py::arg("gelu_in") = py::none());
   m.def("linear_wgrad", &linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("alpha") = 1.0,
         py::arg("alpha_t") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
@@ -1371,18 +1211,9 @@ void register_ops(pybind11::module& m) {
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("H"), py::arg("scale"), py::arg("causal") = true);
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("H"),
         py::arg("scale"), py::arg("causal") = true);
-  m.def("set_gemm_backend", [](int64_t mode) { g_blas_mode = (int)mode; g_blas_choice.clear(); },
-        "0 auto (per-shape autotune vs hipBLASLt), 1 native kernels only, 2 library whenever eligible");
-  m.def("gemm_backend_choices", []() {
-    std::vector<std::tuple<int, int64_t, int64_t, int64_t, int, int>> v;
-    for (auto& kv : g_blas_choice)
-      v.emplace_back(std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first), std::get<3>(kv.first),
-                     std::get<4>(kv.first), kv.second);
-    return v;
-  });
-  m.def("set_gemm256_mode", [](int64_t mode) { g_g256_mode = (int)mode; }, "0 auto, 1 off, 2 force (when supported)");
-  m.def("set_linear_wgrad_dma", [](int64_t v) { g_lwg_arm = (int)v; },
-        "linear_wgrad's LDS-DMA weight-grad arm: -1 autotuned (default), 0 off, 1 forced when eligible");
+  m.def("set_gemm_backend", [](int64_t mode) {
+          TORCH_CHECK(mode == 1, "only the native MFMA GEMM backend exists (mode 1); the vendor-library arm was removed");
+        }, "kept for API compatibility: 1 = native kernels (the only backend)");
   m.def("set_wgrad_wide", [](int64_t v) { g_wgrad_wide = (int)v; },
         "64x256 tile for Cout = 64 weight grads: 0 off, 1 when C <= 16 (default), 2 always");
   m.def("set_conv_tile", [](int64_t mode) { g_dma_tile = (int)mode; },

@@ -1,0 +1,53 @@
+// Host-visible argument block of the persistent dense GEMM (hgemm.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dpe {
+
+// Epilogue of one output tile (or K-split partial of it).
+enum HEpi : int {
+  HE_BF16 = 0,    // C bf16 = act(alpha*acc + bias)           (ACT_GELU: aux_out = pre-activation v)
+  HE_F32 = 1,     // C f32  = alpha*acc + bias (+ residual_f32)
+  HE_ACC_F32 = 2, // C f32 += alpha*acc                       (weight grads into fp32 buckets; no K split)
+  HE_SLAB = 3,    // ws[split] f32 = acc (K-split partial; hgemm_finalize applies the real epilogue)
+};
+// act values beyond igemm.h's Act: gelu backward, C = (alpha*acc) * gelu'(aux_in)
+constexpr int HACT_GELU_BWD = 3;
+
+struct HgemmArgs {
+  const uint16_t* A;        // bf16, K-contiguous A[m][k] (lda) or M-contiguous A[k][m] (lda)
+  const uint16_t* B;        // bf16, K-contiguous B[n][k] (ldb) or N-contiguous B[k][n] (ldb)
+  void* C;                  // output (ldc)
+  const float* bias;        // [N] or nullptr
+  const float* residual_f32;// HE_F32: [M][ldc] added to the result (may alias C)
+  const uint16_t* aux_in;   // HACT_GELU_BWD: pre-activation v, bf16 [M][ldc]
+  uint16_t* aux_out;        // HE_BF16 + ACT_GELU: v stored here, bf16 [M][ldc] (nullptr: not stored)
+  float* ws;                // HE_SLAB: [splits][M][N] f32 partials
+  const float* alpha_ptr;   // optional device scalar multiplied into alpha
+  int M, N, K;
+  int64_t lda, ldb, ldc;
+  float alpha;
+  int act;                  // ACT_NONE / ACT_GELU / HACT_GELU_BWD
+  int splits;               // K splits (HE_SLAB when > 1)
+  int kps;                  // K elements per split, multiple of 64
+  int a_dim, b_dim;         // load extents of A's M / B's N (>= M / N; 0 = M / N): loads may read the
+                            // zero-padded columns of a padded operand, stores stay inside M x N
+};
+
+// Tile configurations (BMxBN, waves WRxWC).
+enum HCfg : int {
+  HC_256x256 = 0,  // 8 waves 2x4, 128 KiB LDS, 1 block/CU
+  HC_128x256 = 1,  // 8 waves 2x4,  96 KiB LDS, 1 block/CU
+  HC_256x128 = 2,  // 8 waves 4x2,  96 KiB LDS, 1 block/CU
+  HC_128x128 = 3,  // 4 waves 2x2,  64 KiB LDS, 2 blocks/CU
+};
+
+}  // namespace dpe
+
+// a_k / b_k: operand K-contiguous (1) or M/N-contiguous (0).  grid = persistent block count.
+// Returns 0, or < 0 when the configuration is outside the kernel's envelope.
+extern "C" int dpe_hgemm_launch(const dpe::HgemmArgs* args, int cfg, int a_k, int b_k, int epi, int grid,
+                                hipStream_t stream);
+// Sum of `splits` f32 partial slabs [M][N] -> the real epilogue (bias, act, residual, bf16/f32 out).
+extern "C" int dpe_hgemm_finalize(const dpe::HgemmArgs* args, int epi, hipStream_t stream);

@@ -1,0 +1,640 @@
+// Persistent dense bf16 GEMM for gfx950 (the transformer Linear path: GPT-2
+// projections / MLP / LM head, fwd "NT", dgrad "NN", wgrad "TN").
+//
+// Replaces ATen addmm/mm (hipBLASLt) behind the reference's nn.Linear
+// (/root/reference/train.py:39,42,45).  Design, MI355X-first:
+//
+//  * one workgroup per CU (two for the 128x128 tile) walks a list of work
+//    units (output tile x K-split); tile order is XCD-aware (consecutive
+//    logical units run on one XCD and share A rows / B columns in its L2);
+//  * main loop = LDS-DMA (global_load_lds_dwordx4) into "half images" with a
+//    4-phase-per-K-tile schedule: each phase ds_reads one accumulator
+//    quadrant's fragments, restages one half image two phases after its last
+//    read, and runs that quadrant's MFMA cluster (16x16x32 bf16) between raw
+//    s_barriers under s_setprio(1); one counted vmcnt per K-tile keeps the two
+//    newest half-images in flight across the barrier; the second half of the
+//    waves runs one barrier behind (ping-pong: one wave per SIMD in MFMA while
+//    its partner issues reads/DMA) -- cdna_hip_programming.md §5 T1-T5;
+//  * epilogue straight from the accumulators (no LDS): its math runs first,
+//    then the NEXT unit's prologue DMA is issued, then the stores -- the store
+//    drain overlaps the next tile's first loads instead of serialising;
+//  * fused epilogues: bias, GELU with the pre-activation kept (aux_out),
+//    GELU-backward multiply (aux_in), fp32 residual add, fp32 accumulate into
+//    gradient buckets, fp32 K-split partial slabs (+ hgemm_finalize).
+//
+// Layout conventions (D^T issue: every lane holds 4 consecutive output columns):
+//   A: K-contiguous A[m][k] or M-contiguous A[k][m];  B: K-contiguous B[n][k] or N-contiguous B[k][n]
+//   fwd   y = x w^T   : A K, B K      dgrad dx = dy w : A K, B N      wgrad dw = dy^T x : A M, B N
+//
+// Half images: the wave grid is WR x WC; wave (wr, wc) owns tile rows
+// wr*(BM/WR) + [0, BM/WR) and columns wc*(BN/WC) + [0, BN/WC), each split in
+// two halves (RH rows / CH columns).  A half image h holds rows
+// {wr*(BM/WR) + h*RH + [0,RH)} of every wr, B half h columns {wc*(BN/WC) +
+// h*CH + [0,CH)} of every wc, so one phase-quadrant of every wave reads exactly
+// one A half and one B half.  K images are [rows][64 k] (128-B rows, chunk ^=
+// (row>>1)&7); M/N-contiguous images are [64 k][128] (256-B rows, read with
+// ds_read_b64_tr_b16).  LDS-DMA writes lane-linearly, so the swizzle is applied
+// to the per-lane SOURCE address and undone on the read.
+#include "common.h"
+#include "igemm.h"
+#include "hgemm.h"
+
+namespace dpe {
+namespace hg {
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int TK = 64;
+
+// Main-loop schedule: 1 (default) = reads retired before each phase's first barrier, restage one
+// phase after the last read, three half images in flight across the per-K-tile wait;
+// 0 = round-1 gemm256 schedule (restage two phases after, two half images in flight).
+#ifndef HG_SCHED
+#define HG_SCHED 1
+#endif
+
+template <int BM, int BN, int WR, int WC>
+struct Geo {
+  static constexpr int NW = WR * WC, NT = NW * 64;
+  static constexpr int RH = BM / WR / 2, CH = BN / WC / 2;  // rows / columns per wave per half
+  static constexpr int FMH = RH / 16, FNH = CH / 16;        // 16x16 fragments per wave per half
+  static constexpr int AHB = BM * 64, BHB = BN * 64;        // bytes per half image (dim/2 x 64 k x 2 B)
+  static constexpr int GA = AHB / 1024 / NW, GB = BHB / 1024 / NW;  // 1-KiB DMA pieces per wave per half
+  static constexpr int B_REGION = 4 * AHB;
+  static constexpr int LDS = 4 * (AHB + BHB);
+  static constexpr int NKEEP = GA + GB;  // DMA instructions left in flight by the per-K-tile wait
+  static_assert(GA >= 1 && GB >= 1 && GA * NW * 1024 == AHB && GB * NW * 1024 == BHB, "piece split");
+  static_assert(FMH >= 1 && FNH >= 1, "fragments");
+};
+
+DPE_DEVICE int kswz(int row) { return (row >> 1) & 7; }
+DPE_DEVICE int mnswz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+
+// half-image index -> tile row / column
+template <int D, int W, int HH>
+DPE_DEVICE int hmap(int h, int r) { return (r / HH) * (D / W) + h * HH + (r % HH); }
+
+template <int N>
+DPE_DEVICE void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+  asm volatile("" ::: "memory");
+}
+
+DPE_DEVICE void glds(const char* src, char* dst) {
+  __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 16, 0, 0);
+}
+
+// K-image fragment read, rows r0 + [0,16), k-step s
+DPE_DEVICE int kread_off(int r0, int s) {
+  const int lane = threadIdx.x & 63;
+  const int row = r0 + (lane & 15), ch = s * 4 + (lane >> 4);
+  return row * 128 + ((ch ^ kswz(row)) << 4);
+}
+// MN-image fragment read, columns c0 + [0,16), k-step 0 (k-step 1 = +8192)
+DPE_DEVICE int mnread_off(int c0) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int k1 = 8 * g + q;
+  const int mc = (c0 >> 3) + (pp >> 1), sub = (pp & 1) * 8;
+  return k1 * 256 + ((mc ^ mnswz(k1)) << 4) + sub;
+}
+DPE_DEVICE bf16x8 lds_b128(const char* a) { return __builtin_bit_cast(bf16x8, *(const u32x4*)a); }
+DPE_DEVICE bf16x8 lds_tr(const char* a) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + 1024));  // rows k1 + 4
+  s16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// per-lane LDS-DMA source offsets (bytes, 32-bit) of one operand's two half images
+template <int D, int W, int HH, int NG, bool KC>
+DPE_DEVICE void stage_setup(int64_t ld, int dim, int d0, int kb, uint32_t (&g)[2][NG]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const int pc = wid * NG + i;  // this lane's 1-KiB piece of the half image
+      if constexpr (KC) {
+        const int r = 8 * pc + (lane >> 3);
+        const int gr = min(d0 + hmap<D, W, HH>(h, r), dim - 1);
+        const int ch = (lane & 7) ^ kswz(r);
+        g[h][i] = (uint32_t)(((int64_t)gr * ld + kb + ch * 8) * 2);
+      } else {
+        const int k = 4 * pc + (lane >> 4);
+        const int c = (lane & 15) ^ mnswz(k);
+        const int gc = min(d0 + hmap<D, W, HH>(h, c * 8), dim - 8);
+        g[h][i] = (uint32_t)(((int64_t)(kb + k) * ld + gc) * 2);
+      }
+    }
+}
+
+#define HG_BARRIER()                   \
+  do {                                 \
+    asm volatile("" ::: "memory");     \
+    __builtin_amdgcn_s_barrier();      \
+    asm volatile("" ::: "memory");     \
+  } while (0)
+
+DPE_DEVICE float gelu_fwd(float x) {
+  // 0.5 x (1 + tanh(u)) == x / (1 + exp(-2u)),  u = sqrt(2/pi) (x + 0.044715 x^3)
+  const float u2 = -1.5957691216057308f * (x + 0.044715f * x * x * x);
+  return x * __builtin_amdgcn_rcpf(1.f + __expf(u2));
+}
+DPE_DEVICE float gelu_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  // tanh(u) = 1 - 2 / (1 + exp(2u)) (exp overflow -> t = 1, underflow -> t = -1)
+  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * k0 * (x + k1 * x * x * x)));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+}
+
+template <int BM, int BN, int WR, int WC, bool AK, bool BK, int EPI, int ACT>
+__global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
+  using G = Geo<BM, BN, WR, WC>;
+  constexpr int NW = G::NW, RH = G::RH, CH = G::CH, FMH = G::FMH, FNH = G::FNH, GA = G::GA, GB = G::GB;
+  constexpr int AHB = G::AHB, BHB = G::BHB;
+  static_assert(AK || BM == 256, "M-contiguous A needs 128-column half images (BM = 256)");
+  static_assert(BK || BN == 256, "N-contiguous B needs 128-column half images (BN = 256)");
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid / WC, wc = wid % WC;
+  const bool late = NW == 8 && wid >= 4;  // second-dispatched half runs one barrier behind
+  const int tilesM = (p.M + BM - 1) / BM, tilesN = (p.N + BN - 1) / BN;
+  const int ntile = tilesM * tilesN, nunits = ntile * p.splits;
+  int u = xcd_remap(blockIdx.x, gridDim.x);
+  if (u >= nunits) return;
+  const float alpha = p.alpha * (p.alpha_ptr ? *p.alpha_ptr : 1.f);
+
+  const char* const Ab = (const char*)p.A;
+  const char* const Bb = (const char*)p.B;
+  const int64_t astep = AK ? (int64_t)TK * 2 : (int64_t)TK * p.lda * 2;
+  const int64_t bstep = BK ? (int64_t)TK * 2 : (int64_t)TK * p.ldb * 2;
+  char* const wdA = smem + wid * GA * 1024;             // this wave's pieces in every A half image
+  char* const wdB = smem + G::B_REGION + wid * GB * 1024;
+
+  // fragment-read lane offsets
+  int ra[FMH][2], rb[FNH][2];
+#pragma unroll
+  for (int i = 0; i < FMH; ++i)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) ra[i][s] = AK ? kread_off(wr * RH + i * 16, s) : mnread_off(wr * RH + i * 16) + s * 8192;
+#pragma unroll
+  for (int j = 0; j < FNH; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      rb[j][s] = G::B_REGION + (BK ? kread_off(wc * CH + j * 16, s) : mnread_off(wc * CH + j * 16) + s * 8192);
+
+  uint32_t ga[2][GA], gb[2][GB];
+  int m0, n0, kb, nt, split;
+  auto decode = [&](int uu) {
+    const int tile = uu % ntile;
+    split = uu / ntile;
+    m0 = (tile / tilesN) * BM;
+    n0 = (tile % tilesN) * BN;
+    kb = split * p.kps;
+    nt = (min(p.K, kb + p.kps) - kb) / TK;
+    stage_setup<BM, WR, RH, GA, AK>(p.lda, p.a_dim > 0 ? p.a_dim : p.M, m0, AK ? kb : 0, ga);
+    stage_setup<BN, WC, CH, GB, BK>(p.ldb, p.b_dim > 0 ? p.b_dim : p.N, n0, BK ? kb : 0, gb);
+    if constexpr (!AK) { for (int h = 0; h < 2; ++h) for (int i = 0; i < GA; ++i) ga[h][i] += (uint32_t)((int64_t)kb * p.lda * 2); }
+    if constexpr (!BK) { for (int h = 0; h < 2; ++h) for (int i = 0; i < GB; ++i) gb[h][i] += (uint32_t)((int64_t)kb * p.ldb * 2); }
+  };
+
+#define STAGE_A(h, buf, t)                                                                   \
+  do {                                                                                       \
+    const char* b_ = Ab + (int64_t)(t) * astep;                                              \
+    _Pragma("unroll") for (int i_ = 0; i_ < GA; ++i_)                                        \
+      glds(b_ + ga[h][i_], wdA + ((buf) * 2 + (h)) * AHB + i_ * 1024);                       \
+  } while (0)
+#define STAGE_B(h, buf, t)                                                                   \
+  do {                                                                                       \
+    const char* b_ = Bb + (int64_t)(t) * bstep;                                              \
+    _Pragma("unroll") for (int i_ = 0; i_ < GB; ++i_)                                        \
+      glds(b_ + gb[h][i_], wdB + ((buf) * 2 + (h)) * BHB + i_ * 1024);                       \
+  } while (0)
+#if HG_SCHED == 1
+  // tile 0 -> buf 0 (all halves), tile 1 -> buf 1 (A0, B1, A1; B0(1) is staged in tile 0's phase 1)
+#define PROLOGUE()                                                                           \
+  do {                                                                                       \
+    STAGE_A(0, 0, 0); STAGE_B(0, 0, 0); STAGE_B(1, 0, 0); STAGE_A(1, 0, 0);                  \
+    if (nt > 1) { STAGE_A(0, 1, 1); STAGE_B(1, 1, 1); STAGE_A(1, 1, 1); }                    \
+  } while (0)
+#else
+#define PROLOGUE()                                                                           \
+  do {                                                                                       \
+    STAGE_A(0, 0, 0); STAGE_B(1, 0, 0); STAGE_A(1, 0, 0); STAGE_B(0, 0, 0);                  \
+    if (nt > 1) { STAGE_A(0, 1, 1); STAGE_B(1, 1, 1); }                                      \
+  } while (0)
+#endif
+
+  f32x4 acc[2 * FMH][2 * FNH];
+  bf16x8 af[FMH][2], bfr[FNH][2];
+
+#define LOAD_A(buf, h)                                                                       \
+  do {                                                                                       \
+    _Pragma("unroll") for (int i_ = 0; i_ < FMH; ++i_)                                       \
+      _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_) {                                     \
+        const char* a_ = smem + ((buf) * 2 + (h)) * AHB + ra[i_][s_];                        \
+        af[i_][s_] = AK ? lds_b128(a_) : lds_tr(a_);                                         \
+      }                                                                                      \
+  } while (0)
+#define LOAD_B(buf, h)                                                                       \
+  do {                                                                                       \
+    _Pragma("unroll") for (int j_ = 0; j_ < FNH; ++j_)                                       \
+      _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_) {                                     \
+        const char* a_ = smem + ((buf) * 2 + (h)) * BHB + rb[j_][s_];                        \
+        bfr[j_][s_] = BK ? lds_b128(a_) : lds_tr(a_);                                        \
+      }                                                                                      \
+  } while (0)
+#define QUAD(mh, nh)                                                                         \
+  do {                                                                                       \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                       \
+    MFMAQ(mh, nh);                                                                           \
+  } while (0)
+#define MFMAQ(mh, nh)                                                                        \
+  do {                                                                                       \
+    __builtin_amdgcn_s_setprio(1);                                                           \
+    _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_)                                         \
+      _Pragma("unroll") for (int i_ = 0; i_ < FMH; ++i_)                                     \
+        _Pragma("unroll") for (int j_ = 0; j_ < FNH; ++j_)                                   \
+          acc[(mh) * FMH + i_][(nh) * FNH + j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(   \
+              bfr[j_][s_], af[i_][s_], acc[(mh) * FMH + i_][(nh) * FNH + j_], 0, 0, 0);      \
+    __builtin_amdgcn_s_setprio(0);                                                           \
+  } while (0)
+
+  decode(u);
+  PROLOGUE();
+  wait_vm<0>();
+  HG_BARRIER();
+
+  const int lm = lane & 15, ln4 = (lane >> 4) * 4;
+  while (true) {
+#pragma unroll
+    for (int i = 0; i < 2 * FMH; ++i)
+#pragma unroll
+      for (int j = 0; j < 2 * FNH; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (late) HG_BARRIER();
+
+#if HG_SCHED == 1
+    // One K-tile per iteration, buffer b = t & 1.  Every phase retires its own
+    // fragment reads (lgkmcnt(0)) BEFORE its first barrier, so a half image can
+    // be restaged one phase after its last read: P1 B0(t+1)->b^1, P2 A0(t+2)->b,
+    // P3 B1(t+2)->b, P4 A1(t+2)->b.  Phase 4's counted vmcnt retires B0(t+1)
+    // and everything older and leaves three half images (A0/B1/A1 of t+2) in
+    // flight across the barrier.
+    for (int t = 0; t < nt; ++t) {
+      const int b = t & 1;
+      const bool h1 = t + 1 < nt, h2 = t + 2 < nt;
+
+      LOAD_A(b, 0); LOAD_B(b, 0);
+      if (h1) STAGE_B(0, b ^ 1, t + 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      HG_BARRIER();
+      MFMAQ(0, 0);
+      HG_BARRIER();
+
+      LOAD_B(b, 1);
+      if (h2) STAGE_A(0, b, t + 2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      HG_BARRIER();
+      MFMAQ(0, 1);
+      HG_BARRIER();
+
+      LOAD_A(b, 1);
+      if (h2) STAGE_B(1, b, t + 2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      HG_BARRIER();
+      MFMAQ(1, 1);
+      HG_BARRIER();
+
+      LOAD_B(b, 0);
+      if (h2) {
+        STAGE_A(1, b, t + 2);
+        wait_vm<2 * GA + GB>();
+      } else {
+        wait_vm<0>();
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      HG_BARRIER();
+      MFMAQ(1, 0);
+      HG_BARRIER();
+    }
+#else
+    // One K-tile per iteration, buffer b = t & 1.  Phase p restages one half
+    // image: A1(t+1)->b^1, B0(t+1)->b^1, A0(t+2)->b, B1(t+2)->b; each target was
+    // last read two phases earlier, and phase 4's counted vmcnt retires tile t+1.
+    for (int t = 0; t < nt; ++t) {
+      const int b = t & 1;
+      const bool h1 = t + 1 < nt, h2 = t + 2 < nt;
+
+      LOAD_A(b, 0); LOAD_B(b, 0);
+      if (h1) STAGE_A(1, b ^ 1, t + 1);
+      HG_BARRIER();
+      QUAD(0, 0);
+      HG_BARRIER();
+
+      LOAD_B(b, 1);
+      if (h1) STAGE_B(0, b ^ 1, t + 1);
+      HG_BARRIER();
+      QUAD(0, 1);
+      HG_BARRIER();
+
+      LOAD_A(b, 1);
+      if (h2) STAGE_A(0, b, t + 2);
+      HG_BARRIER();
+      QUAD(1, 1);
+      HG_BARRIER();
+
+      LOAD_B(b, 0);
+      if (h2) {
+        STAGE_B(1, b, t + 2);
+        wait_vm<G::NKEEP>();
+      } else {
+        wait_vm<0>();
+      }
+      HG_BARRIER();
+      QUAD(1, 0);
+      HG_BARRIER();
+    }
+#endif
+    if (!late) HG_BARRIER();  // rebalance the stagger: every wave is past its last LDS read
+
+    // ------------------------------------------------------------ epilogue
+    // acc[i][j][e]: row m0 + wr*(BM/WR) + (i/FMH)*RH + (i%FMH)*16 + lm,
+    //               col n0 + wc*(BN/WC) + (j/FNH)*CH + (j%FNH)*16 + ln4 + e
+    const int rbase = m0 + wr * (BM / WR) + lm, cbase = n0 + wc * (BN / WC) + ln4;
+    const int next = u + gridDim.x;
+    const int cur_split = split;
+
+    // 1) math (every global load of the epilogue happens here, before any DMA is in flight)
+    u32x2 pk[2 * FMH][2 * FNH];
+    u32x2 pv[(EPI == HE_BF16 && ACT == ACT_GELU) ? 2 * FMH : 1][(EPI == HE_BF16 && ACT == ACT_GELU) ? 2 * FNH : 1];
+    if constexpr (EPI == HE_BF16) {
+      f32x4 bias[2 * FNH];
+#pragma unroll
+      for (int j = 0; j < 2 * FNH; ++j) {
+        const int c = cbase + (j / FNH) * CH + (j % FNH) * 16;
+        bias[j] = (p.bias && c < p.N) ? *(const f32x4*)(p.bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int i = 0; i < 2 * FMH; ++i) {
+        const int r = min(rbase + (i / FMH) * RH + (i % FMH) * 16, p.M - 1);
+#pragma unroll
+        for (int j = 0; j < 2 * FNH; ++j) {
+          const int c = cbase + (j / FNH) * CH + (j % FNH) * 16;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = alpha * acc[i][j][e] + bias[j][e];
+          if constexpr (ACT == ACT_GELU) {
+            pv[i][j][0] = pack_bf2(v[0], v[1]);
+            pv[i][j][1] = pack_bf2(v[2], v[3]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = gelu_fwd(v[e]);
+          } else if constexpr (ACT == HACT_GELU_BWD) {
+            const u32x2 a = c < p.N ? *(const u32x2*)(p.aux_in + (int64_t)r * p.ldc + c) : u32x2{0u, 0u};
+            v[0] *= gelu_grad(__uint_as_float(a[0] << 16));
+            v[1] *= gelu_grad(__uint_as_float(a[0] & 0xffff0000u));
+            v[2] *= gelu_grad(__uint_as_float(a[1] << 16));
+            v[3] *= gelu_grad(__uint_as_float(a[1] & 0xffff0000u));
+          } else if constexpr (ACT == ACT_RELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
+          pk[i][j][0] = pack_bf2(v[0], v[1]);
+          pk[i][j][1] = pack_bf2(v[2], v[3]);
+        }
+        if constexpr (ACT == HACT_GELU_BWD) __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (EPI == HE_F32) {
+      f32x4 bias[2 * FNH];
+#pragma unroll
+      for (int j = 0; j < 2 * FNH; ++j) {
+        const int c = cbase + (j / FNH) * CH + (j % FNH) * 16;
+        bias[j] = (p.bias && c < p.N) ? *(const f32x4*)(p.bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int i = 0; i < 2 * FMH; ++i) {
+        const int r = min(rbase + (i / FMH) * RH + (i % FMH) * 16, p.M - 1);
+#pragma unroll
+        for (int j = 0; j < 2 * FNH; ++j) {
+          const int c = cbase + (j / FNH) * CH + (j % FNH) * 16;
+          f32x4 res = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (p.residual_f32 && c < p.N) res = *(const f32x4*)(p.residual_f32 + (int64_t)r * p.ldc + c);
+          // stored right away (holding 128 fp32 results across the next prologue spills)
+          if (c < p.N && rbase + (i / FMH) * RH + (i % FMH) * 16 < p.M)
+            *(f32x4*)((float*)p.C + (int64_t)r * p.ldc + c) = acc[i][j] * alpha + bias[j] + res;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (EPI == HE_ACC_F32) {
+#pragma unroll
+      for (int i = 0; i < 2 * FMH; ++i) {
+        const int r = min(rbase + (i / FMH) * RH + (i % FMH) * 16, p.M - 1);
+#pragma unroll
+        for (int j = 0; j < 2 * FNH; ++j) {
+          const int c = cbase + (j / FNH) * CH + (j % FNH) * 16;
+          f32x4 old = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (c < p.N) old = *(const f32x4*)((const float*)p.C + (int64_t)r * p.ldc + c);
+          if (c < p.N && rbase + (i / FMH) * RH + (i % FMH) * 16 < p.M)
+            *(f32x4*)((float*)p.C + (int64_t)r * p.ldc + c) = acc[i][j] * alpha + old;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+
+    // 2) the next unit's prologue DMA (LDS is free: every wave passed the rebalance barrier)
+    if (next < nunits) {
+      u = next;
+      decode(u);
+      PROLOGUE();
+    }
+
+    // 3) stores (drain while the prologue loads are in flight)
+    if constexpr (EPI == HE_BF16) {
+      // Widened to 16 B per lane (T21 with a 16-lane exchange): fragments i, i+1 (rows r, r+16) hold
+      // columns 4g..4g+3 in lane group g; v_permlane16_swap gives even groups row r's columns
+      // 8(g/2)..+7 and odd groups row r+16's, so every lane stores 8 consecutive bf16 -- half the
+      // store instructions of the 8-B form (the epilogue tail is store-issue-bound).
+      const int g = lane >> 4;
+      const int c_off = (g >> 1) * 8 - ln4;  // this lane's 8-column chunk relative to cbase
+#pragma unroll
+      for (int i = 0; i < 2 * FMH; i += 2) {
+        const int r = rbase + (i / FMH) * RH + (i % FMH) * 16 + (g & 1) * 16;
+#pragma unroll
+        for (int j = 0; j < 2 * FNH; ++j) {
+          const int c = cbase + (j / FNH) * CH + (j % FNH) * 16 + c_off;
+          u32x2 a = pk[i][j], b = pk[i + 1][j];
+          auto x = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+          auto y = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+          if (r < p.M && c < p.N) *(u32x4*)((uint16_t*)p.C + (int64_t)r * p.ldc + c) = u32x4{x[0], y[0], x[1], y[1]};
+          if constexpr (ACT == ACT_GELU) {
+            u32x2 va = pv[i][j], vb = pv[i + 1][j];
+            auto vx = __builtin_amdgcn_permlane16_swap(va[0], vb[0], false, false);
+            auto vy = __builtin_amdgcn_permlane16_swap(va[1], vb[1], false, false);
+            if (p.aux_out && r < p.M && c < p.N)
+              *(u32x4*)(p.aux_out + (int64_t)r * p.ldc + c) = u32x4{vx[0], vy[0], vx[1], vy[1]};
+          }
+        }
+      }
+    } else if constexpr (EPI == HE_SLAB) {
+#pragma unroll
+      for (int i = 0; i < 2 * FMH; ++i) {
+        const int r = rbase + (i / FMH) * RH + (i % FMH) * 16;
+        if (r >= p.M) continue;
+#pragma unroll
+        for (int j = 0; j < 2 * FNH; ++j) {
+          const int c = cbase + (j / FNH) * CH + (j % FNH) * 16;
+          if (c < p.N) *(f32x4*)(p.ws + ((int64_t)cur_split * p.M + r) * p.N + c) = acc[i][j];
+        }
+      }
+    }
+    if (next >= nunits) break;
+    wait_vm<0>();
+    HG_BARRIER();
+  }
+#undef STAGE_A
+#undef STAGE_B
+#undef PROLOGUE
+#undef LOAD_A
+#undef LOAD_B
+#undef QUAD
+#undef MFMAQ
+}
+
+// sum of K-split partial slabs -> the real epilogue; one thread per 4 output columns
+template <int EPI, int ACT>
+__global__ __launch_bounds__(256) void hgemm_finalize_kernel(HgemmArgs p) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int nq = p.N >> 2;
+  if (q >= (int64_t)p.M * nq) return;
+  const int r = (int)(q / nq), c = (int)(q % nq) * 4;
+  const float alpha = p.alpha * (p.alpha_ptr ? *p.alpha_ptr : 1.f);
+  const int64_t plane = (int64_t)p.M * p.N;
+  f32x4 s = *(const f32x4*)(p.ws + (int64_t)r * p.N + c);
+  for (int k = 1; k < p.splits; ++k) s += *(const f32x4*)(p.ws + k * plane + (int64_t)r * p.N + c);
+  s *= alpha;
+  if (p.bias) s += *(const f32x4*)(p.bias + c);
+  const int64_t o = (int64_t)r * p.ldc + c;
+  if constexpr (EPI == HE_BF16) {
+    float v[4] = {s[0], s[1], s[2], s[3]};
+    if constexpr (ACT == ACT_GELU) {
+      if (p.aux_out) *(u32x2*)(p.aux_out + o) = u32x2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = gelu_fwd(v[e]);
+    } else if constexpr (ACT == HACT_GELU_BWD) {
+      const u32x2 a = *(const u32x2*)(p.aux_in + o);
+      v[0] *= gelu_grad(__uint_as_float(a[0] << 16));
+      v[1] *= gelu_grad(__uint_as_float(a[0] & 0xffff0000u));
+      v[2] *= gelu_grad(__uint_as_float(a[1] << 16));
+      v[3] *= gelu_grad(__uint_as_float(a[1] & 0xffff0000u));
+    } else if constexpr (ACT == ACT_RELU) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    *(u32x2*)((uint16_t*)p.C + o) = u32x2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+  } else if constexpr (EPI == HE_F32) {
+    if (p.residual_f32) s += *(const f32x4*)(p.residual_f32 + o);
+    *(f32x4*)((float*)p.C + o) = s;
+  } else {  // HE_ACC_F32
+    *(f32x4*)((float*)p.C + o) = s + *(const f32x4*)((const float*)p.C + o);
+  }
+}
+
+}  // namespace hg
+}  // namespace dpe
+
+using namespace dpe;
+
+namespace {
+
+template <int BM, int BN, int WR, int WC, bool AK, bool BK>
+int launch_epi(const HgemmArgs& p, int epi, int grid, hipStream_t st) {
+  const dim3 g((unsigned)grid), b(WR * WC * 64);
+#define HL(E, A) hipLaunchKernelGGL((hg::hgemm_kernel<BM, BN, WR, WC, AK, BK, E, A>), g, b, 0, st, p)
+  if (epi == HE_SLAB) {  // raw partials: the activation belongs to hgemm_finalize
+    HL(HE_SLAB, ACT_NONE);
+  } else if (epi == HE_BF16) {
+    if (p.act == ACT_NONE) HL(HE_BF16, ACT_NONE);
+    else if (p.act == ACT_GELU) HL(HE_BF16, ACT_GELU);
+    else if (p.act == HACT_GELU_BWD) HL(HE_BF16, HACT_GELU_BWD);
+    else if (p.act == ACT_RELU) HL(HE_BF16, ACT_RELU);
+    else return -3;
+  } else if (p.act != ACT_NONE) {
+    return -3;
+  } else if (epi == HE_F32) {
+    HL(HE_F32, ACT_NONE);
+  } else if (epi == HE_ACC_F32) {
+    HL(HE_ACC_F32, ACT_NONE);
+  } else {
+    return -2;
+  }
+#undef HL
+  return 0;
+}
+
+template <int BM, int BN, int WR, int WC>
+int launch_layout(const HgemmArgs& p, int a_k, int b_k, int epi, int grid, hipStream_t st) {
+  if (a_k && b_k) return launch_epi<BM, BN, WR, WC, true, true>(p, epi, grid, st);
+  if constexpr (BN == 256) {
+    if (a_k && !b_k) return launch_epi<BM, BN, WR, WC, true, false>(p, epi, grid, st);
+    if constexpr (BM == 256) {
+      if (!a_k && !b_k) return launch_epi<BM, BN, WR, WC, false, false>(p, epi, grid, st);
+    }
+  }
+  return -2;
+}
+
+}  // namespace
+
+extern "C" int dpe_hgemm_launch(const HgemmArgs* a, int cfg, int a_k, int b_k, int epi, int grid, hipStream_t st) {
+  const HgemmArgs& p = *a;
+  if (p.K % 64 || p.kps % 64 || p.kps <= 0 || p.N % 4 || grid <= 0) return -1;
+  if (epi == HE_BF16 && (p.N % 8 || p.ldc % 8)) return -1;  // 16-B output chunks
+  if (p.splits < 1 || (p.splits > 1 && epi != HE_SLAB)) return -1;
+  const int adim = p.a_dim > 0 ? p.a_dim : p.M, bdim = p.b_dim > 0 ? p.b_dim : p.N;
+  if (adim < p.M || bdim < p.N) return -1;
+  if (!a_k && (adim % 8 || p.lda < adim)) return -1;  // M-contiguous A: 16-B chunks of 8 rows
+  if (!b_k && (bdim % 8 || p.ldb < bdim)) return -1;
+  if (p.lda % 8 || p.ldb % 8) return -1;
+  // per-lane LDS-DMA source offsets are 32-bit
+  if ((a_k ? (int64_t)adim * p.lda : (int64_t)p.K * p.lda) * 2 >= (1ll << 32)) return -4;
+  if ((b_k ? (int64_t)bdim * p.ldb : (int64_t)p.K * p.ldb) * 2 >= (1ll << 32)) return -4;
+  switch (cfg) {
+    case HC_256x256: return launch_layout<256, 256, 2, 4>(p, a_k, b_k, epi, grid, st);
+    case HC_128x256: return launch_layout<128, 256, 2, 4>(p, a_k, b_k, epi, grid, st);
+    case HC_256x128: return launch_layout<256, 128, 4, 2>(p, a_k, b_k, epi, grid, st);
+    case HC_128x128: return launch_layout<128, 128, 2, 2>(p, a_k, b_k, epi, grid, st);
+    default: return -1;
+  }
+}
+
+extern "C" int dpe_hgemm_finalize(const HgemmArgs* a, int epi, hipStream_t st) {
+  const HgemmArgs& p = *a;
+  if (p.N % 4) return -1;
+  const int64_t n = (int64_t)p.M * (p.N / 4);
+  const dim3 g((unsigned)((n + 255) / 256)), b(256);
+#define FL(E, A) hipLaunchKernelGGL((hg::hgemm_finalize_kernel<E, A>), g, b, 0, st, p)
+  if (epi == HE_BF16) {
+    if (p.act == ACT_NONE) FL(HE_BF16, ACT_NONE);
+    else if (p.act == ACT_GELU) FL(HE_BF16, ACT_GELU);
+    else if (p.act == HACT_GELU_BWD) FL(HE_BF16, HACT_GELU_BWD);
+    else if (p.act == ACT_RELU) FL(HE_BF16, ACT_RELU);
+    else return -3;
+  } else if (p.act != ACT_NONE) {
+    return -3;
+  } else if (epi == HE_F32) {
+    FL(HE_F32, ACT_NONE);
+  } else if (epi == HE_ACC_F32) {
+    FL(HE_ACC_F32, ACT_NONE);
+  } else {
+    return -2;
+  }
+#undef FL
+  return 0;
+}

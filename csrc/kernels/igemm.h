@@ -79,10 +79,6 @@ struct IgemmArgs {
 extern "C" int dpe_igemm_launch(const dpe::IgemmArgs* args, int bm, int bn, int aload, int bload, int epi,
                                 int splits, hipStream_t stream);
 
-// 256x256x64 LDS-DMA / 8-phase GEMM (gemm256.hip) for large dense shapes.
-// a_k / b_k: operand K-contiguous (1) or M/N-contiguous (0); K % 64 == 0.
-extern "C" int dpe_gemm256_launch(const dpe::IgemmArgs* args, int a_k, int b_k, int epi, int splits, hipStream_t stream);
-
 // LDS-DMA implicit-GEMM (igemm.hip) for forward-form convolutions and dense K-contiguous A
 // (B K- or N-contiguous; EPI_BF16 / EPI_BF16_BNB, no split-K); stages: 2 or 3 (LDS ring depth;
 // 2 only for the 2x2-wave tiles).  -1: outside its envelope.

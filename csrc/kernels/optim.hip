@@ -73,12 +73,13 @@ struct SgdRule {
   }
   DPE_DEVICE void operator()(float& p, float g, float& b, float&) const {
     g *= gscale;
+    if (maximize) g = -g;  // as torch: negate before weight decay and momentum
     if (wd != 0.f) g += wd * p;
     if (mom != 0.f) {
       b = first ? g : mom * b + (1.f - damp) * g;
       g = nesterov ? g + mom * b : b;
     }
-    p = maximize ? p + lr * g : p - lr * g;
+    p -= lr * g;
   }
 };
 

@@ -12,10 +12,10 @@ forward  (x fp32 residual stream [B, T, D])
     qkv = h1 W_qkv^T + b            bf16 [B, T, 3, H, 64], read in place by attention
     a, lse = attn(qkv)              causal flash attention
     x2 = x + a W_o^T + b            fp32, residual add in the GEMM epilogue
-    h2 = LN2(x2) ; v = h2 W_fc^T + b ; u = gelu(v)
+    h2 = LN2(x2) ; v = h2 W_fc^T + b ; u = gelu(v)   one GEMM: u and v from its epilogue
     y  = x2 + u W_p^T + b           fp32
 backward (g = dL/dy fp32, gb its bf16 copy)
-    dW_p += gb^T u ; db_p += colsum(gb) ; du = gb W_p ; dv = gelu'(v) du
+    dW_p += gb^T u ; db_p += colsum(gb) ; dv = gelu'(v) (gb W_p)   (GELU' in the GEMM epilogue)
     dW_fc += dv^T h2 ; db_fc ; dh2 = dv W_fc
     g2, g2b = g + LN2'(dh2)         one kernel: fp32 stream grad + bf16 copy
     dW_o += g2b^T a ; db_o ; da = g2b W_o ; dqkv = attn'(da)
@@ -82,8 +82,9 @@ class BlockFn(Function):
         a = a.view(B, T, D)
         x2 = C.linear_fwd(a, shadow(blk.attn_proj.weight), opt(blk.attn_proj.bias), 0, True, x, None)
         h2, m2, r2 = C.layernorm_fwd(x2, blk.ln_2.weight.detach(), opt(blk.ln_2.bias), blk.ln_2.eps)
-        v = C.linear_fwd(h2, shadow(blk.c_fc.weight), opt(blk.c_fc.bias), 0, False, None, None)
-        u = C.act(v, None, 2)
+        # GELU in the GEMM epilogue; the pre-activation v is written alongside for the backward
+        v = torch.empty((B, T, blk.c_fc.weight.shape[0]), device=x.device, dtype=torch.bfloat16)
+        u = C.linear_fwd(h2, shadow(blk.c_fc.weight), opt(blk.c_fc.bias), 2, False, None, None, v)
         y = C.linear_fwd(u, shadow(blk.mlp_proj.weight), opt(blk.mlp_proj.bias), 0, True, x2, None)
         ctx.save_for_backward(x, h1, m1, r1, qkv5, a, lse, x2, h2, m2, r2, v, u)
         ctx.blk, ctx.scale = blk, scale
@@ -108,8 +109,8 @@ class BlockFn(Function):
             grad_done(p, direct)
             grads[id(p)] = None if direct else buf
 
-        def linear_bwd(lin, dyb, inp, want_dx=True):
-            """dW += dyb^T inp ; db += colsum(dyb) ; return dyb W (bf16)."""
+        def linear_bwd(lin, dyb, inp, want_dx=True, gelu_in=None):
+            """dW += dyb^T inp ; db += colsum(dyb) ; return dyb W (bf16), times gelu'(gelu_in) if given."""
             buf, d = sink(lin.weight)
             C.linear_wgrad(dyb, inp, buf, 1.0)
             done(lin.weight, buf, d)
@@ -117,7 +118,7 @@ class BlockFn(Function):
                 bb, bd = sink(lin.bias)
                 C.colsum(dyb, bb, True)
                 done(lin.bias, bb, bd)
-            return C.linear_dgrad(dyb, shadow(lin.weight)) if want_dx else None
+            return C.linear_dgrad(dyb, shadow(lin.weight), None, None, gelu_in) if want_dx else None
 
         def ln_bwd(ln, dy, xin, mean, rstd, res):
             wb, wd = sink(ln.weight)
@@ -128,8 +129,7 @@ class BlockFn(Function):
                 done(ln.bias, bb, bd)
             return dx, dxb
 
-        du = linear_bwd(blk.mlp_proj, gb, u)
-        dv = C.act(du, v, 3)
+        dv = linear_bwd(blk.mlp_proj, gb, u, gelu_in=v)  # GELU backward in the data-grad epilogue
         dh2 = linear_bwd(blk.c_fc, dv, h2)
         g2, g2b = ln_bwd(blk.ln_2, dh2, x2, m2, r2, g)
         da = linear_bwd(blk.attn_proj, g2b, a)

@@ -56,6 +56,10 @@ class _FusedMixin:
                 st = self.state.get(p)
                 if st and "step" in st:
                     steps[i] = float(st["step"])
+                elif st and st.get("momentum_buffer") is not None:
+                    # a stock torch.optim.SGD state has a momentum buffer but no step counter: the kernel's
+                    # "first step" (b = g) must not discard the loaded buffer
+                    steps[i] = 1.0
             self._steps = steps
         for i, p in enumerate(params):
             st = self.state[p]
@@ -114,9 +118,22 @@ class _FusedMixin:
         for p in self._all_params():
             st = self.state[p]
             sh = getattr(p, "_dpe_shadow", None)
+            s1 = st.get("exp_avg") if self._kind == 0 else st.get("momentum_buffer")
+            s2 = st.get("exp_avg_sq") if self._kind == 0 else None
             ks.append((p.data_ptr(), p.grad.data_ptr() if p.grad is not None else 0,
-                       sh.data_ptr() if sh is not None and getattr(p, "_dpe_shadow_ver", -1) == p._version else 0))
+                       sh.data_ptr() if sh is not None and getattr(p, "_dpe_shadow_ver", -1) == p._version else 0,
+                       s1.data_ptr() if s1 is not None else 0, s2.data_ptr() if s2 is not None else 0))
         return tuple(ks)
+
+    def load_state_dict(self, state_dict):
+        """torch's load puts fresh state tensors in ``self.state`` (the old ones go back to the caching
+        allocator): drop the device table and the step counters so the next fused step rebuilds both
+        from the loaded state instead of touching freed memory."""
+        super().load_state_dict(state_dict)
+        self._steps = None
+        self._tab = None
+        self._tab_key = None
+        self._hp_key = None
 
     def _hp_row(self, g):
         raise NotImplementedError

@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""GPT-2-small GEMMs (8 x 1024 tokens) on the persistent hgemm kernel: every tile
+configuration, the planner's pick, and hipBLASLt (torch matmul, bf16 out) on
+the same random operands.  One JSON line per (GEMM, arm).
+
+    python scripts/bench_hgemm.py [--check] [--only NAME]
+"""
+import argparse
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from distributed_pytorch_example_amd.ops._ext import ext  # noqa: E402
+
+C = ext()
+dev = "cuda"
+T = 8192
+# name, M, N, K, layout (fwd: A K/B K, dgrad: A K/B N, wgrad: A M/B N), epi, act
+SHAPES = [
+    ("qkv.fwd", T, 2304, 768, "fwd", 0, 0),
+    ("proj.fwd", T, 768, 768, "fwd", 1, 0),
+    ("fc.fwd", T, 3072, 768, "fwd", 0, 2),
+    ("mproj.fwd", T, 768, 3072, "fwd", 1, 0),
+    ("lmhead.fwd", T, 50304, 768, "fwd", 0, 0),
+    ("qkv.dgrad", T, 768, 2304, "dgrad", 0, 0),
+    ("proj.dgrad", T, 768, 768, "dgrad", 0, 0),
+    ("fc.dgrad", T, 768, 3072, "dgrad", 0, 0),
+    ("mproj.dgrad", T, 3072, 768, "dgrad", 0, 3),
+    ("lmhead.dgrad", T, 768, 50304, "dgrad", 0, 0),
+    ("qkv.wgrad", 2304, 768, T, "wgrad", 2, 0),
+    ("proj.wgrad", 768, 768, T, "wgrad", 2, 0),
+    ("fc.wgrad", 3072, 768, T, "wgrad", 2, 0),
+    ("mproj.wgrad", 768, 3072, T, "wgrad", 2, 0),
+    ("lmhead.wgrad", 50304, 768, T, "wgrad", 2, 0),
+]
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def operands(M, N, K, layout):
+    g = torch.Generator(device=dev).manual_seed(0)
+    if layout == "fwd":
+        A = torch.randn(M, K, device=dev, generator=g).bfloat16()
+        B = (torch.randn(N, K, device=dev, generator=g) * 0.05).bfloat16()
+        ref = lambda: A @ B.t()  # noqa: E731
+        return A, B, K, K, True, True, ref
+    if layout == "dgrad":
+        A = torch.randn(M, K, device=dev, generator=g).bfloat16()      # dy [tokens, out]
+        B = (torch.randn(K, N, device=dev, generator=g) * 0.05).bfloat16()  # w [out, in]
+        ref = lambda: A @ B  # noqa: E731
+        return A, B, K, N, True, False, ref
+    A = torch.randn(K, M, device=dev, generator=g).bfloat16()          # dy [tokens, out]
+    B = torch.randn(K, N, device=dev, generator=g).bfloat16()          # x  [tokens, in]
+    ref = lambda: A.t() @ B  # noqa: E731
+    return A, B, M, N, False, False, ref
+
+
+def run(name, M, N, K, layout, epi, act, check):
+    A, B, lda, ldb, ak, bk, ref = operands(M, N, K, layout)
+    fl = 2.0 * M * N * K
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16 if epi == 0 else torch.float32)
+    bias = torch.randn(N, device=dev) * 0.1 if layout == "fwd" else None
+    resid = torch.randn(M, N, device=dev) if epi == 1 else None
+    aux_in = torch.randn(M, N, device=dev).bfloat16() if act == 3 else None
+    aux_out = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if act == 2 else None
+    res = []
+    t = timeit(ref)
+    res.append({"gemm": name, "arm": "hipblaslt", "us": round(t, 1), "TF": round(fl / t / 1e6, 1)})
+    plan = C.hgemm_plan(M, N, K, ak, bk, True, 2 if epi == 0 else 4)
+    cfgs = [-1, 0, 1, 2, 3] if layout == "fwd" else ([-1, 0, 1] if layout == "dgrad" else [-1, 0])
+    for cfg in cfgs:
+        for sp in ([-1] if cfg == -1 else [1, 2, 4]):
+            def f():
+                if epi == 2:
+                    out.zero_()
+                C.hgemm(A, B, out, M, N, K, lda, ldb, N, ak, bk, epi, act, bias, resid, aux_in, aux_out, 1.0, cfg, sp)
+            try:
+                t = timeit(f)
+            except RuntimeError as e:  # configuration outside the envelope
+                res.append({"gemm": name, "arm": f"cfg{cfg}/s{sp}", "error": str(e)[:80]})
+                continue
+            r = {"gemm": name, "arm": "plan" if cfg == -1 else f"cfg{cfg}/s{sp}", "us": round(t, 1), "TF": round(fl / t / 1e6, 1)}
+            if cfg == -1:
+                r["plan"] = plan
+            if check:
+                f()
+                torch.cuda.synchronize()
+                y = ref().float()
+                if bias is not None:
+                    y = y + bias
+                if act == 2:
+                    y = torch.nn.functional.gelu(y, approximate="tanh")
+                if act == 3:
+                    xx = aux_in.float().requires_grad_(True)
+                    gg = torch.autograd.grad(torch.nn.functional.gelu(xx, approximate="tanh").sum(), xx)[0]
+                    y = y * gg
+                if resid is not None:
+                    y = y + resid
+                err = ((out.float() - y).norm() / y.norm()).item()
+                r["rel_err"] = float(f"{err:.2e}")
+            res.append(r)
+    for r in res:
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--check", action="store_true")
+    ap.add_argument("--only", default="")
+    ap.add_argument("--square", action="store_true", help="main-loop check: 4096^3 / 8192^3 per layout")
+    a = ap.parse_args()
+    if a.square:
+        SHAPES[:] = [(f"sq{n}.{lay}", n, n, n, lay, 0 if lay != "wgrad" else 2, 0)
+                     for n in (4096, 8192) for lay in ("fwd", "dgrad", "wgrad")]
+    for s in SHAPES:
+        if a.only and a.only not in s[0]:
+            continue
+        run(*s, a.check)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Steady-state per-step kernel breakdown from a rocprofv3 kernel_trace.csv.
+"""Steady-state per-step kernel breakdown from a rocprofv3 kernel trace (kernel_trace.csv or the
+default rocpd results .db).
 
 Keeps only kernels launched after the K-th call of a per-step marker kernel
 (default: the optimizer kernel, one launch per step), so warm-up and GEMM
@@ -11,7 +12,12 @@ path = sys.argv[1]
 skip = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 marker = sys.argv[3] if len(sys.argv) > 3 else "adam_kernel"
 top = int(sys.argv[4]) if len(sys.argv) > 4 else 40
-rows = list(csv.DictReader(open(path)))
+if path.endswith(".db"):
+    import sqlite3
+    q = sqlite3.connect(path).execute("select name, start, end from kernels")
+    rows = [{"Kernel_Name": n, "Start_Timestamp": a, "End_Timestamp": b} for n, a, b in q]
+else:
+    rows = list(csv.DictReader(open(path)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 marks = [r for r in rows if marker in r["Kernel_Name"]]
 t0 = int(marks[skip - 1]["End_Timestamp"])

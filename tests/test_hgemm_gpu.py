@@ -1,0 +1,104 @@
+"""Numerics of the persistent MFMA GEMM (csrc/kernels/hgemm.hip) against fp32 PyTorch.
+
+Every tile configuration x operand layout x epilogue, on shapes with M / N tails
+and K splits, random non-zero operands.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from distributed_pytorch_example_amd.ops._ext import ext  # noqa: E402
+
+DEV = "cuda"
+F = torch.nn.functional
+
+
+def _ops(M, N, K, layout, g):
+    if layout == "nt":   # y = x w^T
+        A = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+        B = torch.randn(N, K, device=DEV, generator=g).bfloat16()
+        return A, B, K, K, True, True, A.float() @ B.float().t()
+    if layout == "nn":   # dx = dy w
+        A = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+        B = torch.randn(K, N, device=DEV, generator=g).bfloat16()
+        return A, B, K, N, True, False, A.float() @ B.float()
+    A = torch.randn(K, M, device=DEV, generator=g).bfloat16()  # tn: dw = dy^T x
+    B = torch.randn(K, N, device=DEV, generator=g).bfloat16()
+    return A, B, M, N, False, False, A.float().t() @ B.float()
+
+
+CFGS = {"nt": [0, 1, 2, 3], "nn": [0, 1], "tn": [0]}
+
+
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_hgemm_layouts(layout, splits):
+    C = ext()
+    g = torch.Generator(device=DEV).manual_seed(1)
+    M, N, K = 520, 776, 64 * 13  # M / N tails for every tile, 13 K-tiles (uneven split)
+    A, B, lda, ldb, ak, bk, ref = _ops(M, N, K, layout, g)
+    for cfg in CFGS[layout]:
+        out = torch.empty(M, N, device=DEV, dtype=torch.float32)
+        C.hgemm(A, B, out, M, N, K, lda, ldb, N, ak, bk, 1, 0, None, None, None, None, 1.0, cfg, splits)
+        torch.cuda.synchronize()
+        err = ((out - ref).norm() / ref.norm()).item()
+        assert err < 1e-5, (layout, cfg, splits, err)
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+def test_hgemm_epilogues(cfg):
+    C = ext()
+    g = torch.Generator(device=DEV).manual_seed(2)
+    M, N, K = 1000, 1032, 512
+    A, B, lda, ldb, ak, bk, ref = _ops(M, N, K, "nt", g)
+    bias = torch.randn(N, device=DEV, generator=g)
+    # bf16 + bias + GELU, pre-activation kept
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    v = torch.empty_like(out)
+    C.hgemm(A, B, out, M, N, K, lda, ldb, N, ak, bk, 0, 2, bias, None, None, v, 0.5, cfg, 1)
+    pre = 0.5 * ref + bias
+    torch.testing.assert_close(v.float(), pre, rtol=2e-2, atol=2e-2 * pre.abs().max().item() / 10)
+    y = F.gelu(pre, approximate="tanh")
+    assert ((out.float() - y).norm() / y.norm()).item() < 1e-2
+    # fp32 + bias + residual (the GPT-2 residual stream)
+    res = torch.randn(M, N, device=DEV, generator=g)
+    o32 = torch.empty(M, N, device=DEV)
+    C.hgemm(A, B, o32, M, N, K, lda, ldb, N, ak, bk, 1, 0, bias, res, None, None, 1.0, cfg, 1)
+    yr = ref + bias + res
+    assert ((o32 - yr).norm() / yr.norm()).item() < 1e-5
+    # in place on the residual stream (out aliases residual)
+    o2 = res.clone()
+    C.hgemm(A, B, o2, M, N, K, lda, ldb, N, ak, bk, 1, 0, bias, o2, None, None, 1.0, cfg, 1)
+    assert ((o2 - yr).norm() / yr.norm()).item() < 1e-5
+    # fp32 accumulate (weight-grad buckets)
+    acc = torch.randn(M, N, device=DEV, generator=g)
+    o3 = acc.clone()
+    C.hgemm(A, B, o3, M, N, K, lda, ldb, N, ak, bk, 2, 0, None, None, None, None, 2.0, cfg, 1)
+    ya = acc + 2.0 * ref
+    assert ((o3 - ya).norm() / ya.norm()).item() < 1e-5
+
+
+@pytest.mark.parametrize("splits", [1, 2])
+def test_hgemm_gelu_backward(splits):
+    C = ext()
+    g = torch.Generator(device=DEV).manual_seed(3)
+    M, N, K = 768, 1024, 512
+    A, B, lda, ldb, ak, bk, ref = _ops(M, N, K, "nn", g)
+    v = torch.randn(M, N, device=DEV, generator=g).bfloat16()
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    C.hgemm(A, B, out, M, N, K, lda, ldb, N, ak, bk, 0, 3, None, None, v, None, 1.0, 0, splits)
+    vv = v.float().requires_grad_(True)
+    gg = torch.autograd.grad(F.gelu(vv, approximate="tanh").sum(), vv)[0]
+    y = ref * gg
+    assert ((out.float() - y).norm() / y.norm()).item() < 1e-2
+
+
+def test_hgemm_plan_is_deterministic():
+    C = ext()
+    a = [C.hgemm_plan(8192, n, k, True, True, True, 2) for n, k in ((2304, 768), (768, 3072), (50304, 768))]
+    b = [C.hgemm_plan(8192, n, k, True, True, True, 2) for n, k in ((2304, 768), (768, 3072), (50304, 768))]
+    assert a == b

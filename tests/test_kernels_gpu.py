@@ -72,22 +72,39 @@ def test_linear_wgrad(C, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(1024, 3072, 768), (2048, 768, 3072), (512, 256, 192)])
-def test_linear_wgrad_lds_dma_arm(C, M, N, K):
-    """linear_wgrad's LDS-DMA split-K arm (a 1x1 conv weight grad), forced on, vs fp32."""
+def test_linear_wgrad_split_k(C, M, N, K):
+    """Weight grads over a long token axis: K-split fp32 slabs + accumulate into the bucket."""
     torch.manual_seed(3)
     dy = bf(torch.randn(M, N, device=dev))
     x = bf(torch.randn(M, K, device=dev))
-    dw = torch.zeros(N, K, device=dev)
-    ref = dy.float().t() @ x.float()
-    C.set_linear_wgrad_dma(1)
-    try:
-        C.linear_wgrad(dy, x, dw, 1.0)
-        torch.cuda.synchronize()
-        assert rel_err(dw, ref) < 1e-3
-        C.linear_wgrad(dy, x, dw, 0.5)
-        assert rel_err(dw, 1.5 * ref) < 1e-3
-    finally:
-        C.set_linear_wgrad_dma(-1)
+    dw = torch.randn(N, K, device=dev)
+    ref = dw + dy.float().t() @ x.float()
+    C.linear_wgrad(dy, x, dw, 1.0)
+    torch.cuda.synchronize()
+    assert rel_err(dw, ref) < 1e-3
+    C.linear_wgrad(dy, x, dw, 0.5)
+    assert rel_err(dw, ref + 0.5 * (dy.float().t() @ x.float())) < 1e-3
+
+
+def test_linear_gelu_fused_fwd_bwd(C):
+    """fc: u = gelu(x w^T + b) with the pre-activation v from the same epilogue; the next layer's
+    data grad times gelu'(v) in its epilogue (GPT-2 MLP)."""
+    torch.manual_seed(9)
+    M, K, H = 1024, 256, 1024
+    x = bf(torch.randn(M, K, device=dev))
+    w = bf(torch.randn(H, K, device=dev) / math.sqrt(K))
+    b = torch.randn(H, device=dev) * 0.1
+    v = torch.empty(M, H, device=dev, dtype=torch.bfloat16)
+    u = C.linear_fwd(x, w, b, 2, False, None, None, v)
+    pre = x.float() @ w.float().t() + b
+    assert rel_err(v, pre) < 1e-2
+    assert rel_err(u, F.gelu(pre, approximate="tanh")) < 1e-2
+    w2 = bf(torch.randn(K, H, device=dev) / math.sqrt(H))
+    dy = bf(torch.randn(M, K, device=dev))
+    dv = C.linear_dgrad(dy, w2, None, None, v)
+    vv = v.float().requires_grad_(True)
+    gg = torch.autograd.grad(F.gelu(vv, approximate="tanh").sum(), vv)[0]
+    assert rel_err(dv, (dy.float() @ w2.float()) * gg) < 1e-2
 
 
 # ------------------------------------------------------------------- conv
@@ -359,50 +376,45 @@ def test_attention_fwd_bwd(C, B, T, H):
         assert rel_err(dqkv[:, :, i].permute(0, 2, 1, 3), g) < 2e-2, i
 
 
-# ------------------------------------------- 256-tile LDS-DMA GEMM (gemm256.hip)
-@pytest.fixture
-def g256(C):
-    C.set_gemm_backend(1)  # native kernels only (no hipBLASLt autotune arm)
-    C.set_gemm256_mode(2)  # force the 256-tile kernel whenever the layout is supported
-    yield C
-    C.set_gemm256_mode(0)
-    C.set_gemm_backend(0)
-
-
-@pytest.mark.parametrize("backend", [1, 2])
-def test_gemm_backends_plain(C, backend):
-    """Native (1) and library (2) arms of the plain-GEMM dispatch agree with fp32 torch."""
-    C.set_gemm_backend(backend)
-    try:
-        torch.manual_seed(8)
-        M, N, K = 1024, 776, 512
-        x = bf(torch.randn(M, K, device=dev))
-        w = bf(torch.randn(N, K, device=dev) / math.sqrt(K))
-        b = torch.randn(N, device=dev)
-        assert rel_err(C.linear_fwd(x, w, b, 0, False), x.float() @ w.float().t() + b) < 1e-2
-        dy = bf(torch.randn(M, N, device=dev))
-        s = torch.tensor([0.5], device=dev)
-        assert rel_err(C.linear_dgrad(dy, w, None, s), 0.5 * (dy.float() @ w.float())) < 1e-2
-        dw = torch.randn(N, K, device=dev)
-        ref = dw + 0.5 * (dy.float().t() @ x.float())
-        C.linear_wgrad(dy, x, dw, 1.0, s)
-        assert rel_err(dw, ref) < 1e-3
-        # fp32 residual stream: y = res + x @ w^T + b
-        res = torch.randn(M, N, device=dev)
-        y = C.linear_fwd(x, w, b, 0, True, res)
-        assert rel_err(y, res + x.float() @ w.float().t() + b) < 1e-4
-        # column-padded dy (vocab-padded LM head): only the first N columns are real
-        dyp = bf(torch.randn(M, N + 56, device=dev))
-        dw2 = torch.zeros(N, K, device=dev)
-        C.linear_wgrad(dyp, x, dw2, 1.0)
-        assert rel_err(dw2, dyp[:, :N].float().t() @ x.float()) < 1e-3
-    finally:
-        C.set_gemm_backend(0)
+# ----------------------------- Linear GEMMs on the persistent MFMA kernel (hgemm.hip)
+def test_linear_plain_paths(C):
+    """The only GEMM backend is native: set_gemm_backend(1) is accepted, the library arm is gone."""
+    C.set_gemm_backend(1)
+    with pytest.raises(RuntimeError):
+        C.set_gemm_backend(2)
+    torch.manual_seed(8)
+    M, N, K = 1024, 776, 512
+    x = bf(torch.randn(M, K, device=dev))
+    w = bf(torch.randn(N, K, device=dev) / math.sqrt(K))
+    b = torch.randn(N, device=dev)
+    assert rel_err(C.linear_fwd(x, w, b, 0, False), x.float() @ w.float().t() + b) < 1e-2
+    dy = bf(torch.randn(M, N, device=dev))
+    s = torch.tensor([0.5], device=dev)
+    assert rel_err(C.linear_dgrad(dy, w, None, s), 0.5 * (dy.float() @ w.float())) < 1e-2
+    dw = torch.randn(N, K, device=dev)
+    ref = dw + 0.5 * (dy.float().t() @ x.float())
+    C.linear_wgrad(dy, x, dw, 1.0, s)
+    assert rel_err(dw, ref) < 1e-3
+    # fp32 residual stream: y = res + x @ w^T + b
+    res = torch.randn(M, N, device=dev)
+    y = C.linear_fwd(x, w, b, 0, True, res)
+    assert rel_err(y, res + x.float() @ w.float().t() + b) < 1e-4
+    # column-padded dy (vocab-padded LM head): only the first N columns are real
+    dyp = bf(torch.randn(M, N + 56, device=dev))
+    dw2 = torch.zeros(N, K, device=dev)
+    C.linear_wgrad(dyp, x, dw2, 1.0)
+    assert rel_err(dw2, dyp[:, :N].float().t() @ x.float()) < 1e-3
+    # odd vocabulary (N % 8 != 0) over a padded dy, as the tied LM head
+    Nv = 771
+    dyv = bf(torch.randn(M, 776, device=dev))
+    dyv[:, Nv:] = 0
+    dw3 = torch.zeros(Nv, K, device=dev)
+    C.linear_wgrad(dyv, x, dw3, 1.0)
+    assert rel_err(dw3, dyv[:, :Nv].float().t() @ x.float()) < 1e-3
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 256), (8192 // 8 + 64, 2304 // 4 + 8, 768), (300, 520, 128)])
-def test_gemm256_fwd(g256, M, N, K):
-    C = g256
+def test_linear_fwd_epilogues(C, M, N, K):
     torch.manual_seed(3)
     x = bf(torch.randn(M, K, device=dev))
     w = bf(torch.randn(N, K, device=dev) / math.sqrt(K))
@@ -420,8 +432,7 @@ def test_gemm256_fwd(g256, M, N, K):
     assert rel_err(yr, x.float() @ w.float().t() + rb.float()) < 1e-2
 
 
-def test_gemm256_asymmetric_layout(g256):
-    C = g256
+def test_linear_asymmetric_layout_persistent(C):
     M, N, K = 256, 256, 128
     x = torch.zeros(M, K, device=dev)
     x[torch.arange(M), torch.arange(M) % K] = 1.0
@@ -435,8 +446,7 @@ def test_gemm256_asymmetric_layout(g256):
 
 
 @pytest.mark.parametrize("M,N,K", [(512, 256, 768), (1024, 768, 2304), (320, 520, 192)])
-def test_gemm256_dgrad(g256, M, N, K):
-    C = g256
+def test_linear_dgrad_persistent(C, M, N, K):
     torch.manual_seed(4)
     dy = bf(torch.randn(M, N, device=dev))
     w = bf(torch.randn(N, K, device=dev))
@@ -444,19 +454,17 @@ def test_gemm256_dgrad(g256, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(2048, 768, 256), (4096, 2304, 768), (1024, 520, 264)])
-def test_gemm256_wgrad(g256, M, N, K):
-    C = g256
+def test_linear_wgrad_persistent(C, M, N, K):
     torch.manual_seed(5)
     dy = bf(torch.randn(M, N, device=dev))
     x = bf(torch.randn(M, K, device=dev))
     dw = torch.randn(N, K, device=dev)
     ref = dw + dy.float().t() @ x.float()
-    C.linear_wgrad(dy, x, dw, 1.0)  # accumulates (split-K atomics)
+    C.linear_wgrad(dy, x, dw, 1.0)  # accumulates (K-split slabs + finalize, or in place)
     assert rel_err(dw, ref) < 1e-3
 
 
-def test_gemm256_alpha_tensor(g256):
-    C = g256
+def test_linear_alpha_tensor(C):
     torch.manual_seed(6)
     M, N, K = 512, 512, 256
     dy = bf(torch.randn(M, N, device=dev))
