@@ -49,9 +49,11 @@ int g_force_cfg = -1, g_force_splits = -1;
 int num_cus() {
   static const int n = [] {
     int dev = 0;
-    hipGetDevice(&dev);
     hipDeviceProp_t pr;
-    hipGetDeviceProperties(&pr, dev);
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&pr, dev) != hipSuccess) {
+      (void)hipGetLastError();
+      return 256;  // no device (CPU planning / tests): MI355X
+    }
     return pr.multiProcessorCount > 0 ? pr.multiProcessorCount : 256;
   }();
   return n;

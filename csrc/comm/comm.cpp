@@ -12,6 +12,8 @@
 
 #include <stdexcept>
 
+#include <pybind11/functional.h>
+
 extern "C" int dpe_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st);
 extern "C" int dpe_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
 
@@ -174,20 +176,8 @@ Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_
                  std::shared_ptr<Communicator> comm, bool timing, bool force, bool comm_bf16, bool sync_debug)
     : buckets_(std::move(buckets)), bparams_(std::move(bucket_params)), comm_(std::move(comm)), timing_(timing),
       force_(force), comm_bf16_(comm_bf16), sync_debug_(sync_debug) {
-  TORCH_CHECK(buckets_.size() == bparams_.size(), "bucket/param list size mismatch");
-  param_bucket_.assign(nparams, -1);
-  expected_.resize(buckets_.size());
-  for (size_t b = 0; b < bparams_.size(); ++b) {
-    TORCH_CHECK(buckets_[b].is_cuda() && buckets_[b].is_contiguous(), "bucket buffers must be contiguous GPU tensors");
-    for (int64_t p : bparams_[b]) {
-      TORCH_CHECK(p >= 0 && p < nparams && param_bucket_[p] == -1, "parameter in several buckets or out of range");
-      param_bucket_[p] = (int64_t)b;
-    }
-    expected_[b] = (int)bparams_[b].size();
-  }
-  pending_ = expected_;
-  ready_.assign(buckets_.size(), 0);
-  seen_.assign(nparams, 0);
+  for (auto& b : buckets_) TORCH_CHECK(b.is_cuda(), "bucket buffers must be GPU tensors (host transport: Reducer.host)");
+  init_tracking(nparams);
   const unsigned flags = timing_ ? hipEventDefault : hipEventDisableTiming;
   ev_ready_.resize(buckets_.size());
   ev_aux_.resize(buckets_.size());
@@ -210,7 +200,34 @@ Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_
   HIP_CHECK(hipEventCreateWithFlags(&ev_step_begin_, flags));
 }
 
+Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params, int64_t nparams,
+                 int world, std::function<void(int64_t)> on_launch, std::function<void()> on_finalize)
+    : buckets_(std::move(buckets)), bparams_(std::move(bucket_params)), timing_(false), force_(false), comm_bf16_(false),
+      sync_debug_(false), host_launch_(std::move(on_launch)), host_finalize_(std::move(on_finalize)), host_world_(world) {
+  TORCH_CHECK(host_launch_, "host-transport reducer needs an on_launch callable");
+  TORCH_CHECK(world >= 1, "world must be >= 1");
+  init_tracking(nparams);
+}
+
+void Reducer::init_tracking(int64_t nparams) {
+  TORCH_CHECK(buckets_.size() == bparams_.size(), "bucket/param list size mismatch");
+  param_bucket_.assign(nparams, -1);
+  expected_.resize(buckets_.size());
+  for (size_t b = 0; b < bparams_.size(); ++b) {
+    TORCH_CHECK(buckets_[b].is_contiguous(), "bucket buffers must be contiguous");
+    for (int64_t p : bparams_[b]) {
+      TORCH_CHECK(p >= 0 && p < nparams && param_bucket_[p] == -1, "parameter in several buckets or out of range");
+      param_bucket_[p] = (int64_t)b;
+    }
+    expected_[b] = (int)bparams_[b].size();
+  }
+  pending_ = expected_;
+  ready_.assign(buckets_.size(), 0);
+  seen_.assign(nparams, 0);
+}
+
 Reducer::~Reducer() {
+  if (host_launch_) return;  // no HIP objects in host-transport mode
   for (auto* v : {&ev_ready_, &ev_aux_, &ev_start_, &ev_end_})
     for (auto e : *v) (void)hipEventDestroy(e);
   (void)hipEventDestroy(ev_bwd_end_);
@@ -229,8 +246,12 @@ void Reducer::prepare() {
 }
 
 void Reducer::launch(int64_t b) {
-  hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
   launch_order_.push_back(b);
+  if (host_launch_) {
+    host_launch_(b);
+    return;
+  }
+  hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
   if (!comm_ || (comm_->world() == 1 && !force_)) return;
   hipStream_t cs = comm_->comm_stream().stream();
   HIP_CHECK(hipEventRecord(ev_ready_[b], cur));
@@ -273,6 +294,12 @@ void Reducer::mark_ready(int64_t p) {
 
 void Reducer::finalize() {
   if (!step_open_) return;
+  if (host_launch_) {
+    while (next_ < (int64_t)buckets_.size()) launch(next_++);
+    if (host_finalize_) host_finalize_();
+    step_open_ = false;
+    return;
+  }
   hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
   if (timing_) HIP_CHECK(hipEventRecord(ev_bwd_end_, cur));
   // Unused parameters: their (zero / stale-accumulated) slices are reduced
@@ -287,7 +314,7 @@ void Reducer::finalize() {
 
 std::vector<std::tuple<int64_t, double, double>> Reducer::last_timings() {
   std::vector<std::tuple<int64_t, double, double>> out;
-  if (!timing_ || !comm_ || (comm_->world() == 1 && !force_)) return out;
+  if (host_launch_ || !timing_ || !comm_ || (comm_->world() == 1 && !force_)) return out;
   HIP_CHECK(hipEventSynchronize(ev_done_));
   for (size_t b = 0; b < buckets_.size(); ++b) {
     float ms = 0.f, rel = 0.f;
@@ -332,6 +359,16 @@ void register_comm(pybind11::module& m) {
                     bool, bool, bool>(),
            py::arg("buckets"), py::arg("bucket_params"), py::arg("nparams"), py::arg("comm"), py::arg("timing") = false,
            py::arg("force") = false, py::arg("comm_bf16") = false, py::arg("sync_debug") = false)
+      .def_static("host", [](std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params,
+                             int64_t nparams, int world, std::function<void(int64_t)> on_launch,
+                             std::function<void()> on_finalize) {
+             return std::make_shared<Reducer>(std::move(buckets), std::move(bucket_params), nparams, world,
+                                              std::move(on_launch), std::move(on_finalize));
+           }, py::arg("buckets"), py::arg("bucket_params"), py::arg("nparams"), py::arg("world"), py::arg("on_launch"),
+           py::arg("on_finalize"),
+           "host-transport reducer: same C++ sequencing, collectives delegated to the callables (gloo on CPU)")
+      .def_property_readonly("world", &Reducer::world)
+      .def_property_readonly("host_mode", &Reducer::host_mode)
       .def("launch_order", &Reducer::launch_order)
       .def("prepare", &Reducer::prepare)
       .def("mark_ready", &Reducer::mark_ready)

@@ -7,6 +7,7 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -77,6 +78,11 @@ class Reducer {
   Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params, int64_t nparams,
           std::shared_ptr<Communicator> comm, bool timing, bool force = false, bool comm_bf16 = false,
           bool sync_debug = false);
+  // Host-transport mode: the same readiness tracking / index-order issue / finalize sequencing with
+  // the collective itself delegated to `on_launch(bucket)` and `on_finalize()` (the gloo control
+  // plane on CPU, world >= 1).  No HIP call is made in this mode, so it runs on a GPU-less host.
+  Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params, int64_t nparams, int world,
+          std::function<void(int64_t)> on_launch, std::function<void()> on_finalize);
   ~Reducer();
   void prepare();
   void mark_ready(int64_t param);
@@ -84,6 +90,8 @@ class Reducer {
   // (bucket, comm_ms, issued_before_backward_end) for the last finalized step
   std::vector<std::tuple<int64_t, double, double>> last_timings();
   int64_t num_buckets() const { return (int64_t)buckets_.size(); }
+  int world() const { return host_launch_ ? host_world_ : (comm_ ? comm_->world() : 1); }
+  bool host_mode() const { return (bool)host_launch_; }
   int64_t buckets_launched() const { return next_; }
   std::vector<int64_t> launch_order() const { return launch_order_; }
 
@@ -104,6 +112,10 @@ class Reducer {
   std::vector<hipEvent_t> ev_ready_, ev_aux_, ev_start_, ev_end_;
   hipEvent_t ev_bwd_end_ = nullptr, ev_done_ = nullptr, ev_step_begin_ = nullptr;
   bool step_open_ = false;
+  std::function<void(int64_t)> host_launch_;
+  std::function<void()> host_finalize_;
+  int host_world_ = 1;
+  void init_tracking(int64_t nparams);
 };
 
 // weight-grad side stream registered for a device (nullptr: none)

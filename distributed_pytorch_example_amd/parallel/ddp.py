@@ -32,7 +32,9 @@ Design (MI355X-first, not a port of c10d::Reducer):
   bucket layout at every (re)build and compares it across ranks through the
   control plane (fail fast instead of hanging in mismatched collectives), and
   synchronises the comm stream after every bucket.
-* **gloo / CPU / custom hooks**: the same bucketing with a Python reducer.
+* **gloo / CPU**: the same C++ reducer in host-transport mode (readiness,
+  index-order issue and finalize in C++; the bucket all-reduce delegated to
+  gloo).  Custom comm hooks run on a Python reducer.
 * **Init sync**: parameters and buffers are broadcast from rank 0 as one flat
   buffer per dtype (c10d's coalesced broadcast, C3).
 * **Buffer sync (C9)**: with ``broadcast_buffers`` the module's floating
@@ -60,6 +62,12 @@ from ..utils.logging import get_logger
 from ..ops._state import aux_wait as _aux_wait
 
 log = get_logger(__name__)
+
+
+def _has_ext() -> bool:
+    from ..ops._ext import has_ext
+
+    return has_ext()
 
 _DEFAULT_FIRST_BUCKET_BYTES = 1024 * 1024
 
@@ -155,6 +163,39 @@ class _PyReducer:
 
     def launch_order(self):
         return list(self.order)
+
+
+class _GlooTransport:
+    """Collective side of the native reducer's host-transport mode (gloo control plane, CPU or
+    host-staged GPU tensors): ``on_launch(b)`` issues bucket b's async all-reduce, ``on_finalize()``
+    waits for all of them and averages.  The readiness tracking, index-order issue and finalize
+    sequencing stay in C++ (``_C.Reducer.host``), the same code the RCCL path runs."""
+
+    def __init__(self, buckets: List[torch.Tensor], world: int, compression: Optional[str]):
+        self.buckets, self.world, self.compression = buckets, world, compression
+        self.works = []
+
+    def on_launch(self, b: int):
+        if self.world == 1:
+            return
+        t = self.buckets[b]
+        if t.is_cuda:
+            _aux_wait(t.device)  # weight grads written on the side stream
+        if self.compression == "bf16":
+            c = t.to(torch.bfloat16)
+            self.works.append((b, c, dist.all_reduce(c, async_op=True)))
+        else:
+            self.works.append((b, None, dist.all_reduce(t, async_op=True)))
+
+    def on_finalize(self):
+        for b, c, w in self.works:
+            w.wait()
+            t = self.buckets[b]
+            if c is not None:
+                t.copy_(c.float().div_(self.world))
+            else:
+                t.div_(self.world)
+        self.works = []
 
 
 class DistributedDataParallel(nn.Module):
@@ -263,7 +304,16 @@ class DistributedDataParallel(nn.Module):
             self.reducer = ext().Reducer(self.buckets, self.bucket_indices, len(self._params), self._comm, self._timing,
                                          self._force, self._compression == "bf16", self._debug)
             self._native = True
+        elif self._hook is None and _has_ext():
+            # gloo / CPU: the C++ reducer in host-transport mode (same sequencing as the RCCL path)
+            from ..ops._ext import ext
+
+            self._transport = _GlooTransport(self.buckets, self.world_size, self._compression)
+            self.reducer = ext().Reducer.host(self.buckets, self.bucket_indices, len(self._params), self.world_size,
+                                              self._transport.on_launch, self._transport.on_finalize)
+            self._native = False
         else:
+            # custom comm hooks (or no native extension built): the Python reducer
             self.reducer = _PyReducer(self.buckets, self.bucket_indices, len(self._params), self._params, self._hook,
                                       self._hook_state, self._compression)
             self._native = False

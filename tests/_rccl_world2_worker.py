@@ -1,0 +1,110 @@
+"""One rank of the 2-process native-reducer test (tests/test_ddp_rccl_world2_gpu.py).
+
+Both ranks share GPU 0; each process gets its own NCCL_HOSTID so RCCL treats them
+as two hosts and connects them through its socket transport -- the C++ Reducer
+then issues real world-2 RCCL all-reduces (Reducer::launch with world() == 2).
+"""
+import copy
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from distributed_pytorch_example_amd.models import resnet18_like  # noqa: E402
+from distributed_pytorch_example_amd.ops import functional as Fx  # noqa: E402
+from distributed_pytorch_example_amd.parallel import DDP  # noqa: E402
+from distributed_pytorch_example_amd.parallel import dist as pdist  # noqa: E402
+
+
+def rel(a, b):
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def avg_local_grads(m, x, y, world):
+    """Rank-averaged plain-backward grads (the all-reduce done on the gloo control plane)."""
+    for p in m.parameters():
+        p.grad = None
+    Fx.cross_entropy(m(x), y).backward()
+    out = []
+    for p in m.parameters():
+        g = p.grad.detach().float().cpu()
+        dist.all_reduce(g)
+        out.append((g / world).to(p.device))
+    return out
+
+
+def main():
+    rank, world, _ = pdist.init_process_group("rccl")
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(100 + rank)  # different init per rank: DDP's init broadcast (RCCL) must align them
+    m = resnet18_like(num_classes=10).to(dev)
+    ref = copy.deepcopy(m)  # plain-autograd twin (copied before DDP attaches bucket views / hooks)
+    ddp = DDP(m, bucket_cap_mb=1, first_bucket_mb=0.25)
+    assert ddp._native and ddp.reducer.world == 2, "native RCCL reducer expected at world 2"
+    ref.load_state_dict(m.state_dict())  # rank 0's weights after the init broadcast
+    for p in m.parameters():  # init sync over RCCL
+        q = p.detach().float().cpu()
+        dist.broadcast(q, 0)
+        assert torch.equal(q.to(dev), p.detach().float())
+    checks = []
+    for step in range(3):  # step 1 runs on the buckets rebuilt from the observed ready order
+        torch.manual_seed(7 + 10 * step + rank)
+        x = torch.randn(8, 3, 32, 32, device=dev)
+        y = torch.randint(0, 10, (8,), device=dev)
+        want = avg_local_grads(ref, x, y, world)
+        for p in m.parameters():
+            p.grad = None
+        Fx.cross_entropy(ddp(x), y).backward()
+        torch.cuda.synchronize()
+        assert ddp.reducer.launch_order() == list(range(ddp.num_buckets()))
+        checks.append(max(rel(p.grad, w) for p, w in zip(m.parameters(), want)))
+    assert ddp.bucket_rebuilds == 1
+    assert max(checks) < 1e-4, checks
+    # no_sync: two local micro-steps + one synced == rank average of the summed grads
+    for p in m.parameters():
+        p.grad = None
+    for p in ref.parameters():
+        p.grad = None
+    xs = []
+    for i in range(3):
+        torch.manual_seed(50 + i + 10 * rank)
+        xs.append((torch.randn(4, 3, 32, 32, device=dev), torch.randint(0, 10, (4,), device=dev)))
+    for i, (x, y) in enumerate(xs):
+        Fx.cross_entropy(ref(x), y).backward()
+        if i < 2:
+            with ddp.no_sync():
+                Fx.cross_entropy(ddp(x), y).backward()
+        else:
+            Fx.cross_entropy(ddp(x), y).backward()
+    torch.cuda.synchronize()
+    for p, r in zip(m.parameters(), ref.parameters()):
+        g = r.grad.detach().float().cpu()
+        dist.all_reduce(g)
+        assert rel(p.grad, (g / world).to(dev)) < 1e-4
+    # bf16 gradient compression on the RCCL path
+    ddp.register_comm_hook(None, __import__("distributed_pytorch_example_amd.parallel.hooks",
+                                            fromlist=["bf16_compress_hook"]).bf16_compress_hook)
+    torch.manual_seed(99 + rank)
+    x = torch.randn(8, 3, 32, 32, device=dev)
+    y = torch.randint(0, 10, (8,), device=dev)
+    want = avg_local_grads(ref, x, y, world)
+    for p in m.parameters():
+        p.grad = None
+    Fx.cross_entropy(ddp(x), y).backward()
+    torch.cuda.synchronize()
+    assert ddp._native and max(rel(p.grad, w) for p, w in zip(m.parameters(), want)) < 2e-2
+    # metric all-reduce + barrier over RCCL (reference C7 / C8)
+    t = torch.tensor([float(rank + 1)], device=dev)
+    pdist.all_reduce(t)
+    assert t.item() == 3.0
+    pdist.barrier()
+    assert pdist.check_health() == ""
+    print(f"rank {rank} ok: world-2 RCCL reducer, max rel err {max(checks):.2e}", flush=True)
+    pdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -30,6 +30,15 @@ def _setup(rank, world, port):
     return pdist.init_process_group("gloo")
 
 
+def _native_host(ddp, world):
+    """With the extension built, gloo DDP runs the C++ Reducer (host-transport mode) at world > 1."""
+    from distributed_pytorch_example_amd.ops._ext import has_ext
+
+    if has_ext():
+        assert ddp.reducer.host_mode and ddp.reducer.world == world
+        assert ddp.reducer.launch_order() == list(range(ddp.num_buckets()))
+
+
 def _w_grad_avg(rank, world, port, q):
     _setup(rank, world, port)
     import torch.distributed as dist
@@ -52,6 +61,7 @@ def _w_grad_avg(rank, world, port, q):
     local = [torch.autograd.grad(torch.nn.functional.cross_entropy(m(x), y), list(m.parameters()))]
     loss = torch.nn.functional.cross_entropy(ddp(x), y)
     loss.backward()
+    _native_host(ddp, world)
     for g_local, p in zip(local[0], m.parameters()):
         avg = g_local.clone()
         dist.all_reduce(avg)
@@ -253,6 +263,7 @@ def _w_rebuild_and_hooks(rank, world, port, q):
         for p in m.parameters():
             p.grad = None
         torch.nn.functional.cross_entropy(ddp(x), y).backward()
+        _native_host(ddp, world)
         for r, p in zip(ref, m.parameters()):
             assert torch.allclose(p.grad, r, atol=1e-6)
     # rebuilt once, from the observed ready order (late.* last), identically on all ranks
@@ -268,6 +279,7 @@ def _w_rebuild_and_hooks(rank, world, port, q):
     for p in m.parameters():
         p.grad = None
     torch.nn.functional.cross_entropy(ddp(x), y).backward()
+    _native_host(ddp, world)  # bf16 compression on the native reducer's transport
     for r, p in zip(ref, m.parameters()):
         assert torch.allclose(p.grad, r, atol=2e-2, rtol=2e-2)
     calls = []
@@ -324,3 +336,30 @@ def test_train_runtime_options(tmp_path):
                  "--grad-accum", "2"])
     assert r.returncode == 0, r.stderr[-2000:]
     assert "Epoch 0 completed" in (r.stdout + r.stderr)
+
+
+def _w_dispatch_identical(rank, world, port, q):
+    """Every rank plans the same GEMM kernel / tile / K split for the same shape: the dispatch is a pure
+    function of the shape (no per-rank timing), so DDP replicas run identical math (reference DDP(model),
+    train.py:233)."""
+    _setup(rank, world, port)
+    import torch.distributed as dist
+
+    from distributed_pytorch_example_amd.ops._ext import ext, has_ext
+
+    if not has_ext():
+        q.put(("ok", rank))
+        return
+    C = ext()
+    shapes = [(8192, 2304, 768, True, True), (8192, 768, 3072, True, True), (8192, 768, 50304, True, False),
+              (2304, 768, 8192, False, False), (50304, 768, 8192, False, False), (1024, 1000, 2048, True, True)]
+    mine = [C.hgemm_plan(M, N, K, ak, bk, True, 2) for M, N, K, ak, bk in shapes]
+    allp = [None] * world
+    dist.all_gather_object(allp, mine)
+    assert all(p == allp[0] for p in allp), allp
+    q.put(("ok", rank))
+    dist.destroy_process_group()
+
+
+def test_gemm_dispatch_identical_across_ranks():
+    _spawn(_w_dispatch_identical, 2)
