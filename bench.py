@@ -45,10 +45,14 @@ def parse():
                     help="per-GPU batch (resnet50: 512 = BASELINE config 5's per-GPU batch, sized for 288 GB HBM; "
                          "gpt2: 8 seqs)")
     ap.add_argument("--seq-len", type=int, default=1024)
-    ap.add_argument("--bucket-mb", type=float, default=25.0)
-    ap.add_argument("--first-bucket-mb", type=float, default=1.0)
-    ap.add_argument("--last-bucket-mb", type=float, default=2.0,
-                    help="re-split the last-ready bucket (the all-reduce that cannot overlap backward) into <= this")
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="bucket cap (default: the 7-link xGMI policy of parallel/buckets.py)")
+    ap.add_argument("--first-bucket-mb", type=float, default=None)
+    ap.add_argument("--last-bucket-mb", type=float, default=None,
+                    help="re-split the last-ready bucket (the all-reduce that cannot overlap backward) into <= this "
+                         "(default: policy, 2 MiB; 0: off)")
+    ap.add_argument("--comm-max-channels", type=int, default=None,
+                    help="cap RCCL's channels (CUs a collective occupies while overlapping backward)")
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--optimizer", default=None)
     ap.add_argument("--lr", type=float, default=None)
@@ -71,7 +75,7 @@ def main():
     from distributed_pytorch_example_amd.ops import functional as Fx
 
     ensure_single_process_env()
-    rank, world, local_rank = pdist.init_process_group("auto")
+    rank, world, local_rank = pdist.init_process_group("auto", comm_max_channels=args.comm_max_channels)
     if world != args.gpus and rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
@@ -129,7 +133,9 @@ def main():
 
     fused_loss = args.model == "gpt2"
     ddp = DDP(model, bucket_cap_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb, force_comm=args.force_comm,
-              last_bucket_mb=args.last_bucket_mb)
+              last_bucket_mb="auto" if args.last_bucket_mb is None else (args.last_bucket_mb or None))
+    if "bucket_mb" in cfg:
+        cfg["bucket_mb"] = round(ddp.bucket_cap_bytes / 2**20, 2)
     opt = build_optimizer(opt_name, model.parameters(), lr=lr, weight_decay=wd)
 
     def step(i):

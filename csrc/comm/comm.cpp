@@ -150,6 +150,18 @@ void Communicator::barrier() {
   HIP_CHECK(hipStreamSynchronize(c10::hip::getCurrentHIPStream(device_).stream()));
 }
 
+uint64_t Communicator::register_buffer(void* ptr, size_t bytes) {
+  if (!comm_ || !ptr || bytes == 0) return 0;
+  void* h = nullptr;
+  const ncclResult_t r = ncclCommRegister(comm_, ptr, bytes, &h);
+  if (r != ncclSuccess || !h) return 0;
+  return (uint64_t)(uintptr_t)h;
+}
+
+void Communicator::deregister_buffer(uint64_t handle) {
+  if (comm_ && handle && !aborted_) (void)ncclCommDeregister(comm_, (void*)(uintptr_t)handle);
+}
+
 std::string Communicator::async_error() {
   ncclResult_t st = ncclSuccess;
   ncclResult_t r = ncclCommGetAsyncError(comm_, &st);
@@ -173,7 +185,8 @@ hipStream_t aux_stream(int device) { return (device >= 0 && device < 64) ? g_aux
 
 // ------------------------------------------------------------------ Reducer
 Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params, int64_t nparams,
-                 std::shared_ptr<Communicator> comm, bool timing, bool force, bool comm_bf16, bool sync_debug)
+                 std::shared_ptr<Communicator> comm, bool timing, bool force, bool comm_bf16, bool sync_debug,
+                 bool register_buckets)
     : buckets_(std::move(buckets)), bparams_(std::move(bucket_params)), comm_(std::move(comm)), timing_(timing),
       force_(force), comm_bf16_(comm_bf16), sync_debug_(sync_debug) {
   for (auto& b : buckets_) TORCH_CHECK(b.is_cuda(), "bucket buffers must be GPU tensors (host transport: Reducer.host)");
@@ -198,6 +211,18 @@ Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_
   HIP_CHECK(hipEventCreateWithFlags(&ev_bwd_end_, flags));
   HIP_CHECK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&ev_step_begin_, flags));
+  // Register the buffers RCCL actually moves (fp32 buckets, or their bf16 staging copies) once per
+  // (re)build; they live exactly as long as this reducer and are deregistered before release.
+  if (register_buckets && comm_ && (comm_->world() > 1 || force_)) {
+    auto& bufs = comm_bf16_ ? staging_ : buckets_;
+    for (auto& t : bufs) reg_handles_.push_back(comm_->register_buffer(t.data_ptr(), t.numel() * t.element_size()));
+  }
+}
+
+int64_t Reducer::registered_buffers() const {
+  int64_t n = 0;
+  for (uint64_t h : reg_handles_) n += h != 0;
+  return n;
 }
 
 Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params, int64_t nparams,
@@ -228,6 +253,8 @@ void Reducer::init_tracking(int64_t nparams) {
 
 Reducer::~Reducer() {
   if (host_launch_) return;  // no HIP objects in host-transport mode
+  if (comm_)
+    for (uint64_t h : reg_handles_) comm_->deregister_buffer(h);
   for (auto* v : {&ev_ready_, &ev_aux_, &ev_start_, &ev_end_})
     for (auto e : *v) (void)hipEventDestroy(e);
   (void)hipEventDestroy(ev_bwd_end_);
@@ -353,12 +380,19 @@ void register_comm(pybind11::module& m) {
       .def("barrier", &Communicator::barrier)
       .def("async_error", &Communicator::async_error)
       .def("abort", &Communicator::abort)
-      .def("comm_stream_ptr", [](Communicator& c) { return (uint64_t)(uintptr_t)c.comm_stream().stream(); });
+      .def("comm_stream_ptr", [](Communicator& c) { return (uint64_t)(uintptr_t)c.comm_stream().stream(); })
+      .def("register_buffer", [](Communicator& c, const at::Tensor& t) {
+             TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "register_buffer: contiguous GPU tensor");
+             return c.register_buffer(t.data_ptr(), t.numel() * t.element_size());
+           }, "ncclCommRegister a tensor's bytes; returns a handle (0: RCCL declined)")
+      .def("deregister_buffer", &Communicator::deregister_buffer);
   py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
       .def(py::init<std::vector<at::Tensor>, std::vector<std::vector<int64_t>>, int64_t, std::shared_ptr<Communicator>, bool,
-                    bool, bool, bool>(),
+                    bool, bool, bool, bool>(),
            py::arg("buckets"), py::arg("bucket_params"), py::arg("nparams"), py::arg("comm"), py::arg("timing") = false,
-           py::arg("force") = false, py::arg("comm_bf16") = false, py::arg("sync_debug") = false)
+           py::arg("force") = false, py::arg("comm_bf16") = false, py::arg("sync_debug") = false,
+           py::arg("register_buckets") = true)
+      .def_property_readonly("registered_buffers", &Reducer::registered_buffers)
       .def_static("host", [](std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params,
                              int64_t nparams, int world, std::function<void(int64_t)> on_launch,
                              std::function<void()> on_finalize) {

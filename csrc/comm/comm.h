@@ -42,6 +42,12 @@ class Communicator {
   // Raw enqueue on the comm stream (no stream ordering): used by the reducer.
   void all_reduce_raw(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s);
 
+  // User-buffer registration (ncclCommRegister): RCCL may then move the buffer's bytes without
+  // staging through its internal FIFOs.  Returns an opaque handle, or 0 when RCCL declined
+  // (registration is an optimisation: never an error).  deregister(0) is a no-op.
+  uint64_t register_buffer(void* ptr, size_t bytes);
+  void deregister_buffer(uint64_t handle);
+
   // Non-blocking health check (ncclCommGetAsyncError); returns error string or "".
   std::string async_error();
   void abort();
@@ -77,7 +83,7 @@ class Reducer {
   //   stream-ordering assertion mode).
   Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_t>> bucket_params, int64_t nparams,
           std::shared_ptr<Communicator> comm, bool timing, bool force = false, bool comm_bf16 = false,
-          bool sync_debug = false);
+          bool sync_debug = false, bool register_buckets = true);
   // Host-transport mode: the same readiness tracking / index-order issue / finalize sequencing with
   // the collective itself delegated to `on_launch(bucket)` and `on_finalize()` (the gloo control
   // plane on CPU, world >= 1).  No HIP call is made in this mode, so it runs on a GPU-less host.
@@ -90,6 +96,7 @@ class Reducer {
   // (bucket, comm_ms, issued_before_backward_end) for the last finalized step
   std::vector<std::tuple<int64_t, double, double>> last_timings();
   int64_t num_buckets() const { return (int64_t)buckets_.size(); }
+  int64_t registered_buffers() const;
   int world() const { return host_launch_ ? host_world_ : (comm_ ? comm_->world() : 1); }
   bool host_mode() const { return (bool)host_launch_; }
   int64_t buckets_launched() const { return next_; }
@@ -112,6 +119,7 @@ class Reducer {
   std::vector<hipEvent_t> ev_ready_, ev_aux_, ev_start_, ev_end_;
   hipEvent_t ev_bwd_end_ = nullptr, ev_done_ = nullptr, ev_step_begin_ = nullptr;
   bool step_open_ = false;
+  std::vector<uint64_t> reg_handles_;  // ncclCommRegister handles of the buckets / bf16 staging buffers
   std::function<void(int64_t)> host_launch_;
   std::function<void()> host_finalize_;
   int host_world_ = 1;

@@ -57,7 +57,7 @@ import torch.nn as nn
 
 from . import dist as pdist
 from . import hooks as _hooks
-from .buckets import assign_buckets
+from .buckets import assign_buckets, xgmi_bucket_policy
 from ..utils.logging import get_logger
 from ..ops._state import aux_wait as _aux_wait
 
@@ -200,11 +200,11 @@ class _GlooTransport:
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers: bool = True,
-                 bucket_cap_mb: Optional[float] = 25.0, first_bucket_mb: float = 1.0,
+                 bucket_cap_mb: Optional[float] = None, first_bucket_mb: Optional[float] = None,
                  find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
                  init_sync: bool = True, timing: bool = False, comm=None, force_comm: bool = False,
                  gradient_compression: Optional[str] = None, rebuild_buckets: bool = True,
-                 debug: Optional[bool] = None, last_bucket_mb: Optional[float] = 2.0):
+                 debug: Optional[bool] = None, last_bucket_mb="auto", register_buckets: bool = True):
         super().__init__()
         self.module = module
         self.broadcast_buffers = broadcast_buffers
@@ -213,12 +213,17 @@ class DistributedDataParallel(nn.Module):
         self.world_size = pdist.get_world_size()
         self._params = [p for p in module.parameters() if p.requires_grad]
         self._index = {id(p): i for i, p in enumerate(self._params)}
-        cap = int((bucket_cap_mb if bucket_cap_mb is not None else 25.0) * 1024 * 1024)
-        first = int(first_bucket_mb * 1024 * 1024) if first_bucket_mb else cap
+        # bucket caps: explicit values win; otherwise the 7-link xGMI policy (buckets.xgmi_bucket_policy)
+        p_first, p_cap, p_last = xgmi_bucket_policy(self.world_size, 4 * sum(p.numel() for p in self._params))
+        cap = int((bucket_cap_mb if bucket_cap_mb is not None else p_cap) * 1024 * 1024)
+        first_mb = p_first if first_bucket_mb is None else first_bucket_mb
+        first = int(first_mb * 1024 * 1024) if first_mb else cap
         self.bucket_cap_bytes, self.first_bucket_bytes = cap, first
         # the last-ready gradients (the only all-reduce that cannot overlap backward) go in
         # small buckets: at 8 GPUs only the final <= last_bucket_mb piece is exposed
-        self.last_bucket_bytes = int(last_bucket_mb * 1024 * 1024) if last_bucket_mb else None
+        last_mb = p_last if last_bucket_mb == "auto" else last_bucket_mb
+        self.last_bucket_bytes = int(last_mb * 1024 * 1024) if last_mb else None
+        self._register = register_buckets
         self._comm = comm if comm is not None else pdist.comm()
         self._force = force_comm
         self._timing = timing
@@ -302,7 +307,7 @@ class DistributedDataParallel(nn.Module):
             from ..ops._ext import ext
 
             self.reducer = ext().Reducer(self.buckets, self.bucket_indices, len(self._params), self._comm, self._timing,
-                                         self._force, self._compression == "bf16", self._debug)
+                                         self._force, self._compression == "bf16", self._debug, self._register)
             self._native = True
         elif self._hook is None and _has_ext():
             # gloo / CPU: the C++ reducer in host-transport mode (same sequencing as the RCCL path)

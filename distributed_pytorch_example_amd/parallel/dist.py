@@ -28,7 +28,7 @@ from ..utils.logging import get_logger
 
 log = get_logger(__name__)
 
-_state = {"backend": None, "comm": None, "device": None}
+_state = {"backend": None, "comm": None, "device": None, "max_channels": None}
 
 
 def resolve_backend(backend: str) -> str:
@@ -44,10 +44,25 @@ def resolve_backend(backend: str) -> str:
     return b
 
 
-def init_process_group(backend: str = "auto", timeout_s: float = 1800.0) -> tuple[int, int, int]:
-    """Initialise the job.  Returns (rank, world_size, local_rank) like the reference's setup_distributed."""
+def init_process_group(backend: str = "auto", timeout_s: float = 1800.0,
+                       comm_max_channels: Optional[int] = None) -> tuple[int, int, int]:
+    """Initialise the job.  Returns (rank, world_size, local_rank) like the reference's setup_distributed.
+
+    ``comm_max_channels`` (or env ``DPE_RCCL_MAX_CHANNELS``): cap on RCCL's channels for the
+    communicator.  Every RCCL channel is one workgroup resident on a CU for the duration of a
+    collective, so while bucket all-reduces overlap backward this bounds how many of the 256 CUs
+    the communication can take from the compute kernels.  Applied through
+    ``NCCL_MAX_NCHANNELS`` before ``ncclCommInitRank`` (read once at communicator creation)."""
     env = read_env()
     backend = resolve_backend(backend)
+    if comm_max_channels is None and os.environ.get("DPE_RCCL_MAX_CHANNELS"):
+        comm_max_channels = int(os.environ["DPE_RCCL_MAX_CHANNELS"])
+    if comm_max_channels:
+        n = max(1, int(comm_max_channels))
+        os.environ["NCCL_MAX_NCHANNELS"] = str(n)
+        if int(os.environ.get("NCCL_MIN_NCHANNELS", "0") or 0) > n:
+            os.environ["NCCL_MIN_NCHANNELS"] = str(n)
+        _state["max_channels"] = n
     if not dist.is_initialized():
         dist.init_process_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s))
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -75,6 +90,11 @@ def _make_comm(rank: int, world: int, local_rank: int):
         uid = store.get(key)
     comm = C.Communicator(bytes(uid), rank, world, local_rank)
     return comm
+
+
+def comm_max_channels() -> Optional[int]:
+    """The RCCL channel cap this process initialised with (None: RCCL's own choice)."""
+    return _state["max_channels"]
 
 
 def backend() -> Optional[str]:

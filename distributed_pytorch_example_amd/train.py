@@ -49,9 +49,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--backend", default="auto", choices=["auto", "rccl", "nccl", "gloo"])
     p.add_argument("--optimizer", default=None, choices=[None, "adam", "adamw", "sgd"])
     p.add_argument("--weight-decay", type=float, default=0.0)
-    p.add_argument("--bucket-mb", type=float, default=25.0)
-    p.add_argument("--last-bucket-mb", type=float, default=2.0,
-                   help="re-split the last-ready gradient bucket into pieces of at most this size (0: off)")
+    p.add_argument("--bucket-mb", type=float, default=None,
+                   help="gradient bucket cap (default: the 7-link xGMI policy, parallel/buckets.py)")
+    p.add_argument("--last-bucket-mb", type=float, default=None,
+                   help="re-split the last-ready gradient bucket into pieces of at most this size (0: off; "
+                        "default: policy, 2 MiB)")
+    p.add_argument("--comm-max-channels", type=int, default=None,
+                   help="cap RCCL's channels (= CUs a collective occupies while it overlaps backward)")
     p.add_argument("--grad-accum", type=int, default=1)
     p.add_argument("--seed", type=int, default=None, help="seed the synthetic data (reference: unseeded)")
     p.add_argument("--loader", default="auto", choices=["auto", "device", "torch"])
@@ -145,7 +149,7 @@ def validate(model, loader, criterion, device, num_classes, max_steps=None):
 def main(argv=None):
     args = build_parser().parse_args(argv)
     ensure_single_process_env()
-    rank, world_size, local_rank = pdist.init_process_group(args.backend)
+    rank, world_size, local_rank = pdist.init_process_group(args.backend, comm_max_channels=args.comm_max_channels)
     logger.info(f"Initialized process group: rank={rank}, world_size={world_size}, local_rank={local_rank}")
     device = pdist.get_device(local_rank)
 
@@ -153,7 +157,8 @@ def main(argv=None):
     logger.info(f"Configuration: epochs={args.epochs}, batch_size={args.batch_size}, lr={args.lr}")
 
     model = get_model(args.model).to(device)
-    model = DDP(model, bucket_cap_mb=args.bucket_mb, last_bucket_mb=args.last_bucket_mb or None,
+    model = DDP(model, bucket_cap_mb=args.bucket_mb,
+                last_bucket_mb="auto" if args.last_bucket_mb is None else (args.last_bucket_mb or None),
                 gradient_compression=None if args.gradient_compression == "none" else args.gradient_compression,
                 debug=args.ddp_debug or None)
     if args.roctx:

@@ -39,6 +39,9 @@ def avg_local_grads(m, x, y, world):
 def main():
     rank, world, _ = pdist.init_process_group("rccl")
     dev = torch.device("cuda", 0)
+    if os.environ.get("DPE_RCCL_MAX_CHANNELS"):  # channel cap applied before ncclCommInitRank
+        assert pdist.comm_max_channels() == int(os.environ["DPE_RCCL_MAX_CHANNELS"])
+        assert os.environ["NCCL_MAX_NCHANNELS"] == os.environ["DPE_RCCL_MAX_CHANNELS"]
     torch.manual_seed(100 + rank)  # different init per rank: DDP's init broadcast (RCCL) must align them
     m = resnet18_like(num_classes=10).to(dev)
     ref = copy.deepcopy(m)  # plain-autograd twin (copied before DDP attaches bucket views / hooks)
@@ -102,7 +105,8 @@ def main():
     assert t.item() == 3.0
     pdist.barrier()
     assert pdist.check_health() == ""
-    print(f"rank {rank} ok: world-2 RCCL reducer, max rel err {max(checks):.2e}", flush=True)
+    print(f"rank {rank} ok: world-2 RCCL reducer, max rel err {max(checks):.2e}, "
+          f"{ddp.reducer.registered_buffers}/{ddp.num_buckets()} bucket buffers ncclCommRegister'ed", flush=True)
     pdist.destroy_process_group()
 
 

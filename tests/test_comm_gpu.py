@@ -140,3 +140,32 @@ def _check_wgrad_side_stream(resnet18_like, _state, Fx, DDP):
         assert _state._aux_streams, "side stream was not used"
         for (n, a), b in zip(m1.named_parameters(), early):
             assert ((a.grad - b).norm() / (a.grad.norm() + 1e-12)).item() < 2e-2, n
+
+
+def test_bucket_registration_world1(C, comm):
+    """ncclCommRegister of the flat buckets: the reducer registers them at
+    (re)build and deregisters before release; gradients are unchanged with registration on."""
+    from distributed_pytorch_example_amd.models import resnet18_like
+    from distributed_pytorch_example_amd.ops import functional as Fx
+    from distributed_pytorch_example_amd.parallel import DDP
+
+    t = torch.zeros(1 << 20, device=dev)
+    h = comm.register_buffer(t)
+    comm.deregister_buffer(h)  # 0 (declined) is a no-op as well
+    torch.manual_seed(4)
+    m1 = resnet18_like(num_classes=10).to(dev)
+    m2 = copy.deepcopy(m1)
+    ddp = DDP(m2, comm=comm, force_comm=True, bucket_cap_mb=2, register_buckets=True)
+    assert 0 <= ddp.reducer.registered_buffers <= ddp.num_buckets()
+    x = torch.randn(8, 3, 32, 32, device=dev)
+    y = torch.randint(0, 10, (8,), device=dev)
+    Fx.cross_entropy(m1(x), y).backward()
+    for _ in range(2):  # second step: rebuilt (re-registered) buckets
+        for p in m2.parameters():
+            p.grad = None
+        Fx.cross_entropy(ddp(x), y).backward()
+    torch.cuda.synchronize()
+    assert comm.async_error() == ""
+    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert ((a.grad - b.grad).norm() / (a.grad.norm() + 1e-12)).item() < 2e-2, n
+    print(f"registered {ddp.reducer.registered_buffers}/{ddp.num_buckets()} buckets")

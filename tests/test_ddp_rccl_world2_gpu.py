@@ -37,7 +37,8 @@ def test_native_reducer_world2_rccl():
         env.update({"RANK": str(r), "WORLD_SIZE": "2", "LOCAL_RANK": "0", "LOCAL_WORLD_SIZE": "2",
                     "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "PYTHONPATH": ROOT,
                     "NCCL_HOSTID": f"dpe-test-host-{r}", "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1",
-                    "HSA_ENABLE_IPC_MODE_LEGACY": "0", "OMP_NUM_THREADS": "1"})
+                    "HSA_ENABLE_IPC_MODE_LEGACY": "0", "OMP_NUM_THREADS": "1",
+                    "DPE_RCCL_MAX_CHANNELS": "4"})  # the CU cap for overlapped collectives, exercised
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "_rccl_world2_worker.py")],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
@@ -51,3 +52,5 @@ def test_native_reducer_world2_rccl():
     codes = [p.returncode for p in procs]
     assert codes == [0, 0], "\n".join(o[-3000:] for o in outs)
     assert all("ok: world-2 RCCL reducer" in o for o in outs)
+    for o in outs:
+        print([ln for ln in o.splitlines() if "ok: world-2" in ln][0])
