@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--force-comm", action="store_true",
                     help="run the RCCL bucket all-reduces even at world size 1 (reducer/overlap mechanics check)")
     ap.add_argument("--nbatches", type=int, default=4, help="distinct synthetic batches cycled")
+    ap.add_argument("--dtype", default=None, choices=[None, "fp32", "bf16"],
+                    help="simplenet compute dtype (default fp32, the reference's); resnet50/gpt2 are bf16")
     return ap.parse_args()
 
 
@@ -121,13 +123,15 @@ def main():
         num_classes = V
     else:
         bs = args.batch_size or 64
-        model = get_model("simplenet").to(dev)
+        sdt = args.dtype or "fp32"
+        model = get_model("simplenet", compute_dtype=sdt).to(dev)
         opt_name, lr = args.optimizer or "adam", args.lr or 1e-3
         wd = 0.0
         xs = [torch.randn(bs, 784, device=dev) for _ in range(args.nbatches)]
         ys = [torch.randint(0, 10, (bs,), device=dev) for _ in range(args.nbatches)]
         samples_per_step = bs * args.grad_accum
-        cfg = {"model": "simplenet-mlp", "global_batch": bs * world, "seq_len": None, "parallelism": f"dp{world}"}
+        cfg = {"model": "simplenet-mlp", "global_batch": bs * world, "seq_len": None, "parallelism": f"dp{world}",
+               "compute_dtype": sdt}
         metric, unit = "samples/sec (whole node), SimpleNet MLP", "samples/s"
         num_classes = 10
 
@@ -197,7 +201,8 @@ def main():
     if rank == 0:
         line = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-                "vs_baseline": None, "dtype": "bf16" if dev.type == "cuda" else "fp32",
+                "vs_baseline": None,
+                "dtype": ("bf16" if args.model != "simplenet" else sdt) if dev.type == "cuda" else "fp32",
                 "data": "synthetic (device-resident, random)",
                 "config": cfg, "loss": float(loss.item())}
         line.update(extra)

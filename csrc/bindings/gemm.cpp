@@ -121,7 +121,70 @@ int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_by
   return pl.cfg;
 }
 
+}  // namespace dpe_gemm
+
+extern "C" int dpe_gemm_f32(const float* A, const float* B, float* C, int64_t sam, int64_t sak, int64_t sbk, int64_t sbn,
+                            int64_t ldc, int M, int N, int K, const float* bias, float alpha, int relu, float drop_p,
+                            uint64_t seed, uint64_t offset, const float* mask_src, float mask_scale, int accumulate,
+                            hipStream_t st);
+
+namespace dpe_gemm {
 namespace {
+
+// ------------------------------------------------ fp32 Linear (exact-f32 MFMA, gemm_f32.hip)
+void check_f32(const Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), what,
+              " must be a contiguous fp32 GPU tensor");
+}
+void launch_f32(int rc) {
+  const hipError_t e = hipGetLastError();
+  TORCH_CHECK(rc == 0 && e == hipSuccess, "gemm_f32 launch failed rc=", rc, " ", hipGetErrorString(e));
+}
+
+// y[M,N] = dropout(relu(x[M,K] w[N,K]^T + b))  (relu / dropout optional; dropout mask = dpe_dropout's)
+Tensor linear32_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool relu, double drop_p,
+                    int64_t seed, int64_t offset) {
+  check_f32(x, "x"); check_f32(w, "w");
+  const int64_t K = x.size(-1), N = w.size(0), M = x.numel() / K;
+  TORCH_CHECK(w.size(1) == K, "linear32_fwd: weight shape mismatch");
+  const float* b = nullptr;
+  if (bias && bias->defined()) { check_f32(*bias, "bias"); b = (const float*)bias->data_ptr(); }
+  auto sizes = x.sizes().vec();
+  sizes.back() = N;
+  Tensor y = at::empty(sizes, x.options());
+  launch_f32(dpe_gemm_f32((const float*)x.data_ptr(), (const float*)w.data_ptr(), (float*)y.data_ptr(), K, 1, 1, K, N,
+                          (int)M, (int)N, (int)K, b, 1.f, relu, (float)drop_p, (uint64_t)seed, (uint64_t)offset, nullptr,
+                          1.f, 0, cur_stream()));
+  return y;
+}
+
+// dx[M,K] = (dy[M,N] w[N,K]) * (mask_src > 0) * mask_scale   (mask_src: the previous layer's output)
+Tensor linear32_dgrad(const Tensor& dy, const Tensor& w, const c10::optional<Tensor>& mask_src, double mask_scale) {
+  check_f32(dy, "dy"); check_f32(w, "w");
+  const int64_t N = w.size(0), K = w.size(1), M = dy.numel() / N;
+  TORCH_CHECK(dy.size(-1) == N, "linear32_dgrad: shape mismatch");
+  const float* ms = nullptr;
+  if (mask_src && mask_src->defined()) {
+    check_f32(*mask_src, "mask_src");
+    TORCH_CHECK(mask_src->numel() == M * K, "linear32_dgrad: mask_src shape mismatch");
+    ms = (const float*)mask_src->data_ptr();
+  }
+  auto sizes = dy.sizes().vec();
+  sizes.back() = K;
+  Tensor dx = at::empty(sizes, dy.options());
+  launch_f32(dpe_gemm_f32((const float*)dy.data_ptr(), (const float*)w.data_ptr(), (float*)dx.data_ptr(), N, 1, K, 1, K,
+                          (int)M, (int)K, (int)N, nullptr, 1.f, 0, 0.f, 0, 0, ms, (float)mask_scale, 0, cur_stream()));
+  return dx;
+}
+
+// dw[N,K] += alpha * dy[M,N]^T x[M,K]
+void linear32_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha) {
+  check_f32(dy, "dy"); check_f32(x, "x"); check_f32(dw, "dw");
+  const int64_t N = dw.size(0), K = dw.size(1), M = dy.numel() / N;
+  TORCH_CHECK(dy.size(-1) == N && x.size(-1) == K && x.numel() / K == M, "linear32_wgrad: shape mismatch");
+  launch_f32(dpe_gemm_f32((const float*)dy.data_ptr(), (const float*)x.data_ptr(), (float*)dw.data_ptr(), 1, N, K, 1, K,
+                          (int)N, (int)K, (int)M, nullptr, (float)alpha, 0, 0.f, 0, 0, nullptr, 1.f, 1, cur_stream()));
+}
 
 // Raw entry for tests and benchmarks: C (M x N, ldc) from A / B with explicit layouts.
 Tensor hgemm_raw(const Tensor& A, const Tensor& B, Tensor C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
@@ -178,6 +241,13 @@ void register_gemm(pybind11::module& m) {
           return std::make_tuple(p.cfg, p.splits, p.kps, p.grid, p.est_s * 1e6);
         }, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("a_k"), py::arg("b_k"), py::arg("allow_split") = true,
         py::arg("out_bytes") = 2, "the planner's (cfg, splits, k per split, grid, estimated us) for a GEMM");
+  m.def("linear32_fwd", &linear32_fwd, py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("relu") = false,
+        py::arg("drop_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0,
+        "fp32 Linear on the exact-f32 MFMA: dropout(relu(x w^T + b)), mask identical to dropout()");
+  m.def("linear32_dgrad", &linear32_dgrad, py::arg("dy"), py::arg("w"), py::arg("mask_src") = py::none(),
+        py::arg("mask_scale") = 1.0, "fp32 dy w, times (mask_src > 0) * mask_scale (relu+dropout backward)");
+  m.def("linear32_wgrad", &linear32_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("alpha") = 1.0,
+        "fp32 dw += alpha dy^T x");
   m.def("set_hgemm_force", [](int64_t cfg, int64_t splits) { g_force_cfg = (int)cfg; g_force_splits = (int)splits; },
         py::arg("cfg") = -1, py::arg("splits") = -1, "pin the planner's tile / split (-1: free); A/B testing only");
 }

@@ -47,6 +47,9 @@ def build_parser() -> argparse.ArgumentParser:
     # ---- additive
     p.add_argument("--model", default="simplenet", choices=["simplenet", "resnet50", "resnet_tiny", "gpt2", "gpt2-tiny"])
     p.add_argument("--backend", default="auto", choices=["auto", "rccl", "nccl", "gloo"])
+    p.add_argument("--dtype", default=None, choices=[None, "fp32", "bf16"],
+                   help="compute dtype on the GPU (default: fp32 for simplenet as the reference, bf16 otherwise; "
+                        "fp32 masters and gradients always)")
     p.add_argument("--optimizer", default=None, choices=[None, "adam", "adamw", "sgd"])
     p.add_argument("--weight-decay", type=float, default=0.0)
     p.add_argument("--bucket-mb", type=float, default=None,
@@ -146,6 +149,15 @@ def validate(model, loader, criterion, device, num_classes, max_steps=None):
 
 
 @record
+def _dtype_kw(args) -> dict:
+    """--dtype -> model kwargs: SimpleNet runs fp32 (reference) or bf16; the BASELINE-scope models are bf16."""
+    if args.model == "simplenet":
+        return {"compute_dtype": args.dtype or "fp32"}
+    if args.dtype == "fp32":
+        raise SystemExit(f"--dtype fp32 is implemented for simplenet only ({args.model} runs bf16 with fp32 masters)")
+    return {}
+
+
 def main(argv=None):
     args = build_parser().parse_args(argv)
     ensure_single_process_env()
@@ -156,7 +168,7 @@ def main(argv=None):
     logger.info(f"Starting distributed training with {world_size} processes")
     logger.info(f"Configuration: epochs={args.epochs}, batch_size={args.batch_size}, lr={args.lr}")
 
-    model = get_model(args.model).to(device)
+    model = get_model(args.model, **_dtype_kw(args)).to(device)
     model = DDP(model, bucket_cap_mb=args.bucket_mb,
                 last_bucket_mb="auto" if args.last_bucket_mb is None else (args.last_bucket_mb or None),
                 gradient_compression=None if args.gradient_compression == "none" else args.gradient_compression,
