@@ -166,7 +166,12 @@ class Watchdog:
     ``timeout_s`` (a peer died mid-collective, a hang), it logs, aborts the
     communicator (``ncclCommAbort`` releases ranks blocked in collectives) and
     exits the process non-zero so the launcher's fail-fast path tears the job
-    down -- instead of the reference's 30-minute gloo timeout."""
+    down -- instead of the reference's 30-minute gloo timeout.
+
+    The training loop beats every step and every validation batch; checkpoint
+    writes and the barrier behind them run under ``suspended()``.  The timeout
+    must still cover the first training step (kernel/module load, bucket build).
+    GEMM dispatch is planned analytically, so there is no autotuning pause."""
 
     def __init__(self, timeout_s: float = 600.0, interval_s: float = 2.0, on_fail=None):
         import threading
@@ -176,6 +181,7 @@ class Watchdog:
         self._time = time
         self._last = time.monotonic()
         self._stop = threading.Event()
+        self._paused = 0
         self._on_fail = on_fail
         self.failure: Optional[str] = None
         self._thread = threading.Thread(target=self._run, name="dpe-watchdog", daemon=True)
@@ -184,6 +190,22 @@ class Watchdog:
     def beat(self) -> None:
         self._last = self._time.monotonic()
 
+    def suspended(self):
+        """Context: no stall check inside (checkpoint writes, the barrier behind them); RCCL async
+        errors are still polled.  The heartbeat restarts when the block ends."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def _ctx():
+            self._paused += 1
+            try:
+                yield self
+            finally:
+                self._paused -= 1
+                self.beat()
+
+        return _ctx()
+
     def stop(self) -> None:
         self._stop.set()
         self._thread.join(timeout=5)
@@ -191,7 +213,7 @@ class Watchdog:
     def _run(self):
         while not self._stop.wait(self.interval_s):
             err = check_health()
-            stalled = self._time.monotonic() - self._last
+            stalled = 0.0 if self._paused else self._time.monotonic() - self._last
             if err or stalled > self.timeout_s:
                 self.failure = f"RCCL async error: {err}" if err else f"no progress for {stalled:.0f}s"
                 log.error(f"watchdog: {self.failure}; aborting communicator")

@@ -101,12 +101,15 @@ def train_epoch(model, loader, optimizer, criterion, device, epoch, rank, grad_a
     total_loss = torch.zeros((), dtype=torch.float64, device=device)
     num_batches = 0
     nb = len(loader)
+    # the epoch's last micro-batch always syncs and steps, also when --max-steps cuts the epoch
+    # short: leftover no_sync gradients must not leak into the next epoch's first update
+    n_eff = min(nb, max_steps) if max_steps is not None else nb
     for batch_idx, (data, target) in enumerate(loader):
         if max_steps is not None and batch_idx >= max_steps:
             break
         fault.maybe_inject(epoch, batch_idx)
         data, target = data.to(device, non_blocking=True), target.to(device, non_blocking=True)
-        sync = (batch_idx + 1) % grad_accum == 0 or batch_idx + 1 == nb
+        sync = (batch_idx + 1) % grad_accum == 0 or batch_idx + 1 == n_eff
         ctx = model.no_sync() if (not sync and hasattr(model, "no_sync")) else _null()
         with ctx:
             with tracing.range("forward"):
@@ -128,7 +131,7 @@ def train_epoch(model, loader, optimizer, criterion, device, epoch, rank, grad_a
 
 
 @torch.no_grad()
-def validate(model, loader, criterion, device, num_classes, max_steps=None):
+def validate(model, loader, criterion, device, num_classes, max_steps=None, watchdog=None):
     """Reference `validate` (`train.py:154-175`): mean of per-batch losses, accuracy in %."""
     model.eval()
     total_loss = torch.zeros((), dtype=torch.float64, device=device)
@@ -145,10 +148,11 @@ def validate(model, loader, criterion, device, num_classes, max_steps=None):
         correct += c
         total += target.numel()
         nbatches += 1
+        if watchdog is not None:
+            watchdog.beat()
     return (total_loss / max(1, nbatches)).item(), (100.0 * correct / max(1, total)).item()
 
 
-@record
 def _dtype_kw(args) -> dict:
     """--dtype -> model kwargs: SimpleNet runs fp32 (reference) or bf16; the BASELINE-scope models are bf16."""
     if args.model == "simplenet":
@@ -158,6 +162,7 @@ def _dtype_kw(args) -> dict:
     return {}
 
 
+@record
 def main(argv=None):
     args = build_parser().parse_args(argv)
     ensure_single_process_env()
@@ -211,7 +216,7 @@ def main(argv=None):
         train_sampler.set_epoch(epoch)
         train_loss = train_epoch(model, train_loader, optimizer, criterion, device, epoch, rank, args.grad_accum,
                                  args.max_steps, watchdog)
-        val_loss, val_accuracy = validate(model, val_loader, criterion, device, num_classes, args.max_steps)
+        val_loss, val_accuracy = validate(model, val_loader, criterion, device, num_classes, args.max_steps, watchdog)
 
         metrics = torch.tensor([train_loss, val_loss, val_accuracy], device=device)
         pdist.all_reduce(metrics, "sum")
@@ -219,6 +224,9 @@ def main(argv=None):
         avg_train_loss, avg_val_loss, avg_val_accuracy = (v.item() for v in metrics)
 
         epoch_time = time.time() - epoch_start
+        # rank 0 writes checkpoints while the others wait in the barrier: no step heartbeat there
+        wd_pause = watchdog.suspended() if watchdog is not None else _null()
+        wd_pause.__enter__()
         if rank == 0:
             logger.info(f"Epoch {epoch} completed in {epoch_time:.2f}s")
             logger.info(f"  Train Loss: {avg_train_loss:.4f}")
@@ -234,6 +242,7 @@ def main(argv=None):
         if prof is not None:
             prof.step()
         pdist.barrier()
+        wd_pause.__exit__(None, None, None)
 
     wait_pending()
     if watchdog is not None:

@@ -51,3 +51,55 @@ def test_launcher_worker_env():
     assert env["LOCAL_WORLD_SIZE"] == "4" and env["GROUP_RANK"] == "1"
     assert env["MASTER_ADDR"] == "h0" and env["MASTER_PORT"] == "777" and env["OMP_NUM_THREADS"] == "1"
     assert a.script == "t.py" and a.script_args == ["--x"]
+
+
+def test_grad_accum_syncs_at_max_steps_cutoff():
+    """with --max-steps not a multiple of --grad-accum the epoch's last micro-batch still
+    syncs and steps (no leftover no_sync gradients leaking into the next epoch)."""
+    import torch
+
+    from distributed_pytorch_example_amd.train import train_epoch
+
+    class Opt:
+        def __init__(self):
+            self.steps = []
+
+        def step(self):
+            self.steps.append(len(seen))
+
+        def zero_grad(self):
+            pass
+
+    class Model(torch.nn.Linear):
+        def no_sync(self):
+            import contextlib
+            return contextlib.nullcontext()
+
+    seen = []
+    m = Model(4, 2)
+    loader = [(torch.randn(3, 4), torch.randint(0, 2, (3,))) for _ in range(5)]
+
+    def crit(out, tgt):
+        seen.append(1)
+        return torch.nn.functional.cross_entropy(out, tgt)
+
+    opt = Opt()
+    train_epoch(m, loader, opt, crit, torch.device("cpu"), 0, 1, grad_accum=2, max_steps=3)
+    assert opt.steps == [2, 3]  # after micro-batch 2 (accum boundary) and after the cut-off batch 3
+
+
+def test_watchdog_suspended_during_checkpoint_and_barrier():
+    import time
+
+    from distributed_pytorch_example_amd.parallel.dist import Watchdog
+
+    fails = []
+    wd = Watchdog(timeout_s=0.3, interval_s=0.05, on_fail=fails.append)
+    try:
+        with wd.suspended():
+            time.sleep(0.8)  # a long checkpoint write: no stall reported
+        assert not fails
+        time.sleep(0.8)  # no heartbeat outside a suspended block: stall detected
+        assert fails and "no progress" in fails[0]
+    finally:
+        wd.stop()
