@@ -158,17 +158,6 @@ bool wgrad_dma_on() {
 }
 int g_wgrad_wide = [] { const char* e = getenv("DPE_WGRAD_WIDE"); return !(e && e[0] == '0'); }();  // 64x256 wgrad tile
 
-// LDS ring depth of the 4-wave (<= 128x128) DMA tiles: 2 (default: one K-step of loads in flight but
-// 2/3 of the LDS, so 4 instead of 3 blocks per CU -- measured ~10 % faster on 3x3 weight grads, neutral
-// on forward convs) or 3 (two K-steps in flight).  DPE_DMA_STAGES=2|3.  8-wave tiles keep 3.
-int dma_stages(int bm, int bn) {
-  static const int st = [] { const char* e = getenv("DPE_DMA_STAGES"); return (e && e[0] == '3') ? 3 : 2; }();
-  // DPE_DMA_PF=1: forward DMA kernels use the fragment-prefetch loop (3 buffers, "stages" 4)
-  static const bool pf = [] { const char* e = getenv("DPE_DMA_PF"); return e && e[0] == '1'; }();
-  if (pf && bm <= 128 && bn <= 128) return 4;  // (8-wave tiles: a second fragment set spills at 128 VGPRs)
-  return (bm <= 128 && bn <= 128) ? st : 3;
-}
-
 // DPE_WGRAD_DMA=2: dense 1x1 weight grads on the LDS-DMA kernel too (measured 10-15 % slower; A/B only)
 bool wgrad_dma_dense() {
   static const bool on = [] { const char* e = getenv("DPE_WGRAD_DMA"); return e && e[0] == '2'; }();
@@ -192,10 +181,8 @@ void dma_tile(const dpe::IgemmArgs& a, int aload, int bload, int& bm, int& bn) {
   int mode = dma_tile_mode();
   const bool taps = aload == dpe::A_CONV_FWD && a.g.R * a.g.S > 1;
   if (a.N <= 64) {  // N = 64: 256x64 only when forced (measured 240 -> 282 us on 64->64 3x3 at 56x56:
-    // 61 KiB LDS halves the blocks per CU) or, with DPE_DMA_W64=1, for short K (the s2d stem, K = 256),
-    // where every 128-row tile re-reading the whole filter is a third of the L2->LDS bytes
-    static const bool w64 = [] { const char* e = getenv("DPE_DMA_W64"); return e && e[0] == '1'; }();
-    if (mode >= 2 || (mode == 0 && w64 && a.K <= 256 && a.M >= (1 << 20))) { bm = 256; bn = 64; }
+    // 61 KiB LDS halves the blocks per CU; also slower on the short-K s2d stem, docs/perf_notes.md)
+    if (mode >= 2) { bm = 256; bn = 64; }
     return;
   }
   if (mode == 0) {
@@ -207,19 +194,7 @@ void dma_tile(const dpe::IgemmArgs& a, int aload, int bload, int& bm, int& bn) {
   else if (mode >= 2 && a.N > 64) { bm = 256; bn = 128; }
 }
 
-// DPE_EPI_NT_STORE=1: bf16 conv outputs larger than the 256 MiB Infinity Cache are written with
-// non-temporal stores (they are evicted before their consumer reads them anyway)
-bool epi_nt_store() {
-  static const bool on = [] { const char* e = getenv("DPE_EPI_NT_STORE"); return e && e[0] == '1'; }();
-  return on;
-}
-
 void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_split, bool conv = false) {
-  static const int mfma_prio = [] { const char* e = getenv("DPE_MFMA_PRIO"); return (e && e[0] == '1') ? 1 : 0; }();
-  a.mfma_prio = mfma_prio;
-  if (conv && (epi == dpe::EPI_BF16 || epi == dpe::EPI_BF16_BNB) && epi_nt_store() &&
-      (int64_t)a.M * a.ldc * 2 > (320ll << 20))
-    a.c_nt = 1;
   Cfg c = pick_cfg(a.M, a.N, a.K, allow_split && epi == dpe::EPI_ATOMIC_F32);
   a.k_split = c.k_split;
   // weight grads over an im2col B (3x3 / strided; split-K fp32 atomics): LDS-DMA kernel, measured 1.3-1.5x
@@ -239,7 +214,7 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
       a.k_split = (int)(kps * 32);
       splits = (int)((ksteps + kps - 1) / kps);
     }
-    const int rc = dpe_igemm_wgrad_dma_launch(&a, bm, bn, bload, splits, std::min(dma_stages(bm, bn), 3), cur_stream());
+    const int rc = dpe_igemm_wgrad_dma_launch(&a, bm, bn, bload, splits, cur_stream());
     a.k_split = c.k_split;  // (register-staged fallback uses pick_cfg's split)
     if (rc == 0) {
       const hipError_t e = hipGetLastError();
@@ -262,7 +237,7 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
     // (same tile shape, so BatchNorm partial layouts are unchanged)
     int bm = c.bm, bn = c.bn;
     dma_tile(a, aload, bload, bm, bn);
-    const int rc = dpe_igemm_dma_launch(&a, bm, bn, aload, bload, epi, dma_stages(bm, bn), cur_stream());
+    const int rc = dpe_igemm_dma_launch(&a, bm, bn, aload, bload, epi, cur_stream());
     if (rc == 0) {
       const hipError_t e = hipGetLastError();
       TORCH_CHECK(e == hipSuccess, "igemm_dma launch failed: ", hipGetErrorString(e));

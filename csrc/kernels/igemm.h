@@ -59,8 +59,6 @@ struct IgemmArgs {
                              //   8 columns ([M][ldc/8], bit e = column 8j+e, written by bn_apply), and
                              //   the STORED value is the masked dz, not v
   int res_nt;                // residual is at its last use: stream it (non-temporal loads)
-  int c_nt;                  // bf16 output far larger than the Infinity Cache: non-temporal stores
-  int mfma_prio;             // LDS-DMA kernels: s_setprio(1) around each K-step's MFMA cluster
   const uint8_t* res_mask;   // optional ReLU-mask bits ([M][ldc/8]) applied to the residual before the add
                              //   (residual = dy of a BN+residual+ReLU output: dz = dy * relu'(y) on the fly)
   int stats_ld;              // partial columns per channel (0 -> tilesM of this launch)
@@ -80,12 +78,12 @@ extern "C" int dpe_igemm_launch(const dpe::IgemmArgs* args, int bm, int bn, int 
                                 int splits, hipStream_t stream);
 
 // LDS-DMA implicit-GEMM (igemm.hip) for forward-form convolutions and dense K-contiguous A
-// (B K- or N-contiguous; EPI_BF16 / EPI_BF16_BNB, no split-K); stages: 2 or 3 (LDS ring depth;
-// 2 only for the 2x2-wave tiles).  -1: outside its envelope.
+// (B K- or N-contiguous; EPI_BF16 / EPI_BF16_BNB, no split-K); LDS ring depth 2 for tiles up to
+// 128x128 (4 blocks per CU), 3 for the 8-wave tiles.  -1: outside its envelope.
 extern "C" int dpe_igemm_dma_launch(const dpe::IgemmArgs* args, int bm, int bn, int aload, int bload, int epi,
-                                    int stages, hipStream_t stream);
+                                    hipStream_t stream);
 
 // LDS-DMA weight-grad kernel (igemm.hip): A = dy (A_DENSE_M), B = x (B_DENSE_N) or its im2col
 // (B_CONV_WGRAD), EPI_ATOMIC_F32 with split-K.  -1: outside its envelope.
 extern "C" int dpe_igemm_wgrad_dma_launch(const dpe::IgemmArgs* args, int bm, int bn, int bload, int splits,
-                                          int stages, hipStream_t stream);
+                                          hipStream_t stream);

@@ -394,8 +394,7 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* sm
       }
     }
     if (vec_row) {
-      if (p.c_nt) __builtin_nontemporal_store(v, (u32x4*)dst);
-      else *(u32x4*)dst = v;
+      *(u32x4*)dst = v;
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -865,13 +864,11 @@ void igemm_dma_kernel(IgemmArgs p, int a_dense) {
     }
   };
   auto mfmas = [&](const bf16x8 (&a)[RM], const bf16x8 (&b)[RN]) {
-    if (p.mfma_prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
       for (int j = 0; j < RN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
-    if (p.mfma_prio) __builtin_amdgcn_s_setprio(0);
   };
   auto barrier = [&]() {
     asm volatile("" ::: "memory");
@@ -879,37 +876,10 @@ void igemm_dma_kernel(IgemmArgs p, int a_dense) {
     asm volatile("" ::: "memory");
   };
 
-  if constexpr (NS == 4) {
-    // 3-buffer ring with fragment double-buffering: the wave reads stage t+1's fragments
-    // while its MFMAs consume stage t (already in registers); DMA runs 3 stages ahead of
-    // the MFMAs (stage t+3 is issued into stage t's buffer, free once every wave's reads
-    // of it retired -- lgkmcnt(0) before the barrier).
-    bf16x8 fa0[RM], fb0[RN], fa1[RM], fb1[RN];
-    if (nt > 0) issue(0);
-    if (nt > 1) issue(1);
-    if (nt > 2) issue(2);
-    if (nt > 2) wait_vm<2 * (PA + PB)>(); else if (nt > 1) wait_vm<PA + PB>(); else wait_vm<0>();
-    barrier();
-    if (nt > 0) read_frags(0, fa0, fb0);
-    auto step = [&](int t, const bf16x8 (&ca)[RM], const bf16x8 (&cb)[RN], bf16x8 (&na)[RM], bf16x8 (&nb)[RN]) {
-      if (t + 1 < nt) {
-        if (t + 2 < nt) wait_vm<PA + PB>(); else wait_vm<0>();  // stage t+1 landed (own DMA)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // own reads of stage t's buffer retired
-        barrier();
-        if (t + 3 < nt) issue((t + 3) % 3);
-        read_frags((t + 1) % 3, na, nb);
-      }
-      mfmas(ca, cb);
-    };
-    int t = 0;
-    for (; t + 1 < nt; t += 2) {
-      step(t, fa0, fb0, fa1, fb1);
-      step(t + 1, fa1, fb1, fa0, fb0);
-    }
-    if (t < nt) step(t, fa0, fb0, fa1, fb1);
-  } else {
+  {
     // NS-stage ring: stages t+1 .. t+NS-2 stay in flight while stage t is consumed
-    static_assert(NS == 2 || NS == 3, "2- or 3-stage ring (4: 3 buffers + fragment prefetch)");
+    // (a fragment-prefetch 3-buffer variant measured slower -- occupancy-bound: docs/perf_notes.md)
+    static_assert(NS == 2 || NS == 3, "2- or 3-stage ring");
     if (nt > 0) issue(0);
     if (NS == 3 && nt > 1) issue(1);
     for (int t = 0; t < nt; ++t) {
@@ -1064,13 +1034,11 @@ __global__ __launch_bounds__(NT) void igemm_wgrad_dma_kernel(IgemmArgs p) {
     for (int i = 0; i < RM; ++i) af[i] = mnfrag<BM>(As, wm + 16 * i);
 #pragma unroll
     for (int j = 0; j < RN; ++j) bfr[j] = mnfrag<BN>(Bs, wn + 16 * j);
-    if (p.mfma_prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll
       for (int j = 0; j < RN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    if (p.mfma_prio) __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();
   if (p.alpha_ptr) p.alpha *= *p.alpha_ptr;
@@ -1127,7 +1095,7 @@ extern "C" int dpe_igemm_launch(const IgemmArgs* args, int bm, int bn, int aload
 // LDS-DMA kernel for forward-form convolutions / dense K-contiguous A.  Returns -1
 // when the problem is outside its envelope (the caller then uses dpe_igemm_launch).
 extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int aload, int bload, int epi,
-                                    int stages, hipStream_t st) {
+                                    hipStream_t st) {
   const IgemmArgs& a = *args;
   if (a.M <= 0 || a.N <= 0) return 0;
   if (aload != A_DENSE_K && aload != A_CONV_FWD) return -1;
@@ -1147,15 +1115,9 @@ extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int a
   const int dn = dense ? 1 : 0;
 #define DPE_DMA(BM_, BN_, WGM_, WGN_, BL_, EP_)                                                             \
   if (bm == BM_ && bn == BN_ && bload == BL_ && epi == EP_) {                                               \
-    if (stages == 2)                                                                                        \
-      hipLaunchKernelGGL((igemm_dma_kernel<BM_, BN_, WGM_, WGN_, BL_, EP_, 2>), dim3(tiles),                 \
-                         dim3(64 * WGM_ * WGN_), 0, st, a, dn);                                             \
-    else if (stages == 4)                                                                                   \
-      hipLaunchKernelGGL((igemm_dma_kernel<BM_, BN_, WGM_, WGN_, BL_, EP_, 4>), dim3(tiles),                 \
-                         dim3(64 * WGM_ * WGN_), 0, st, a, dn);                                             \
-    else                                                                                                    \
-      hipLaunchKernelGGL((igemm_dma_kernel<BM_, BN_, WGM_, WGN_, BL_, EP_>), dim3(tiles),                    \
-                         dim3(64 * WGM_ * WGN_), 0, st, a, dn);                                             \
+    constexpr int NS_ = (BM_ <= 128 && BN_ <= 128) ? 2 : 3; /* 4 blocks/CU vs two K-steps in flight */      \
+    hipLaunchKernelGGL((igemm_dma_kernel<BM_, BN_, WGM_, WGN_, BL_, EP_, NS_>), dim3(tiles),                 \
+                       dim3(64 * WGM_ * WGN_), 0, st, a, dn);                                               \
     return 0;                                                                                               \
   }
 #define DPE_DMA_T(BL_, EP_) \
@@ -1179,7 +1141,7 @@ extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int a
 
 // LDS-DMA weight-grad kernel (A = dy M-contiguous; B = x or im2col(x) N-contiguous;
 // EPI_ATOMIC_F32, split-K).  -1: outside its envelope (caller uses dpe_igemm_launch).
-extern "C" int dpe_igemm_wgrad_dma_launch(const IgemmArgs* args, int bm, int bn, int bload, int splits, int stages,
+extern "C" int dpe_igemm_wgrad_dma_launch(const IgemmArgs* args, int bm, int bn, int bload, int splits,
                                           hipStream_t st) {
   const IgemmArgs& a = *args;
   if (a.M <= 0 || a.N <= 0) return 0;
@@ -1199,10 +1161,7 @@ extern "C" int dpe_igemm_wgrad_dma_launch(const IgemmArgs* args, int bm, int bn,
   const int tiles = ((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
 #define DPE_WG(BM_, BN_, BL_)                                                                                \
   if (bm == BM_ && bn == BN_ && bload == BL_) {                                                               \
-    if (stages == 2)                                                                                          \
-      hipLaunchKernelGGL((igemm_wgrad_dma_kernel<BM_, BN_, BL_, 2, 2, 2>), dim3(tiles * splits), dim3(NT), 0, st, a); \
-    else                                                                                                      \
-      hipLaunchKernelGGL((igemm_wgrad_dma_kernel<BM_, BN_, BL_>), dim3(tiles * splits), dim3(NT), 0, st, a);     \
+    hipLaunchKernelGGL((igemm_wgrad_dma_kernel<BM_, BN_, BL_, 2, 2, 2>), dim3(tiles * splits), dim3(NT), 0, st, a); \
     return 0;                                                                                                 \
   }
 #define DPE_WG_T(BL_) DPE_WG(128, 128, BL_) DPE_WG(128, 64, BL_) DPE_WG(64, 128, BL_) DPE_WG(64, 64, BL_)

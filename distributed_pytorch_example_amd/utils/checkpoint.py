@@ -14,8 +14,9 @@ Fixes for the two hazards the survey found:
   1. the resume file was opened per rank (only rank 0 ever writes it), and
   2. it was loaded *after* DDP's initial broadcast, so ranks could diverge.
 Here rank 0 alone reads the file and the model/optimizer state and epoch are
-broadcast to every rank over the control-plane process group; all ranks
-therefore resume identical state at the same epoch.  ``async_save`` writes
+broadcast to every rank (tensor bytes as one flat buffer per dtype over RCCL,
+only the small skeleton through the control plane); all ranks therefore
+resume identical state at the same epoch.  ``async_save`` writes
 from a background thread after snapshotting tensors to host memory.
 """
 from __future__ import annotations
@@ -89,6 +90,92 @@ def wait_pending() -> None:
         _pending.pop().join()
 
 
+class _TRef:
+    """Placeholder for tensor #i of a broadcast checkpoint (shape / dtype / 0-d host scalar)."""
+
+    __slots__ = ("i", "shape", "dtype", "host")
+
+    def __init__(self, i, shape, dtype, host):
+        self.i, self.shape, self.dtype, self.host = i, shape, dtype, host
+
+    def __reduce__(self):
+        return (_TRef, (self.i, self.shape, self.dtype, self.host))
+
+
+def _split_tensors(obj, out: list):
+    if torch.is_tensor(obj):
+        out.append(obj)
+        return _TRef(len(out) - 1, tuple(obj.shape), str(obj.dtype).replace("torch.", ""), obj.dim() == 0)
+    if isinstance(obj, dict):
+        return type(obj)((k, _split_tensors(v, out)) for k, v in obj.items())
+    if isinstance(obj, list):
+        return [_split_tensors(v, out) for v in obj]
+    if isinstance(obj, tuple):
+        return tuple(_split_tensors(v, out) for v in obj)
+    return obj
+
+
+def _join_tensors(obj, tensors: list):
+    if isinstance(obj, _TRef):
+        return tensors[obj.i]
+    if isinstance(obj, dict):
+        return type(obj)((k, _join_tensors(v, tensors)) for k, v in obj.items())
+    if isinstance(obj, list):
+        return [_join_tensors(v, tensors) for v in obj]
+    if isinstance(obj, tuple):
+        return tuple(_join_tensors(v, tensors) for v in obj)
+    return obj
+
+
+def broadcast_state(ckpt: Optional[dict], device: torch.device) -> dict:
+    """Rank 0's checkpoint to every rank: the tensor-free skeleton (keys, shapes, dtypes, numbers)
+    through the control plane, the tensor bytes as ONE flat buffer per dtype through
+    ``parallel.dist.broadcast`` -- RCCL over xGMI on GPU jobs, not a pickle through gloo."""
+    from ..parallel import dist as pdist
+
+    rank = dist.get_rank()
+    tensors: list = []
+    skel = _split_tensors(ckpt, tensors) if rank == 0 else None
+    box = [skel]
+    dist.broadcast_object_list(box, src=0)
+    skel = box[0]
+    refs: list = []
+    _collect_refs(skel, refs)
+    refs.sort(key=lambda r: r.i)
+    out = [None] * len(refs)
+    by_dtype: dict = {}
+    for r in refs:
+        by_dtype.setdefault(r.dtype, []).append(r)
+    for dt, rs in by_dtype.items():
+        tdt = getattr(torch, dt)
+        numels = [int(torch.Size(r.shape).numel()) for r in rs]
+        total = sum(numels)
+        if rank == 0:
+            flat = torch.cat([tensors[r.i].reshape(-1) for r in rs]).to(device) if total else \
+                torch.empty(0, dtype=tdt, device=device)
+        else:
+            flat = torch.empty(total, dtype=tdt, device=device)
+        if total:
+            pdist.broadcast(flat, 0)
+        off = 0
+        for r, n in zip(rs, numels):
+            t = flat[off: off + n].view(r.shape).clone()
+            out[r.i] = t.cpu() if r.host else t  # 0-d (optimizer step counters) stay host scalars
+            off += n
+    return _join_tensors(skel, out)
+
+
+def _collect_refs(obj, refs: list):
+    if isinstance(obj, _TRef):
+        refs.append(obj)
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            _collect_refs(v, refs)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            _collect_refs(v, refs)
+
+
 def load_checkpoint(model, optimizer, path: str, device: torch.device, broadcast: bool = True) -> int:
     """Rank 0 reads ``path`` (weights_only), every rank receives the same state.  Returns the epoch."""
     distributed = broadcast and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
@@ -97,9 +184,7 @@ def load_checkpoint(model, optimizer, path: str, device: torch.device, broadcast
     if rank == 0:
         ckpt = torch.load(path, map_location="cpu", weights_only=True)
     if distributed:
-        box = [ckpt]
-        dist.broadcast_object_list(box, src=0)
-        ckpt = box[0]
+        ckpt = broadcast_state(ckpt, device)
     unwrap(model).load_state_dict(ckpt["model_state_dict"])
     if optimizer is not None:
         optimizer.load_state_dict(ckpt["optimizer_state_dict"])

@@ -363,3 +363,32 @@ def _w_dispatch_identical(rank, world, port, q):
 
 def test_gemm_dispatch_identical_across_ranks():
     _spawn(_w_dispatch_identical, 2)
+
+
+def _w_broadcast_state(rank, world, port, q):
+    _setup(rank, world, port)
+    import torch.distributed as dist
+
+    from distributed_pytorch_example_amd.utils.checkpoint import broadcast_state
+
+    ck = None
+    if rank == 0:
+        torch.manual_seed(0)
+        ck = {"epoch": 3, "loss": 0.25, "model_state_dict": {"w": torch.randn(5, 7), "n": torch.tensor(4, dtype=torch.int64)},
+              "optimizer_state_dict": {"state": {0: {"step": torch.tensor(12.0), "exp_avg": torch.randn(5, 7)}},
+                                       "param_groups": [{"lr": 1e-3, "betas": (0.9, 0.999), "params": [0]}]}}
+    out = broadcast_state(ck, torch.device("cpu"))
+    mine = [out["model_state_dict"]["w"], out["optimizer_state_dict"]["state"][0]["exp_avg"]]
+    for t in mine:
+        ref = t.clone()
+        dist.broadcast(ref, 0)
+        assert torch.equal(t, ref)
+    assert out["epoch"] == 3 and out["optimizer_state_dict"]["param_groups"][0]["betas"] == (0.9, 0.999)
+    st = out["optimizer_state_dict"]["state"][0]["step"]
+    assert st.dim() == 0 and float(st) == 12.0 and out["model_state_dict"]["n"].dtype == torch.int64
+    q.put(("ok", rank))
+    dist.destroy_process_group()
+
+
+def test_resume_state_broadcast_as_flat_tensors():
+    _spawn(_w_broadcast_state, 2)
