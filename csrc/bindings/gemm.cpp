@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 
 #include "../kernels/hgemm.h"
 #include "../kernels/igemm.h"
@@ -97,12 +98,25 @@ Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int
   return best;
 }
 
+// Tile rows per grouped-order band.  An XCD runs grid/8 consecutive units at a time; with 4-row
+// bands those 32 (1 block/CU) units form a 4 x 8 tile block sharing A rows and B columns in the
+// XCD's L2.  Interleaved A/B (scripts/ab_hgemm.py, profiles/hgemm_group_ab_r2.jsonl), TF/s vs
+// row-major: 8192^3 NT 1340 -> 1478, NN 1054 -> 1201, TN 989 -> 1132; GPT-2 LM head fwd 973 ->
+// 1055; 4096^3 and the small GPT-2 GEMMs neutral; 8-row bands equal on squares, worse on the LM
+// head; 16-row bands worse everywhere.
+int group_rows(const Plan& pl) {
+  static const int env = [] { const char* e = getenv("DPE_HGEMM_GROUP"); return e ? atoi(e) : 0; }();  // A/B only
+  if (env != 0) return env;
+  return pl.grid >= 64 ? 4 : 1;
+}
+
 int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_bytes) {
   TORCH_CHECK(a.K % 64 == 0 && a.K > 0, "hgemm: K must be a positive multiple of 64 (got ", a.K, ")");
   const Plan pl = plan(a.M, a.N, a.K, ak, bk, allow_split, out_bytes);
   TORCH_CHECK(pl.cfg >= 0, "hgemm: no tile configuration for M=", a.M, " N=", a.N, " K=", a.K, " layout ", ak, bk);
   a.splits = pl.splits;
   a.kps = pl.kps;
+  if (a.group_m == 0) a.group_m = group_rows(pl);
   Tensor ws;
   if (pl.splits > 1) {
     ws = at::empty({(int64_t)pl.splits * a.M * a.N}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA));
@@ -190,7 +204,7 @@ void linear32_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha)
 Tensor hgemm_raw(const Tensor& A, const Tensor& B, Tensor C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                  int64_t ldc, bool ak, bool bk, int64_t epi, int64_t act, const c10::optional<Tensor>& bias,
                  const c10::optional<Tensor>& residual, const c10::optional<Tensor>& aux_in,
-                 const c10::optional<Tensor>& aux_out, double alpha, int64_t cfg, int64_t splits) {
+                 const c10::optional<Tensor>& aux_out, double alpha, int64_t cfg, int64_t splits, int64_t group_m) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "hgemm: GPU tensors");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "hgemm: bf16 operands");
   TORCH_CHECK(C.scalar_type() == (epi == dpe::HE_BF16 ? at::kBFloat16 : at::kFloat), "hgemm: output dtype");
@@ -212,6 +226,7 @@ Tensor hgemm_raw(const Tensor& A, const Tensor& B, Tensor C, int64_t M, int64_t 
   TORCH_CHECK(pl.cfg >= 0, "hgemm: no configuration (cfg=", cfg, " splits=", splits, ")");
   a.splits = pl.splits;
   a.kps = pl.kps;
+  a.group_m = group_m != 0 ? (int)group_m : group_rows(pl);
   Tensor ws;
   if (pl.splits > 1) {
     ws = at::empty({(int64_t)pl.splits * M * N}, A.options().dtype(at::kFloat));
@@ -235,7 +250,8 @@ void register_gemm(pybind11::module& m) {
         py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("a_k"), py::arg("b_k"), py::arg("epi") = 0,
         py::arg("act") = 0, py::arg("bias") = py::none(), py::arg("residual") = py::none(), py::arg("aux_in") = py::none(),
         py::arg("aux_out") = py::none(), py::arg("alpha") = 1.0, py::arg("cfg") = -1, py::arg("splits") = -1,
-        "persistent MFMA GEMM with explicit layouts (cfg / splits -1: planner's choice)");
+        py::arg("group_m") = 0,
+        "persistent MFMA GEMM with explicit layouts (cfg / splits -1: planner's choice; group_m 0: planner's, <0: row-major)");
   m.def("hgemm_plan", [](int64_t M, int64_t N, int64_t K, bool ak, bool bk, bool allow_split, int64_t out_bytes) {
           const Plan p = plan(M, N, K, ak, bk, allow_split, (int)out_bytes);
           return std::make_tuple(p.cfg, p.splits, p.kps, p.grid, p.est_s * 1e6);

@@ -31,6 +31,7 @@ struct HgemmArgs {
   int act;                  // ACT_NONE / ACT_GELU / HACT_GELU_BWD
   int splits;               // K splits (HE_SLAB when > 1)
   int kps;                  // K elements per split, multiple of 64
+  int group_m;              // tile rows per grouped-order band (L2 reuse per XCD); <= 0: row-major
   int a_dim, b_dim;         // load extents of A's M / B's N (>= M / N; 0 = M / N): loads may read the
                             // zero-padded columns of a padded operand, stores stay inside M x N
 };

@@ -81,19 +81,21 @@ def run(name, M, N, K, layout, epi, act, check):
     res.append({"gemm": name, "arm": "hipblaslt", "us": round(t, 1), "TF": round(fl / t / 1e6, 1)})
     plan = C.hgemm_plan(M, N, K, ak, bk, True, 2 if epi == 0 else 4)
     cfgs = [-1, 0, 1, 2, 3] if layout == "fwd" else ([-1, 0, 1] if layout == "dgrad" else [-1, 0])
-    for cfg in cfgs:
-        for sp in ([-1] if cfg == -1 else [1, 2, 4]):
+    arms = [(c, sp, 0) for c in cfgs for sp in ([-1] if c == -1 else [1, 2, 4])] + [(-1, -1, -1)]
+    for cfg, sp, gm in arms:
+        if True:
             def f():
                 if epi == 2:
                     out.zero_()
-                C.hgemm(A, B, out, M, N, K, lda, ldb, N, ak, bk, epi, act, bias, resid, aux_in, aux_out, 1.0, cfg, sp)
+                C.hgemm(A, B, out, M, N, K, lda, ldb, N, ak, bk, epi, act, bias, resid, aux_in, aux_out, 1.0, cfg, sp, gm)
             try:
                 t = timeit(f)
             except RuntimeError as e:  # configuration outside the envelope
-                res.append({"gemm": name, "arm": f"cfg{cfg}/s{sp}", "error": str(e)[:80]})
+                res.append({"gemm": name, "arm": f"cfg{cfg}/s{sp}/g{gm}", "error": str(e)[:80]})
                 continue
-            r = {"gemm": name, "arm": "plan" if cfg == -1 else f"cfg{cfg}/s{sp}", "us": round(t, 1), "TF": round(fl / t / 1e6, 1)}
-            if cfg == -1:
+            arm = ("plan" if gm == 0 else "plan_rowmajor") if cfg == -1 else f"cfg{cfg}/s{sp}"
+            r = {"gemm": name, "arm": arm, "us": round(t, 1), "TF": round(fl / t / 1e6, 1)}
+            if cfg == -1 and gm == 0:
                 r["plan"] = plan
             if check:
                 f()
