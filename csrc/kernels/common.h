@@ -25,8 +25,13 @@ DPE_DEVICE uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+// One two-source v_cvt_pk_bf16_f32 (RNE, NaN-preserving).  Packing two scalar f2bf() results
+// instead costs two converts plus a shift and an or where the compiler does not merge them.
 DPE_DEVICE uint32_t pack_bf2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{lo, hi}), bf16x2_t));
 }
 
 DPE_DEVICE void unpack8(const u32x4& v, float* f) {

@@ -27,6 +27,13 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 
+# per-file device flags.  attn.hip: max / sum / product chains over MFMA and v_exp results stay
+# single-issue VALU (no NaN-quieting canonicalisation v_max before each fmaxf, no SLP packing into
+# v_pk_*_f32, which costs extra issue cycles beside MFMAs) -- without inline asm, whose
+# operands would miss the compiler's hazard wait states.  NaN inputs are not honoured there.
+FILE_FLAGS = {"attn.hip": ["-fno-slp-vectorize", "-fno-honor-nans"]}
+
+
 def _torch_dirs():
     import torch
 
@@ -89,8 +96,8 @@ def build(verbose: bool = True, jobs: int | None = None, force: bool = False, ex
                           "-ffp-contract=fast", "-munsafe-fp-atomics",
                           # MFMA C/D in arch VGPRs (gfx950 unified file): avoids per-K-step
                           # v_accvgpr_read/write shuffles of the accumulators in the main loops
-                          "-mllvm", "-amdgpu-mfma-vgpr-form", *extra_defines,
-                          "-c", src, "-o", obj])
+                          "-mllvm", "-amdgpu-mfma-vgpr-form", *FILE_FLAGS.get(os.path.basename(src), []),
+                          *extra_defines, "-c", src, "-o", obj])
     for src in cpp_srcs:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
