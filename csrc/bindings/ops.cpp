@@ -18,6 +18,9 @@ using at::Tensor;
 
 extern "C" {
 int dpe_bn_stats_nblocks(int64_t M, int C);
+int dpe_pw_stream_rowgroups(int64_t M, int64_t N, int64_t K);
+int dpe_pw_stream_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int64_t M, int64_t N, int64_t K,
+                         int rg, hipStream_t st);
 int dpe_bn_stats(const uint16_t* x, int64_t M, int C, int nb, float* part, hipStream_t st);
 int dpe_bn_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* beta, float* rmean,
                     float* rvar, float momentum, float eps, float* coef, hipStream_t st);
@@ -457,6 +460,18 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
   a.lda = g.C; a.ldb = a.K; a.ldc = g.K;
   a.bias = fpo(bias);
   Tensor stats;
+  // write-heavy pointwise convs (K <= 256, N >= 2K; the bottleneck conv3 shapes): persistent
+  // streaming kernel (csrc/kernels/pwconv.hip), BN partials per row group.  DPE_PW_STREAM=0: off.
+  static const bool pw_on = [] { const char* e = getenv("DPE_PW_STREAM"); return !(e && e[0] == '0'); }();
+  const int pw_rg = (pw_on && is_pointwise(g) && !a.bias) ? dpe_pw_stream_rowgroups(a.M, a.N, a.K) : 0;
+  if (pw_rg > 0) {
+    if (want_stats) stats = at::empty({2, g.K, pw_rg}, x.options().dtype(at::kFloat));
+    CHECK_RC(dpe_pw_stream_launch(bp(x), bp(w), bpm(y), want_stats ? fp(stats) : nullptr, a.M, a.N, a.K, pw_rg,
+                                  cur_stream()), "pw_stream");
+    const hipError_t e = hipGetLastError();
+    TORCH_CHECK(e == hipSuccess, "pw_stream launch failed: ", hipGetErrorString(e));
+    return {y, stats};
+  }
   if (want_stats) {
     // [2][K][tilesM] partial (sum, sumsq) per output channel and M-tile, reduced by bn_fwd_train
     const Cfg c = pick_cfg(a.M, a.N, a.K, false);

@@ -55,6 +55,28 @@ __global__ __launch_bounds__(256) void k3c(const u32x4* __restrict__ a, const u3
   }
 }
 
+// write-heavy probe: read 1 chunk, write W chunks (the pointwise-conv 1:4 pattern)
+template <int W, bool NTS>
+__global__ __launch_bounds__(256) void kw(const u32x4* __restrict__ a, u32x4* __restrict__ y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const u32x4 v = a[i];
+#pragma unroll
+  for (int k = 0; k < W; ++k) {
+    const u32x4 r = v + (uint32_t)k;
+    if (NTS) __builtin_nontemporal_store(r, y + (int64_t)k * n + i);
+    else y[(int64_t)k * n + i] = r;
+  }
+}
+// write-heavy with row-contiguous output: thread i writes W consecutive chunks (one 16*W-byte row)
+template <int W>
+__global__ __launch_bounds__(256) void kwr(const u32x4* __restrict__ a, u32x4* __restrict__ y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n * W) return;
+  const u32x4 v = a[i / W];
+  y[i] = v + (uint32_t)(i % W);
+}
+
 int main() {
   const int64_t sizes[] = {(int64_t)512 * 56 * 56 * 64 * 2, (int64_t)512 * 56 * 56 * 256 * 2, (int64_t)512 * 28 * 28 * 128 * 2,
                            (int64_t)512 * 14 * 14 * 1024 * 2};
@@ -68,6 +90,28 @@ int main() {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
+  {
+    const int64_t rb = (int64_t)512 * 56 * 56 * 64 * 2, n = rb / 16;  // 205 MB read, 822 MB written
+    for (int rep = 0; rep < 2; ++rep) {
+      auto runw = [&](const char* name, auto launch) {
+        for (int s = 0; s < SETS; ++s) launch(bufs[3 * s], bufs[3 * s + 2]);
+        hipDeviceSynchronize();
+        hipEventRecord(e0);
+        for (int r = 0; r < 8; ++r)
+          for (int s = 0; s < SETS; ++s) launch(bufs[3 * s], bufs[3 * s + 2]);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        const double us = ms * 1e3 / (8 * SETS);
+        printf("1R:4W 205+822 MB  %-28s %8.1f us  %5.2f TB/s\n", name, us, 5.0 * rb / us / 1e6);
+      };
+      runw("planes W=4", [&](u32x4* a, u32x4* y) { hipLaunchKernelGGL((kw<4, false>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, a, y, n); });
+      runw("planes W=4 nts", [&](u32x4* a, u32x4* y) { hipLaunchKernelGGL((kw<4, true>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, a, y, n); });
+      runw("rows W=4", [&](u32x4* a, u32x4* y) { hipLaunchKernelGGL((kwr<4>), dim3((unsigned)((4 * n + 255) / 256)), dim3(256), 0, 0, a, y, n); });
+      runw("copy-only write 822MB", [&](u32x4* a, u32x4* y) { hipMemsetAsync(y, 0, 4 * rb, 0); });
+    }
+  }
   for (int64_t bytes : sizes) {
     const int64_t n = bytes / 16;
     auto run = [&](const char* name, auto launch) {

@@ -125,6 +125,11 @@ CONV_CASES = [
     (2, 56, 56, 256, 512, 1, 2, 0),
     (5, 7, 7, 512, 512, 3, 1, 1),
     (3, 14, 14, 96, 200, 3, 1, 1),
+    # write-heavy pointwise convs on the streaming kernel (pwconv.hip): K 64 / 128 / 256, M tails
+    (1, 5, 5, 64, 256, 1, 1, 0),
+    (3, 7, 7, 128, 512, 1, 1, 0),
+    (2, 9, 9, 256, 1024, 1, 1, 0),
+    (4, 30, 30, 64, 512, 1, 1, 0),
     # C = 16 (s2d stem form): two filter taps per 32-wide K-step on the LDS-DMA kernel
     (2, 12, 12, 16, 64, 4, 1, 2),
     (2, 9, 9, 16, 48, 2, 2, 0),
