@@ -12,15 +12,14 @@
 
 #include "../kernels/igemm.h"
 #include "../kernels/hgemm.h"
+#include "../kernels/pwconv.h"
 #include "gemm_plan.h"
 
 using at::Tensor;
 
 extern "C" {
 int dpe_bn_stats_nblocks(int64_t M, int C);
-int dpe_pw_stream_rowgroups(int64_t M, int64_t N, int64_t K);
-int dpe_pw_stream_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int64_t M, int64_t N, int64_t K,
-                         int rg, hipStream_t st);
+
 int dpe_bn_stats(const uint16_t* x, int64_t M, int C, int nb, float* part, hipStream_t st);
 int dpe_bn_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* beta, float* rmean,
                     float* rvar, float momentum, float eps, float* coef, hipStream_t st);
@@ -436,6 +435,18 @@ dpe::ConvGeom geom(const Tensor& x, const Tensor& w, int64_t sh, int64_t sw, int
   return g;
 }
 
+// DPE_PW_STREAM=0 / set_pw_stream(false): the write-heavy pointwise convs stay on the implicit-GEMM
+// kernels (A/B reference and the equivalence tests)
+int g_pw_stream = -1;
+bool pw_stream_on() {
+  if (g_pw_stream < 0) {
+    const char* e = getenv("DPE_PW_STREAM");
+    g_pw_stream = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_pw_stream == 1;
+}
+void set_pw_stream(bool on) { g_pw_stream = on ? 1 : 0; }
+
 bool is_pointwise(const dpe::ConvGeom& g) {
   return g.R == 1 && g.S == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0;
 }
@@ -461,15 +472,14 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
   a.bias = fpo(bias);
   Tensor stats;
   // write-heavy pointwise convs (K <= 256, N >= 2K; the bottleneck conv3 shapes): persistent
-  // streaming kernel (csrc/kernels/pwconv.hip), BN partials per row group.  DPE_PW_STREAM=0: off.
-  static const bool pw_on = [] { const char* e = getenv("DPE_PW_STREAM"); return !(e && e[0] == '0'); }();
-  const int pw_rg = (pw_on && is_pointwise(g) && !a.bias) ? dpe_pw_stream_rowgroups(a.M, a.N, a.K) : 0;
+  // streaming kernel (csrc/kernels/pwconv.hip), BN partials per row group.
+  const int pw_rg = (pw_stream_on() && is_pointwise(g) && !a.bias) ? dpe_pw_rowgroups(a.M, a.N, a.K, dpe::PW_FWD) : 0;
   if (pw_rg > 0) {
     if (want_stats) stats = at::empty({2, g.K, pw_rg}, x.options().dtype(at::kFloat));
-    CHECK_RC(dpe_pw_stream_launch(bp(x), bp(w), bpm(y), want_stats ? fp(stats) : nullptr, a.M, a.N, a.K, pw_rg,
-                                  cur_stream()), "pw_stream");
-    const hipError_t e = hipGetLastError();
-    TORCH_CHECK(e == hipSuccess, "pw_stream launch failed: ", hipGetErrorString(e));
+    dpe::PwArgs pa{};
+    pa.x = bp(x); pa.w = bp(w); pa.y = bpm(y); pa.stats = want_stats ? fp(stats) : nullptr;
+    pa.M = a.M; pa.N = a.N; pa.K = a.K; pa.rg = pw_rg;
+    CHECK_RC(dpe_pw_launch(&pa, dpe::PW_FWD, cur_stream()), "pw_stream fwd");
     return {y, stats};
   }
   if (want_stats) {
@@ -483,7 +493,6 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
   return {y, stats};
 }
 
-// dx NHWC [N,H,W,C] = conv_transpose(dy, w); optional residual added into dx
 // dx NHWC [N,H,W,C] = conv_transpose(dy, w); optional residual added into dx.
 // With bn_x/bn_coef (dx is dL/d relu(BN(bn_x))), the epilogue also emits the
 // BatchNorm-backward partials [2][C][tiles] (sum dz, sum dz*(x-mean)).
@@ -548,6 +557,22 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
     }
   }
   Tensor part;
+  // write-heavy pointwise data grads (a bottleneck's conv1: K = Cout <= 256, N = Cin >= 2K), with the
+  // residual / BN-backward epilogue: streaming kernel (pwconv.hip), BN partials per row group
+  const int pw_rg = (pw_stream_on() && is_pointwise(g) && !acc_into) ? dpe_pw_rowgroups(a.M, a.N, a.K, dpe::PW_DGRAD) : 0;
+  if (pw_rg > 0) {
+    dpe::PwArgs pa{};
+    pa.x = bp(dy); pa.w = bp(w); pa.y = bpm(dx);
+    pa.residual = a.residual; pa.res_mask = a.res_mask;
+    pa.st_x = a.st_x; pa.st_coef = a.st_coef; pa.st_mask = a.st_mask;
+    pa.M = a.M; pa.N = a.N; pa.K = a.K; pa.rg = pw_rg;
+    if (want_bn) {
+      part = at::empty({2, g.C, pw_rg}, dy.options().dtype(at::kFloat));
+      pa.stats = fp(part);
+    }
+    CHECK_RC(dpe_pw_launch(&pa, dpe::PW_DGRAD, cur_stream()), "pw_stream dgrad");
+    return {dx, part};
+  }
   auto tiles_of = [&](int64_t M, int64_t K) { const Cfg c = pick_cfg(M, g.C, K, false); return (M + c.bm - 1) / c.bm; };
   if (!is_pointwise(g) && g.sh == 1 && g.sw == 1 && g.dh == 1 && g.dw == 1 && dgrad_as_fwd()) {
     // Stride-1 data grad as a forward conv: dx = conv(dy, flipT(w), pad R-1-p) on the
@@ -1198,6 +1223,7 @@ void register_ops(pybind11::module& m) {
   m.def("layernorm_fwd", &layernorm_fwd, py::arg("x"), py::arg("w"), py::arg("b") = py::none(), py::arg("eps") = 1e-5);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
         py::arg("dw"), py::arg("db") = py::none(), py::arg("dx_out") = py::none());
+  m.def("set_pw_stream", &set_pw_stream, "streaming pointwise-conv kernel on/off (pwconv.hip)");
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("H"), py::arg("scale"), py::arg("causal") = true);
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("H"),
         py::arg("scale"), py::arg("causal") = true);

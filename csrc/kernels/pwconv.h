@@ -1,0 +1,32 @@
+// Host-visible arguments of the streaming pointwise-conv kernel (pwconv.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dpe {
+
+enum PwEpi : int {
+  PW_FWD = 0,    // y = x . W^T; stats = BatchNorm-forward (sum, sum of squares) of the stored y
+  PW_DGRAD = 1,  // y = x . W (+ residual [masked]); stats = BatchNorm-backward (sum dz, sum dz*(st_x - mean))
+};
+
+struct PwArgs {
+  const uint16_t* x;         // [M][K] bf16 (forward: the conv input; data grad: dy)
+  const uint16_t* w;         // PW_FWD: [N][K] (conv weight [Cout][Cin]); PW_DGRAD: [K][N] (the same tensor)
+  uint16_t* y;               // [M][N] bf16
+  float* stats;              // [2][N][row groups] partials, or nullptr
+  const uint16_t* residual;  // PW_DGRAD: bf16 [M][N] added to y, or nullptr
+  const uint8_t* res_mask;   // PW_DGRAD: ReLU bits of the residual's producer ([M][N/8]), or nullptr
+  const uint16_t* st_x;      // PW_DGRAD BN backward: pre-BN input [M][N]; nullptr = no stats
+  const float* st_coef;      // [4][N]: scale, shift, mean, invstd of that BatchNorm
+  const uint8_t* st_mask;    // ReLU bits of the BN output ([M][N/8]); the stored y is then the masked dz
+  int64_t M, N, K;
+  int rg;                    // row groups (= partial columns), from dpe_pw_rowgroups
+};
+
+}  // namespace dpe
+
+// Row groups of the launch for (M, N, K, epi), or 0 outside the kernel's envelope
+// (K in {64, 128, 256}, N a multiple of the block's column slice, N >= 2K).
+extern "C" int dpe_pw_rowgroups(int64_t M, int64_t N, int64_t K, int epi);
+extern "C" int dpe_pw_launch(const dpe::PwArgs* args, int epi, hipStream_t stream);

@@ -1,6 +1,10 @@
-// Streaming pointwise (1x1, stride 1) convolution forward for the write-heavy ResNet
-// shapes: y[M][N] = x[M][K] . W[N][K]^T, K in {64, 128, 256}, N a multiple of 4*WN, with the
-// BatchNorm-forward statistics (sum, sum of squares of the stored bf16 values).
+// Streaming pointwise (1x1, stride 1) convolution GEMMs for the write-heavy ResNet shapes
+// (K in {64, 128, 256}, N >= 2K: every bottleneck's conv3 forward and conv1 data grad):
+//   PW_FWD:   y[M][N] = x[M][K] . W[N][K]^T, with the BatchNorm-forward sums of the stored y;
+//   PW_DGRAD: y[M][N] = dy[M][K] . W[K][N] (+ residual, optionally ReLU-masked by its producer's
+//             bits), with the BatchNorm-backward partials (sum dz, sum dz*(x - mean)) of the BN
+//             whose output this y is the gradient of (ReLU from its coefficients, or from the
+//             saved output's mask bits -- then the stored y is the masked dz itself).
 //
 // Why a separate kernel: at K <= 256 the implicit-GEMM tile does 2-8 K-steps and then spends
 // most of its life in the prologue DMA wait and the LDS-staged epilogue; one tile per block at
@@ -12,8 +16,11 @@
 //     (NS-1 tiles in flight while one is consumed), so the HBM latency overlaps the MFMAs and
 //     the stores of earlier tiles; every wave reads the same tile (A = x fragments via the
 //     swizzled K-image, as igemm);
-//   * the output goes straight from the accumulators: each lane owns 4 consecutive channels of
-//     one pixel (8-B stores; the 4 lane groups complete each 128-B row segment in L2);
+//   * the output is staged per wave, half a tile at a time, through the wave's own LDS region
+//     and stored as whole 16-B row chunks (one store instruction = 8 full 128-B row segments;
+//     stores straight from the accumulator layout -- 16 rows x 32 B per instruction -- ran at
+//     ~4 TB/s and were the limiter); the epilogue operands (residual, pre-BN input, mask bits)
+//     are loaded in the same row-chunk layout before the staging writes;
 //   * BatchNorm sums accumulate in registers over all of the block's rows and are reduced once
 //     at the end: one partial column per row group ([2][N][row groups]) instead of one per
 //     128-row tile, and no per-tile LDS reduction or barrier.
@@ -21,6 +28,7 @@
 
 #include "common.h"
 #include "igemm.h"
+#include "pwconv.h"
 
 namespace dpe {
 namespace pw {
@@ -48,10 +56,8 @@ DPE_DEVICE void wait_vm() {  // s_waitcnt vmcnt(N): loads, LDS-DMA and stores co
 }
 
 // K: reduction depth; WN: output columns per wave (4 waves -> 4*WN per block); NS: ring depth
-template <int K, int WN, int NS>
-__global__ __launch_bounds__(256, K == 64 ? 3 : 2) void pw_stream_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
-                                                           uint16_t* __restrict__ y, float* __restrict__ stats, int M,
-                                                           int N, int RG) {
+template <int K, int WN, int NS, int EPI>
+__global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_stream_kernel(PwArgs a) {
   constexpr int KC = K / 32;                  // 32-deep K chunks
   constexpr int TILE = BM * K * 2;            // bytes of one x tile in LDS ([KC][64 rows][64 B])
   constexpr int P = TILE / 1024 / 4;          // 1-KiB DMA pieces per wave per tile
@@ -59,32 +65,56 @@ __global__ __launch_bounds__(256, K == 64 ? 3 : 2) void pw_stream_kernel(const u
   static_assert(P >= 1 && P * 4096 == TILE, "pieces");
   // output staging: each wave stages half a tile (32 rows x WN channels, padded rows) in its own
   // LDS region and stores whole 16-B row chunks: one store instruction = RPP full row segments
-  constexpr int ROWB = WN * 2 + 16, CPRW = WN / 8, RPP = 64 / CPRW;
+  constexpr int ROWB = WN * 2 + 16, CPRW = WN / 8, RPP = 64 / CPRW, NPS = 32 / RPP;
   constexpr int STG = 32 * ROWB;
-  // stores outstanding per wave per tile, for the counted vmcnt below
-  constexpr int S = 2 * (32 / RPP);
+  // stores outstanding per wave per tile, for the counted vmcnt below (the epilogue's operand
+  // loads are consumed -- waited for -- inside the tile, so they are not outstanding here)
+  constexpr int S = 2 * NPS;
   constexpr int VM = (NS - 1) * S + (NS - 2) * P;
   static_assert(VM < 64, "vmcnt range");
   __shared__ __attribute__((aligned(16))) char smem[NS * TILE + 4 * STG];
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int M = (int)a.M, N = (int)a.N, RG = a.rg;
   const int nbN = N / (4 * WN);
   const int bid = xcd_remap(blockIdx.x, gridDim.x);  // the nbN column slices of a row group share an XCD
   const int rg = bid / nbN, nb = bid % nbN;
   const int n0w = nb * 4 * WN + wid * WN;  // the wave's first output channel
   const int tiles = (M + BM - 1) / BM;
+  const int ch = lane % CPRW;              // the lane's 16-B chunk of each staged row
+  const int nch = n0w + ch * 8;            // its first channel
 
-  // weights as MFMA A operands: wf[ni][kc] = W[n0w + 16 ni + li][32 kc + 8 g .. +7]
+  // weights as MFMA A operands: wf[ni][kc] = W^T[n0w + 16 ni + li][32 kc + 8 g .. +7]
   bf16x8 wf[NI][KC];
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc)
-      wf[ni][kc] = __builtin_bit_cast(bf16x8, *(const u32x4*)(w + (int64_t)(n0w + 16 * ni + li) * K + 32 * kc + 8 * g));
+    for (int kc = 0; kc < KC; ++kc) {
+      const int n = n0w + 16 * ni + li, k0 = 32 * kc + 8 * g;
+      if constexpr (EPI == PW_FWD) {
+        wf[ni][kc] = __builtin_bit_cast(bf16x8, *(const u32x4*)(a.w + (int64_t)n * K + k0));
+      } else {  // W stored [K][N]: gather the column (once per block)
+        s16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (short)a.w[(int64_t)(k0 + e) * N + n];
+        wf[ni][kc] = __builtin_bit_cast(bf16x8, v);
+      }
+    }
+  // BatchNorm-backward coefficients of the lane's 8 channels
+  float bsc[8], bsh[8], bmu[8];
+  const bool bnb = EPI == PW_DGRAD && a.st_x != nullptr;
+  if (bnb) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bsc[e] = a.st_coef[nch + e];
+      bsh[e] = a.st_coef[N + nch + e];
+      bmu[e] = a.st_coef[2 * N + nch + e];
+    }
+  }
 
   // DMA pieces: piece q (of 4P per tile) = K chunk q / 4, rows 16 (q % 4) .. +15; lane -> (row, 16-B chunk)
-  const __amdgpu_buffer_rsrc_t xr = rsrc(x, (uint32_t)((int64_t)M * K * 2));
+  const __amdgpu_buffer_rsrc_t xr = rsrc(a.x, (uint32_t)((int64_t)M * K * 2));
   uint32_t voff[P];
 #pragma unroll
   for (int i = 0; i < P; ++i) {
@@ -104,11 +134,9 @@ __global__ __launch_bounds__(256, K == 64 ? 3 : 2) void pw_stream_kernel(const u
     }
   };
 
-  float s[NI][4], ss[NI][4];
+  float s[8], ss[8];
 #pragma unroll
-  for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) { s[ni][e] = 0.f; ss[ni][e] = 0.f; }
+  for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
 
   // this row group's tiles: rg, rg + RG, ...
   const int nt = rg < tiles ? (tiles - 1 - rg) / RG + 1 : 0;
@@ -116,8 +144,15 @@ __global__ __launch_bounds__(256, K == 64 ? 3 : 2) void pw_stream_kernel(const u
   for (int j = 0; j < NS - 1; ++j)
     if (j < nt) issue(rg + j * RG, j);
   for (int j = 0; j < nt; ++j) {
-    // tile j landed (its DMA is older than NS-2 later tiles' DMAs and NS-1 tiles' stores)
-    if (j + NS - 2 < nt) wait_vm<VM>(); else wait_vm<0>();
+    // Tile j landed.  In steady state NS-2 later tiles' DMAs and NS-1 tiles' stores were issued
+    // after it (VM); a prologue tile j < NS-1 has only the NS-2 prologue DMAs and j tiles'
+    // stores behind it, so it waits for fewer (a larger count would let the wave read a tile
+    // still in flight); near the end fewer DMAs follow -> vmcnt(0).
+    if (j + NS - 2 >= nt) wait_vm<0>();
+    else if (j == 0) wait_vm<(NS - 2) * P>();
+    else if (NS >= 3 && j == 1) wait_vm<S + (NS - 2) * P>();
+    else if (NS >= 4 && j == 2) wait_vm<2 * S + (NS - 2) * P>();
+    else wait_vm<VM>();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's pieces of tile j are in; slot (j-1)%NS is free
     asm volatile("" ::: "memory");
@@ -141,11 +176,25 @@ __global__ __launch_bounds__(256, K == 64 ? 3 : 2) void pw_stream_kernel(const u
     }
     // y rows: lane holds channels n0w + 16 ni + 4 g + e of pixel m0 + 16 mi + li; staged per
     // 32-row half through the wave's LDS region (LDS ops of one wave complete in order, so the
-    // next half's writes never overtake this half's reads)
+    // next half's writes never overtake this half's reads), then finished per 16-B row chunk
     const int m0 = (rg + j * RG) * BM;
     char* stg = smem + NS * TILE + wid * STG;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
+      // the half's epilogue operands first: their latency overlaps the staging below
+      u32x4 rv[NPS], xv[NPS];
+      uint32_t rmb[NPS], smb[NPS];
+      if constexpr (EPI == PW_DGRAD) {
+#pragma unroll
+        for (int ps = 0; ps < NPS; ++ps) {
+          const int m = min(m0 + 32 * hf + ps * RPP + lane / CPRW, M - 1);
+          const int64_t off = (int64_t)m * N + nch;
+          if (a.residual) rv[ps] = *(const u32x4*)(a.residual + off);
+          rmb[ps] = a.res_mask ? (uint32_t)a.res_mask[off >> 3] : 0xffu;
+          if (bnb) xv[ps] = *(const u32x4*)(a.st_x + off);
+          smb[ps] = (bnb && a.st_mask) ? (uint32_t)a.st_mask[off >> 3] : 0xffu;
+        }
+      }
 #pragma unroll
       for (int mh = 0; mh < 2; ++mh) {
         const int mi = 2 * hf + mh;
@@ -154,46 +203,72 @@ __global__ __launch_bounds__(256, K == 64 ? 3 : 2) void pw_stream_kernel(const u
           u32x2 pk;
           pk[0] = pack_bf2(acc[mi][ni][0], acc[mi][ni][1]);
           pk[1] = pack_bf2(acc[mi][ni][2], acc[mi][ni][3]);
-          // statistics of the stored (rounded) values; rows past M are zeros
-          const float v0 = __uint_as_float(pk[0] << 16), v1 = __uint_as_float(pk[0] & 0xffff0000u);
-          const float v2 = __uint_as_float(pk[1] << 16), v3 = __uint_as_float(pk[1] & 0xffff0000u);
-          s[ni][0] += v0; ss[ni][0] = fmaf(v0, v0, ss[ni][0]);
-          s[ni][1] += v1; ss[ni][1] = fmaf(v1, v1, ss[ni][1]);
-          s[ni][2] += v2; ss[ni][2] = fmaf(v2, v2, ss[ni][2]);
-          s[ni][3] += v3; ss[ni][3] = fmaf(v3, v3, ss[ni][3]);
           *(u32x2*)(stg + (16 * mh + li) * ROWB + (16 * ni + 4 * g) * 2) = pk;
         }
       }
 #pragma unroll
-      for (int ps = 0; ps < 32 / RPP; ++ps) {
-        const int row = ps * RPP + lane / CPRW, ch = lane % CPRW;
-        const u32x4 v = *(const u32x4*)(stg + row * ROWB + ch * 16);
+      for (int ps = 0; ps < NPS; ++ps) {
+        const int row = ps * RPP + lane / CPRW;
+        u32x4 v = *(const u32x4*)(stg + row * ROWB + ch * 16);
         const int m = m0 + 32 * hf + row;
-        if (m < M) *(u32x4*)(y + (int64_t)m * N + n0w + ch * 8) = v;
+        const bool valid = m < M;
+        float f[8];
+        unpack8(v, f);
+        if constexpr (EPI == PW_FWD) {
+          // statistics of the stored (rounded) values; rows past M are zeros
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { s[e] += f[e]; ss[e] = fmaf(f[e], f[e], ss[e]); }
+        } else {
+          if (a.residual) {  // + residual (dz of a BN + residual + ReLU output: masked by its bits)
+            float r[8];
+            unpack8(rv[ps], r);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] += ((rmb[ps] >> e) & 1u) ? r[e] : 0.f;
+            v = pack8(f);
+            unpack8(v, f);
+          }
+          if (bnb && valid) {  // (sum dz, sum dz*(x - mean)), dz = v * relu'(BN output)
+            float x8[8];
+            unpack8(xv[ps], x8);
+            if (a.st_mask) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                f[e] = ((smb[ps] >> e) & 1u) ? f[e] : 0.f;
+                s[e] += f[e];
+                ss[e] = fmaf(f[e], x8[e] - bmu[e], ss[e]);
+              }
+              v = pack8(f);  // the stored gradient is dz itself
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const float dz = fmaf(x8[e], bsc[e], bsh[e]) > 0.f ? f[e] : 0.f;
+                s[e] += dz;
+                ss[e] = fmaf(dz, x8[e] - bmu[e], ss[e]);
+              }
+            }
+          }
+        }
+        if (valid) *(u32x4*)(a.y + (int64_t)m * N + nch) = v;
       }
     }
   }
-  // statistics: reduce over the 16 pixels of each lane group, one partial column per row group
-  if (stats) {
+  // statistics: reduce over the lanes holding the same channel chunk (lane = row * CPRW + ch),
+  // one partial column per row group
+  if (a.stats) {
 #pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
+    for (int e = 0; e < 8; ++e) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          s[ni][e] += __shfl_xor(s[ni][e], o, 64);
-          ss[ni][e] += __shfl_xor(ss[ni][e], o, 64);
-        }
+      for (int o = CPRW; o < 64; o <<= 1) {
+        s[e] += __shfl_xor(s[e], o, 64);
+        ss[e] += __shfl_xor(ss[e], o, 64);
       }
-    if (li == 0) {
+    }
+    if (lane < CPRW) {
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int n = n0w + 16 * ni + 4 * g + e;
-          stats[(int64_t)n * RG + rg] = s[ni][e];
-          stats[(int64_t)(N + n) * RG + rg] = ss[ni][e];
-        }
+      for (int e = 0; e < 8; ++e) {
+        a.stats[(int64_t)(nch + e) * RG + rg] = s[e];
+        a.stats[(int64_t)(N + nch + e) * RG + rg] = ss[e];
+      }
     }
   }
 }
@@ -203,48 +278,58 @@ __global__ __launch_bounds__(256, K == 64 ? 3 : 2) void pw_stream_kernel(const u
 
 using namespace dpe;
 
-// Shape of the launch for (M, N, K): row groups (= BatchNorm partial columns) or 0 when the
-// problem is outside this kernel's envelope (the caller then uses the implicit-GEMM kernels).
 static int pw_wn(int K) { return K <= 128 ? 64 : 32; }
 
 // Every block carries the same number of tiles, so the grid must be exactly the resident
 // capacity (blocks per CU from the occupancy API x CUs): a grid that lets the dispatcher put
 // 3 blocks on some CUs and 1 on others finishes at the pace of the fullest CU.
-template <int K, int WN, int NS>
+template <int K, int WN, int NS, int EPI>
 static int pw_slots() {
   static int slots = [] {
     int dev = 0, cus = 0, per = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pw::pw_stream_kernel<K, WN, NS>, 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pw::pw_stream_kernel<K, WN, NS, EPI>, 256, 0);
     return std::max(1, per) * std::max(1, cus);
   }();
   return slots;
 }
+template <int EPI>
 static int pw_capacity(int K) {
-  return K == 64 ? pw_slots<64, 64, 4>() : K == 128 ? pw_slots<128, 64, 3>() : pw_slots<256, 32, 2>();
+  return K == 64 ? pw_slots<64, 64, 4, EPI>() : K == 128 ? pw_slots<128, 64, 3, EPI>() : pw_slots<256, 32, 2, EPI>();
 }
 
-extern "C" int dpe_pw_stream_rowgroups(int64_t M, int64_t N, int64_t K) {
+extern "C" int dpe_pw_rowgroups(int64_t M, int64_t N, int64_t K, int epi) {
   if (K != 64 && K != 128 && K != 256) return 0;
+  if (epi != PW_FWD && epi != PW_DGRAD) return 0;
   const int bnb = 4 * pw_wn((int)K);
   if (N % bnb || N < 2 * K) return 0;  // write-heavy shapes only (N >= 2K)
-  if (M * K * 2 >= (1ll << 31) - 4096 || M >= (1ll << 31)) return 0;
+  if (M * K * 2 >= (1ll << 31) - 4096 || M * N >= (1ll << 31)) return 0;
   const int64_t tiles = (M + pw::BM - 1) / pw::BM;
   const int64_t nbN = N / bnb;
-  int64_t rg = pw_capacity((int)K) / nbN;  // one resident wave of blocks over the whole launch
+  const int cap = epi == PW_FWD ? pw_capacity<PW_FWD>((int)K) : pw_capacity<PW_DGRAD>((int)K);
+  int64_t rg = cap / nbN;  // one resident wave of blocks over the whole launch
   if (rg < 1) rg = 1;
   if (rg > tiles) rg = tiles;
   return (int)rg;
 }
 
-extern "C" int dpe_pw_stream_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int64_t M, int64_t N,
-                                    int64_t K, int rg, hipStream_t st) {
-  if (rg <= 0 || rg != dpe_pw_stream_rowgroups(M, N, K)) return -1;
-  const int nbN = (int)(N / (4 * pw_wn((int)K)));
-  const dim3 grid((unsigned)(rg * nbN)), block(256);
-  if (K == 64) hipLaunchKernelGGL((pw::pw_stream_kernel<64, 64, 4>), grid, block, 0, st, x, w, y, stats, (int)M, (int)N, rg);
-  else if (K == 128) hipLaunchKernelGGL((pw::pw_stream_kernel<128, 64, 3>), grid, block, 0, st, x, w, y, stats, (int)M, (int)N, rg);
-  else hipLaunchKernelGGL((pw::pw_stream_kernel<256, 32, 2>), grid, block, 0, st, x, w, y, stats, (int)M, (int)N, rg);
-  return 0;
+extern "C" int dpe_pw_launch(const PwArgs* args, int epi, hipStream_t st) {
+  const PwArgs& a = *args;
+  if (a.rg <= 0 || a.rg != dpe_pw_rowgroups(a.M, a.N, a.K, epi)) return -1;
+  if (epi == PW_FWD && (a.residual || a.st_x)) return -1;
+  if (a.st_x && !a.st_coef) return -1;
+  const int nbN = (int)(a.N / (4 * pw_wn((int)a.K)));
+  const dim3 grid((unsigned)(a.rg * nbN)), block(256);
+#define PW_L(K_, WN_, NS_)                                                                              \
+  if (a.K == K_) {                                                                                      \
+    if (epi == PW_FWD) hipLaunchKernelGGL((pw::pw_stream_kernel<K_, WN_, NS_, PW_FWD>), grid, block, 0, st, a); \
+    else hipLaunchKernelGGL((pw::pw_stream_kernel<K_, WN_, NS_, PW_DGRAD>), grid, block, 0, st, a);    \
+    return 0;                                                                                           \
+  }
+  PW_L(64, 64, 4)
+  PW_L(128, 64, 3)
+  PW_L(256, 32, 2)
+#undef PW_L
+  return -1;
 }

@@ -762,3 +762,46 @@ def test_bn_bwd_dual_matches_two_backwards(C):
     refd, _ = C.bn_bwd(dz, None, hd, gd, cd, b_gd, b_bd, False)
     assert torch.equal(dh3, ref3) and torch.allclose(a_g3, b_g3) and torch.allclose(a_b3, b_b3)
     assert rel_err(dhd, refd) < 1e-2 and rel_err(a_gd, b_gd) < 1e-4 and rel_err(a_bd, b_bd) < 1e-4
+
+
+@pytest.mark.parametrize("N,H,W,Ci,Co", [(2, 9, 9, 256, 64), (3, 7, 7, 512, 128), (2, 6, 6, 1024, 256),
+                                         (4, 28, 28, 256, 64),
+                                         # several row tiles per persistent block: the DMA-ring prologue
+                                         (32, 64, 64, 256, 64), (64, 28, 28, 512, 128), (64, 16, 16, 1024, 256)])
+def test_pw_stream_matches_igemm(C, N, H, W, Ci, Co):
+    """The streaming pointwise-conv kernel (pwconv.hip) == the implicit-GEMM path on the same inputs:
+    conv3-style forward (Co -> Ci, BN stats) and conv1-style data grads with every epilogue variant
+    (plain, + residual, + bits-masked residual, BN-backward partials with the ReLU from the
+    coefficients or from the saved output's bits).  Outputs bitwise, partial sums to fp32 order."""
+    torch.manual_seed(29)
+    w = bf(torch.randn(Co, 1, 1, Ci, device=dev) / math.sqrt(Ci))        # conv1: Ci -> Co
+    w3 = bf(torch.randn(Ci, 1, 1, Co, device=dev) / math.sqrt(Co))       # conv3: Co -> Ci
+    a2 = bf(torch.randn(N, H, W, Co, device=dev))
+    dy = bf(torch.randn(N, H, W, Co, device=dev))
+    h = bf(torch.randn(N, H, W, Ci, device=dev))
+    coef = _bn_coef(C, Ci)
+    _, bits = C.bn_apply(h, coef, bf(torch.randn(N, H, W, Ci, device=dev)), None, True, True)
+    dout = bf(torch.randn(N, H, W, Ci, device=dev))
+    h0, c0 = bf(torch.randn(N, H, W, Ci, device=dev)), _bn_coef(C, Ci)
+    _, bits0 = C.bn_apply(h0, c0, h, None, True, True)
+    sh = [N, H, W, Ci]
+    z = [1, 1], [0, 0], [1, 1]
+    runs = {}
+    for on in (True, False):
+        C.set_pw_stream(on)
+        try:
+            runs[on] = [
+                C.conv_fwd(a2, w3, *z, True, None),
+                (C.conv_dgrad(dy, w, sh, *z, None), None),
+                (C.conv_dgrad(dy, w, sh, *z, dout), None),
+                (C.conv_dgrad(dy, w, sh, *z, dout, bits), None),
+                tuple(C.conv_dgrad_bn(dy, w, sh, *z, None, h, coef)),
+                tuple(C.conv_dgrad_bn(dy, w, sh, *z, dout, h0, c0, bits0, bits)),
+            ]
+        finally:
+            C.set_pw_stream(True)
+    for i, ((y1, s1), (y2, s2)) in enumerate(zip(runs[True], runs[False])):
+        assert torch.equal(y1, y2), i
+        if s1 is not None:
+            assert s1.shape[:2] == s2.shape[:2]
+            assert rel_err(s1.sum(-1), s2.sum(-1)) < 1e-4, i
