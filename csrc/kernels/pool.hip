@@ -1,5 +1,7 @@
 // NHWC pooling: max-pool (with per-element argmax byte for an index-free
 // backward gather) and global average pool.  bf16 in/out, 8 channels/lane.
+#include <algorithm>
+
 #include "common.h"
 
 namespace dpe {
@@ -7,50 +9,76 @@ namespace dpe {
 // coef != nullptr: the input is the PRE-BatchNorm stem output h and each tap is
 // relu(h*scale + shift) rounded to bf16 exactly as a materialised BN output
 // would be -- the BN+ReLU tensor is never written (stem fusion).
-template <bool BNRELU>
+template <bool BNRELU, int KK>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                           uint8_t* __restrict__ idx, int N, int H, int W, int C, int OH,
-                                                          int OW, int k, int s, int p, const float* __restrict__ coef) {
+                                                          int OW, int k_rt, int s, int p, const float* __restrict__ coef) {
+  // one 8-channel output chunk per thread over an exact grid, 32-bit index math (the host
+  // checks N*OH*OW*C/8 < 2^31).  KK > 0: the window size is a compile-time constant and all
+  // KK*KK tap loads are issued before the first use (one load in flight per thread left the
+  // stem pool latency-bound).
+  const int k = KK > 0 ? KK : k_rt;
   const int CPR = C >> 3;
-  const int64_t total = (int64_t)N * OH * OW * CPR;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int c8 = (int)(i % CPR) * 8;
-    int64_t t = i / CPR;
-    const int ow = (int)(t % OW); t /= OW;
-    const int oh = (int)(t % OH);
-    const int n = (int)(t / OH);
-    float sc[8], sh[8];
+  const int total = N * OH * OW * CPR;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int c8 = (i % CPR) * 8;
+  int t = i / CPR;
+  const int ow = t % OW; t /= OW;
+  const int oh = t % OH;
+  const int n = t / OH;
+  float sc[8], sh[8];
+  if constexpr (BNRELU) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = coef[c8 + e]; sh[e] = coef[C + c8 + e]; }
+  }
+  float best[8];
+  uint8_t bi[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+  auto take = [&](const u32x4& raw, int tap) {
+    float f[8];
+    unpack8(raw, f);
     if constexpr (BNRELU) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { sc[e] = coef[c8 + e]; sh[e] = coef[C + c8 + e]; }
+      for (int e = 0; e < 8; ++e) f[e] = bf2f(f2bf(fmaxf(fmaf(f[e], sc[e], sh[e]), 0.f)));
     }
-    float best[8];
-    uint8_t bi[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int e = 0; e < 8; ++e)
+      if (f[e] > best[e]) { best[e] = f[e]; bi[e] = (uint8_t)tap; }
+  };
+  const uint16_t* xn = x + (int64_t)n * H * W * C + c8;
+  if constexpr (KK > 0) {
+    u32x4 raw[KK * KK];
+    bool ok[KK * KK];
+#pragma unroll
+    for (int r = 0; r < KK; ++r)
+#pragma unroll
+      for (int q = 0; q < KK; ++q) {
+        const int ih = oh * s - p + r, iw = ow * s - p + q;
+        ok[r * KK + q] = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        const int ihc = min(max(ih, 0), H - 1), iwc = min(max(iw, 0), W - 1);
+        raw[r * KK + q] = *(const u32x4*)(xn + ((int64_t)ihc * W + iwc) * C);
+      }
+#pragma unroll
+    for (int tp = 0; tp < KK * KK; ++tp)
+      if (ok[tp]) take(raw[tp], tp);
+  } else {
     for (int r = 0; r < k; ++r) {
       const int ih = oh * s - p + r;
       if ((unsigned)ih >= (unsigned)H) continue;
       for (int q = 0; q < k; ++q) {
         const int iw = ow * s - p + q;
         if ((unsigned)iw >= (unsigned)W) continue;
-        float f[8];
-        unpack8(*(const u32x4*)(x + (((int64_t)n * H + ih) * W + iw) * C + c8), f);
-        if constexpr (BNRELU) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = bf2f(f2bf(fmaxf(fmaf(f[e], sc[e], sh[e]), 0.f)));
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (f[e] > best[e]) { best[e] = f[e]; bi[e] = (uint8_t)(r * k + q); }
+        take(*(const u32x4*)(xn + ((int64_t)ih * W + iw) * C), r * k + q);
       }
     }
-    *(u32x4*)(y + i * 8) = pack8(best);
-    u32x2 pk;
-    pk[0] = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
-    pk[1] = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
-    *(u32x2*)(idx + i * 8) = pk;
   }
+  *(u32x4*)(y + (int64_t)i * 8) = pack8(best);
+  u32x2 pk;
+  pk[0] = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+  pk[1] = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+  *(u32x2*)(idx + (int64_t)i * 8) = pk;
 }
 
 // d(pool input)[n,h,w,c8..c8+7]: sum of dy over the windows containing (h, w) whose argmax it is
@@ -253,22 +281,34 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_reduce_quad_kernel(const u
     sc[e] = coef[c * 8 + e]; sh[e] = coef[C + c * 8 + e]; mean[e] = coef[2 * C + c * 8 + e];
   }
   if (r < QPI) {
-    for (int qd = qb + r; qd < qe; qd += QPI) {
-      const int j = qd % OW, t = qd / OW;
-      const int i = t % OH, n = t / OH;
-      float d[4][8];
-      pool_grad_quad(dy, idx, n, i, j, c * 8, C, OH, OW, d);
+    // U quads per thread per iteration, all of their (dy, argmax, x) loads issued before the first
+    // use: one quad at a time left this pass latency-bound (1.08 GB in 357 us)
+    constexpr int U = 4;
+    for (int q0 = qb + r; q0 < qe; q0 += U * QPI) {
+      float d[U][4][8], xv[U][4][8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const size_t row = ((size_t)n * H + 2 * i + (u >> 1)) * W + 2 * j + (u & 1);
-        float xv[8];
-        unpack8(*(const u32x4*)(x + row * C + c * 8), xv);
+      for (int u = 0; u < U; ++u) {
+        const int qd = min(q0 + u * QPI, qe - 1);
+        const int j = qd % OW, t = qd / OW;
+        const int i = t % OH, n = t / OH;
+        pool_grad_quad(dy, idx, n, i, j, c * 8, C, OH, OW, d[u]);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float dz = fmaf(xv[e], sc[e], sh[e]) > 0.f ? d[u][e] : 0.f;
-          sm[e] += dz;
-          sq[e] += dz * (xv[e] - mean[e]);
+        for (int v = 0; v < 4; ++v) {
+          const size_t row = ((size_t)n * H + 2 * i + (v >> 1)) * W + 2 * j + (v & 1);
+          unpack8(*(const u32x4*)(x + row * C + c * 8), xv[u][v]);
         }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (q0 + u * QPI >= qe) break;
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float dz = fmaf(xv[u][v][e], sc[e], sh[e]) > 0.f ? d[u][v][e] : 0.f;
+            sm[e] += dz;
+            sq[e] += dz * (xv[u][v][e] - mean[e]);
+          }
       }
     }
   }
@@ -362,6 +402,8 @@ __global__ __launch_bounds__(256) void gavgpool_bwd_kernel(const uint16_t* __res
 
 using namespace dpe;
 
+static unsigned exact_grid(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + 255) / 256); }
+
 static int gs(int64_t n) {
   int64_t g = (n + 255) / 256;
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
@@ -369,17 +411,23 @@ static int gs(int64_t n) {
 
 extern "C" int dpe_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH, int OW,
                                int k, int s, int p, hipStream_t st) {
-  if (C % 8 || k * k > 255) return -1;
-  hipLaunchKernelGGL(maxpool_fwd_kernel<false>, dim3(gs((int64_t)N * OH * OW * C / 8)), dim3(256), 0, st, x, y, idx, N, H, W,
-                     C, OH, OW, k, s, p, nullptr);
+  if (C % 8 || k * k > 255 || (int64_t)N * OH * OW * C / 8 >= (1ll << 31)) return -1;
+  const dim3 g(exact_grid((int64_t)N * OH * OW * C / 8));
+  if (k == 3)
+    hipLaunchKernelGGL((maxpool_fwd_kernel<false, 3>), g, dim3(256), 0, st, x, y, idx, N, H, W, C, OH, OW, k, s, p, nullptr);
+  else
+    hipLaunchKernelGGL((maxpool_fwd_kernel<false, 0>), g, dim3(256), 0, st, x, y, idx, N, H, W, C, OH, OW, k, s, p, nullptr);
   return 0;
 }
 
 extern "C" int dpe_bnrelu_maxpool_fwd(const uint16_t* h, const float* coef, uint16_t* y, uint8_t* idx, int N, int H, int W,
                                       int C, int OH, int OW, int k, int s, int p, hipStream_t st) {
-  if (C % 8 || k * k > 255) return -1;
-  hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3(gs((int64_t)N * OH * OW * C / 8)), dim3(256), 0, st, h, y, idx, N, H, W,
-                     C, OH, OW, k, s, p, coef);
+  if (C % 8 || k * k > 255 || (int64_t)N * OH * OW * C / 8 >= (1ll << 31)) return -1;
+  const dim3 g(exact_grid((int64_t)N * OH * OW * C / 8));
+  if (k == 3)
+    hipLaunchKernelGGL((maxpool_fwd_kernel<true, 3>), g, dim3(256), 0, st, h, y, idx, N, H, W, C, OH, OW, k, s, p, coef);
+  else
+    hipLaunchKernelGGL((maxpool_fwd_kernel<true, 0>), g, dim3(256), 0, st, h, y, idx, N, H, W, C, OH, OW, k, s, p, coef);
   return 0;
 }
 
