@@ -14,6 +14,7 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 
@@ -79,7 +80,9 @@ Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int
     if (!layout_ok(c.cfg, ak, bk)) continue;
     const int64_t tiles = ((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
     const int64_t slots = (int64_t)ncu * c.bpc;
-    const int max_split = allow_split ? 8 : 1;
+    // up to 8 K splits in general; more when the tiles alone leave most CUs idle (a 1x1 conv weight
+    // grad: a few output tiles over 25K-400K pixels), so the split fills one round of slots
+    const int max_split = allow_split ? (int)std::max<int64_t>(8, std::min<int64_t>(128, slots / std::max<int64_t>(1, tiles))) : 1;
     for (int s = 1; s <= max_split; ++s) {
       if (force_splits > 0 && s != force_splits) continue;
       const int64_t kt = (ktiles + s - 1) / s;

@@ -447,6 +447,17 @@ bool pw_stream_on() {
 }
 void set_pw_stream(bool on) { g_pw_stream = on ? 1 : 0; }
 
+// DPE_WGRAD_HGEMM=0 / set_wgrad_hgemm(false): every conv weight grad stays on the implicit GEMM
+int g_wgrad_hgemm = -1;
+bool wgrad_hgemm_on() {
+  if (g_wgrad_hgemm < 0) {
+    const char* e = getenv("DPE_WGRAD_HGEMM");
+    g_wgrad_hgemm = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_wgrad_hgemm == 1;
+}
+void set_wgrad_hgemm(bool on) { g_wgrad_hgemm = on ? 1 : 0; }
+
 bool is_pointwise(const dpe::ConvGeom& g) {
   return g.R == 1 && g.S == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0;
 }
@@ -686,6 +697,22 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64
   a.M = g.K; a.N = g.R * g.S * g.C; a.K = g.N * g.OH * g.OW;
   a.lda = g.K; a.ldb = g.C; a.ldc = a.N;
   a.alpha = (float)alpha;
+  // 1x1 stride-1 weight grads with both channel counts >= 256 (ResNet layers 3-4 and the 512->256
+  // entry of layer 3: 53 GFLOP over a few output tiles) are a plain TN GEMM over the pixels: the
+  // persistent hgemm kernel with the planner's K split and a deterministic slab finalize, as
+  // linear_wgrad.  With 128 channels the TN layout's only tile (256x256) wastes half its MFMAs and
+  // the implicit GEMM is faster (profiles/wgrad_hgemm_ab_r2.txt).
+  if (wgrad_hgemm_on() && is_pointwise(g) && a.K % 64 == 0 && g.K >= 256 && g.C >= 256 && g.K % 8 == 0 &&
+      g.C % 8 == 0) {
+    auto h = hargs();
+    h.A = bp(dy); h.B = bp(x); h.C = dw.data_ptr();
+    h.M = a.M; h.N = a.N; h.K = a.K;
+    h.lda = g.K; h.ldb = g.C; h.ldc = g.C;
+    h.a_dim = (int)((g.K + 7) / 8 * 8);
+    h.alpha = (float)alpha;
+    dpe_gemm::run(h, 0, 0, dpe::HE_ACC_F32, true, 4);
+    return;
+  }
   run_igemm(a, dpe::A_DENSE_M, is_pointwise(g) ? dpe::B_DENSE_N : dpe::B_CONV_WGRAD, dpe::EPI_ATOMIC_F32, true, true);
 }
 
@@ -1224,6 +1251,7 @@ void register_ops(pybind11::module& m) {
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
         py::arg("dw"), py::arg("db") = py::none(), py::arg("dx_out") = py::none());
   m.def("set_pw_stream", &set_pw_stream, "streaming pointwise-conv kernel on/off (pwconv.hip)");
+  m.def("set_wgrad_hgemm", &set_wgrad_hgemm, "1x1 conv weight grads on the persistent hgemm kernel on/off");
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("H"), py::arg("scale"), py::arg("causal") = true);
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("H"),
         py::arg("scale"), py::arg("causal") = true);

@@ -179,6 +179,24 @@ def test_conv_wgrad(C, N, H, W, Ci, Co, k, s, p):
     assert rel_err(dw, ref.permute(0, 2, 3, 1)) < 1e-3
 
 
+@pytest.mark.parametrize("N,H,Ci,Co", [(4, 8, 128, 256), (16, 14, 256, 1024), (64, 28, 512, 128), (64, 7, 512, 2048),
+                                       (8, 28, 128, 512)])
+def test_conv_wgrad_pointwise_hgemm(C, N, H, Ci, Co):
+    # 1x1 weight grads with pixels % 64 == 0 and both channel counts >= 128 run on the persistent
+    # hgemm kernel (TN, K split over the pixels + slab finalize); accumulate with alpha
+    torch.manual_seed(15)
+    x = bf(torch.randn(N, H, H, Ci, device=dev))
+    dy = bf(torch.randn(N, H, H, Co, device=dev))
+    ref = dy.float().reshape(-1, Co).t() @ x.float().reshape(-1, Ci)
+    init = torch.randn(Co, 1, 1, Ci, device=dev)
+    dw = init.clone()
+    C.conv_wgrad(dy, x, dw, [1, 1], [0, 0], [1, 1], 0.5)
+    assert rel_err(dw.reshape(Co, Ci), init.reshape(Co, Ci) + 0.5 * ref) < 1e-3
+    dw.zero_()
+    C.conv_wgrad(dy, x, dw, [1, 1], [0, 0], [1, 1], 1.0)
+    assert rel_err(dw.reshape(Co, Ci), ref) < 1e-3
+
+
 def test_resnet_scale_shapes(C):
     # a real ResNet-50 layer1 shape at batch 32: fwd/dgrad/wgrad
     torch.manual_seed(6)
