@@ -58,6 +58,7 @@ int dpe_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st);
 int dpe_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
 int dpe_act(const void* a, const void* b, void* out, int64_t n, int op, int bf16, hipStream_t st);
 int dpe_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset, int bf16, hipStream_t st);
+int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, float* sink, hipStream_t st);
 int dpe_add(const void* a, const void* b, void* out, int64_t n, float alpha, int bf16, hipStream_t st);
 int dpe_colsum(const void* dy, int64_t M, int N, int64_t ld, float* db, int accumulate, int bf16, hipStream_t st);
 int dpe_nchw_to_s2d(const float* x, uint16_t* y, int N, int C, int H, int W, hipStream_t st);
@@ -182,9 +183,13 @@ void dma_tile(const dpe::IgemmArgs& a, int aload, int bload, int& bm, int& bn) {
   if (bm != 128 || bload != dpe::B_DENSE_K) return;
   int mode = dma_tile_mode();
   const bool taps = aload == dpe::A_CONV_FWD && a.g.R * a.g.S > 1;
-  if (a.N <= 64) {  // N = 64: 256x64 only when forced (measured 240 -> 282 us on 64->64 3x3 at 56x56:
-    // 61 KiB LDS halves the blocks per CU; also slower on the short-K s2d stem, docs/perf_notes.md)
-    if (mode >= 2) { bm = 256; bn = 64; }
+  if (a.N <= 64) {
+    // N = 64 with K >= 256 (layer-1 3x3 forward / data grad, 1x1 256->64): 256x64 tile, 4 waves of
+    // 64x64 on a 2-stage ring (40 KiB, 4 blocks/CU): 236 -> 229 / 227 -> 213 / 215 -> 203 us
+    // (profiles/conv_w64_ab_r2.txt; a 3-stage ring's 60 KiB halved the blocks per CU: 296 / 271 us).
+    // Not the C = 16 s2d stem (short K, measured slower).
+    const bool stem = aload == dpe::A_CONV_FWD && a.g.C == 16;
+    if (mode >= 2 || (mode == 0 && a.K >= 256 && !stem)) { bm = 256; bn = 64; }
     return;
   }
   if (mode == 0) {
@@ -1251,6 +1256,11 @@ void register_ops(pybind11::module& m) {
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
         py::arg("dw"), py::arg("db") = py::none(), py::arg("dx_out") = py::none());
   m.def("set_pw_stream", &set_pw_stream, "streaming pointwise-conv kernel on/off (pwconv.hip)");
+  m.def("cu_hog", [](int64_t nblocks, int64_t threads, int64_t lds_bytes, double us) {
+          static Tensor sink = at::empty({1024}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA));
+          CHECK_RC(dpe_cu_hog((int)nblocks, (int)threads, (int)lds_bytes, us, (float*)sink.data_ptr(), cur_stream()), "cu_hog");
+        }, py::arg("nblocks"), py::arg("threads") = 256, py::arg("lds_bytes") = 0, py::arg("us") = 1000.0,
+        "occupancy probe: nblocks workgroups holding a CU slot for `us` microseconds (current stream)");
   m.def("set_wgrad_hgemm", &set_wgrad_hgemm, "1x1 conv weight grads on the persistent hgemm kernel on/off");
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("H"), py::arg("scale"), py::arg("causal") = true);
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("H"),

@@ -368,3 +368,22 @@ extern "C" int dpe_embedding_bwd(const int64_t* idx, const float* dout, float* d
   hipLaunchKernelGGL(embedding_bwd_kernel, dim3(egrid(rows * D)), dim3(ET), 0, st, idx, dout, dwte, dwpe, rows, T, D);
   return 0;
 }
+
+// CU-occupancy probe: nblocks workgroups that each hold their CU slot (waves, LDS) for `ticks`
+// of the 100 MHz wall clock and then exit -- a stand-in for RCCL's channel workgroups sharing
+// the CUs with backward kernels (scripts/hog_probe.py).  Every wave leaves after the deadline.
+__global__ void cu_hog_kernel(int64_t ticks, float* sink) {
+  extern __shared__ float lds[];
+  const int64_t t0 = wall_clock64();
+  float acc = 0.f;
+  while (wall_clock64() - t0 < ticks) {
+#pragma unroll 1
+    for (int i = 0; i < 64; ++i) acc = acc * 0.999f + 1.f;
+  }
+  if (acc == -1.f) sink[threadIdx.x] = lds[threadIdx.x];  // never true: keeps acc / lds live
+}
+extern "C" int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, float* sink, hipStream_t st) {
+  if (nblocks <= 0 || threads <= 0 || threads > 1024 || us <= 0 || us > 1e6) return -1;
+  hipLaunchKernelGGL(cu_hog_kernel, dim3(nblocks), dim3(threads), lds_bytes, st, (int64_t)(us * 100.0), sink);
+  return (int)hipGetLastError();
+}

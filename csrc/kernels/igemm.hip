@@ -1113,9 +1113,18 @@ extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int a
   if (abytes >= lim || bbytes >= lim) return -1;
   const int tiles = ((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
   const int dn = dense ? 1 : 0;
+// 4-wave tiles: a 2-stage ring keeps 4 blocks/CU; tiles up to DPE_DMA_NS3_MAX elements take the
+// 3-stage ring (two K-steps in flight)
+#ifndef DPE_DMA_NS3_MAX
+#define DPE_DMA_NS3_MAX 0
+#endif
+#ifndef DPE_DMA_W64_NS2
+#define DPE_DMA_W64_NS2 1  // 256x64: 2-stage ring (40 KiB, 4 blocks/CU) instead of 3 (60 KiB, 2)
+#endif
 #define DPE_DMA(BM_, BN_, WGM_, WGN_, BL_, EP_)                                                             \
   if (bm == BM_ && bn == BN_ && bload == BL_ && epi == EP_) {                                               \
-    constexpr int NS_ = (BM_ <= 128 && BN_ <= 128) ? 2 : 3; /* 4 blocks/CU vs two K-steps in flight */      \
+    constexpr int NS_ = ((BM_ <= 128 && BN_ <= 128 && BM_ * BN_ > DPE_DMA_NS3_MAX) ||                        \
+                         (BM_ == 256 && BN_ == 64 && DPE_DMA_W64_NS2)) ? 2 : 3;                                 \
     hipLaunchKernelGGL((igemm_dma_kernel<BM_, BN_, WGM_, WGN_, BL_, EP_, NS_>), dim3(tiles),                 \
                        dim3(64 * WGM_ * WGN_), 0, st, a, dn);                                               \
     return 0;                                                                                               \
