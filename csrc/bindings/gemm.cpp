@@ -82,7 +82,10 @@ Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int
     const int64_t slots = (int64_t)ncu * c.bpc;
     // up to 8 K splits in general; more when the tiles alone leave most CUs idle (a 1x1 conv weight
     // grad: a few output tiles over 25K-400K pixels), so the split fills one round of slots
-    const int max_split = allow_split ? (int)std::max<int64_t>(8, std::min<int64_t>(128, slots / std::max<int64_t>(1, tiles))) : 1;
+    static const int64_t split_cap = [] { const char* e = getenv("DPE_HGEMM_SPLIT_CAP"); return e ? atoll(e) : 128; }();  // A/B
+    const int max_split =
+        allow_split ? (int)std::max<int64_t>(std::min<int64_t>(8, split_cap), std::min<int64_t>(split_cap, slots / std::max<int64_t>(1, tiles)))
+                    : 1;
     for (int s = 1; s <= max_split; ++s) {
       if (force_splits > 0 && s != force_splits) continue;
       const int64_t kt = (ktiles + s - 1) / s;
