@@ -187,7 +187,7 @@ void dma_tile(const dpe::IgemmArgs& a, int aload, int bload, int& bm, int& bn) {
     // N = 64 with K >= 256 (layer-1 3x3 forward / data grad, 1x1 256->64): 256x64 tile, 4 waves of
     // 64x64 on a 2-stage ring (40 KiB, 4 blocks/CU): 236 -> 229 / 227 -> 213 / 215 -> 203 us
     // (profiles/conv_w64_ab_r2.txt; a 3-stage ring's 60 KiB halved the blocks per CU: 296 / 271 us).
-    // Not the C = 16 s2d stem (short K, measured slower).
+    // Not the C = 16 s2d stem (short K: 519 -> 539 us on 256x64 with the 2-stage ring).
     const bool stem = aload == dpe::A_CONV_FWD && a.g.C == 16;
     if (mode >= 2 || (mode == 0 && a.K >= 256 && !stem)) { bm = 256; bn = 64; }
     return;
