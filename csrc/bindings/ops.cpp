@@ -59,6 +59,8 @@ int dpe_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
 int dpe_act(const void* a, const void* b, void* out, int64_t n, int op, int bf16, hipStream_t st);
 int dpe_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset, int bf16, hipStream_t st);
 int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, float* sink, hipStream_t st);
+int dpe_stem_blocks(int N, int H, int W);
+int dpe_stem_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H, int W, hipStream_t st);
 int dpe_add(const void* a, const void* b, void* out, int64_t n, float alpha, int bf16, hipStream_t st);
 int dpe_colsum(const void* dy, int64_t M, int N, int64_t ld, float* db, int accumulate, int bf16, hipStream_t st);
 int dpe_nchw_to_s2d(const float* x, uint16_t* y, int N, int C, int H, int W, hipStream_t st);
@@ -452,6 +454,17 @@ bool pw_stream_on() {
 }
 void set_pw_stream(bool on) { g_pw_stream = on ? 1 : 0; }
 
+// DPE_STEM=0 / set_stem_kernel(false): the s2d stem conv stays on the implicit-GEMM tile
+int g_stem = -1;
+bool stem_on() {
+  if (g_stem < 0) {
+    const char* e = getenv("DPE_STEM");
+    g_stem = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_stem == 1;
+}
+void set_stem_kernel(bool on) { g_stem = on ? 1 : 0; }
+
 // DPE_WGRAD_HGEMM=0 / set_wgrad_hgemm(false): every conv weight grad stays on the implicit GEMM
 int g_wgrad_hgemm = -1;
 bool wgrad_hgemm_on() {
@@ -487,6 +500,17 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
   a.lda = g.C; a.ldb = a.K; a.ldc = g.K;
   a.bias = fpo(bias);
   Tensor stats;
+  // the space-to-depth ResNet stem (16 channels, 4x4 / s1 / pad 2-2-1-1 -> 64): row-walking
+  // kernel with the filter in VGPRs and each input row loaded once (csrc/kernels/stem.hip)
+  const int stem_nb = (stem_on() && g.C == 16 && g.K == 64 && R == 4 && S == 4 && g.sh == 1 && g.sw == 1 && g.ph == 2 &&
+                       g.pw == 2 && pb == 1 && pr == 1 && g.dh == 1 && g.dw == 1 && OH == H && OW == W && !a.bias)
+                          ? dpe_stem_blocks(g.N, g.H, g.W) : 0;
+  if (stem_nb > 0) {
+    if (want_stats) stats = at::empty({2, g.K, stem_nb}, x.options().dtype(at::kFloat));
+    CHECK_RC(dpe_stem_launch(bp(x), bp(w), bpm(y), want_stats ? fp(stats) : nullptr, g.N, g.H, g.W, cur_stream()),
+             "stem conv");
+    return {y, stats};
+  }
   // write-heavy pointwise convs (K <= 256, N >= 2K; the bottleneck conv3 shapes): persistent
   // streaming kernel (csrc/kernels/pwconv.hip), BN partials per row group.
   const int pw_rg = (pw_stream_on() && is_pointwise(g) && !a.bias) ? dpe_pw_rowgroups(a.M, a.N, a.K, dpe::PW_FWD) : 0;
@@ -1261,6 +1285,7 @@ void register_ops(pybind11::module& m) {
           CHECK_RC(dpe_cu_hog((int)nblocks, (int)threads, (int)lds_bytes, us, (float*)sink.data_ptr(), cur_stream()), "cu_hog");
         }, py::arg("nblocks"), py::arg("threads") = 256, py::arg("lds_bytes") = 0, py::arg("us") = 1000.0,
         "occupancy probe: nblocks workgroups holding a CU slot for `us` microseconds (current stream)");
+  m.def("set_stem_kernel", &set_stem_kernel, "s2d stem conv on its row-walking kernel (stem.hip) on/off");
   m.def("set_wgrad_hgemm", &set_wgrad_hgemm, "1x1 conv weight grads on the persistent hgemm kernel on/off");
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("H"), py::arg("scale"), py::arg("causal") = true);
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("H"),

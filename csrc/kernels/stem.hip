@@ -1,0 +1,183 @@
+// ResNet-50 stem convolution over the space-to-depth input: y[n][oh][ow][64] =
+// sum_{dy,dx<4} sum_{c<16} xs[n][oh-2+dy][ow-2+dx][c] * w[o][dy][dx][c]  (4x4, stride 1, pad 2/2/1/1,
+// the 7x7/s2 conv of ops/functional.py's s2d form), plus the BatchNorm-forward (sum, sum of squares)
+// partials of the stored bf16 output.
+//
+// On the implicit-GEMM tile this shape ran at ~234 TF (519 us at batch 512): K = 256 is only eight
+// 32-wide K-steps, the im2col operand re-reads every input pixel 16 times through L2 and each
+// 128x64 tile re-reads the whole 32 KiB filter.  Here a block walks consecutive output rows of one
+// image:
+//   * the filter sits in VGPRs for the whole block (wave (mh, nh): 32 output channels x K = 256
+//     as MFMA operands, 64 VGPRs);
+//   * the four input rows an output row needs live in a 5-slot LDS ring ([132 pixels][16 ch],
+//     zero pixels at both ends); each input row is loaded from HBM once per block (register
+//     prefetch two rows ahead, written into the free slot after the row's MFMAs);
+//   * an output row (112 pixels x 64 channels) is staged in one of two LDS buffers and stored as
+//     whole 16-B chunks of contiguous pixels; BN sums accumulate per thread over the block's rows
+//     and are reduced once: one partial column per block ([2][64][blocks]).
+// One barrier per output row.  Same K order as the implicit GEMM (two taps per K-step), so the
+// output is bitwise identical to it.
+#include "common.h"
+
+namespace dpe {
+namespace stem {
+
+constexpr int CO = 64, KK = 8;            // output channels, 32-wide K-steps (K = 256)
+constexpr int SLOT_PX = 132;              // ring slot pixels: 2 zero + <= 112 data + zero tail
+constexpr int SLOT = SLOT_PX * 32;        // bytes per slot (16 ch bf16 per pixel)
+constexpr int NSLOT = 5;
+constexpr int OROW = 144;                 // staged output row stride (128 B + 16 pad)
+constexpr int OBUF = 112 * OROW;
+constexpr int LDS = NSLOT * SLOT + 2 * OBUF;
+static_assert(LDS <= 163840 / 3, "three blocks per CU");
+
+DPE_DEVICE u32x4 zero16() { return u32x4{0u, 0u, 0u, 0u}; }
+
+__global__ __launch_bounds__(256, 3) void stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                           uint16_t* __restrict__ y, float* __restrict__ stats, int H,
+                                                           int W, int parts) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+  char* const ring = smem;
+  char* const obuf = smem + NSLOT * SLOT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mh = wid & 1, nh = wid >> 1;  // pixel half (frags 0-3 / 4-6), channel half (32 each)
+  const int nfr = mh ? 3 : 4;             // 16-pixel MFMA fragments of this wave (W = 112)
+  const int blk = blockIdx.x;
+  const int n = blk / parts, part = blk - n * parts;
+  const int oh_beg = (int)((int64_t)H * part / parts), oh_end = (int)((int64_t)H * (part + 1) / parts);
+  const int lm = lane & 15, kc = lane >> 4;
+
+  // filter fragments: output channel 32 nh + 16 j + lm, K elements 32 kk + 8 kc .. +7
+  bf16x8 wf[KK][2];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      wf[kk][j] = __builtin_bit_cast(bf16x8, *(const u32x4*)(w + (32 * nh + 16 * j + lm) * 256 + 32 * kk + 8 * kc));
+
+  // zero the ring (pad pixels stay zero; rows outside the image are written as zeros)
+  for (int i = tid; i < NSLOT * SLOT / 16; i += 256) *(u32x4*)(ring + i * 16) = zero16();
+
+  // one input row = W pixels x 32 B = up to 224 16-B chunks: thread t < 2W owns chunk t
+  const int64_t img = (int64_t)n * H * W * 16;
+  auto load_row = [&](int ih) -> u32x4 {
+    if (tid < 2 * W && (unsigned)ih < (unsigned)H) return *(const u32x4*)(x + img + ((int64_t)ih * W) * 16 + tid * 8);
+    return zero16();
+  };
+  auto write_row = [&](int ih, const u32x4& v) {  // input row ih -> slot (ih + 2) % 5, pixel iw + 2
+    if (tid < 2 * W) *(u32x4*)(ring + ((ih + 2 + 5 * 4) % NSLOT) * SLOT + 64 + tid * 16) = v;
+  };
+  __syncthreads();  // ring zeroed before the first rows land
+#pragma unroll
+  for (int d = -2; d < 2; ++d) write_row(oh_beg + d, load_row(oh_beg + d));
+  u32x4 pf0 = load_row(oh_beg + 2), pf1 = load_row(oh_beg + 3);  // rows oh + 2 / oh + 3 of the first iteration
+  __syncthreads();
+
+  float s[8], ss[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
+  const int sc = tid & 7;  // this thread's 8-channel chunk in the store phase
+
+  for (int oh = oh_beg; oh < oh_end; ++oh) {
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // K-step kk: filter row dy = kk / 2, taps dx = 2 (kk & 1) + {0, 1}; lane chunk kc -> tap
+    // dx0 + kc / 2, channels 8 (kc & 1) .. +7.  Input row oh - 2 + dy sits in slot (oh + dy) % 5.
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const char* sl = ring + ((oh + (kk >> 1)) % NSLOT) * SLOT + ((kk & 1) * 2 + (kc >> 1)) * 32 + (kc & 1) * 16;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i < nfr) {
+          const int ow = (mh * 4 + i) * 16 + lm;
+          const bf16x8 af = __builtin_bit_cast(bf16x8, *(const u32x4*)(sl + ow * 32));
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kk][j], af, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    // input row oh + 2 into the slot of row oh - 3 (no longer read); prefetch row oh + 4
+    write_row(oh + 2, pf0);
+    pf0 = pf1;
+    pf1 = load_row(oh + 4);
+    // stage the output row: acc[i][j][e] = pixel (mh*4+i)*16 + lm, channel 32 nh + 16 j + 4 kc + e
+    char* ob = obuf + (oh & 1) * OBUF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i < nfr) {
+        const int ow = (mh * 4 + i) * 16 + lm;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          u32x2 pk;
+          pk[0] = pack_bf2(acc[i][j][0], acc[i][j][1]);
+          pk[1] = pack_bf2(acc[i][j][2], acc[i][j][3]);
+          *(u32x2*)(ob + ow * OROW + (32 * nh + 16 * j + 4 * kc) * 2) = pk;
+        }
+      }
+    }
+    __syncthreads();
+    // store: thread t -> chunk t & 7 of pixels t / 8 + 32 k (whole 128-B pixel rows per 8 lanes)
+    uint16_t* yrow = y + ((int64_t)n * H + oh) * W * CO;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int px = (tid >> 3) + 32 * k;
+      if (px < W) {
+        const u32x4 v = *(const u32x4*)(ob + px * OROW + sc * 16);
+        *(u32x4*)(yrow + px * CO + sc * 8) = v;
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { s[e] += f[e]; ss[e] = fmaf(f[e], f[e], ss[e]); }
+      }
+    }
+  }
+  if (stats) {
+    // reduce over the 32 threads of each chunk: lanes sc + 8 t (xor 8, 16, 32), then 4 waves via LDS
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) {
+        s[e] += __shfl_xor(s[e], o, 64);
+        ss[e] += __shfl_xor(ss[e], o, 64);
+      }
+    __syncthreads();
+    float* red = (float*)ring;  // [2][4 waves][64]
+    if (lane < 8)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[wid * CO + sc * 8 + e] = s[e];
+        red[4 * CO + wid * CO + sc * 8 + e] = ss[e];
+      }
+    __syncthreads();
+    if (tid < CO) {
+      const int nb = gridDim.x;
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { a += red[q * CO + tid]; b += red[4 * CO + q * CO + tid]; }
+      stats[(int64_t)tid * nb + blk] = a;
+      stats[(int64_t)(CO + tid) * nb + blk] = b;
+    }
+  }
+}
+
+}  // namespace stem
+}  // namespace dpe
+
+// Blocks of the launch for an [N, H, W, 16] s2d input (0: outside the kernel's envelope).
+extern "C" int dpe_stem_blocks(int N, int H, int W) {
+  if (N <= 0 || H < 3 || W < 97 || W > 112) return 0;  // 7 pixel fragments, 4 + 3 per wave pair
+  return N * 3;
+}
+
+// y [N, H, W, 64] bf16, stats [2][64][dpe_stem_blocks] or nullptr; w [64][4][4][16] bf16.
+extern "C" int dpe_stem_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H, int W,
+                               hipStream_t st) {
+  const int nb = dpe_stem_blocks(N, H, W);
+  if (nb <= 0) return -1;
+  hipLaunchKernelGGL(dpe::stem::stem_conv_kernel, dim3(nb), dim3(256), 0, st, x, w, y, stats, H, W, 3);
+  return (int)hipGetLastError();
+}

@@ -823,3 +823,27 @@ def test_pw_stream_matches_igemm(C, N, H, W, Ci, Co):
         if s1 is not None:
             assert s1.shape[:2] == s2.shape[:2]
             assert rel_err(s1.sum(-1), s2.sum(-1)) < 1e-4, i
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 112, 112), (3, 112, 112), (1, 7, 100), (4, 3, 112)])
+def test_stem_kernel_matches_igemm(C, N, H, W):
+    """The row-walking s2d stem kernel (stem.hip: filter in VGPRs, 5-row LDS ring, per-block BN
+    partials) == the implicit-GEMM tile on the same inputs: output bitwise (same K order), BN sums
+    to fp32 summation order; and both match the fp32 reference conv."""
+    torch.manual_seed(37)
+    xs = bf(torch.randn(N, H, W, 16, device=dev))
+    w = bf(torch.randn(64, 4, 4, 16, device=dev) / 16)
+    runs = {}
+    for on in (True, False):
+        C.set_stem_kernel(on)
+        try:
+            runs[on] = C.conv_fwd(xs, w, [1, 1], [2, 2, 1, 1], [1, 1], True, None)
+        finally:
+            C.set_stem_kernel(True)
+    (y1, s1), (y2, s2) = runs[True], runs[False]
+    ref = F.conv2d(F.pad(xs.permute(0, 3, 1, 2).float(), (2, 1, 2, 1)), w.permute(0, 3, 1, 2).float()).permute(0, 2, 3, 1)
+    assert y1.shape == ref.shape and rel_err(y1, ref) < 1e-2
+    assert torch.equal(y1, y2)
+    assert rel_err(s1.sum(-1), s2.sum(-1)) < 1e-4
+    yf = y1.float().reshape(-1, 64)
+    assert rel_err(s1.sum(-1)[0], yf.sum(0)) < 1e-3 and rel_err(s1.sum(-1)[1], (yf * yf).sum(0)) < 1e-3
