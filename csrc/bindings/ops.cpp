@@ -59,6 +59,9 @@ int dpe_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
 int dpe_act(const void* a, const void* b, void* out, int64_t n, int op, int bf16, hipStream_t st);
 int dpe_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset, int bf16, hipStream_t st);
 int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, float* sink, hipStream_t st);
+int dpe_conv3x3_rows_blocks(int N, int H, int W);
+int dpe_conv3x3_rows_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* st_x,
+                            const float* st_coef, int N, int H, int W, int bnb, hipStream_t st);
 int dpe_stem_blocks(int N, int H, int W);
 int dpe_stem_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H, int W, hipStream_t st);
 int dpe_add(const void* a, const void* b, void* out, int64_t n, float alpha, int bf16, hipStream_t st);
@@ -454,6 +457,23 @@ bool pw_stream_on() {
 }
 void set_pw_stream(bool on) { g_pw_stream = on ? 1 : 0; }
 
+// DPE_ROWCONV=0 / set_rowconv(false): the 64-channel 3x3 convs stay on the implicit-GEMM tiles
+int g_rowconv = -1;
+bool rowconv_on() {
+  if (g_rowconv < 0) {
+    const char* e = getenv("DPE_ROWCONV");
+    g_rowconv = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_rowconv == 1;
+}
+void set_rowconv(bool on) { g_rowconv = on ? 1 : 0; }
+// 3x3 / stride 1 / pad 1 / dilation 1, 64 -> 64 channels, W <= 64: the row-walking kernel's envelope
+bool rowconv_geom(const dpe::ConvGeom& g) {
+  return rowconv_on() && g.C == 64 && g.K == 64 && g.R == 3 && g.S == 3 && g.sh == 1 && g.sw == 1 && g.ph == 1 &&
+         g.pw == 1 && g.dh == 1 && g.dw == 1 && g.OH == g.H && g.OW == g.W &&
+         dpe_conv3x3_rows_blocks(g.N, g.H, g.W) > 0;
+}
+
 // DPE_STEM=0 / set_stem_kernel(false): the s2d stem conv stays on the implicit-GEMM tile
 int g_stem = -1;
 bool stem_on() {
@@ -505,6 +525,15 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
   const int stem_nb = (stem_on() && g.C == 16 && g.K == 64 && R == 4 && S == 4 && g.sh == 1 && g.sw == 1 && g.ph == 2 &&
                        g.pw == 2 && pb == 1 && pr == 1 && g.dh == 1 && g.dw == 1 && OH == H && OW == W && !a.bias)
                           ? dpe_stem_blocks(g.N, g.H, g.W) : 0;
+  if (rowconv_geom(g) && pb == 1 && pr == 1 && !a.bias) {
+    // 64-channel 3x3 (layer 1 conv2): row-walking kernel, filter in VGPRs (csrc/kernels/rowconv.hip)
+    const int nb = dpe_conv3x3_rows_blocks(g.N, g.H, g.W);
+    if (want_stats) stats = at::empty({2, g.K, nb}, x.options().dtype(at::kFloat));
+    CHECK_RC(dpe_conv3x3_rows_launch(bp(x), bp(w), bpm(y), want_stats ? fp(stats) : nullptr, nullptr, nullptr, g.N, g.H,
+                                     g.W, 0, cur_stream()),
+             "conv3x3 rows fwd");
+    return {y, stats};
+  }
   if (stem_nb > 0) {
     if (want_stats) stats = at::empty({2, g.K, stem_nb}, x.options().dtype(at::kFloat));
     CHECK_RC(dpe_stem_launch(bp(x), bp(w), bpm(y), want_stats ? fp(stats) : nullptr, g.N, g.H, g.W, cur_stream()),
@@ -620,6 +649,16 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
     Tensor wt = at::empty({g.C, g.R, g.S, g.K}, w.options());
     CHECK_RC(dpe_conv_w_flipT(bp(w), bpm(wt), g.K, g.R, g.S, g.C, 0, 1, g.R, 0, 1, g.S, cur_stream()), "conv_w_flipT");
     auto f = geom(dy, wt, 1, 1, g.R - 1 - g.ph, g.S - 1 - g.pw, 1, 1, g.H, g.W);
+    if (rowconv_geom(f) && !acc_into && !a.residual && !a.st_mask) {
+      // 64-channel 3x3 data grad (layer 1): the row-walking forward kernel over dy with the flipped
+      // filter; BN-backward partials per block
+      const int nb = dpe_conv3x3_rows_blocks(f.N, f.H, f.W);
+      if (want_bn) part = at::empty({2, g.C, nb}, dy.options().dtype(at::kFloat));
+      CHECK_RC(dpe_conv3x3_rows_launch(bp(dy), bp(wt), bpm(dx), want_bn ? fp(part) : nullptr, a.st_x, a.st_coef, f.N, f.H,
+                                       f.W, want_bn ? 1 : 0, cur_stream()),
+               "conv3x3 rows dgrad");
+      return {dx, part};
+    }
     auto b = a;
     b.g = f;
     b.B = bp(wt);
@@ -1285,6 +1324,7 @@ void register_ops(pybind11::module& m) {
           CHECK_RC(dpe_cu_hog((int)nblocks, (int)threads, (int)lds_bytes, us, (float*)sink.data_ptr(), cur_stream()), "cu_hog");
         }, py::arg("nblocks"), py::arg("threads") = 256, py::arg("lds_bytes") = 0, py::arg("us") = 1000.0,
         "occupancy probe: nblocks workgroups holding a CU slot for `us` microseconds (current stream)");
+  m.def("set_rowconv", &set_rowconv, "64-channel 3x3 convs on the row-walking kernel (rowconv.hip) on/off");
   m.def("set_stem_kernel", &set_stem_kernel, "s2d stem conv on its row-walking kernel (stem.hip) on/off");
   m.def("set_wgrad_hgemm", &set_wgrad_hgemm, "1x1 conv weight grads on the persistent hgemm kernel on/off");
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("H"), py::arg("scale"), py::arg("causal") = true);

@@ -847,3 +847,36 @@ def test_stem_kernel_matches_igemm(C, N, H, W):
     assert rel_err(s1.sum(-1), s2.sum(-1)) < 1e-4
     yf = y1.float().reshape(-1, 64)
     assert rel_err(s1.sum(-1)[0], yf.sum(0)) < 1e-3 and rel_err(s1.sum(-1)[1], (yf * yf).sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 56, 56), (3, 56, 56), (5, 8, 8), (3, 14, 14), (1, 20, 40), (2, 9, 17), (2, 5, 64),
+                                   (1, 2, 3)])
+def test_rowconv_matches_igemm(C, N, H, W):
+    """The row-walking 64-channel 3x3 kernel (rowconv.hip: filter in VGPRs, swizzled 4-row LDS ring,
+    per-block partials) == the implicit-GEMM tiles on the same inputs: forward with BN sums, the
+    stride-1 data grad, and the data grad with the BN-backward epilogue.  Outputs bitwise (same K
+    order), partial sums to fp32 summation order; the forward also against the fp32 reference."""
+    torch.manual_seed(41)
+    x = bf(torch.randn(N, H, W, 64, device=dev))
+    w = bf(torch.randn(64, 3, 3, 64, device=dev) / 24)
+    dy = bf(torch.randn(N, H, W, 64, device=dev))
+    h = bf(torch.randn(N, H, W, 64, device=dev))
+    coef = _bn_coef(C, 64)
+    sh = [N, H, W, 64]
+    z = [1, 1], [1, 1], [1, 1]
+    runs = {}
+    for on in (True, False):
+        C.set_rowconv(on)
+        try:
+            runs[on] = [
+                C.conv_fwd(x, w, *z, True, None),
+                (C.conv_dgrad(dy, w, sh, *z, None), None),
+                tuple(C.conv_dgrad_bn(dy, w, sh, *z, None, h, coef)),
+            ]
+        finally:
+            C.set_rowconv(True)
+    assert rel_err(runs[True][0][0], _conv_ref(x, w, 1, 1)) < 1e-2
+    for i, ((y1, s1), (y2, s2)) in enumerate(zip(runs[True], runs[False])):
+        assert torch.equal(y1, y2), i
+        if s1 is not None:
+            assert rel_err(s1.sum(-1), s2.sum(-1)) < 1e-4, i
