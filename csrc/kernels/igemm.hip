@@ -911,16 +911,23 @@ DPE_DEVICE int mn_swz(int k) {
   else return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1;
 }
 
+// 4 or 8 waves.  Tiles with 64x128 wave tiles (128x256 / 256x128 / 256x256: half the L2 bytes
+// per flop of 128x128) measured 1.2-1.8x SLOWER on every ResNet-50 weight-grad shape
+// (profiles/wgrad_bigtile_ab_r2.txt): at ~210 VGPRs they run 2 waves per SIMD where 128x128
+// runs 4, and the one-barrier-per-32-K ring does not hide the DMA latency at that occupancy.
+// Not instantiated; the waves-per-EU bound below is what such a tile needs.
 template <int BM, int BN, int BL, int WGM = 2, int WGN = 2, int NS = DSTAGES>
-__global__ __launch_bounds__(NT) void igemm_wgrad_dma_kernel(IgemmArgs p) {
-  static_assert(WGM * WGN == 4, "4 waves");
+__global__ __launch_bounds__(64 * WGM * WGN, (BN / WGN > 64) ? 2 : 1) void igemm_wgrad_dma_kernel(IgemmArgs p) {
+  constexpr int NW = WGM * WGN;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr bool CONV = (BL == B_CONV_WGRAD);
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int LDS_MAIN = NS * STAGE, LDS_ST = (BM / WGM) * (BN + 4) * 4;
   constexpr int LDS = LDS_MAIN > LDS_ST ? LDS_MAIN : LDS_ST;
   constexpr int RM = BM / WGM / 16, RN = BN / WGN / 16;
-  constexpr int PA = BM / 64, PB = BN / 64;  // 1-KiB pieces per wave per stage (4 waves)
+  constexpr int PA = BM / (16 * NW), PB = BN / (16 * NW);  // 1-KiB pieces per wave per stage
+  static_assert(PA >= 1 && PB >= 1, "every wave issues A and B pieces");
   constexpr int ACPR = BM / 8, AKR = 64 / ACPR, BCPR = BN / 8, BKR = 64 / BCPR;
   __shared__ __attribute__((aligned(16))) char smem[LDS];
 

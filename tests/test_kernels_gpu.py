@@ -693,7 +693,9 @@ def test_conv_tiles_lds_dma(C, mode, N, H, W, Ci, Co, k, s, p):
 @pytest.mark.parametrize("N,H,W,Ci,Co,k,s,p", [(8, 14, 14, 64, 64, 3, 1, 1), (32, 7, 7, 128, 200, 3, 1, 1),
                                                (8, 28, 28, 96, 128, 3, 2, 1), (4, 56, 56, 64, 256, 1, 1, 0),
                                                (8, 28, 28, 256, 512, 1, 2, 0), (32, 7, 7, 512, 512, 3, 1, 1),
-                                               (16, 14, 14, 64, 48, 3, 1, 1), (8, 28, 28, 32, 64, 3, 1, 1)])
+                                               (16, 14, 14, 64, 48, 3, 1, 1), (8, 28, 28, 32, 64, 3, 1, 1),
+                                               (8, 14, 14, 256, 256, 3, 1, 1), (8, 14, 14, 128, 384, 3, 2, 1),
+                                               (8, 28, 28, 128, 512, 1, 1, 0), (8, 28, 28, 512, 128, 1, 1, 0)])
 def test_conv_wgrad_lds_dma(C, N, H, W, Ci, Co, k, s, p):
     """LDS-DMA weight-grad kernel (pixel count % 32 == 0): im2col pixel walk across image
     boundaries (OW = 7 / 14 / 28), taps spanning a column tile (C = 64 / 96), split-K, M / N
