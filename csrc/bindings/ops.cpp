@@ -60,6 +60,9 @@ int dpe_act(const void* a, const void* b, void* out, int64_t n, int op, int bf16
 int dpe_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset, int bf16, hipStream_t st);
 int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, float* sink, hipStream_t st);
 int dpe_conv3x3_rows_blocks(int N, int H, int W);
+int64_t dpe_wgrad3x3_rows_scratch(int N, int H, int W);
+int dpe_wgrad3x3_rows_launch(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H, int W,
+                             float alpha, hipStream_t st);
 int dpe_conv3x3_rows_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* st_x,
                             const float* st_coef, int N, int H, int W, int bnb, hipStream_t st);
 int dpe_stem_blocks(int N, int H, int W);
@@ -467,6 +470,16 @@ bool rowconv_on() {
   return g_rowconv == 1;
 }
 void set_rowconv(bool on) { g_rowconv = on ? 1 : 0; }
+// DPE_ROW_WGRAD=0 / set_row_wgrad(false): their weight grads stay on the im2col weight-grad tile
+int g_row_wgrad = -1;
+bool row_wgrad_on() {
+  if (g_row_wgrad < 0) {
+    const char* e = getenv("DPE_ROW_WGRAD");
+    g_row_wgrad = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_row_wgrad == 1;
+}
+void set_row_wgrad(bool on) { g_row_wgrad = on ? 1 : 0; }
 // 3x3 / stride 1 / pad 1 / dilation 1, 64 -> 64 channels, W <= 64: the row-walking kernel's envelope
 bool rowconv_geom(const dpe::ConvGeom& g) {
   return rowconv_on() && g.C == 64 && g.K == 64 && g.R == 3 && g.S == 3 && g.sh == 1 && g.sw == 1 && g.ph == 1 &&
@@ -765,6 +778,13 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64
   a.M = g.K; a.N = g.R * g.S * g.C; a.K = g.N * g.OH * g.OW;
   a.lda = g.K; a.ldb = g.C; a.ldc = a.N;
   a.alpha = (float)alpha;
+  // 64 -> 64 3x3 (ResNet layer 1): the row-walking weight-grad kernel (rowconv.hip)
+  if (row_wgrad_on() && rowconv_geom(g) && dpe_wgrad3x3_rows_scratch(g.N, g.H, g.W) > 0) {
+    auto scratch = at::empty({dpe_wgrad3x3_rows_scratch(g.N, g.H, g.W)}, dw.options());
+    CHECK_RC(dpe_wgrad3x3_rows_launch(bp(x), bp(dy), fp(dw), fp(scratch), g.N, g.H, g.W, (float)alpha, cur_stream()),
+             "wgrad3x3_rows");
+    return;
+  }
   // 1x1 stride-1 weight grads with both channel counts >= 256 (ResNet layers 3-4 and the 512->256
   // entry of layer 3: 53 GFLOP over a few output tiles) are a plain TN GEMM over the pixels: the
   // persistent hgemm kernel with the planner's K split and a deterministic slab finalize, as
@@ -1324,6 +1344,7 @@ void register_ops(pybind11::module& m) {
           CHECK_RC(dpe_cu_hog((int)nblocks, (int)threads, (int)lds_bytes, us, (float*)sink.data_ptr(), cur_stream()), "cu_hog");
         }, py::arg("nblocks"), py::arg("threads") = 256, py::arg("lds_bytes") = 0, py::arg("us") = 1000.0,
         "occupancy probe: nblocks workgroups holding a CU slot for `us` microseconds (current stream)");
+  m.def("set_row_wgrad", &set_row_wgrad, "64-channel 3x3 weight grads on the row-walking kernel (rowconv.hip) on/off");
   m.def("set_rowconv", &set_rowconv, "64-channel 3x3 convs on the row-walking kernel (rowconv.hip) on/off");
   m.def("set_stem_kernel", &set_stem_kernel, "s2d stem conv on its row-walking kernel (stem.hip) on/off");
   m.def("set_wgrad_hgemm", &set_wgrad_hgemm, "1x1 conv weight grads on the persistent hgemm kernel on/off");

@@ -220,6 +220,156 @@ __global__ __launch_bounds__(256, 2) void conv3x3_rows_kernel(RowArgs p) {
   }
 }
 
+
+// ------------------------------------------------------------------ weight grad
+// dW[co][r][s][ci] += alpha * sum_{n, oh, ow} dy[n, oh, ow, co] * x[n, oh + r - 1, ow + s - 1, ci]
+// for the same 64 -> 64 3x3 / stride-1 / pad-1 layer.  As a GEMM this is M = 64, N = 576 (9 taps x
+// 64), K = the 1.6 M output pixels at batch 512; the im2col weight-grad tile (igemm_wgrad_dma,
+// 64x128) reads every activation once per tap through L2 and ran at ~320 TF (365 us).  Here a
+// block walks the output rows of one image and keeps the whole 64 x 576 gradient of that image in
+// registers: wave w owns input channels 16 w .. +15 for all 9 taps and all 64 output channels
+// (4 x 9 accumulator tiles, 144 VGPRs).  Per output row the dy row (K = pixels, M = co) and the three
+// x rows (K = pixels shifted by the tap column, N = ci) are LDS images read with the transposing
+// ds_read_b64_tr_b16, so each input row is read from HBM once per block.  The block's gradient is
+// stored as one coalesced fp32 partial ([blocks][64 x 576], in accumulator order) and a second
+// kernel sums the partials into dW (fp32 atomics across 16 partial groups).
+namespace wg {
+constexpr int XSLOT = 66 * 128;              // x row: zero pixel, W (<= 64) pixels, zero pixels
+constexpr int DSLOT = 64 * 128;              // dy row: W pixels, zero rows up to 64
+constexpr int LDS = NSLOT * XSLOT + 2 * DSLOT;
+constexpr int PART = 64 * 576;               // floats of one block's partial
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// [pixel rows][64 ch] image, 16-B chunks XOR-swizzled by bits 1 and 3 of the row: the transposing
+// reads below (rows 8g+q and 8g+q+4 of any 32-row window, shifted by 0-2 rows) are conflict-free
+DPE_DEVICE int img_off(int k, int chunk) {
+  const int h = (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1;
+  return k * 128 + ((chunk ^ h) << 4);
+}
+// MFMA operand fragment: channels c0 .. c0 + 15 (lane & 15), K = image rows row0 + 8 (lane >> 4) .. +7
+DPE_DEVICE bf16x8 trfrag(const char* img, int row0, int c0) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int k1 = row0 + 8 * g + q;
+  const int mc = (c0 >> 3) + (pp >> 1), sub = (pp & 1) * 8;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + img_off(k1, mc) + sub));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + img_off(k1 + 4, mc) + sub));
+  s16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+__global__ __launch_bounds__(256, 2) void wgrad3x3_rows_kernel(const uint16_t* __restrict__ x,
+                                                               const uint16_t* __restrict__ dy,
+                                                               float* __restrict__ part, int H, int W) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+  char* const ring = smem;                     // x rows: input row ih in slot (ih + 1) % 4
+  char* const dbuf = smem + NSLOT * XSLOT;     // dy rows: output row oh in slot oh & 1
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // input channels 16 w .. +15
+  const int n = blockIdx.x;
+  const int64_t img = (int64_t)n * H * W * 64;
+  const int nch = W * 8;
+
+  for (int i = tid; i < LDS / 16; i += 256) *(u32x4*)(smem + i * 16) = zero16();
+
+  auto load = [&](const uint16_t* src, int row, u32x4 (&v)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = tid + 256 * u;
+      v[u] = (c < nch && (unsigned)row < (unsigned)H) ? *(const u32x4*)(src + img + (int64_t)row * W * 64 + c * 8)
+                                                      : zero16();
+    }
+  };
+  auto put = [&](char* sl, int px0, const u32x4 (&v)[2]) {  // chunk c -> pixel row px0 + c / 8
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = tid + 256 * u;
+      if (c < nch) *(u32x4*)(sl + img_off(px0 + (c >> 3), c & 7)) = v[u];
+    }
+  };
+  auto xslot = [&](int ih) { return ring + ((ih + 1 + NSLOT) % NSLOT) * XSLOT; };
+  __syncthreads();
+  {
+    u32x4 t0[2], t1[2], t2[2];
+    load(x, -1, t0);
+    load(x, 0, t1);
+    load(dy, 0, t2);
+    put(xslot(-1), 1, t0);
+    put(xslot(0), 1, t1);
+    put(dbuf, 0, t2);
+    load(x, 1, t0);
+    put(xslot(1), 1, t0);
+  }
+  u32x4 px0[2], px1[2], pd0[2], pd1[2];  // prefetch: x rows oh + 2, oh + 3; dy rows oh + 1, oh + 2
+  load(x, 2, px0);
+  load(x, 3, px1);
+  load(dy, 1, pd0);
+  load(dy, 2, pd1);
+  __syncthreads();
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nks = W > 32 ? 2 : 1;  // 32-pixel K-steps per row (pixels >= W are zero rows of dy)
+
+  for (int oh = 0; oh < H; ++oh) {
+    const char* ds = dbuf + (oh & 1) * DSLOT;
+    for (int ks = 0; ks < nks; ++ks) {
+      bf16x8 a[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) a[m] = trfrag(ds, 32 * ks, 16 * m);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int r = t / 3, sc = t % 3;
+        // x row oh - 1 + r (slot (oh + r) % 4); output pixel ow reads slot pixel ow + sc
+        const bf16x8 b = trfrag(ring + ((oh + r) % NSLOT) * XSLOT, 32 * ks + sc, 16 * w);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a[m], acc[m][t], 0, 0, 0);
+      }
+    }
+    // x row oh + 2 into the slot of row oh - 2, dy row oh + 1 into the slot of row oh - 1 (both free)
+    put(xslot(oh + 2), 1, px0);
+    put(dbuf + ((oh + 1) & 1) * DSLOT, 0, pd0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) { px0[u] = px1[u]; pd0[u] = pd1[u]; }
+    load(x, oh + 4, px1);
+    load(dy, oh + 3, pd1);
+    __syncthreads();
+  }
+  // acc[m][t][e]: co = 16 m + (lane & 15), ci = 16 w + 4 (lane >> 4) + e, tap t
+  float* pb = part + (int64_t)n * PART;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) *(f32x4*)(pb + (((m * 9 + t) * 4 + w) * 64 + lane) * 4) = acc[m][t];
+}
+
+// dW [64][3][3][64] += alpha * sum of the partials; grid (PART / 1024, groups), 256 threads: one
+// float4 of accumulator order per thread over nparts / groups partials
+__global__ __launch_bounds__(256) void wgrad3x3_rows_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw,
+                                                                   int nparts, int per, float alpha) {
+  const int q = blockIdx.x * 256 + threadIdx.x;  // float4 index, < PART / 4
+  const int b0 = blockIdx.y * per, b1 = min(nparts, b0 + per);
+  f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0;
+  const f32x4* src = (const f32x4*)part + q;
+  int b = b0;
+  for (; b + 1 < b1; b += 2) {
+    s0 += src[(int64_t)b * (PART / 4)];
+    s1 += src[(int64_t)(b + 1) * (PART / 4)];
+  }
+  if (b < b1) s0 += src[(int64_t)b * (PART / 4)];
+  s0 += s1;
+  const int lane = q & 63, w = (q >> 6) & 3, mt = q >> 8, t = mt % 9, m = mt / 9;
+  float* d = dw + (16 * m + (lane & 15)) * 576 + t * 64 + 16 * w + 4 * (lane >> 4);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) atomicAdd(d + e, alpha * s0[e]);
+}
+}  // namespace wg
 }  // namespace rowconv
 }  // namespace dpe
 
@@ -238,5 +388,23 @@ extern "C" int dpe_conv3x3_rows_launch(const uint16_t* x, const uint16_t* w, uin
   dpe::rowconv::RowArgs a{x, w, y, stats, st_x, st_coef, N, H, W, 2};
   if (bnb) hipLaunchKernelGGL(dpe::rowconv::conv3x3_rows_kernel<true>, dim3(nb), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(dpe::rowconv::conv3x3_rows_kernel<false>, dim3(nb), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// Scratch floats of the weight-grad launch (the per-image partials), 0: outside the envelope.
+extern "C" int64_t dpe_wgrad3x3_rows_scratch(int N, int H, int W) {
+  if (N <= 0 || H < 1 || W < 1 || W > 64) return 0;
+  return (int64_t)N * dpe::rowconv::wg::PART;
+}
+
+// dw (+)= alpha * dW of conv3x3(x) w.r.t. its filter, given dy (64 -> 64, stride 1, pad 1).
+extern "C" int dpe_wgrad3x3_rows_launch(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H,
+                                        int W, float alpha, hipStream_t st) {
+  if (dpe_wgrad3x3_rows_scratch(N, H, W) <= 0 || !scratch) return -1;
+  using namespace dpe::rowconv::wg;
+  hipLaunchKernelGGL(wgrad3x3_rows_kernel, dim3(N), dim3(256), 0, st, x, dy, scratch, H, W);
+  const int groups = N >= 64 ? 16 : 1;
+  const int per = (N + groups - 1) / groups;
+  hipLaunchKernelGGL(wgrad3x3_rows_reduce_kernel, dim3(PART / 1024, groups), dim3(256), 0, st, scratch, dw, N, per, alpha);
   return (int)hipGetLastError();
 }

@@ -882,3 +882,29 @@ def test_rowconv_matches_igemm(C, N, H, W):
         assert torch.equal(y1, y2), i
         if s1 is not None:
             assert rel_err(s1.sum(-1), s2.sum(-1)) < 1e-4, i
+
+
+@pytest.mark.parametrize("N,H,W", [(3, 56, 56), (2, 9, 20), (70, 7, 7), (2, 5, 64)])
+def test_row_wgrad_matches_reference(C, N, H, W):
+    """Row-walking 64-channel 3x3 weight grad (rowconv.hip: per-image gradient in registers, dy and
+    x rows as LDS images read with ds_read_b64_tr_b16, coalesced per-image partials + a reduce
+    kernel): vs the fp32 reference and the im2col weight-grad tile, accumulating into an existing
+    gradient with alpha; W <= 32 takes one K-step per row, N >= 64 the grouped partial reduce."""
+    torch.manual_seed(43)
+    x = bf(torch.randn(N, H, W, 64, device=dev))
+    dy = bf(torch.randn(N, H, W, 64, device=dev))
+    w = torch.randn(64, 64, 3, 3, device=dev, requires_grad=True)
+    y = F.conv2d(x.permute(0, 3, 1, 2).float(), w, None, 1, 1)
+    (ref,) = torch.autograd.grad(y, w, dy.permute(0, 3, 1, 2).float())
+    dw0 = torch.randn(64, 3, 3, 64, device=dev)
+    outs = {}
+    for on in (True, False):
+        C.set_row_wgrad(on)
+        try:
+            dw = dw0.clone()
+            C.conv_wgrad(dy, x, dw, [1, 1], [1, 1], [1, 1], 0.5)
+        finally:
+            C.set_row_wgrad(True)
+        outs[on] = dw - dw0
+    assert rel_err(outs[True], 0.5 * ref.permute(0, 2, 3, 1)) < 1e-4
+    assert rel_err(outs[True], outs[False]) < 1e-4
