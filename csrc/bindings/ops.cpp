@@ -62,9 +62,9 @@ int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, float* sink, 
 int dpe_conv3x3_rows_blocks(int N, int H, int W);
 int64_t dpe_wgrad3x3_rows_scratch(int N, int H, int W);
 int dpe_wgrad3x3_rows_launch(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H, int W,
-                             float alpha, hipStream_t st);
+                             float alpha, const float* in_coef, hipStream_t st);
 int dpe_conv3x3_rows_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* st_x,
-                            const float* st_coef, int N, int H, int W, int bnb, hipStream_t st);
+                            const float* st_coef, int N, int H, int W, int bnb, const float* in_coef, hipStream_t st);
 int dpe_stem_blocks(int N, int H, int W);
 int dpe_stem_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H, int W, hipStream_t st);
 int dpe_add(const void* a, const void* b, void* out, int64_t n, float alpha, int bf16, hipStream_t st);
@@ -514,8 +514,11 @@ bool is_pointwise(const dpe::ConvGeom& g) {
 }
 
 // x NHWC bf16 [N,H,W,C], w [K,R,S,C] bf16 -> y NHWC [N,OH,OW,K]
+// in_coef: x is the pre-BN tensor of a BatchNorm+ReLU whose output was never stored ([4][C] coefficients;
+// relu(x * scale + shift) is applied on load) -- only on the row-walking 64-channel 3x3 kernel
 std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64_t> stride, std::vector<int64_t> pad,
-                             std::vector<int64_t> dil, bool want_stats, const c10::optional<Tensor>& bias) {
+                             std::vector<int64_t> dil, bool want_stats, const c10::optional<Tensor>& bias,
+                             const c10::optional<Tensor>& in_coef) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && x.size(3) == w.size(3), "conv: NHWC x / KRSC w shape mismatch");
   TORCH_CHECK(x.size(3) % 8 == 0 && w.size(0) % 8 == 0, "conv: channels must be multiples of 8");
@@ -538,12 +541,15 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
   const int stem_nb = (stem_on() && g.C == 16 && g.K == 64 && R == 4 && S == 4 && g.sh == 1 && g.sw == 1 && g.ph == 2 &&
                        g.pw == 2 && pb == 1 && pr == 1 && g.dh == 1 && g.dw == 1 && OH == H && OW == W && !a.bias)
                           ? dpe_stem_blocks(g.N, g.H, g.W) : 0;
+  const float* icoef = fpo(in_coef);
+  TORCH_CHECK(!icoef || (rowconv_geom(g) && pb == 1 && pr == 1 && !a.bias),
+              "conv_fwd: in_coef (BN+ReLU on load) needs the row-walking 64-channel 3x3 kernel");
   if (rowconv_geom(g) && pb == 1 && pr == 1 && !a.bias) {
     // 64-channel 3x3 (layer 1 conv2): row-walking kernel, filter in VGPRs (csrc/kernels/rowconv.hip)
     const int nb = dpe_conv3x3_rows_blocks(g.N, g.H, g.W);
     if (want_stats) stats = at::empty({2, g.K, nb}, x.options().dtype(at::kFloat));
     CHECK_RC(dpe_conv3x3_rows_launch(bp(x), bp(w), bpm(y), want_stats ? fp(stats) : nullptr, nullptr, nullptr, g.N, g.H,
-                                     g.W, 0, cur_stream()),
+                                     g.W, 0, icoef, cur_stream()),
              "conv3x3 rows fwd");
     return {y, stats};
   }
@@ -668,7 +674,7 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
       const int nb = dpe_conv3x3_rows_blocks(f.N, f.H, f.W);
       if (want_bn) part = at::empty({2, g.C, nb}, dy.options().dtype(at::kFloat));
       CHECK_RC(dpe_conv3x3_rows_launch(bp(dy), bp(wt), bpm(dx), want_bn ? fp(part) : nullptr, a.st_x, a.st_coef, f.N, f.H,
-                                       f.W, want_bn ? 1 : 0, cur_stream()),
+                                       f.W, want_bn ? 1 : 0, nullptr, cur_stream()),
                "conv3x3 rows dgrad");
       return {dx, part};
     }
@@ -767,8 +773,9 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape
 }
 
 // dw [K,R,S,C] fp32 (+)= alpha * dy^T (x) im2col(x)
+// in_coef: as conv_fwd's (x pre-BN, BN+ReLU applied on load; row-walking 64-channel 3x3 kernel only)
 void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64_t> stride, std::vector<int64_t> pad,
-                std::vector<int64_t> dil, double alpha) {
+                std::vector<int64_t> dil, double alpha, const c10::optional<Tensor>& in_coef) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(x); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
   auto g = geom(x, dw, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], dy.size(1), dy.size(2));
   TORCH_CHECK(dy.size(3) == g.K && dy.size(0) == g.N, "conv_wgrad: dy shape mismatch");
@@ -779,9 +786,13 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64
   a.lda = g.K; a.ldb = g.C; a.ldc = a.N;
   a.alpha = (float)alpha;
   // 64 -> 64 3x3 (ResNet layer 1): the row-walking weight-grad kernel (rowconv.hip)
-  if (row_wgrad_on() && rowconv_geom(g) && dpe_wgrad3x3_rows_scratch(g.N, g.H, g.W) > 0) {
+  const float* icoef = fpo(in_coef);
+  const bool row = rowconv_geom(g) && dpe_wgrad3x3_rows_scratch(g.N, g.H, g.W) > 0;
+  TORCH_CHECK(!icoef || row, "conv_wgrad: in_coef (BN+ReLU on load) needs the row-walking 64-channel 3x3 kernel");
+  if (row && (row_wgrad_on() || icoef)) {
     auto scratch = at::empty({dpe_wgrad3x3_rows_scratch(g.N, g.H, g.W)}, dw.options());
-    CHECK_RC(dpe_wgrad3x3_rows_launch(bp(x), bp(dy), fp(dw), fp(scratch), g.N, g.H, g.W, (float)alpha, cur_stream()),
+    CHECK_RC(dpe_wgrad3x3_rows_launch(bp(x), bp(dy), fp(dw), fp(scratch), g.N, g.H, g.W, (float)alpha, icoef,
+                                      cur_stream()),
              "wgrad3x3_rows");
     return;
   }
@@ -1279,7 +1290,20 @@ void register_ops(pybind11::module& m) {
   m.def("linear_wgrad", &linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("alpha") = 1.0,
         py::arg("alpha_t") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
-        py::arg("want_stats") = false, py::arg("bias") = py::none());
+        py::arg("want_stats") = false, py::arg("bias") = py::none(), py::arg("in_coef") = py::none());
+  m.def("row_bn_on_load", [](std::vector<int64_t> xs, std::vector<int64_t> ws, std::vector<int64_t> stride,
+                             std::vector<int64_t> pad, std::vector<int64_t> dil) {
+          // the row-walking 64-channel 3x3 kernels (fwd + wgrad) take the pre-BN input (in_coef)
+          if (xs.size() != 4 || ws.size() != 4 || stride.size() != 2 || pad.size() != 2 || dil.size() != 2) return false;
+          dpe::ConvGeom g{};
+          g.N = (int)xs[0]; g.H = (int)xs[1]; g.W = (int)xs[2]; g.C = (int)xs[3];
+          g.K = (int)ws[0]; g.R = (int)ws[1]; g.S = (int)ws[2];
+          g.sh = (int)stride[0]; g.sw = (int)stride[1]; g.ph = (int)pad[0]; g.pw = (int)pad[1];
+          g.dh = (int)dil[0]; g.dw = (int)dil[1];
+          g.OH = (g.H + 2 * g.ph - g.dh * (g.R - 1) - 1) / g.sh + 1;
+          g.OW = (g.W + 2 * g.pw - g.dw * (g.S - 1) - 1) / g.sw + 1;
+          return ws[3] == xs[3] && rowconv_geom(g) && dpe_wgrad3x3_rows_scratch(g.N, g.H, g.W) > 0;
+        }, py::arg("x_shape"), py::arg("w_shape"), py::arg("stride"), py::arg("pad"), py::arg("dil"));
   m.def("conv_dgrad_acc", &conv_dgrad_acc, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), "dx += data grad of conv(w) in place (parities without taps untouched)");
   m.def("conv_dgrad_bn", [](const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape, std::vector<int64_t> stride,
@@ -1304,7 +1328,7 @@ void register_ops(pybind11::module& m) {
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), py::arg("residual") = py::none(), py::arg("residual_mask") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
-        py::arg("dil"), py::arg("alpha") = 1.0);
+        py::arg("dil"), py::arg("alpha") = 1.0, py::arg("in_coef") = py::none());
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),
         py::arg("momentum"), py::arg("eps"), py::arg("relu"), py::arg("residual") = py::none(), py::arg("stats") = py::none());
   m.def("bn_fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),

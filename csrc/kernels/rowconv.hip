@@ -33,6 +33,15 @@ constexpr int LDS = NSLOT * SLOT + 2 * OBUF;
 static_assert(LDS <= 163840 / 2, "two blocks per CU");
 
 DPE_DEVICE u32x4 zero16() { return u32x4{0u, 0u, 0u, 0u}; }
+// relu(v * scale + shift) of 8 channels: the BatchNorm+ReLU of the producing conv's output applied
+// on load (same arithmetic as bn_apply, so the operand is bitwise the tensor bn_apply would store)
+DPE_DEVICE u32x4 bnrelu8(const u32x4& v, const float* sc, const float* sh) {
+  float f[8];
+  unpack8(v, f);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], sc[e], sh[e]), 0.f);
+  return pack8(f);
+}
 DPE_DEVICE int pix_off(int sp, int chunk) { return sp * 128 + ((chunk ^ (sp & 7)) << 4); }
 
 struct RowArgs {
@@ -43,9 +52,10 @@ struct RowArgs {
   const uint16_t* st_x;   // BNB: pre-BN input [N][H][W][64]
   const float* st_coef;   // BNB: [4][64] scale, shift, mean, invstd
   int N, H, W, parts;
+  const float* in_coef;   // INBN: x is the pre-BN tensor; the operand is relu(x * in_coef[c] + in_coef[64 + c])
 };
 
-template <bool BNB>
+template <bool BNB, bool INBN = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_rows_kernel(RowArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[LDS];
   char* const ring = smem;
@@ -79,12 +89,28 @@ __global__ __launch_bounds__(256, 2) void conv3x3_rows_kernel(RowArgs p) {
       v[u] = (c < nch && (unsigned)ih < (unsigned)H) ? *(const u32x4*)(p.x + img + (int64_t)ih * W * 64 + c * 8) : zero16();
     }
   };
+  // INBN: this thread's input channels are 8 (tid & 7) .. +7 for every row (256 % 8 == 0)
+  float isc[INBN ? 8 : 1], ish[INBN ? 8 : 1];
+  if constexpr (INBN) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      isc[e] = p.in_coef[(tid & 7) * 8 + e];
+      ish[e] = p.in_coef[CO + (tid & 7) * 8 + e];
+    }
+  }
   auto write_row = [&](int ih, const u32x4 (&v)[2]) {  // input row ih -> slot (ih + 1) % 4, pixel iw + 1
     char* sl = ring + ((ih + 1 + 4 * NSLOT) % NSLOT) * SLOT;
+    const bool inr = (unsigned)ih < (unsigned)H;  // padding rows stay zero (not relu(shift))
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int c = tid + 256 * u;
-      if (c < nch) *(u32x4*)(sl + pix_off((c >> 3) + 1, c & 7)) = v[u];
+      if (c < nch) {
+        u32x4 val = v[u];
+        if constexpr (INBN) {
+          if (inr) val = bnrelu8(val, isc, ish);
+        }
+        *(u32x4*)(sl + pix_off((c >> 3) + 1, c & 7)) = val;
+      }
     }
   };
   __syncthreads();
@@ -261,9 +287,11 @@ DPE_DEVICE bf16x8 trfrag(const char* img, int row0, int c0) {
   return __builtin_bit_cast(bf16x8, r);
 }
 
+template <bool INBN>
 __global__ __launch_bounds__(256, 2) void wgrad3x3_rows_kernel(const uint16_t* __restrict__ x,
                                                                const uint16_t* __restrict__ dy,
-                                                               float* __restrict__ part, int H, int W) {
+                                                               float* __restrict__ part, int H, int W,
+                                                               const float* __restrict__ in_coef) {
   __shared__ __attribute__((aligned(16))) char smem[LDS];
   char* const ring = smem;                     // x rows: input row ih in slot (ih + 1) % 4
   char* const dbuf = smem + NSLOT * XSLOT;     // dy rows: output row oh in slot oh & 1
@@ -291,17 +319,35 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_rows_kernel(const uint16_t* _
     }
   };
   auto xslot = [&](int ih) { return ring + ((ih + 1 + NSLOT) % NSLOT) * XSLOT; };
+  // INBN: x rows are the pre-BN tensor; this thread's channels are 8 (tid & 7) .. +7 for every chunk
+  float isc[INBN ? 8 : 1], ish[INBN ? 8 : 1];
+  if constexpr (INBN) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      isc[e] = in_coef[(tid & 7) * 8 + e];
+      ish[e] = in_coef[64 + (tid & 7) * 8 + e];
+    }
+  }
+  auto putx = [&](int ih, u32x4 (&v)[2]) {
+    if constexpr (INBN) {
+      if ((unsigned)ih < (unsigned)H) {  // padding rows stay zero (not relu(shift))
+#pragma unroll
+        for (int u = 0; u < 2; ++u) v[u] = bnrelu8(v[u], isc, ish);
+      }
+    }
+    put(xslot(ih), 1, v);
+  };
   __syncthreads();
   {
     u32x4 t0[2], t1[2], t2[2];
     load(x, -1, t0);
     load(x, 0, t1);
     load(dy, 0, t2);
-    put(xslot(-1), 1, t0);
-    put(xslot(0), 1, t1);
+    putx(-1, t0);
+    putx(0, t1);
     put(dbuf, 0, t2);
     load(x, 1, t0);
-    put(xslot(1), 1, t0);
+    putx(1, t0);
   }
   u32x4 px0[2], px1[2], pd0[2], pd1[2];  // prefetch: x rows oh + 2, oh + 3; dy rows oh + 1, oh + 2
   load(x, 2, px0);
@@ -333,7 +379,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_rows_kernel(const uint16_t* _
       }
     }
     // x row oh + 2 into the slot of row oh - 2, dy row oh + 1 into the slot of row oh - 1 (both free)
-    put(xslot(oh + 2), 1, px0);
+    putx(oh + 2, px0);
     put(dbuf + ((oh + 1) & 1) * DSLOT, 0, pd0);
 #pragma unroll
     for (int u = 0; u < 2; ++u) { px0[u] = px1[u]; pd0[u] = pd1[u]; }
@@ -381,12 +427,15 @@ extern "C" int dpe_conv3x3_rows_blocks(int N, int H, int W) {
 
 // y = conv3x3(x, w) (stride 1, pad 1, 64 -> 64 channels); bnb: stats are the BN-backward partials
 // of the BN with pre-BN input st_x and coefficients st_coef, else the BN-forward sums of y.
+// in_coef (forward only, not with bnb): x is the pre-BN tensor of a BatchNorm+ReLU, applied on load.
 extern "C" int dpe_conv3x3_rows_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* st_x,
-                                       const float* st_coef, int N, int H, int W, int bnb, hipStream_t st) {
+                                       const float* st_coef, int N, int H, int W, int bnb, const float* in_coef,
+                                       hipStream_t st) {
   const int nb = dpe_conv3x3_rows_blocks(N, H, W);
-  if (nb <= 0 || (bnb && (!stats || !st_x || !st_coef))) return -1;
-  dpe::rowconv::RowArgs a{x, w, y, stats, st_x, st_coef, N, H, W, 2};
+  if (nb <= 0 || (bnb && (!stats || !st_x || !st_coef)) || (bnb && in_coef)) return -1;
+  dpe::rowconv::RowArgs a{x, w, y, stats, st_x, st_coef, N, H, W, 2, in_coef};
   if (bnb) hipLaunchKernelGGL(dpe::rowconv::conv3x3_rows_kernel<true>, dim3(nb), dim3(256), 0, st, a);
+  else if (in_coef) hipLaunchKernelGGL((dpe::rowconv::conv3x3_rows_kernel<false, true>), dim3(nb), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(dpe::rowconv::conv3x3_rows_kernel<false>, dim3(nb), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
@@ -398,11 +447,13 @@ extern "C" int64_t dpe_wgrad3x3_rows_scratch(int N, int H, int W) {
 }
 
 // dw (+)= alpha * dW of conv3x3(x) w.r.t. its filter, given dy (64 -> 64, stride 1, pad 1).
+// in_coef: x is the pre-BN tensor of a BatchNorm+ReLU ([scale | shift] of 64 channels), applied on load.
 extern "C" int dpe_wgrad3x3_rows_launch(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H,
-                                        int W, float alpha, hipStream_t st) {
+                                        int W, float alpha, const float* in_coef, hipStream_t st) {
   if (dpe_wgrad3x3_rows_scratch(N, H, W) <= 0 || !scratch) return -1;
   using namespace dpe::rowconv::wg;
-  hipLaunchKernelGGL(wgrad3x3_rows_kernel, dim3(N), dim3(256), 0, st, x, dy, scratch, H, W);
+  if (in_coef) hipLaunchKernelGGL(wgrad3x3_rows_kernel<true>, dim3(N), dim3(256), 0, st, x, dy, scratch, H, W, in_coef);
+  else hipLaunchKernelGGL(wgrad3x3_rows_kernel<false>, dim3(N), dim3(256), 0, st, x, dy, scratch, H, W, in_coef);
   const int groups = N >= 64 ? 16 : 1;
   const int per = (N + groups - 1) / groups;
   hipLaunchKernelGGL(wgrad3x3_rows_reduce_kernel, dim3(PART / 1024, groups), dim3(256), 0, st, scratch, dw, N, per, alpha);

@@ -33,10 +33,17 @@ by block i's forward and consumed by block i+1; if the gradient block i
 receives is not the tensor that epilogue produced, block i falls back to the
 standalone path (masking an already-masked gradient again is idempotent).
 
-(A variant that also fused BN1/BN2 + ReLU into the consumer convs' load
+(A variant that also fused BN1/BN2 + ReLU into the implicit-GEMM convs' load
 prologues, never materialising a1/a2, measured slower on MI355X: the
 transform sits on the loaders' critical path and the inner BN tensors carry
-only 1/4 of the block's channels -- so the outputs are materialised.)
+only 1/4 of the block's channels -- so those outputs are materialised.  The
+exception is a1 of the 64-channel layer-1 blocks (DPE_ROW_BNIN=1, default):
+conv2 and its weight grad run on the row-walking kernels (rowconv.hip), which
+stage every input row through registers one row ahead of its use, so
+relu(BN1(h1)) is applied there off the critical path and a1 (205 MB at batch
+512) is neither written nor re-read: conv2 reads h1 + BN1's coefficients, the
+weight grad recomputes a1 the same way, and BN1's backward already takes its
+ReLU mask from h1.)
 
 Weight gradients are accumulated straight into the DDP bucket views and each
 parameter is announced to the reducer as soon as its gradient is final, in
@@ -59,6 +66,13 @@ _EPI_BNB = os.environ.get("DPE_BN_EPI", "1") != "0"
 _BN3_CHAIN = _EPI_BNB and os.environ.get("DPE_BN3_CHAIN", "1") != "0"
 # DPE_BN_DUAL=0: downsample blocks run BN3's and BN_d's backward as separate passes
 _BN_DUAL = os.environ.get("DPE_BN_DUAL", "1") != "0"
+# DPE_ROW_BNIN=0: layer-1 a1 = relu(BN1(h1)) materialised by a bn_apply pass (A/B reference)
+_ROW_BNIN = _EPI_BNB and os.environ.get("DPE_ROW_BNIN", "1") != "0"
+
+
+def _out_hw(hw, conv):
+    k, s, p, d = conv.kernel_size[0], conv.stride[0], conv.padding[0], conv.dilation[0]
+    return (hw + 2 * p - d * (k - 1) - 1) // s + 1
 
 
 class _BN3Link:
@@ -106,8 +120,19 @@ class BottleneckFn(Function):
             hd, cd = conv_coef(3, x)  # BN_d is applied inside BN3's pass (bn_apply with residual_coef)
         else:
             hd, cd = None, None
-        h1, a1, c1 = convbn(0, x, True)
-        h2, a2, c2 = convbn(1, a1, True)
+        c1conv, c2conv = convs[0].conv, convs[1].conv
+        h1_shape = [x.shape[0], _out_hw(x.shape[1], c1conv), _out_hw(x.shape[2], c1conv), c1conv.out_channels]
+        if _ROW_BNIN and C.row_bn_on_load(h1_shape, list(ws[1].shape), *_conv_conf(c2conv)):
+            # a1 never materialised: conv2 applies relu(BN1(h1)) to its input rows on load
+            h1, c1 = conv_coef(0, x)
+            a1 = None
+            h2, st2 = C.conv_fwd(h1, ws[1], *_conv_conf(c2conv), True, None, c1)
+            bn2 = convs[1].bn
+            a2, c2 = C.bn_fwd_train(h2, bn2.weight.detach(), bn2.bias.detach(), bn2.running_mean, bn2.running_var,
+                                    bn2.momentum, bn2.eps, True, None, st2)
+        else:
+            h1, a1, c1 = convbn(0, x, True)
+            h2, a2, c2 = convbn(1, a1, True)
         # the next block's fused data-grad epilogue reads this output's ReLU mask as bits
         want_bits = True  # 1/16 of out: read by the next block's fused epilogue or by this block's BN3 backward
         h3, c3 = conv_coef(2, a2)
@@ -162,14 +187,14 @@ class BottleneckFn(Function):
             bn_done(bn, gb, gd, bb, bd)
             return dh, dz
 
-        def wgrad(i, dy, inp):
+        def wgrad(i, dy, inp, in_coef=None):
             w = convs[i].conv.weight
             s, p, d = _conv_conf(convs[i].conv)
             buf, direct = grad_sink(w)
             if direct:  # bucket view: on the weight-grad side stream (the reducers wait for it)
-                run_on_aux(dy.device, lambda: C.conv_wgrad(dy, inp, buf, s, p, d, 1.0), dy, inp)
+                run_on_aux(dy.device, lambda: C.conv_wgrad(dy, inp, buf, s, p, d, 1.0, in_coef), dy, inp, in_coef)
             else:
-                C.conv_wgrad(dy, inp, buf, s, p, d, 1.0)
+                C.conv_wgrad(dy, inp, buf, s, p, d, 1.0, in_coef)
             grad_done(w, direct)
             grads[id(w)] = None if direct else buf
 
@@ -218,8 +243,11 @@ class BottleneckFn(Function):
             lk.h3 = lk.coef = lk.mask = None
         wgrad(2, dh3, a2)
         dh2 = dgrad_bnb(2, dh3, 1, a2, h2, c2)
-        wgrad(1, dh2, a1)
-        dh1 = dgrad_bnb(1, dh2, 0, a1, h1, c1)
+        if a1 is None:  # a1 = relu(BN1(h1)) recomputed on load by the row-walking weight grad
+            wgrad(1, dh2, h1, c1)
+        else:
+            wgrad(1, dh2, a1)
+        dh1 = dgrad_bnb(1, dh2, 0, a1, h1, c1)  # (a1 unused: _EPI_BNB recomputes the mask from h1)
         wgrad(0, dh1, x)
         dx = None
         if ctx.needs_input_grad[0]:

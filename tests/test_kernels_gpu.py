@@ -908,3 +908,27 @@ def test_row_wgrad_matches_reference(C, N, H, W):
         outs[on] = dw - dw0
     assert rel_err(outs[True], 0.5 * ref.permute(0, 2, 3, 1)) < 1e-4
     assert rel_err(outs[True], outs[False]) < 1e-4
+
+
+@pytest.mark.parametrize("N,H,W", [(3, 56, 56), (2, 9, 20)])
+def test_row_kernels_bn_on_load(C, N, H, W):
+    """The row-walking 64-channel 3x3 forward and weight grad with in_coef (x = pre-BN h, operand =
+    relu(h * scale + shift) applied on load, padding rows/pixels still zero) == the same kernels on
+    the tensor bn_apply materialises: bitwise for the output, the BN sums and the weight grad."""
+    torch.manual_seed(47)
+    h = bf(torch.randn(N, H, W, 64, device=dev))
+    coef = _bn_coef(C, 64)
+    a, _ = C.bn_apply(h, coef, None, None, True, False)
+    w = bf(torch.randn(64, 3, 3, 64, device=dev) / 24)
+    z = [1, 1], [1, 1], [1, 1]
+    y1, s1 = C.conv_fwd(h, w, *z, True, None, coef)
+    y2, s2 = C.conv_fwd(a, w, *z, True, None)
+    assert torch.equal(y1, y2) and torch.equal(s1, s2)
+    dy = bf(torch.randn(N, H, W, 64, device=dev))
+    dw1 = torch.zeros(64, 3, 3, 64, device=dev)
+    dw2 = torch.zeros_like(dw1)
+    C.conv_wgrad(dy, h, dw1, *z, 1.0, coef)
+    C.conv_wgrad(dy, a, dw2, *z, 1.0)
+    assert rel_err(dw1, dw2) < 1e-6
+    assert C.row_bn_on_load([N, H, W, 64], [64, 3, 3, 64], *z)
+    assert not C.row_bn_on_load([N, H, W, 64], [64, 3, 3, 64], [2, 2], [1, 1], [1, 1])
