@@ -66,6 +66,9 @@ int dpe_wgrad3x3_rows_launch(const uint16_t* x, const uint16_t* dy, float* dw, f
 int dpe_conv3x3_rows_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* st_x,
                             const float* st_coef, int N, int H, int W, int bnb, const float* in_coef, hipStream_t st);
 int dpe_stem_blocks(int N, int H, int W);
+int64_t dpe_stem_wgrad_scratch(int N, int H, int W);
+int dpe_stem_wgrad_launch(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H, int W,
+                          float alpha, hipStream_t st);
 int dpe_stem_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H, int W, hipStream_t st);
 int dpe_add(const void* a, const void* b, void* out, int64_t n, float alpha, int bf16, hipStream_t st);
 int dpe_colsum(const void* dy, int64_t M, int N, int64_t ld, float* db, int accumulate, int bf16, hipStream_t st);
@@ -794,6 +797,15 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64
     CHECK_RC(dpe_wgrad3x3_rows_launch(bp(x), bp(dy), fp(dw), fp(scratch), g.N, g.H, g.W, (float)alpha, icoef,
                                       cur_stream()),
              "wgrad3x3_rows");
+    return;
+  }
+  // the s2d stem (16 channels, 4x4 / s1 / pad 2-2-1-1 -> 64): the row-walking weight grad (stem.hip)
+  static const bool stem_wg_env = [] { const char* e = getenv("DPE_STEM_WGRAD"); return !(e && e[0] == '0'); }();
+  if (stem_on() && stem_wg_env && g.C == 16 && g.K == 64 && g.R == 4 && g.S == 4 && g.sh == 1 && g.sw == 1 && g.ph == 2 && g.pw == 2 &&
+      g.dh == 1 && g.dw == 1 && g.OH == g.H && g.OW == g.W && dpe_stem_wgrad_scratch(g.N, g.H, g.W) > 0) {
+    auto scratch = at::empty({dpe_stem_wgrad_scratch(g.N, g.H, g.W)}, dw.options());
+    CHECK_RC(dpe_stem_wgrad_launch(bp(x), bp(dy), fp(dw), fp(scratch), g.N, g.H, g.W, (float)alpha, cur_stream()),
+             "stem wgrad");
     return;
   }
   // 1x1 stride-1 weight grads with both channel counts >= 256 (ResNet layers 3-4 and the 512->256

@@ -363,7 +363,10 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_rows_kernel(const uint16_t* _
     for (int t = 0; t < 9; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nks = W > 32 ? 2 : 1;  // 32-pixel K-steps per row (pixels >= W are zero rows of dy)
 
-  for (int oh = 0; oh < H; ++oh) {
+  // one output row; pxA / pdA hold x row oh + 2 / dy row oh + 1 and are refilled in place with rows
+  // oh + 4 / oh + 3 (two rows per loop trip with two buffer sets: a prefetch is first waited on two
+  // rows after it was issued)
+  auto step = [&](int oh, u32x4 (&pxA)[2], u32x4 (&pdA)[2]) {
     const char* ds = dbuf + (oh & 1) * DSLOT;
     for (int ks = 0; ks < nks; ++ks) {
       bf16x8 a[4];
@@ -379,13 +382,15 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_rows_kernel(const uint16_t* _
       }
     }
     // x row oh + 2 into the slot of row oh - 2, dy row oh + 1 into the slot of row oh - 1 (both free)
-    putx(oh + 2, px0);
-    put(dbuf + ((oh + 1) & 1) * DSLOT, 0, pd0);
-#pragma unroll
-    for (int u = 0; u < 2; ++u) { px0[u] = px1[u]; pd0[u] = pd1[u]; }
-    load(x, oh + 4, px1);
-    load(dy, oh + 3, pd1);
+    putx(oh + 2, pxA);
+    put(dbuf + ((oh + 1) & 1) * DSLOT, 0, pdA);
+    load(x, oh + 4, pxA);
+    load(dy, oh + 3, pdA);
     __syncthreads();
+  };
+  for (int oh = 0; oh < H; oh += 2) {
+    step(oh, px0, pd0);
+    if (oh + 1 < H) step(oh + 1, px1, pd1);
   }
   // acc[m][t][e]: co = 16 m + (lane & 15), ci = 16 w + 4 (lane >> 4) + e, tap t
   float* pb = part + (int64_t)n * PART;

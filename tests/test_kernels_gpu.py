@@ -932,3 +932,29 @@ def test_row_kernels_bn_on_load(C, N, H, W):
     assert rel_err(dw1, dw2) < 1e-6
     assert C.row_bn_on_load([N, H, W, 64], [64, 3, 3, 64], *z)
     assert not C.row_bn_on_load([N, H, W, 64], [64, 3, 3, 64], [2, 2], [1, 1], [1, 1])
+
+
+@pytest.mark.parametrize("N,H,W", [(3, 112, 112), (2, 9, 100), (70, 4, 20), (1, 5, 33)])
+def test_stem_wgrad_matches_reference(C, N, H, W):
+    """Row-walking s2d stem weight grad (stem.hip: per-image 64 x 256 gradient in registers, dY and
+    x rows as LDS images read with ds_read_b64_tr_b16, 4-tap column shifts, pad 2-2-1-1) vs the fp32
+    reference and the im2col weight-grad tile, accumulating with alpha; N >= 64 takes the grouped
+    partial reduce, W not a multiple of 32 a partial last K-step."""
+    torch.manual_seed(53)
+    xs = bf(torch.randn(N, H, W, 16, device=dev))
+    dy = bf(torch.randn(N, H, W, 64, device=dev))
+    w = torch.randn(64, 16, 4, 4, device=dev, requires_grad=True)
+    y = F.conv2d(F.pad(xs.permute(0, 3, 1, 2).float(), (2, 1, 2, 1)), w)
+    (ref,) = torch.autograd.grad(y, w, dy.permute(0, 3, 1, 2).float())
+    dw0 = torch.randn(64, 4, 4, 16, device=dev)
+    outs = {}
+    for on in (True, False):
+        C.set_stem_kernel(on)
+        try:
+            dw = dw0.clone()
+            C.conv_wgrad(dy, xs, dw, [1, 1], [2, 2], [1, 1], 0.5)
+        finally:
+            C.set_stem_kernel(True)
+        outs[on] = dw - dw0
+    assert rel_err(outs[True], 0.5 * ref.permute(0, 2, 3, 1)) < 1e-4
+    assert rel_err(outs[True], outs[False]) < 1e-4
