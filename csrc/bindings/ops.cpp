@@ -244,8 +244,11 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
   //   im2col A (3x3 / strided), K-contiguous B: always;
   //   dense 1x1 forward (A_DENSE_K x B_DENSE_K): unless K and N are both 64 (store-bound);
   //   1x1 data grads (A_DENSE_K x B_DENSE_N): for 128 <= N <= 512 (8-27 % faster; N = 64 and
-  //   N >= 1024 measured 2-10 % slower).  DPE_DMA_ALL=1: every forward-form role.
-  static const bool dma_all = [] { const char* e = getenv("DPE_DMA_ALL"); return e && e[0] == '1'; }();
+  //   N >= 1024 measured 2-10 % slower in round 1).
+  // Since the round-2 kernel changes every forward-form role on the LDS-DMA kernel measures +0.2 %
+  // on the ResNet-50 step (5 alternating pairs: +0.14 / +0.29 / +0.17 / +0.63 / -0.16 %,
+  // profiles/dma_all_ab_r2.txt), so that is the default; DPE_DMA_ALL=0 restores the role table.
+  static const bool dma_all = [] { const char* e = getenv("DPE_DMA_ALL"); return !(e && e[0] == '0'); }();
   bool dma_role = false;
   if (aload == dpe::A_CONV_FWD) dma_role = bload == dpe::B_DENSE_K || dma_all;
   else if (aload == dpe::A_DENSE_K && bload == dpe::B_DENSE_K) dma_role = dma_all || a.K >= 128 || a.N >= 256;
