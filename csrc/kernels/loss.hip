@@ -93,12 +93,33 @@ DPE_DEVICE void ce_load8<float>(const float* p, float* f) {
   f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3]; f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
 }
 
+// The row is held as loaded (bf16: one u32x4 per 8 columns, half the VGPRs of fp32) and unpacked
+// per pass: at ~60 VGPRs two 1024-thread blocks share a CU, so one row's block reductions overlap
+// the other's loads (the LM-head rows, 50 K columns, were VGPR/occupancy-bound at one block per CU).
+template <typename TIn>
+struct RowChunk;
+template <>
+struct RowChunk<uint16_t> {
+  u32x4 v;
+  DPE_DEVICE void load(const uint16_t* p) { v = *(const u32x4*)p; }
+  DPE_DEVICE void get(float* f) const { unpack8(v, f); }
+};
+template <>
+struct RowChunk<float> {
+  f32x4 a, b;
+  DPE_DEVICE void load(const float* p) { a = *(const f32x4*)p; b = *(const f32x4*)(p + 4); }
+  DPE_DEVICE void get(float* f) const {
+    f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3]; f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+  }
+};
+
 template <typename TIn, typename TOut, int NT, int MAXC>
-__global__ __launch_bounds__(NT) void ce_vec_kernel(const TIn* logits, const int64_t* __restrict__ labels, int V,
+__global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 1) void ce_vec_kernel(const TIn* logits, const int64_t* __restrict__ labels, int V,
                                                     int64_t ld, float grad_scale, TOut* dlogits,
                                                     float* __restrict__ loss_rows, float* __restrict__ loss_sum,
                                                     float* __restrict__ correct, int ignore_index) {
   constexpr int NW = NT / 64;
+  constexpr float L2E = 1.4426950408889634f;
   __shared__ float shm[NW], shs[NW], shz[NW];
   __shared__ int sha[NW];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -106,24 +127,41 @@ __global__ __launch_bounds__(NT) void ce_vec_kernel(const TIn* logits, const int
   const int nch = (int)(ld >> 3);
   const int64_t label = labels[row];
   const bool ignored = (label == ignore_index);
-  float f[MAXC][8];
+  const int lch = (int)(label >> 3);
+  RowChunk<TIn> rc[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = tid + c * NT;
+    if (ch < nch) rc[c].load(z + (int64_t)ch * 8);
+  }
+  // columns >= V (padding) read as -inf; only the tail chunk needs the compares
+  auto chunk = [&](int c, int ch, float* f) {
+    rc[c].get(f);
+    if (ch * 8 + 8 > V) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (ch * 8 + e >= V) f[e] = -INFINITY;
+    }
+  };
   float m = -INFINITY, zy = 0.f;
   int am = 0x7fffffff;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int ch = tid + c * NT;
     if (ch < nch) {
-      ce_load8<TIn>(z + (int64_t)ch * 8, f[c]);
+      float f[8];
+      chunk(c, ch, f);
+      if (ch == lch) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int col = ch * 8 + e;
-        if (col >= V) f[c][e] = -INFINITY;
-        if (col == label) zy = f[c][e];
-        if (f[c][e] > m) { m = f[c][e]; am = col; }
+        for (int e = 0; e < 8; ++e)
+          if (e == (int)(label & 7)) zy = f[e];
       }
-    } else {
+      float cm = f[0];
+      int ce = 0;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[c][e] = -INFINITY;
+      for (int e = 1; e < 8; ++e)
+        if (f[e] > cm) { cm = f[e]; ce = e; }
+      if (cm > m) { m = cm; am = ch * 8 + ce; }
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -138,11 +176,19 @@ __global__ __launch_bounds__(NT) void ce_vec_kernel(const TIn* logits, const int
 #pragma unroll
   for (int w = 1; w < NW; ++w)
     if (shm[w] > m || (shm[w] == m && sha[w] < am)) { m = shm[w]; am = sha[w]; }
+  // exp(v - m) as one fma + the bare v_exp_f32 (arguments <= 0: results in (0, 1], denormals flush)
+  const float mb = -m * L2E;
   float s = 0.f;
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c)
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = tid + c * NT;
+    if (ch < nch) {
+      float f[8];
+      chunk(c, ch, f);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) s += __expf(f[c][e] - m);
+      for (int e = 0; e < 8; ++e) s += __builtin_amdgcn_exp2f(fmaf(f[e], L2E, mb));
+    }
+  }
   s = warp_sum(s);
   zy = warp_sum(zy);
   if (lane == 0) { shs[wid] = s; shz[wid] = zy; }
@@ -165,11 +211,14 @@ __global__ __launch_bounds__(NT) void ce_vec_kernel(const TIn* logits, const int
     for (int c = 0; c < MAXC; ++c) {
       const int ch = tid + c * NT;
       if (ch < nch) {
-        float g[8];
+        float f[8], g[8];
+        chunk(c, ch, f);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int col = ch * 8 + e;
-          g[e] = __expf(f[c][e] - m) * k - ((col == label && !ignored) ? grad_scale : 0.f);
+        for (int e = 0; e < 8; ++e) g[e] = __builtin_amdgcn_exp2f(fmaf(f[e], L2E, mb)) * k;
+        if (ch == lch && !ignored) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (e == (int)(label & 7)) g[e] -= grad_scale;
         }
         if constexpr (sizeof(TOut) == 2) {
           *(u32x4*)(d + (int64_t)ch * 8) = pack8(g);
@@ -187,6 +236,7 @@ bool ce_vec_launch(const TIn* logits, const int64_t* labels, int B, int V, int64
                    float* ls, float* cor, int ign, hipStream_t st) {
   if (ld % 8) return false;
   const int64_t nch = ld / 8;
+
 #define DPE_CE_VEC(NT, MC)                                                                                         \
   if (nch <= (int64_t)(NT) * (MC)) {                                                                               \
     hipLaunchKernelGGL((ce_vec_kernel<TIn, TOut, NT, MC>), dim3(B), dim3(NT), 0, st, logits, labels, V, ld, gs, d, lr, \
