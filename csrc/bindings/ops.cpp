@@ -132,9 +132,12 @@ Cfg pick_cfg(int64_t M, int64_t N, int64_t K, bool allow_split) {
     c.bn = N <= 64 ? 64 : 128;
     const int64_t t = tiles(c.bm, c.bn);
     const int64_t ksteps = (K + 31) / 32;
+    // ~3 resident blocks per CU of the 128x128 weight-grad tiles: ResNet-50 step, alternating
+    // (profiles/wgrad_blocks_ab_r2.txt): 256 -8 %, 384 -2.4 %, 512 0, 768 +1.6-1.8 %, 1024 -0.5 %,
+    // 1536 -0.5 %, 2048 -1 %; 704-768 best of 640-896
     static const int64_t target_blocks = [] {
       const char* e = getenv("DPE_WGRAD_BLOCKS");
-      return (int64_t)(e ? std::max(64, atoi(e)) : 512);
+      return (int64_t)(e ? std::max(64, atoi(e)) : 768);
     }();
     int64_t splits = std::max<int64_t>(1, std::min<int64_t>((target_blocks + t - 1) / t, ksteps / 8));
     const int64_t kps = (ksteps + splits - 1) / splits;
