@@ -132,12 +132,11 @@ Cfg pick_cfg(int64_t M, int64_t N, int64_t K, bool allow_split) {
     c.bn = N <= 64 ? 64 : 128;
     const int64_t t = tiles(c.bm, c.bn);
     const int64_t ksteps = (K + 31) / 32;
-    // ~3 resident blocks per CU of the 128x128 weight-grad tiles: ResNet-50 step, alternating
-    // (profiles/wgrad_blocks_ab_r2.txt): 256 -8 %, 384 -2.4 %, 512 0, 768 +1.6-1.8 %, 1024 -0.5 %,
-    // 1536 -0.5 %, 2048 -1 %; 704-768 best of 640-896
+    // register-staged weight-grad tiles (1x1 with 128 channels): 512 blocks; the LDS-DMA im2col
+    // weight-grad kernel re-derives its split for DPE_WGRAD_DMA_BLOCKS (run_igemm)
     static const int64_t target_blocks = [] {
       const char* e = getenv("DPE_WGRAD_BLOCKS");
-      return (int64_t)(e ? std::max(64, atoi(e)) : 768);
+      return (int64_t)(e ? std::max(64, atoi(e)) : 512);
     }();
     int64_t splits = std::max<int64_t>(1, std::min<int64_t>((target_blocks + t - 1) / t, ksteps / 8));
     const int64_t kps = (ksteps + splits - 1) / splits;
@@ -224,6 +223,21 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
   if (conv && epi == dpe::EPI_ATOMIC_F32 && aload == dpe::A_DENSE_M && igemm_dma_on() && wgrad_dma_on() &&
       (bload == dpe::B_CONV_WGRAD || (bload == dpe::B_DENSE_N && wgrad_dma_dense()))) {
     int bm = c.bm, bn = c.bn, splits = c.splits;
+    {
+      // ~3 resident 128x128 blocks per CU (4 fit): ResNet-50 step, alternating
+      // (profiles/wgrad_blocks_ab_r2.txt, all split-K weight grads at one target): 256 -8 %, 384 -2.4 %,
+      // 512 0, 768 +1.4-1.8 %, 1024 -0.5 %, 1536 -0.5 %, 2048 -1 %; 704-768 best of 640-896.  The
+      // register-staged 1x1 tiles measured best at 512 and keep pick_cfg's split.
+      static const int64_t dma_target = [] {
+        const char* e = getenv("DPE_WGRAD_DMA_BLOCKS");
+        return (int64_t)(e ? std::max(64, atoi(e)) : 768);
+      }();
+      const int64_t t = (int64_t)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn), ksteps = (a.K + 31) / 32;
+      const int64_t sp = std::max<int64_t>(1, std::min<int64_t>((dma_target + t - 1) / t, ksteps / 8));
+      const int64_t kps = (ksteps + sp - 1) / sp;
+      a.k_split = (int)(kps * 32);
+      splits = (int)((ksteps + kps - 1) / kps);
+    }
     if (c.bm == 64 && bload == dpe::B_CONV_WGRAD && a.N >= 256 && g_wgrad_wide && (a.g.C <= 16 || g_wgrad_wide > 1)) {
       // Cout = 64 with few channels per tap (the stem): 64x256 tile (4 waves across N), split-K
       // re-derived for its tile count.  Measured: stem 1167 -> 783 us; 64->64 3x3 388 -> 512 us
