@@ -156,6 +156,29 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's pieces of tile j are in; slot (j-1)%NS is free
     asm volatile("" ::: "memory");
+    // K = 256 data grads: this tile's epilogue operands (residual, pre-BN input, masks) are issued
+    // before the next ring stage's DMAs and the MFMAs, so their latency overlaps the K loop (issued
+    // in the epilogue they stalled each half for a full HBM round trip).  They are older than the
+    // stage's DMAs, so the compiler's wait for them leaves the ring's counted vmcnt intact.  The
+    // wider-WN tiles have no registers for it (they would spill).
+    constexpr bool HOIST = (EPI == PW_DGRAD) && (WN == 32);
+    constexpr int HN = HOIST ? NPS : 1;
+    const int m0 = (rg + j * RG) * BM;
+    u32x4 hrv[2][HN], hxv[2][HN];
+    uint32_t hrmb[2][HN], hsmb[2][HN];
+    if constexpr (HOIST) {
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int ps = 0; ps < HN; ++ps) {
+          const int m = min(m0 + 32 * hf + ps * RPP + lane / CPRW, M - 1);
+          const int64_t off = (int64_t)m * N + nch;
+          if (a.residual) hrv[hf][ps] = *(const u32x4*)(a.residual + off);
+          hrmb[hf][ps] = a.res_mask ? (uint32_t)a.res_mask[off >> 3] : 0xffu;
+          if (bnb) hxv[hf][ps] = *(const u32x4*)(a.st_x + off);
+          hsmb[hf][ps] = (bnb && a.st_mask) ? (uint32_t)a.st_mask[off >> 3] : 0xffu;
+        }
+    }
     if (j + NS - 1 < nt) issue(rg + (j + NS - 1) * RG, (j + NS - 1) % NS);
     const char* img = smem + (j % NS) * TILE;
     f32x4 acc[MI][NI];
@@ -177,14 +200,21 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
     // y rows: lane holds channels n0w + 16 ni + 4 g + e of pixel m0 + 16 mi + li; staged per
     // 32-row half through the wave's LDS region (LDS ops of one wave complete in order, so the
     // next half's writes never overtake this half's reads), then finished per 16-B row chunk
-    const int m0 = (rg + j * RG) * BM;
     char* stg = smem + NS * TILE + wid * STG;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       // the half's epilogue operands first: their latency overlaps the staging below
       u32x4 rv[NPS], xv[NPS];
       uint32_t rmb[NPS], smb[NPS];
-      if constexpr (EPI == PW_DGRAD) {
+      if constexpr (HOIST) {
+#pragma unroll
+        for (int ps = 0; ps < HN; ++ps) {
+          rv[ps] = hrv[hf][ps];
+          xv[ps] = hxv[hf][ps];
+          rmb[ps] = hrmb[hf][ps];
+          smb[ps] = hsmb[hf][ps];
+        }
+      } else if constexpr (EPI == PW_DGRAD) {
 #pragma unroll
         for (int ps = 0; ps < NPS; ++ps) {
           const int m = min(m0 + 32 * hf + ps * RPP + lane / CPRW, M - 1);
