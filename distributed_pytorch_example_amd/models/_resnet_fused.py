@@ -276,13 +276,16 @@ class BottleneckFn(Function):
         return (dx, None, None, None, *pgrads)
 
 
-def bottleneck_forward(block, x, link_in=None, chain=False):
+def bottleneck_forward(block, x, link_in=None, chain=False, count_batches=True):
     """Fused block forward.  ``chain=True`` (the ResNet's own block loop, where
     this block's output feeds only the next block) returns ``(out, link)`` for
-    the next block's ``link_in``."""
+    the next block's ``link_in``.  ``count_batches=False``: the ResNet advanced
+    every block's num_batches_tracked in one launch already."""
     params = block._fused_params
-    nbt = [cb.bn.num_batches_tracked for cb in [block.c1, block.c2, block.c3] + ([block.down] if block.down is not None else [])]
-    torch._foreach_add_(nbt, 1)
+    if count_batches:
+        nbt = [cb.bn.num_batches_tracked
+               for cb in [block.c1, block.c2, block.c3] + ([block.down] if block.down is not None else [])]
+        torch._foreach_add_(nbt, 1)
     link_out = _BN3Link() if (chain and _BN3_CHAIN) else None
     out = BottleneckFn.apply(x, block, link_in if _BN3_CHAIN else None, link_out, *params)
     return (out, link_out) if chain else out

@@ -59,13 +59,14 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         return self.forward_chained(x, None, chain=False)
 
-    def forward_chained(self, x, link=None, chain=True):
+    def forward_chained(self, x, link=None, chain=True, count_batches=True):
         """``chain=True``: returns (out, link); the link lets the next block's
-        backward fuse this block's BN3 backward (``_resnet_fused``)."""
+        backward fuse this block's BN3 backward (``_resnet_fused``).
+        ``count_batches=False``: the caller already advanced the BNs' num_batches_tracked."""
         if x.is_cuda and self.training and self.fused:
             from ._resnet_fused import bottleneck_forward
 
-            return bottleneck_forward(self, x, link, chain)
+            return bottleneck_forward(self, x, link, chain, count_batches)
         out = self._forward_per_op(x)
         return (out, None) if chain else out
 
@@ -121,8 +122,14 @@ class ResNet(nn.Module):
                 x = Fx.to_nhwc_input(x, self.in_pad)
             h = Fx.max_pool2d_nhwc(self.stem(x), 3, 2, 1)
         link = None
+        fused = h.is_cuda and self.training and all(b.fused for b in self.blocks)
+        if fused:
+            # every block's num_batches_tracked in one multi-tensor launch (not one per block); the
+            # list is rebuilt per step (host-side only) so moved / reloaded buffers are never stale
+            torch._foreach_add_([m.num_batches_tracked for b in self.blocks for m in b.modules()
+                                 if getattr(m, "num_batches_tracked", None) is not None], 1)
         for blk in self.blocks:  # each block's output feeds only the next block
-            h, link = blk.forward_chained(h, link)
+            h, link = blk.forward_chained(h, link, count_batches=not fused)
         h = Fx.global_avg_pool_nhwc(h)
         return self.fc(h)
 

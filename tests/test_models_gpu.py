@@ -239,3 +239,17 @@ def test_gpt2_fused_block_matches_per_op(C):
         for n, p in m1.named_parameters():
             assert cos(p.grad, g2[n].grad) > 0.999, n
             assert rel(p.grad, g2[n].grad) < 0.02, n
+
+
+def test_resnet_counts_batches_once_per_forward(C):
+    """The fused ResNet advances every BatchNorm's num_batches_tracked once per training forward
+    (one multi-tensor launch for all blocks; a standalone block still counts its own)."""
+    from distributed_pytorch_example_amd.models import get_model
+
+    torch.manual_seed(3)
+    model = get_model("resnet18_like").to(dev)
+    x = torch.randn(4, 3, 32, 32, device=dev)
+    for _ in range(2):
+        model(x)
+    counts = {n: int(b.item()) for n, b in model.named_buffers() if n.endswith("num_batches_tracked")}
+    assert counts and all(v == 2 for v in counts.values()), counts
