@@ -369,9 +369,9 @@ class DistributedDataParallel(nn.Module):
                     p.grad = v
                     reattached = True
         if zero or reattached:
-            # set_to_none=True zero_grad dropped the views: grads restart from zero
-            for b in self.buckets:
-                b.zero_()
+            # set_to_none=True zero_grad dropped the views: grads restart from zero (all buckets in
+            # one multi-tensor launch)
+            torch._foreach_zero_(list(self.buckets))
 
     # ---------------------------------------------------------- per-step
     def _on_ready(self, p):
