@@ -65,7 +65,8 @@ def parse():
     ap.add_argument("--graph", type=int, default=0,
                     help="1: capture one whole training step (forward, backward, reducer, optimizer) in a HIP graph "
                          "after the warm-up and replay it; each step copies its batch into the graph's input "
-                         "buffers (world 1, grad-accum 1)")
+                         "buffers (world 1, grad-accum 1; dropout masks, seeded from a host counter, are "
+                         "frozen at capture -- SimpleNet's)")
     ap.add_argument("--dtype", default=None, choices=[None, "fp32", "bf16"],
                     help="simplenet compute dtype (default fp32, the reference's); resnet50/gpt2 are bf16")
     return ap.parse_args()
@@ -221,7 +222,9 @@ def _graph_step(args, world, ddp, opt, model, xs, ys, fused_loss, num_classes, F
     step function that refills the static input buffers and replays it.  Every kernel of the step is
     in the graph: the launch gaps between ~400 short kernels (GPT-2) go away.  The fused optimizers
     keep their step counters and hyper-parameters on the device, so the replayed update is the
-    eager one; the DDP buckets are re-zeroed by the captured forward."""
+    eager one; the DDP buckets are re-zeroed by the captured forward.  The gradients are the DDP
+    bucket views, so the optimizer's device table (raw gradient pointers) is valid in every replay;
+    tests/test_models_gpu.py::test_graph_replayed_step_matches_eager checks replay == eager."""
     if world != 1 or args.grad_accum != 1:
         raise SystemExit("--graph: world size 1 and --grad-accum 1 only")
     sx, sy = xs[0].clone(), ys[0].clone()

@@ -253,3 +253,55 @@ def test_resnet_counts_batches_once_per_forward(C):
         model(x)
     counts = {n: int(b.item()) for n, b in model.named_buffers() if n.endswith("num_batches_tracked")}
     assert counts and all(v == 2 for v in counts.values()), counts
+
+
+def test_graph_replayed_step_matches_eager(C):
+    """A whole SimpleNet training step (forward, fused CE, backward, fused Adam with its device-side
+    step counters and hyper-parameters) captured once in a HIP graph and replayed == the same steps
+    run eagerly (the bench.py --graph path, without the DDP wrapper)."""
+    from distributed_pytorch_example_amd.models import get_model
+    from distributed_pytorch_example_amd.ops import functional as Fx
+    from distributed_pytorch_example_amd.optim import Adam
+
+    torch.manual_seed(11)
+    m1 = get_model("simplenet").to(dev)
+    m1.layers[2].p = m1.layers[5].p = 0.0  # dropout seeds come from a host counter: a replay reuses its masks
+    m2 = copy.deepcopy(m1)
+    o1, o2 = Adam(m1.parameters(), lr=1e-3), Adam(m2.parameters(), lr=1e-3)
+    xs = [torch.randn(64, 784, device=dev) for _ in range(5)]
+    ys = [torch.randint(0, 10, (64,), device=dev) for _ in range(5)]
+
+    def step(model, opt, x, y):
+        loss = Fx.cross_entropy(model(x), y, 10)
+        loss.backward()
+        opt.step()
+        # gradients stay allocated (zeroed in place): the fused optimizer's device table holds their
+        # pointers, which a graph replay must find unchanged (under DDP they are the bucket views)
+        opt.zero_grad(set_to_none=False)
+        return loss
+
+    for m in (m1, m2):
+        for p in m.parameters():
+            p.grad = torch.zeros_like(p)
+    step(m1, o1, xs[0], ys[0])  # eager warm-up step on both (optimizer state exists before capture)
+    step(m2, o2, xs[0], ys[0])
+    sx, sy = xs[1].clone(), ys[1].clone()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step(m1, o1, sx, sy)  # step 2 on the side stream (capture warm-up)
+    torch.cuda.current_stream().wait_stream(side)
+    o1.graph_safe = True
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        gl = step(m1, o1, sx, sy)  # captured (this does not run step 3)
+    step(m2, o2, xs[1], ys[1])
+    for i in (2, 3, 4):
+        sx.copy_(xs[i])
+        sy.copy_(ys[i])
+        g.replay()
+        l2 = step(m2, o2, xs[i], ys[i])
+    torch.cuda.synchronize()
+    assert abs(gl.item() - l2.item()) <= 1e-4 * max(1.0, abs(l2.item()))
+    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert rel(a.detach(), b.detach()) < 1e-4, n
