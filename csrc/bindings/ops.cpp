@@ -220,8 +220,9 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
   // weight grads over an im2col B (3x3 / strided; split-K fp32 atomics): LDS-DMA kernel, measured 1.3-1.5x
   // faster (scripts/bench_convs.py); on the dense 1x1 ones it measured 10-15 % slower, so those stay
   // register-staged (DPE_WGRAD_DMA=0: all register-staged, 2: dense 1x1 too)
-  if (conv && epi == dpe::EPI_ATOMIC_F32 && aload == dpe::A_DENSE_M && igemm_dma_on() && wgrad_dma_on() &&
-      (bload == dpe::B_CONV_WGRAD || (bload == dpe::B_DENSE_N && wgrad_dma_dense()))) {
+  if (conv && epi == dpe::EPI_ATOMIC_F32 && aload == dpe::A_DENSE_M &&
+      ((igemm_dma_on() && wgrad_dma_on() && (bload == dpe::B_CONV_WGRAD || (bload == dpe::B_DENSE_N && wgrad_dma_dense()))) ||
+       (bload == dpe::B_DENSE_N && a.b_coef))) {
     int bm = c.bm, bn = c.bn, splits = c.splits;
     {
       // ~3 resident 128x128 blocks per CU (4 fit): ResNet-50 step, alternating
@@ -250,6 +251,7 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
       splits = (int)((ksteps + kps - 1) / kps);
     }
     const int rc = dpe_igemm_wgrad_dma_launch(&a, bm, bn, bload, splits, cur_stream());
+    TORCH_CHECK(rc == 0 || !a.b_coef, "weight grad with BN on load: outside the LDS-DMA kernel's envelope (rc=", rc, ")");
     a.k_split = c.k_split;  // (register-staged fallback uses pick_cfg's split)
     if (rc == 0) {
       const hipError_t e = hipGetLastError();
@@ -565,8 +567,10 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
                        g.pw == 2 && pb == 1 && pr == 1 && g.dh == 1 && g.dw == 1 && OH == H && OW == W && !a.bias)
                           ? dpe_stem_blocks(g.N, g.H, g.W) : 0;
   const float* icoef = fpo(in_coef);
-  TORCH_CHECK(!icoef || (rowconv_geom(g) && pb == 1 && pr == 1 && !a.bias),
-              "conv_fwd: in_coef (BN+ReLU on load) needs the row-walking 64-channel 3x3 kernel");
+  const int pw_rg_in = (pw_stream_on() && is_pointwise(g) && !a.bias) ? dpe_pw_rowgroups(a.M, a.N, a.K, dpe::PW_FWD) : 0;
+  TORCH_CHECK(!icoef || (rowconv_geom(g) && pb == 1 && pr == 1 && !a.bias) || pw_rg_in > 0,
+              "conv_fwd: in_coef (BN+ReLU on load) needs the row-walking 64-channel 3x3 kernel or the streaming "
+              "pointwise kernel");
   if (rowconv_geom(g) && pb == 1 && pr == 1 && !a.bias) {
     // 64-channel 3x3 (layer 1 conv2): row-walking kernel, filter in VGPRs (csrc/kernels/rowconv.hip)
     const int nb = dpe_conv3x3_rows_blocks(g.N, g.H, g.W);
@@ -589,6 +593,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
     if (want_stats) stats = at::empty({2, g.K, pw_rg}, x.options().dtype(at::kFloat));
     dpe::PwArgs pa{};
     pa.x = bp(x); pa.w = bp(w); pa.y = bpm(y); pa.stats = want_stats ? fp(stats) : nullptr;
+    pa.in_coef = icoef;
     pa.M = a.M; pa.N = a.N; pa.K = a.K; pa.rg = pw_rg;
     CHECK_RC(dpe_pw_launch(&pa, dpe::PW_FWD, cur_stream()), "pw_stream fwd");
     return {y, stats};
@@ -811,7 +816,14 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64
   // 64 -> 64 3x3 (ResNet layer 1): the row-walking weight-grad kernel (rowconv.hip)
   const float* icoef = fpo(in_coef);
   const bool row = rowconv_geom(g) && dpe_wgrad3x3_rows_scratch(g.N, g.H, g.W) > 0;
-  TORCH_CHECK(!icoef || row, "conv_wgrad: in_coef (BN+ReLU on load) needs the row-walking 64-channel 3x3 kernel");
+  if (icoef && !row) {
+    // 1x1 weight grad over a pre-BN input: the LDS-DMA weight-grad kernel applies BN + ReLU to its
+    // B fragments (b_coef); outside that kernel's envelope there is no such path
+    TORCH_CHECK(is_pointwise(g), "conv_wgrad: in_coef needs a 1x1 conv or the row-walking 64-channel 3x3 kernel");
+    a.b_coef = icoef;
+    run_igemm(a, dpe::A_DENSE_M, dpe::B_DENSE_N, dpe::EPI_ATOMIC_F32, true, true);
+    return;
+  }
   if (row && (row_wgrad_on() || icoef)) {
     auto scratch = at::empty({dpe_wgrad3x3_rows_scratch(g.N, g.H, g.W)}, dw.options());
     CHECK_RC(dpe_wgrad3x3_rows_launch(bp(x), bp(dy), fp(dw), fp(scratch), g.N, g.H, g.W, (float)alpha, icoef,
@@ -1336,6 +1348,14 @@ void register_ops(pybind11::module& m) {
           g.OW = (g.W + 2 * g.pw - g.dw * (g.S - 1) - 1) / g.sw + 1;
           return ws[3] == xs[3] && rowconv_geom(g) && dpe_wgrad3x3_rows_scratch(g.N, g.H, g.W) > 0;
         }, py::arg("x_shape"), py::arg("w_shape"), py::arg("stride"), py::arg("pad"), py::arg("dil"));
+  m.def("pw_bn_on_load", [](std::vector<int64_t> xs, int64_t cout) {
+          // a 1x1 / stride-1 conv over a pre-BN input [N, H, W, C]: the streaming pointwise forward and the
+          // LDS-DMA weight grad (K = pixels % 32, M = Cout, N = C) take the BN coefficients (in_coef)
+          if (xs.size() != 4) return false;
+          const int64_t M = xs[0] * xs[1] * xs[2], C = xs[3];
+          return pw_stream_on() && C == 64 && cout % 8 == 0 && M % 32 == 0 &&
+                 dpe_pw_rowgroups(M, cout, C, dpe::PW_FWD) > 0;
+        }, py::arg("x_shape"), py::arg("cout"));
   m.def("conv_dgrad_acc", &conv_dgrad_acc, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), "dx += data grad of conv(w) in place (parities without taps untouched)");
   m.def("conv_dgrad_bn", [](const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape, std::vector<int64_t> stride,

@@ -70,6 +70,8 @@ struct IgemmArgs {
   int act;
   int k_split;  // K elements per split (multiple of 32); >= K means no split
   ConvGeom g;
+  const float* b_coef;  // LDS-DMA weight grad, B_DENSE_N: B is a pre-BN tensor; the operand is
+                        //   relu(B * b_coef[n] + b_coef[N + n]) (the BN output is never stored)
 };
 
 }  // namespace dpe

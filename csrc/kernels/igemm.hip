@@ -1023,6 +1023,16 @@ __global__ __launch_bounds__(64 * WGM * WGN, (BN / WGN > 64) ? 2 : 1) void igemm
   for (int i = 0; i < RM; ++i)
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // b_coef (dense B only): BN + ReLU of B's producer on the fragments; a B fragment holds one
+  // column (channel wn + 16 j + lane % 16) over 8 pixels.  Loaded before the ring's first DMA.
+  const bool bnin = !CONV && p.b_coef != nullptr;
+  float bsc[RN], bsh[RN];
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int n = min(n0 + wn + 16 * j + (lane & 15), p.N - 1);
+    bsc[j] = bnin ? p.b_coef[n] : 1.f;
+    bsh[j] = bnin ? p.b_coef[p.N + n] : 0.f;
+  }
 
   // NS-stage ring: stages t+1 .. t+NS-2 stay in flight while stage t is consumed
   static_assert(NS == 2 || NS == 3, "2- or 3-stage ring");
@@ -1041,6 +1051,16 @@ __global__ __launch_bounds__(64 * WGM * WGN, (BN / WGN > 64) ? 2 : 1) void igemm
     for (int i = 0; i < RM; ++i) af[i] = mnfrag<BM>(As, wm + 16 * i);
 #pragma unroll
     for (int j = 0; j < RN; ++j) bfr[j] = mnfrag<BN>(Bs, wn + 16 * j);
+    if (bnin) {
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        float f[8];
+        unpack8(__builtin_bit_cast(u32x4, bfr[j]), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], bsc[j], bsh[j]), 0.f);
+        bfr[j] = __builtin_bit_cast(bf16x8, pack8(f));
+      }
+    }
 #pragma unroll
     for (int i = 0; i < RM; ++i)
 #pragma unroll

@@ -22,6 +22,7 @@ struct PwArgs {
   const uint8_t* st_mask;    // ReLU bits of the BN output ([M][N/8]); the stored y is then the masked dz
   int64_t M, N, K;
   int rg;                    // row groups (= partial columns), from dpe_pw_rowgroups
+  const float* in_coef;      // PW_FWD: x is the pre-BN tensor; the operand is relu(x * in_coef[k] + in_coef[K + k])
 };
 
 }  // namespace dpe

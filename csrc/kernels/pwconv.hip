@@ -73,6 +73,7 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
   constexpr int VM = (NS - 1) * S + (NS - 2) * P;
   static_assert(VM < 64, "vmcnt range");
   __shared__ __attribute__((aligned(16))) char smem[NS * TILE + 4 * STG];
+  __shared__ __attribute__((aligned(16))) float bnin[2 * K];  // in_coef: [scale | shift] of the K input channels
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -138,6 +139,11 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
 
+  if (EPI == PW_FWD && a.in_coef) {  // before the ring's first DMA (its counted waits start after this)
+    for (int i = tid; i < 2 * K; i += 256) bnin[i] = a.in_coef[i];
+    __syncthreads();
+  }
+
   // this row group's tiles: rg, rg + RG, ...
   const int nt = rg < tiles ? (tiles - 1 - rg) / RG + 1 : 0;
 #pragma unroll
@@ -191,6 +197,23 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
       bf16x8 xf[MI];
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) xf[mi] = kfrag(img + kc * (BM * 64), 16 * mi);
+      if (a.in_coef) {
+        // BN + ReLU of the producer applied to the operand (channels 32 kc + 8 g .. +7 of this lane;
+        // rows past M are never stored and are kept out of the statistics)
+        const f32x4* cs = (const f32x4*)(bnin + 32 * kc + 8 * g);
+        const f32x4* ch = (const f32x4*)(bnin + K + 32 * kc + 8 * g);
+        const f32x4 s0 = cs[0], s1 = cs[1], h0 = ch[0], h1 = ch[1];
+        const float sc8[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+        const float sh8[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) {
+          float f[8];
+          unpack8(__builtin_bit_cast(u32x4, xf[mi]), f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], sc8[e], sh8[e]), 0.f);
+          xf[mi] = __builtin_bit_cast(bf16x8, pack8(f));
+        }
+      }
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -245,9 +268,15 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
         float f[8];
         unpack8(v, f);
         if constexpr (EPI == PW_FWD) {
-          // statistics of the stored (rounded) values; rows past M are zeros
+          // statistics of the stored (rounded) values (rows past M: zeros, or relu(shift) terms
+          // with in_coef -- masked)
+          const float vm = valid ? 1.f : 0.f;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) { s[e] += f[e]; ss[e] = fmaf(f[e], f[e], ss[e]); }
+          for (int e = 0; e < 8; ++e) {
+            const float fv = f[e] * vm;
+            s[e] += fv;
+            ss[e] = fmaf(fv, fv, ss[e]);
+          }
         } else {
           if (a.residual) {  // + residual (dz of a BN + residual + ReLU output: masked by its bits)
             float r[8];

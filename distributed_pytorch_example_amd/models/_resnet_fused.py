@@ -68,6 +68,8 @@ _BN3_CHAIN = _EPI_BNB and os.environ.get("DPE_BN3_CHAIN", "1") != "0"
 _BN_DUAL = os.environ.get("DPE_BN_DUAL", "1") != "0"
 # DPE_ROW_BNIN=0: layer-1 a1 = relu(BN1(h1)) materialised by a bn_apply pass (A/B reference)
 _ROW_BNIN = _EPI_BNB and os.environ.get("DPE_ROW_BNIN", "1") != "0"
+# DPE_PW_BNIN=0: layer-1 a2 = relu(BN2(h2)) materialised by a bn_apply pass (A/B reference)
+_PW_BNIN = _ROW_BNIN and os.environ.get("DPE_PW_BNIN", "1") != "0"
 
 
 def _out_hw(hw, conv):
@@ -107,10 +109,10 @@ class BottleneckFn(Function):
                                      bn.momentum, bn.eps, relu, residual, st)
             return h, y, coef
 
-        def conv_coef(i, inp):
+        def conv_coef(i, inp, in_coef=None):
             cb = convs[i]
             s, p, d = _conv_conf(cb.conv)
-            h, st = C.conv_fwd(inp, ws[i], s, p, d, True, None)
+            h, st = C.conv_fwd(inp, ws[i], s, p, d, True, None, in_coef)
             bn = cb.bn
             M = h.numel() // h.shape[-1]
             return h, C.bn_coef(st, M, bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var, bn.momentum,
@@ -128,14 +130,21 @@ class BottleneckFn(Function):
             a1 = None
             h2, st2 = C.conv_fwd(h1, ws[1], *_conv_conf(c2conv), True, None, c1)
             bn2 = convs[1].bn
-            a2, c2 = C.bn_fwd_train(h2, bn2.weight.detach(), bn2.bias.detach(), bn2.running_mean, bn2.running_var,
-                                    bn2.momentum, bn2.eps, True, None, st2)
+            if _PW_BNIN and C.pw_bn_on_load(list(h2.shape), convs[2].conv.out_channels):
+                # a2 never materialised either: the streaming conv3 forward and its LDS-DMA weight
+                # grad apply relu(BN2(h2)) to their operand fragments
+                c2 = C.bn_coef(st2, h2.numel() // h2.shape[-1], bn2.weight.detach(), bn2.bias.detach(),
+                               bn2.running_mean, bn2.running_var, bn2.momentum, bn2.eps)
+                a2 = None
+            else:
+                a2, c2 = C.bn_fwd_train(h2, bn2.weight.detach(), bn2.bias.detach(), bn2.running_mean,
+                                        bn2.running_var, bn2.momentum, bn2.eps, True, None, st2)
         else:
             h1, a1, c1 = convbn(0, x, True)
             h2, a2, c2 = convbn(1, a1, True)
         # the next block's fused data-grad epilogue reads this output's ReLU mask as bits
         want_bits = True  # 1/16 of out: read by the next block's fused epilogue or by this block's BN3 backward
-        h3, c3 = conv_coef(2, a2)
+        h3, c3 = conv_coef(2, h2, c2) if a2 is None else conv_coef(2, a2)
         if block.down is not None:
             out, bits = C.bn_apply(h3, c3, hd, cd, True, want_bits)
         else:
@@ -241,8 +250,11 @@ class BottleneckFn(Function):
         ctx.bits = None
         if lk is not None:
             lk.h3 = lk.coef = lk.mask = None
-        wgrad(2, dh3, a2)
-        dh2 = dgrad_bnb(2, dh3, 1, a2, h2, c2)
+        if a2 is None:  # a2 = relu(BN2(h2)) recomputed on the weight grad's B fragments
+            wgrad(2, dh3, h2, c2)
+        else:
+            wgrad(2, dh3, a2)
+        dh2 = dgrad_bnb(2, dh3, 1, a2, h2, c2)  # (a2 unused: _EPI_BNB recomputes the mask from h2)
         if a1 is None:  # a1 = relu(BN1(h1)) recomputed on load by the row-walking weight grad
             wgrad(1, dh2, h1, c1)
         else:

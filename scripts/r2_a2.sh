@@ -1,0 +1,10 @@
+# layer-1 a2 never materialised (pw_stream forward + LDS-DMA weight grad with BN2 on load): numerics + step A/B
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > gpurun_out/a2_tests.log 2>&1 || { grep -E "FAIL|Error|error|assert" gpurun_out/a2_tests.log | head -30; tail -30 gpurun_out/a2_tests.log; exit 1; }
+tail -1 gpurun_out/a2_tests.log
+for r in 1 2 3; do for v in 0 1; do
+  DPE_PW_BNIN=$v timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 > gpurun_out/a2.log 2>&1 || exit 1
+  echo "pw_bnin=$v $(tail -1 gpurun_out/a2.log | cut -c100-175)"
+done; done
