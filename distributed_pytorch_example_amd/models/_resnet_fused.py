@@ -43,7 +43,9 @@ stage every input row through registers one row ahead of its use, so
 relu(BN1(h1)) is applied there off the critical path and a1 (205 MB at batch
 512) is neither written nor re-read: conv2 reads h1 + BN1's coefficients, the
 weight grad recomputes a1 the same way, and BN1's backward already takes its
-ReLU mask from h1.)
+ReLU mask from h1.  Likewise a2 (DPE_PW_BNIN=1, default): the streaming
+pointwise conv3 forward and its LDS-DMA weight grad apply relu(BN2(h2)) to
+their operand fragments.)
 
 Weight gradients are accumulated straight into the DDP bucket views and each
 parameter is announced to the reducer as soon as its gradient is final, in
