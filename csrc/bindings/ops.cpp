@@ -1353,7 +1353,8 @@ void register_ops(pybind11::module& m) {
           // LDS-DMA weight grad (K = pixels % 32, M = Cout, N = C) take the BN coefficients (in_coef)
           if (xs.size() != 4) return false;
           const int64_t M = xs[0] * xs[1] * xs[2], C = xs[3];
-          return pw_stream_on() && C == 64 && cout % 8 == 0 && M % 32 == 0 &&
+          static const int cmax = [] { const char* e = getenv("DPE_PW_BNIN_CMAX"); return e ? atoi(e) : 128; }();
+          return pw_stream_on() && (C == 64 || C == 128) && C <= cmax && cout % 8 == 0 && M % 32 == 0 &&
                  dpe_pw_rowgroups(M, cout, C, dpe::PW_FWD) > 0;
         }, py::arg("x_shape"), py::arg("cout"));
   m.def("conv_dgrad_acc", &conv_dgrad_acc, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"),

@@ -71,7 +71,7 @@ _BN_DUAL = os.environ.get("DPE_BN_DUAL", "1") != "0"
 # DPE_ROW_BNIN=0: layer-1 a1 = relu(BN1(h1)) materialised by a bn_apply pass (A/B reference)
 _ROW_BNIN = _EPI_BNB and os.environ.get("DPE_ROW_BNIN", "1") != "0"
 # DPE_PW_BNIN=0: layer-1 a2 = relu(BN2(h2)) materialised by a bn_apply pass (A/B reference)
-_PW_BNIN = _ROW_BNIN and os.environ.get("DPE_PW_BNIN", "1") != "0"
+_PW_BNIN = _EPI_BNB and os.environ.get("DPE_PW_BNIN", "1") != "0"
 
 
 def _out_hw(hw, conv):
@@ -131,19 +131,19 @@ class BottleneckFn(Function):
             h1, c1 = conv_coef(0, x)
             a1 = None
             h2, st2 = C.conv_fwd(h1, ws[1], *_conv_conf(c2conv), True, None, c1)
-            bn2 = convs[1].bn
-            if _PW_BNIN and C.pw_bn_on_load(list(h2.shape), convs[2].conv.out_channels):
-                # a2 never materialised either: the streaming conv3 forward and its LDS-DMA weight
-                # grad apply relu(BN2(h2)) to their operand fragments
-                c2 = C.bn_coef(st2, h2.numel() // h2.shape[-1], bn2.weight.detach(), bn2.bias.detach(),
-                               bn2.running_mean, bn2.running_var, bn2.momentum, bn2.eps)
-                a2 = None
-            else:
-                a2, c2 = C.bn_fwd_train(h2, bn2.weight.detach(), bn2.bias.detach(), bn2.running_mean,
-                                        bn2.running_var, bn2.momentum, bn2.eps, True, None, st2)
         else:
             h1, a1, c1 = convbn(0, x, True)
-            h2, a2, c2 = convbn(1, a1, True)
+            h2, st2 = C.conv_fwd(a1, ws[1], *_conv_conf(c2conv), True, None)
+        bn2 = convs[1].bn
+        if _PW_BNIN and C.pw_bn_on_load(list(h2.shape), convs[2].conv.out_channels):
+            # a2 never materialised: the streaming conv3 forward and its LDS-DMA weight grad apply
+            # relu(BN2(h2)) to their operand fragments (64- and 128-channel bottlenecks)
+            c2 = C.bn_coef(st2, h2.numel() // h2.shape[-1], bn2.weight.detach(), bn2.bias.detach(),
+                           bn2.running_mean, bn2.running_var, bn2.momentum, bn2.eps)
+            a2 = None
+        else:
+            a2, c2 = C.bn_fwd_train(h2, bn2.weight.detach(), bn2.bias.detach(), bn2.running_mean,
+                                    bn2.running_var, bn2.momentum, bn2.eps, True, None, st2)
         # the next block's fused data-grad epilogue reads this output's ReLU mask as bits
         want_bits = True  # 1/16 of out: read by the next block's fused epilogue or by this block's BN3 backward
         h3, c3 = conv_coef(2, h2, c2) if a2 is None else conv_coef(2, a2)

@@ -960,25 +960,25 @@ def test_stem_wgrad_matches_reference(C, N, H, W):
     assert rel_err(outs[True], outs[False]) < 1e-4
 
 
-@pytest.mark.parametrize("N,H,W,Co", [(8, 56, 56, 256), (3, 7, 30, 128)])
-def test_pointwise_bn_on_load(C, N, H, W, Co):
+@pytest.mark.parametrize("N,H,W,Ci,Co", [(8, 56, 56, 64, 256), (3, 7, 30, 64, 128), (8, 28, 28, 128, 512)])
+def test_pointwise_bn_on_load(C, N, H, W, Ci, Co):
     """Layer-1 conv3 over a pre-BN input: the streaming pointwise forward and the LDS-DMA weight grad
     with in_coef (relu(h * scale + shift) applied to the operand fragments) == the same convs over
     the tensor bn_apply materialises (forward bitwise incl. BN sums; weight grad to fp32 order)."""
     torch.manual_seed(59)
-    h = bf(torch.randn(N, H, W, 64, device=dev))
-    coef = _bn_coef(C, 64)
+    h = bf(torch.randn(N, H, W, Ci, device=dev))
+    coef = _bn_coef(C, Ci)
     a, _ = C.bn_apply(h, coef, None, None, True, False)
-    w = bf(torch.randn(Co, 1, 1, 64, device=dev) / 8)
+    w = bf(torch.randn(Co, 1, 1, Ci, device=dev) / 8)
     z = [1, 1], [0, 0], [1, 1]
-    assert C.pw_bn_on_load([N, H, W, 64], Co) == ((N * H * W) % 32 == 0)
+    assert C.pw_bn_on_load([N, H, W, Ci], Co) == ((N * H * W) % 32 == 0)
     if (N * H * W) % 32:
         return
     y1, s1 = C.conv_fwd(h, w, *z, True, None, coef)
     y2, s2 = C.conv_fwd(a, w, *z, True, None)
     assert torch.equal(y1, y2) and torch.equal(s1, s2)
     dy = bf(torch.randn(N, H, W, Co, device=dev))
-    dw1 = torch.zeros(Co, 1, 1, 64, device=dev)
+    dw1 = torch.zeros(Co, 1, 1, Ci, device=dev)
     dw2 = torch.zeros_like(dw1)
     C.conv_wgrad(dy, h, dw1, *z, 1.0, coef)
     C.conv_wgrad(dy, a, dw2, *z, 1.0)
