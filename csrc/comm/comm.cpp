@@ -253,8 +253,13 @@ void Reducer::init_tracking(int64_t nparams) {
 
 Reducer::~Reducer() {
   if (host_launch_) return;  // no HIP objects in host-transport mode
-  if (comm_)
+  if (comm_) {
+    // the last step's all-reduces may still be running on the comm stream (finalize only makes the
+    // compute stream wait): drain them before their buffers are deregistered / released and a
+    // rebuilt reducer registers its own
+    if (!comm_->aborted()) (void)hipStreamSynchronize(comm_->comm_stream().stream());
     for (uint64_t h : reg_handles_) comm_->deregister_buffer(h);
+  }
   for (auto* v : {&ev_ready_, &ev_aux_, &ev_start_, &ev_end_})
     for (auto e : *v) (void)hipEventDestroy(e);
   (void)hipEventDestroy(ev_bwd_end_);

@@ -51,6 +51,7 @@ class Communicator {
   // Non-blocking health check (ncclCommGetAsyncError); returns error string or "".
   std::string async_error();
   void abort();
+  bool aborted() const { return aborted_; }
 
  private:
   void pre(const at::Tensor& t);

@@ -122,14 +122,15 @@ class ResNet(nn.Module):
                 x = Fx.to_nhwc_input(x, self.in_pad)
             h = Fx.max_pool2d_nhwc(self.stem(x), 3, 2, 1)
         link = None
-        fused = h.is_cuda and self.training and all(b.fused for b in self.blocks)
-        if fused:
-            # every block's num_batches_tracked in one multi-tensor launch (not one per block); the
-            # list is rebuilt per step (host-side only) so moved / reloaded buffers are never stale
-            torch._foreach_add_([m.num_batches_tracked for b in self.blocks for m in b.modules()
+        # the blocks that take the fused path (the same test forward_chained makes per block): their
+        # num_batches_tracked counters advance in one multi-tensor launch instead of one per block;
+        # the list is rebuilt per step (host-side only) so moved / reloaded buffers are never stale
+        fused = [h.is_cuda and self.training and b.training and b.fused for b in self.blocks]
+        if any(fused):
+            torch._foreach_add_([m.num_batches_tracked for b, f in zip(self.blocks, fused) if f for m in b.modules()
                                  if getattr(m, "num_batches_tracked", None) is not None], 1)
-        for blk in self.blocks:  # each block's output feeds only the next block
-            h, link = blk.forward_chained(h, link, count_batches=not fused)
+        for blk, f in zip(self.blocks, fused):  # each block's output feeds only the next block
+            h, link = blk.forward_chained(h, link, count_batches=not f)
         h = Fx.global_avg_pool_nhwc(h)
         return self.fc(h)
 

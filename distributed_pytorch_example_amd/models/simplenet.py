@@ -28,20 +28,22 @@ from ..ops.layers import Dropout, Flatten, Linear, ReLU
 
 class _SimpleNet32Fn(Function):
     @staticmethod
-    def forward(ctx, x, p: float, training: bool, w0, b0, w1, b1, w2, b2):
+    def forward(ctx, x, p0: float, p1: float, training: bool, w0, b0, w1, b1, w2, b2):
         C = ext()
         h = x.reshape(x.shape[0], -1)
         h = (h if h.dtype == torch.float32 else h.float()).contiguous()
-        drop = training and p > 0.0
         acts = [h]
-        for w, b in ((w0, b0), (w1, b1)):
+        scales = []
+        for w, b, p in ((w0, b0, p0), (w1, b1, p1)):  # each hidden layer's own Dropout(p)
+            drop = training and p > 0.0
             seed, off = Fx._RNG.next(h.shape[0] * w.shape[0]) if drop else (0, 0)
             h = C.linear32_fwd(h, w.detach(), b.detach(), True, p if drop else 0.0, seed, off)
             acts.append(h)
+            scales.append(1.0 / (1.0 - p) if drop else 1.0)
         logits = C.linear32_fwd(h, w2.detach(), b2.detach())
         ctx.save_for_backward(*acts)
         ctx.params = (w0, b0, w1, b1, w2, b2)
-        ctx.scale = 1.0 / (1.0 - p) if drop else 1.0
+        ctx.scales = tuple(scales)
         ctx.xshape = x.shape
         for t in ctx.params:
             note_use(t)
@@ -67,12 +69,13 @@ class _SimpleNet32Fn(Function):
             return None if direct else buf
 
         gw2, gb2 = wgrad(w2, g, y1), bgrad(b2, g)
-        dh1 = C.linear32_dgrad(g, w2.detach(), y1, ctx.scale)   # relu+dropout backward of layer 1 fused
+        s0, s1 = ctx.scales
+        dh1 = C.linear32_dgrad(g, w2.detach(), y1, s1)   # relu+dropout(p1) backward of layer 1 fused
         gw1, gb1 = wgrad(w1, dh1, y0), bgrad(b1, dh1)
-        dh0 = C.linear32_dgrad(dh1, w1.detach(), y0, ctx.scale)
+        dh0 = C.linear32_dgrad(dh1, w1.detach(), y0, s0)
         gw0, gb0 = wgrad(w0, dh0, x), bgrad(b0, dh0)
         dx = C.linear32_dgrad(dh0, w0.detach()).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
-        return dx, None, None, gw0, gb0, gw1, gb1, gw2, gb2
+        return dx, None, None, None, gw0, gb0, gw1, gb1, gw2, gb2
 
 
 class SimpleNet(nn.Module):
@@ -97,7 +100,7 @@ class SimpleNet(nn.Module):
         x = self.flatten(x)
         l0, _, d0, l1, _, d1, l2 = self.layers
         if x.is_cuda and self.compute_dtype == "fp32":
-            return _SimpleNet32Fn.apply(x, d0.p, self.training, l0.weight, l0.bias, l1.weight, l1.bias, l2.weight,
+            return _SimpleNet32Fn.apply(x, d0.p, d1.p, self.training, l0.weight, l0.bias, l1.weight, l1.bias, l2.weight,
                                         l2.bias)
         if x.is_cuda:
             # bf16: fused epilogues, Linear+bias+ReLU in one GEMM launch

@@ -37,8 +37,9 @@ Design (MI355X-first, not a port of c10d::Reducer):
   gloo).  Custom comm hooks run on a Python reducer.
 * **Init sync**: parameters and buffers are broadcast from rank 0 as one flat
   buffer per dtype (c10d's coalesced broadcast, C3).
-* **Buffer sync (C9)**: with ``broadcast_buffers`` the module's floating
-  buffers (BatchNorm running stats: 53,120 floats for ResNet-50) are re-homed
+* **Buffer sync (C9)**: with ``broadcast_buffers`` the module's buffers
+  (BatchNorm running stats: 53,120 floats for ResNet-50, plus the 53 int64
+  ``num_batches_tracked`` counters) are re-homed
   once as views of ONE flat tensor per dtype/device, so the per-forward
   broadcast is a single RCCL call with no concatenate / scatter-back copies
   (c10d coalesces into a temporary and copies back: ~2 tiny kernels per
@@ -262,7 +263,7 @@ class DistributedDataParallel(nn.Module):
             by_dtype.setdefault((t.dtype, t.device), []).append(t)
         for (dt, dev), ts in by_dtype.items():
             flat = torch.cat([t.reshape(-1) for t in ts])
-            pdist.broadcast(flat, 0)
+            pdist.broadcast(flat if dt != torch.bool else flat.view(torch.uint8), 0)
             off = 0
             for t in ts:
                 n = t.numel()
@@ -432,11 +433,13 @@ class DistributedDataParallel(nn.Module):
 
     @torch.no_grad()
     def _flatten_buffers(self):
-        """Re-home every floating buffer as a view of one flat tensor per (dtype, device)."""
+        """Re-home every buffer -- floating (BN running stats) and integer (``num_batches_tracked``)
+        alike, as stock DDP's ``broadcast_buffers`` syncs them all -- as a view of one flat tensor
+        per (dtype, device): one broadcast per dtype per forward."""
         groups, seen = {}, set()
         for mod in self.module.modules():
             for name, b in mod._buffers.items():
-                if b is None or not b.is_floating_point() or id(b) in seen:
+                if b is None or id(b) in seen:
                     continue
                 seen.add(id(b))
                 groups.setdefault((b.dtype, b.device), []).append((mod, name, b))
@@ -459,7 +462,7 @@ class DistributedDataParallel(nn.Module):
         if any(mod._buffers.get(name) is not v for mod, name, v in self._flat_views):
             self._flatten_buffers()  # a buffer was re-assigned: re-home it
         for flat in self._flat_bufs:
-            pdist.broadcast(flat, 0)
+            pdist.broadcast(flat if flat.dtype != torch.bool else flat.view(torch.uint8), 0)
 
     @contextlib.contextmanager
     def no_sync(self):

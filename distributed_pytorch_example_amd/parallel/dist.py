@@ -168,8 +168,9 @@ class Watchdog:
     exits the process non-zero so the launcher's fail-fast path tears the job
     down -- instead of the reference's 30-minute gloo timeout.
 
-    The training loop beats every step and every validation batch; checkpoint
-    writes and the barrier behind them run under ``suspended()``.  The timeout
+    The training loop beats every step and every validation batch; rank 0's
+    checkpoint writes run under ``suspended()``, the barrier behind them under
+    ``grace(extra_s)`` (a longer but still bounded stall deadline).  The timeout
     must still cover the first training step (kernel/module load, bucket build).
     GEMM dispatch is planned analytically, so there is no autotuning pause."""
 
@@ -182,6 +183,7 @@ class Watchdog:
         self._last = time.monotonic()
         self._stop = threading.Event()
         self._paused = 0
+        self._grace = 0.0
         self._on_fail = on_fail
         self.failure: Optional[str] = None
         self._thread = threading.Thread(target=self._run, name="dpe-watchdog", daemon=True)
@@ -206,6 +208,24 @@ class Watchdog:
 
         return _ctx()
 
+    def grace(self, extra_s: float):
+        """Context: the stall deadline is ``timeout_s + extra_s`` inside (a barrier that waits for a
+        peer's checkpoint write).  Detection stays on, so a peer dying there still aborts the job."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def _ctx():
+            old = self._grace
+            self._grace = max(old, float(extra_s))
+            self.beat()
+            try:
+                yield self
+            finally:
+                self._grace = old
+                self.beat()
+
+        return _ctx()
+
     def stop(self) -> None:
         self._stop.set()
         self._thread.join(timeout=5)
@@ -214,7 +234,7 @@ class Watchdog:
         while not self._stop.wait(self.interval_s):
             err = check_health()
             stalled = 0.0 if self._paused else self._time.monotonic() - self._last
-            if err or stalled > self.timeout_s:
+            if err or stalled > self.timeout_s + self._grace:
                 self.failure = f"RCCL async error: {err}" if err else f"no progress for {stalled:.0f}s"
                 log.error(f"watchdog: {self.failure}; aborting communicator")
                 c = _state["comm"]

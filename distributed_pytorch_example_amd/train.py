@@ -75,6 +75,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--watchdog-timeout", type=float, default=0.0,
                    help="abort the job when no training step completes for this many seconds or RCCL reports an "
                         "async error (0 = off)")
+    p.add_argument("--watchdog-checkpoint-grace", type=float, default=600.0,
+                   help="extra seconds the watchdog allows in the end-of-epoch barrier (rank 0 writes checkpoints)")
     return p
 
 
@@ -224,25 +226,26 @@ def main(argv=None):
         avg_train_loss, avg_val_loss, avg_val_accuracy = (v.item() for v in metrics)
 
         epoch_time = time.time() - epoch_start
-        # rank 0 writes checkpoints while the others wait in the barrier: no step heartbeat there
-        wd_pause = watchdog.suspended() if watchdog is not None else _null()
-        wd_pause.__enter__()
         if rank == 0:
             logger.info(f"Epoch {epoch} completed in {epoch_time:.2f}s")
             logger.info(f"  Train Loss: {avg_train_loss:.4f}")
             logger.info(f"  Val Loss: {avg_val_loss:.4f}, Val Accuracy: {avg_val_accuracy:.2f}%")
             nb = min(len(train_loader), args.max_steps or len(train_loader))
             logger.info(f"  Throughput: {nb * args.batch_size * world_size / epoch_time:.1f} samples/s (incl. validation)")
-            if avg_val_accuracy > best_accuracy:
-                best_accuracy = avg_val_accuracy
+            # no step heartbeat while rank 0 writes (RCCL async errors are still polled)
+            with (watchdog.suspended() if watchdog is not None else _null()):
+                if avg_val_accuracy > best_accuracy:
+                    best_accuracy = avg_val_accuracy
+                    save_checkpoint(model, optimizer, epoch, avg_train_loss,
+                                    os.path.join(args.checkpoint_dir, "best_model.pt"), args.async_checkpoint)
                 save_checkpoint(model, optimizer, epoch, avg_train_loss,
-                                os.path.join(args.checkpoint_dir, "best_model.pt"), args.async_checkpoint)
-            save_checkpoint(model, optimizer, epoch, avg_train_loss,
-                            os.path.join(args.checkpoint_dir, "latest_model.pt"), args.async_checkpoint)
+                                os.path.join(args.checkpoint_dir, "latest_model.pt"), args.async_checkpoint)
         if prof is not None:
             prof.step()
-        pdist.barrier()
-        wd_pause.__exit__(None, None, None)
+        # the other ranks wait here for rank 0's write: stall detection stays on, with a bounded
+        # extra allowance for the checkpoint (a peer dying in this barrier still aborts the job)
+        with (watchdog.grace(args.watchdog_checkpoint_grace) if watchdog is not None else _null()):
+            pdist.barrier()
 
     wait_pending()
     if watchdog is not None:

@@ -127,6 +127,12 @@ def _join_tensors(obj, tensors: list):
     return obj
 
 
+# dtypes RCCL reduces / broadcasts natively (comm.cpp to_nccl); anything else (bool, complex, fp8,
+# uint16, ...) crosses the wire as a byte view of the same flat buffer and keeps its dtype
+_WIRE_DTYPES = (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int32, torch.int64, torch.uint8,
+                torch.int8)
+
+
 def broadcast_state(ckpt: Optional[dict], device: torch.device) -> dict:
     """Rank 0's checkpoint to every rank: the tensor-free skeleton (keys, shapes, dtypes, numbers)
     through the control plane, the tensor bytes as ONE flat buffer per dtype through
@@ -156,7 +162,7 @@ def broadcast_state(ckpt: Optional[dict], device: torch.device) -> dict:
         else:
             flat = torch.empty(total, dtype=tdt, device=device)
         if total:
-            pdist.broadcast(flat, 0)
+            pdist.broadcast(flat if tdt in _WIRE_DTYPES else flat.view(torch.uint8), 0)  # e.g. bool: as bytes
         off = 0
         for r, n in zip(rs, numels):
             t = flat[off: off + n].view(r.shape).clone()

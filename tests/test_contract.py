@@ -88,7 +88,7 @@ def test_grad_accum_syncs_at_max_steps_cutoff():
     assert opt.steps == [2, 3]  # after micro-batch 2 (accum boundary) and after the cut-off batch 3
 
 
-def test_watchdog_suspended_during_checkpoint_and_barrier():
+def test_watchdog_suspended_during_checkpoint_write():
     import time
 
     from distributed_pytorch_example_amd.parallel.dist import Watchdog
@@ -101,5 +101,39 @@ def test_watchdog_suspended_during_checkpoint_and_barrier():
         assert not fails
         time.sleep(0.8)  # no heartbeat outside a suspended block: stall detected
         assert fails and "no progress" in fails[0]
+    finally:
+        wd.stop()
+
+
+def test_watchdog_grace_is_bounded():
+    """The end-of-epoch barrier runs under grace(): a longer deadline, but a stall past it (a peer
+    that died while rank 0 was writing) is still detected (no unbounded suspension)."""
+    import time
+
+    from distributed_pytorch_example_amd.parallel.dist import Watchdog
+
+    fails = []
+    wd = Watchdog(timeout_s=0.2, interval_s=0.05, on_fail=fails.append)
+    try:
+        with wd.grace(0.4):
+            time.sleep(0.35)  # longer than timeout_s, inside timeout_s + grace: fine
+            assert not fails
+            time.sleep(0.6)   # past timeout_s + grace: stall detected inside the block
+            assert fails and "no progress" in fails[0]
+    finally:
+        wd.stop()
+
+
+def test_watchdog_suspension_ends_on_exception():
+    from distributed_pytorch_example_amd.parallel.dist import Watchdog
+
+    wd = Watchdog(timeout_s=10, interval_s=1.0)
+    try:
+        try:
+            with wd.suspended():
+                raise OSError("disk full")
+        except OSError:
+            pass
+        assert wd._paused == 0
     finally:
         wd.stop()

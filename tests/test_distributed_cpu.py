@@ -107,21 +107,28 @@ def _w_buffers(rank, world, port, q):
     rm = m.stem.bn.running_mean.clone()
     dist.broadcast(rm, 0)
     assert rank == 0 or not torch.equal(rm, m.stem.bn.running_mean)
-    # forward 2 (eval: no stats update) broadcasts rank 0's running stats before running
+    # rank 1 counts one extra batch: num_batches_tracked (int64) differs across ranks too
+    if rank == 1:
+        for b in m.modules():
+            if getattr(b, "num_batches_tracked", None) is not None:
+                b.num_batches_tracked += 1
+    # forward 2 (eval: no stats update) broadcasts rank 0's buffers -- floating AND integer, like
+    # stock DDP's broadcast_buffers -- before running
     m.eval()
     with torch.no_grad():
         ddp(torch.randn(2, 3, 32, 32))
-    n = 0
+    n = ni = 0
     for b in m.buffers():
-        if b.is_floating_point():
-            ref = b.clone()
-            dist.broadcast(ref, 0)
-            assert torch.equal(b, ref)
-            n += 1
-    assert n > 0
-    # all floating buffers live in ONE flat tensor: one broadcast per forward, no cat/copy kernels
-    assert len(ddp._flat_bufs) == 1
-    assert m.stem.bn.running_mean.untyped_storage().data_ptr() == ddp._flat_bufs[0].untyped_storage().data_ptr()
+        ref = b.clone()
+        dist.broadcast(ref, 0)
+        assert torch.equal(b, ref)
+        n += 1
+        ni += not b.is_floating_point()
+    assert n > 0 and ni > 0
+    # one flat tensor per dtype (fp32 running stats, int64 counters): one broadcast each per forward
+    assert sorted(str(f.dtype) for f in ddp._flat_bufs) == ["torch.float32", "torch.int64"]
+    fl = next(f for f in ddp._flat_bufs if f.dtype == torch.float32)
+    assert m.stem.bn.running_mean.untyped_storage().data_ptr() == fl.untyped_storage().data_ptr()
     q.put(("ok", rank))
     dist.destroy_process_group()
 
@@ -374,7 +381,10 @@ def _w_broadcast_state(rank, world, port, q):
     ck = None
     if rank == 0:
         torch.manual_seed(0)
-        ck = {"epoch": 3, "loss": 0.25, "model_state_dict": {"w": torch.randn(5, 7), "n": torch.tensor(4, dtype=torch.int64)},
+        ck = {"epoch": 3, "loss": 0.25, "model_state_dict": {"w": torch.randn(5, 7), "n": torch.tensor(4, dtype=torch.int64),
+                                                          "mask": torch.arange(10) % 3 == 0,
+                                                          "z": torch.complex(torch.arange(4.0), -torch.arange(4.0)),
+                                                          "u16": torch.arange(6).to(torch.uint16)},
               "optimizer_state_dict": {"state": {0: {"step": torch.tensor(12.0), "exp_avg": torch.randn(5, 7)}},
                                        "param_groups": [{"lr": 1e-3, "betas": (0.9, 0.999), "params": [0]}]}}
     out = broadcast_state(ck, torch.device("cpu"))
@@ -386,6 +396,11 @@ def _w_broadcast_state(rank, world, port, q):
     assert out["epoch"] == 3 and out["optimizer_state_dict"]["param_groups"][0]["betas"] == (0.9, 0.999)
     st = out["optimizer_state_dict"]["state"][0]["step"]
     assert st.dim() == 0 and float(st) == 12.0 and out["model_state_dict"]["n"].dtype == torch.int64
+    # dtypes outside RCCL's set travel as byte views and come back with their dtype and values
+    msd = out["model_state_dict"]
+    assert msd["mask"].dtype == torch.bool and torch.equal(msd["mask"], torch.arange(10) % 3 == 0)
+    assert msd["z"].dtype == torch.complex64 and torch.equal(msd["z"], torch.complex(torch.arange(4.0), -torch.arange(4.0)))
+    assert msd["u16"].dtype == torch.uint16 and torch.equal(msd["u16"].to(torch.int64), torch.arange(6))
     q.put(("ok", rank))
     dist.destroy_process_group()
 
