@@ -24,6 +24,8 @@
 
 using at::Tensor;
 
+extern "C" int dpe_cu_reserve();  // comm.cpp: slots to leave to in-flight collectives
+
 namespace dpe_gemm {
 
 namespace {
@@ -71,6 +73,7 @@ bool layout_ok(int cfg, int ak, int bk) {
 Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int out_bytes, int force_cfg,
           int force_splits) {
   const int ncu = num_cus();
+  const int reserve = dpe_cu_reserve();
   const int64_t ktiles = K / 64;
   Plan best{-1, 1, (int)K, 0, 1e30};
   if (force_cfg < 0) force_cfg = g_force_cfg;
@@ -79,13 +82,14 @@ Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int
     if (force_cfg >= 0 && c.cfg != force_cfg) continue;
     if (!layout_ok(c.cfg, ak, bk)) continue;
     const int64_t tiles = ((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
-    const int64_t slots = (int64_t)ncu * c.bpc;
-    // up to 8 K splits in general; more when the tiles alone leave most CUs idle (a 1x1 conv weight
-    // grad: a few output tiles over 25K-400K pixels), so the split fills one round of slots
-    static const int64_t split_cap = [] { const char* e = getenv("DPE_HGEMM_SPLIT_CAP"); return e ? atoll(e) : 128; }();  // A/B
+    // resident slots, minus those left to RCCL channel blocks while a bucket all-reduce overlaps
+    // (comm.cpp CU budget): a full-residency static grid would push blocks into a second wave
+    const int64_t slots = std::max<int64_t>(c.bpc, (int64_t)ncu * c.bpc - reserve);
+    // up to 8 K splits in general; more (<= 128) when the tiles alone leave most CUs idle (a 1x1 conv
+    // weight grad: a few output tiles over 25K-400K pixels), so the split fills one round of slots
+    // (cap swept 8-128: neutral, profiles/hgemm_split_cap_ab_r2.txt)
     const int max_split =
-        allow_split ? (int)std::max<int64_t>(std::min<int64_t>(8, split_cap), std::min<int64_t>(split_cap, slots / std::max<int64_t>(1, tiles)))
-                    : 1;
+        allow_split ? (int)std::max<int64_t>(8, std::min<int64_t>(128, slots / std::max<int64_t>(1, tiles))) : 1;
     for (int s = 1; s <= max_split; ++s) {
       if (force_splits > 0 && s != force_splits) continue;
       const int64_t kt = (ktiles + s - 1) / s;
@@ -110,11 +114,7 @@ Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int
 // row-major: 8192^3 NT 1340 -> 1478, NN 1054 -> 1201, TN 989 -> 1132; GPT-2 LM head fwd 973 ->
 // 1055; 4096^3 and the small GPT-2 GEMMs neutral; 8-row bands equal on squares, worse on the LM
 // head; 16-row bands worse everywhere.
-int group_rows(const Plan& pl) {
-  static const int env = [] { const char* e = getenv("DPE_HGEMM_GROUP"); return e ? atoi(e) : 0; }();  // A/B only
-  if (env != 0) return env;
-  return pl.grid >= 64 ? 4 : 1;
-}
+int group_rows(const Plan& pl) { return pl.grid >= 64 ? 4 : 1; }
 
 int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_bytes) {
   TORCH_CHECK(a.K % 64 == 0 && a.K > 0, "hgemm: K must be a positive multiple of 64 (got ", a.K, ")");
@@ -125,8 +125,11 @@ int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_by
   if (a.group_m == 0) a.group_m = group_rows(pl);
   Tensor ws;
   if (pl.splits > 1) {
-    ws = at::empty({(int64_t)pl.splits * a.M * a.N}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA));
+    // one allocation: [splits][M][N] partial slabs (+ [splits][M] bias-gradient partials)
+    const int64_t slab = (int64_t)pl.splits * a.M * a.N;
+    ws = at::empty({slab + (a.dbias ? (int64_t)pl.splits * a.M : 0)}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA));
     a.ws = (float*)ws.data_ptr();
+    if (a.dbias) a.ws_bias = a.ws + slab;
     const int rc = dpe_hgemm_launch(&a, pl.cfg, ak, bk, dpe::HE_SLAB, pl.grid, cur_stream());
     hipError_t e = hipGetLastError();
     TORCH_CHECK(rc == 0 && e == hipSuccess, "hgemm (split) launch failed rc=", rc, " ", hipGetErrorString(e));
@@ -210,7 +213,8 @@ void linear32_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha)
 Tensor hgemm_raw(const Tensor& A, const Tensor& B, Tensor C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                  int64_t ldc, bool ak, bool bk, int64_t epi, int64_t act, const c10::optional<Tensor>& bias,
                  const c10::optional<Tensor>& residual, const c10::optional<Tensor>& aux_in,
-                 const c10::optional<Tensor>& aux_out, double alpha, int64_t cfg, int64_t splits, int64_t group_m) {
+                 const c10::optional<Tensor>& aux_out, double alpha, int64_t cfg, int64_t splits, int64_t group_m,
+                 const c10::optional<Tensor>& dbias) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "hgemm: GPU tensors");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "hgemm: bf16 operands");
   TORCH_CHECK(C.scalar_type() == (epi == dpe::HE_BF16 ? at::kBFloat16 : at::kFloat), "hgemm: output dtype");
@@ -227,6 +231,12 @@ Tensor hgemm_raw(const Tensor& A, const Tensor& B, Tensor C, int64_t M, int64_t 
   if (aux_in && aux_in->defined()) { TORCH_CHECK(aux_in->scalar_type() == at::kBFloat16); a.aux_in = (const uint16_t*)aux_in->data_ptr(); }
   if (aux_out && aux_out->defined()) { TORCH_CHECK(aux_out->scalar_type() == at::kBFloat16); a.aux_out = (uint16_t*)aux_out->data_ptr(); }
   TORCH_CHECK(act != dpe::HACT_GELU_BWD || a.aux_in, "hgemm: gelu backward needs aux_in");
+  if (dbias && dbias->defined()) {
+    TORCH_CHECK(dbias->is_cuda() && dbias->scalar_type() == at::kFloat && dbias->is_contiguous() && dbias->numel() >= M,
+                "hgemm: dbias is a contiguous fp32 [M] GPU tensor");
+    TORCH_CHECK(!ak && !bk, "hgemm: dbias (fused bias gradient) needs the TN layout");
+    a.dbias = (float*)dbias->data_ptr();
+  }
   const int out_bytes = epi == dpe::HE_BF16 ? 2 : 4;
   const Plan pl = plan(M, N, K, ak, bk, splits != 1, out_bytes, (int)cfg, (int)splits);
   TORCH_CHECK(pl.cfg >= 0, "hgemm: no configuration (cfg=", cfg, " splits=", splits, ")");
@@ -235,8 +245,10 @@ Tensor hgemm_raw(const Tensor& A, const Tensor& B, Tensor C, int64_t M, int64_t 
   a.group_m = group_m != 0 ? (int)group_m : group_rows(pl);
   Tensor ws;
   if (pl.splits > 1) {
-    ws = at::empty({(int64_t)pl.splits * M * N}, A.options().dtype(at::kFloat));
+    const int64_t slab = (int64_t)pl.splits * M * N;
+    ws = at::empty({slab + (a.dbias ? (int64_t)pl.splits * M : 0)}, A.options().dtype(at::kFloat));
     a.ws = (float*)ws.data_ptr();
+    if (a.dbias) a.ws_bias = a.ws + slab;
     int rc = dpe_hgemm_launch(&a, pl.cfg, ak, bk, dpe::HE_SLAB, pl.grid, cur_stream());
     TORCH_CHECK(rc == 0 && hipGetLastError() == hipSuccess, "hgemm split launch rc=", rc);
     rc = dpe_hgemm_finalize(&a, (int)epi, cur_stream());
@@ -256,7 +268,7 @@ void register_gemm(pybind11::module& m) {
         py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("a_k"), py::arg("b_k"), py::arg("epi") = 0,
         py::arg("act") = 0, py::arg("bias") = py::none(), py::arg("residual") = py::none(), py::arg("aux_in") = py::none(),
         py::arg("aux_out") = py::none(), py::arg("alpha") = 1.0, py::arg("cfg") = -1, py::arg("splits") = -1,
-        py::arg("group_m") = 0,
+        py::arg("group_m") = 0, py::arg("dbias") = py::none(),
         "persistent MFMA GEMM with explicit layouts (cfg / splits -1: planner's choice; group_m 0: planner's, <0: row-major)");
   m.def("hgemm_plan", [](int64_t M, int64_t N, int64_t K, bool ak, bool bk, bool allow_split, int64_t out_bytes) {
           const Plan p = plan(M, N, K, ak, bk, allow_split, (int)out_bytes);

@@ -58,7 +58,9 @@ int dpe_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st);
 int dpe_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
 int dpe_act(const void* a, const void* b, void* out, int64_t n, int op, int bf16, hipStream_t st);
 int dpe_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset, int bf16, hipStream_t st);
-int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, float* sink, hipStream_t st);
+int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, int vgprs, const unsigned* stop, float* sink,
+               hipStream_t st);
+int dpe_hog_stop(unsigned* stop, unsigned v, hipStream_t st);
 int dpe_conv3x3_rows_blocks(int N, int H, int W);
 int64_t dpe_wgrad3x3_rows_scratch(int N, int H, int W);
 int dpe_wgrad3x3_rows_launch(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H, int W,
@@ -132,12 +134,9 @@ Cfg pick_cfg(int64_t M, int64_t N, int64_t K, bool allow_split) {
     c.bn = N <= 64 ? 64 : 128;
     const int64_t t = tiles(c.bm, c.bn);
     const int64_t ksteps = (K + 31) / 32;
-    // register-staged weight-grad tiles (1x1 with 128 channels): 512 blocks; the LDS-DMA im2col
-    // weight-grad kernel re-derives its split for DPE_WGRAD_DMA_BLOCKS (run_igemm)
-    static const int64_t target_blocks = [] {
-      const char* e = getenv("DPE_WGRAD_BLOCKS");
-      return (int64_t)(e ? std::max(64, atoi(e)) : 512);
-    }();
+    // register-staged weight-grad tiles (1x1 with 128 channels): 512 blocks (768 / 1024 / 1536 measured
+    // worse, docs/perf_notes.md); the LDS-DMA im2col weight-grad kernel re-derives its split (run_igemm)
+    constexpr int64_t target_blocks = 512;
     int64_t splits = std::max<int64_t>(1, std::min<int64_t>((target_blocks + t - 1) / t, ksteps / 8));
     const int64_t kps = (ksteps + splits - 1) / splits;
     c.k_split = (int)(kps * 32);
@@ -168,29 +167,20 @@ bool igemm_dma_on() {
   return on;
 }
 
+// DPE_WGRAD_DMA=0: im2col weight grads on the register-staged kernel (documented fallback)
 bool wgrad_dma_on() {
   static const bool on = [] { const char* e = getenv("DPE_WGRAD_DMA"); return !(e && e[0] == '0'); }();
   return on;
 }
-int g_wgrad_wide = [] { const char* e = getenv("DPE_WGRAD_WIDE"); return !(e && e[0] == '0'); }();  // 64x256 wgrad tile
-
-// DPE_WGRAD_DMA=2: dense 1x1 weight grads on the LDS-DMA kernel too (measured 10-15 % slower; A/B only)
-bool wgrad_dma_dense() {
-  static const bool on = [] { const char* e = getenv("DPE_WGRAD_DMA"); return e && e[0] == '2'; }();
-  return on;
-}
+// 64x256 weight-grad tile: 1 = for the C <= 16 stem, 2 = also for C > 16 (test hook set_wgrad_wide;
+// measured slower there: 388 -> 512 us on the 64->64 3x3), 0 = never
+int g_wgrad_wide = 1;
 
 // Tile of the LDS-DMA conv kernel: 0 auto, 1 128-tile (pick_cfg), 2 256x128, 3 256x256
 // (8 waves; only where pick_cfg chose a 128-row tile, so BN partial layouts never change).
-// DPE_DMA_TILE=128|256x128|256x256 or set_conv_tile().
-int g_dma_tile = -1;
-int dma_tile_mode() {
-  if (g_dma_tile < 0) {
-    const char* e = getenv("DPE_DMA_TILE");
-    g_dma_tile = !e ? 0 : !strcmp(e, "128") ? 1 : !strcmp(e, "256x128") ? 2 : !strcmp(e, "256x256") ? 3 : 0;
-  }
-  return g_dma_tile;
-}
+// Forced tiles are a test hook (set_conv_tile): every one is numerics-tested, only "auto" is timed.
+int g_dma_tile = 0;
+int dma_tile_mode() { return g_dma_tile; }
 
 void dma_tile(const dpe::IgemmArgs& a, int aload, int bload, int& bm, int& bn) {
   if (bm != 128 || bload != dpe::B_DENSE_K) return;
@@ -219,9 +209,9 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
   a.k_split = c.k_split;
   // weight grads over an im2col B (3x3 / strided; split-K fp32 atomics): LDS-DMA kernel, measured 1.3-1.5x
   // faster (scripts/bench_convs.py); on the dense 1x1 ones it measured 10-15 % slower, so those stay
-  // register-staged (DPE_WGRAD_DMA=0: all register-staged, 2: dense 1x1 too)
+  // register-staged (DPE_WGRAD_DMA=0: all register-staged)
   if (conv && epi == dpe::EPI_ATOMIC_F32 && aload == dpe::A_DENSE_M &&
-      ((igemm_dma_on() && wgrad_dma_on() && (bload == dpe::B_CONV_WGRAD || (bload == dpe::B_DENSE_N && wgrad_dma_dense()))) ||
+      ((igemm_dma_on() && wgrad_dma_on() && bload == dpe::B_CONV_WGRAD) ||
        (bload == dpe::B_DENSE_N && a.b_coef))) {
     int bm = c.bm, bn = c.bn, splits = c.splits;
     {
@@ -229,10 +219,7 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
       // (profiles/wgrad_blocks_ab_r2.txt, all split-K weight grads at one target): 256 -8 %, 384 -2.4 %,
       // 512 0, 768 +1.4-1.8 %, 1024 -0.5 %, 1536 -0.5 %, 2048 -1 %; 704-768 best of 640-896.  The
       // register-staged 1x1 tiles measured best at 512 and keep pick_cfg's split.
-      static const int64_t dma_target = [] {
-        const char* e = getenv("DPE_WGRAD_DMA_BLOCKS");
-        return (int64_t)(e ? std::max(64, atoi(e)) : 768);
-      }();
+      constexpr int64_t dma_target = 768;
       const int64_t t = (int64_t)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn), ksteps = (a.K + 31) / 32;
       const int64_t sp = std::max<int64_t>(1, std::min<int64_t>((dma_target + t - 1) / t, ksteps / 8));
       const int64_t kps = (ksteps + sp - 1) / sp;
@@ -266,8 +253,8 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
   //   N >= 1024 measured 2-10 % slower in round 1).
   // Since the round-2 kernel changes every forward-form role on the LDS-DMA kernel measures +0.2 %
   // on the ResNet-50 step (5 alternating pairs: +0.14 / +0.29 / +0.17 / +0.63 / -0.16 %,
-  // profiles/dma_all_ab_r2.txt), so that is the default; DPE_DMA_ALL=0 restores the role table.
-  static const bool dma_all = [] { const char* e = getenv("DPE_DMA_ALL"); return !(e && e[0] == '0'); }();
+  // profiles/dma_all_ab_r2.txt), so that is the default (the round-1 role table is gone).
+  constexpr bool dma_all = true;
   bool dma_role = false;
   if (aload == dpe::A_CONV_FWD) dma_role = bload == dpe::B_DENSE_K || dma_all;
   else if (aload == dpe::A_DENSE_K && bload == dpe::B_DENSE_K) dma_role = dma_all || a.K >= 128 || a.N >= 256;
@@ -432,7 +419,8 @@ Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const c10::optional<Tenso
 dpe::ConvGeom geom(const Tensor& x, const Tensor& w, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
                    int64_t OH, int64_t OW);
 
-void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha, const c10::optional<Tensor>& alpha_t) {
+void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha, const c10::optional<Tensor>& alpha_t,
+                  const c10::optional<Tensor>& dbias) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(x); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
   const int64_t N = dw.size(0), K = dw.size(1), ldy = dy.size(-1);
   TORCH_CHECK(ldy >= N && x.size(-1) == K && dy.numel() / ldy == x.numel() / K, "linear_wgrad: shape mismatch");
@@ -447,8 +435,20 @@ void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha, c
     a.a_dim = (int)((N + 7) / 8 * 8);
     a.alpha = (float)alpha;
     a.alpha_ptr = alpha_ptr_of(alpha_t);
+    if (dbias.has_value() && dbias->defined()) {
+      // bias gradient from the same launch: row sums of dy^T taken from the A fragments (hgemm BG)
+      CHECK_F32((*dbias)); CHECK_CONTIG((*dbias));
+      TORCH_CHECK(dbias->numel() == N, "linear_wgrad: dbias must have out_features elements");
+      a.dbias = fp(*dbias);
+    }
     dpe_gemm::run(a, 0, 0, dpe::HE_ACC_F32, true, 4);
     return;
+  }
+  if (dbias.has_value() && dbias->defined()) {
+    CHECK_F32((*dbias)); CHECK_CONTIG((*dbias));
+    TORCH_CHECK(dbias->numel() == N, "linear_wgrad: dbias must have out_features elements");
+    TORCH_CHECK(alpha == 1.0 && !alpha_ptr_of(alpha_t), "linear_wgrad: dbias with M % 64 != 0 needs alpha == 1");
+    CHECK_RC(dpe_colsum(dy.data_ptr(), M, (int)N, ldy, fp(*dbias), 1, 1, cur_stream()), "colsum");
   }
   auto a = base_args();
   a.A = bp(dy); a.B = bp(x); a.C = dw.data_ptr();
@@ -1332,7 +1332,7 @@ void register_ops(pybind11::module& m) {
   m.def("linear_dgrad", &linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("residual") = py::none(),
         py::arg("alpha_t") = py::none(), py::arg("gelu_in") = py::none());
   m.def("linear_wgrad", &linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("alpha") = 1.0,
-        py::arg("alpha_t") = py::none());
+        py::arg("alpha_t") = py::none(), py::arg("dbias") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("want_stats") = false, py::arg("bias") = py::none(), py::arg("in_coef") = py::none());
   m.def("row_bn_on_load", [](std::vector<int64_t> xs, std::vector<int64_t> ws, std::vector<int64_t> stride,
@@ -1416,11 +1416,24 @@ void register_ops(pybind11::module& m) {
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
         py::arg("dw"), py::arg("db") = py::none(), py::arg("dx_out") = py::none());
   m.def("set_pw_stream", &set_pw_stream, "streaming pointwise-conv kernel on/off (pwconv.hip)");
-  m.def("cu_hog", [](int64_t nblocks, int64_t threads, int64_t lds_bytes, double us) {
+  m.def("cu_hog", [](int64_t nblocks, int64_t threads, int64_t lds_bytes, double us, int64_t vgprs,
+                     const c10::optional<Tensor>& stop) {
           static Tensor sink = at::empty({1024}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA));
-          CHECK_RC(dpe_cu_hog((int)nblocks, (int)threads, (int)lds_bytes, us, (float*)sink.data_ptr(), cur_stream()), "cu_hog");
+          const unsigned* sp = nullptr;
+          if (stop.has_value() && stop->defined()) {
+            TORCH_CHECK(stop->is_cuda() && stop->scalar_type() == at::kInt && stop->numel() >= 1, "cu_hog: stop is an int32 GPU tensor");
+            sp = (const unsigned*)stop->data_ptr();
+          }
+          CHECK_RC(dpe_cu_hog((int)nblocks, (int)threads, (int)lds_bytes, us, (int)vgprs, sp, (float*)sink.data_ptr(), cur_stream()),
+                   "cu_hog");
         }, py::arg("nblocks"), py::arg("threads") = 256, py::arg("lds_bytes") = 0, py::arg("us") = 1000.0,
-        "occupancy probe: nblocks workgroups holding a CU slot for `us` microseconds (current stream)");
+        py::arg("vgprs") = 8, py::arg("stop") = py::none(),
+        "occupancy probe: nblocks workgroups holding a CU slot (threads, LDS, ~vgprs per lane) until stop[0] != 0 or `us` "
+        "microseconds pass (current stream)");
+  m.def("hog_stop", [](Tensor& stop, int64_t v) {
+          TORCH_CHECK(stop.is_cuda() && stop.scalar_type() == at::kInt, "hog_stop: int32 GPU tensor");
+          CHECK_RC(dpe_hog_stop((unsigned*)stop.data_ptr(), (unsigned)v, cur_stream()), "hog_stop");
+        }, py::arg("stop"), py::arg("value") = 1, "set a cu_hog stop flag, ordered on the current stream");
   m.def("set_row_wgrad", &set_row_wgrad, "64-channel 3x3 weight grads on the row-walking kernel (rowconv.hip) on/off");
   m.def("set_rowconv", &set_rowconv, "64-channel 3x3 convs on the row-walking kernel (rowconv.hip) on/off");
   m.def("set_stem_kernel", &set_stem_kernel, "s2d stem conv on its row-walking kernel (stem.hip) on/off");

@@ -10,12 +10,19 @@
 #include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPGuard.h>
 
+#include <algorithm>
+#include <atomic>
 #include <stdexcept>
 
 #include <pybind11/functional.h>
 
 extern "C" int dpe_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st);
 extern "C" int dpe_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
+
+// persistent-kernel slots to leave free right now (0 unless a collective may be resident)
+extern "C" int dpe_cu_reserve() {
+  return dpe::comm_active_reserve();
+}
 
 namespace dpe {
 
@@ -177,6 +184,23 @@ void Communicator::abort() {
   }
 }
 
+// ------------------------------------------------ CU budget while collectives overlap compute
+// Every RCCL channel is one workgroup resident on a CU for the duration of a collective.  The
+// persistent compute kernels (hgemm, pw_stream) size their grids to exactly the resident capacity and
+// give every block a static share; a foreign workgroup on a CU whose slots they fill displaces one of
+// their blocks into a second wave (x1.45-1.7 measured, profiles/cu_hog_probe_r2.txt).  While the
+// reducer has a bucket all-reduce in flight (first launch of a backward .. finalize) those kernels
+// plan with `reserve` slots fewer (bindings/gemm.cpp plan(), pwconv.hip pw_capacity()).  The
+// reserve is the communicator's channel count (parallel/dist.py).  Host-side state: every rank
+// issues the same launch sequence, so every rank plans the same grids.
+static std::atomic<int> g_cu_reserve{0};
+static std::atomic<int> g_comm_active{0};
+
+void set_comm_active(bool on) { g_comm_active.store(on ? 1 : 0, std::memory_order_relaxed); }
+int comm_active_reserve() {
+  return g_comm_active.load(std::memory_order_relaxed) ? g_cu_reserve.load(std::memory_order_relaxed) : 0;
+}
+
 // ------------------------------------------------ weight-grad side streams
 // Per-device stream that the model's backward writes some gradients on
 // (ops/_state.py run_on_aux); bucket all-reduces wait for it as well.
@@ -286,6 +310,7 @@ void Reducer::launch(int64_t b) {
   hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
   if (!comm_ || (comm_->world() == 1 && !force_)) return;
   hipStream_t cs = comm_->comm_stream().stream();
+  set_comm_active(true);  // compute kernels enqueued from here on may share the CUs with RCCL
   HIP_CHECK(hipEventRecord(ev_ready_[b], cur));
   HIP_CHECK(hipStreamWaitEvent(cs, ev_ready_[b], 0));
   // gradients written on the weight-grad side stream (set_aux_stream) are covered too
@@ -341,6 +366,7 @@ void Reducer::finalize() {
     HIP_CHECK(hipEventRecord(ev_done_, comm_->comm_stream().stream()));
     HIP_CHECK(hipStreamWaitEvent(cur, ev_done_, 0));
   }
+  set_comm_active(false);  // later compute kernels are ordered after the last collective
   step_open_ = false;
 }
 
@@ -365,6 +391,12 @@ void register_comm(pybind11::module& m) {
     TORCH_CHECK(device >= 0 && device < 64, "set_aux_stream: bad device");
     g_aux_streams[device] = (hipStream_t)(uintptr_t)stream;
   }, "register the weight-grad side stream of a device (bucket all-reduces wait for it)");
+  m.def("set_cu_reserve", [](int64_t n) { g_cu_reserve.store((int)std::max<int64_t>(0, n), std::memory_order_relaxed); },
+        py::arg("slots"), "persistent-kernel slots left free while a bucket all-reduce is in flight (0: none)");
+  m.def("cu_reserve_config", []() { return g_cu_reserve.load(std::memory_order_relaxed); });
+  m.def("set_comm_active", &set_comm_active, py::arg("on"),
+        "mark collectives as (not) resident beside compute (the reducer does this itself; probes / tests)");
+  m.def("cu_reserve", []() { return dpe_cu_reserve(); }, "slots the persistent kernels leave free right now");
   m.def("rccl_version", []() {
     int v = 0;
     ncclGetVersion(&v);

@@ -127,6 +127,10 @@ class Reducer {
   void init_tracking(int64_t nparams);
 };
 
+// CU budget: mark collectives resident beside compute; slots persistent kernels leave free now
+void set_comm_active(bool on);
+int comm_active_reserve();
+
 // weight-grad side stream registered for a device (nullptr: none)
 hipStream_t aux_stream(int device);
 

@@ -369,21 +369,43 @@ extern "C" int dpe_embedding_bwd(const int64_t* idx, const float* dout, float* d
   return 0;
 }
 
-// CU-occupancy probe: nblocks workgroups that each hold their CU slot (waves, LDS) for `ticks`
-// of the 100 MHz wall clock and then exit -- a stand-in for RCCL's channel workgroups sharing
-// the CUs with backward kernels (scripts/hog_probe.py).  Every wave leaves after the deadline.
-__global__ void cu_hog_kernel(int64_t ticks, float* sink) {
+// CU-occupancy probe: nblocks workgroups that each hold their CU slot (waves, LDS, ~V VGPRs per lane)
+// until `stop` becomes non-zero or `ticks` of the 100 MHz wall clock pass -- a stand-in for RCCL's
+// channel workgroups sharing the CUs with backward kernels (scripts/hog_probe.py).  Every wave leaves
+// at the deadline, so a stop flag that is never set cannot hang the device.
+template <int V>
+__global__ void cu_hog_kernel(int64_t ticks, const unsigned* stop, float* sink) {
   extern __shared__ float lds[];
   const int64_t t0 = wall_clock64();
-  float acc = 0.f;
+  float r[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) r[i] = (float)(threadIdx.x + i);
   while (wall_clock64() - t0 < ticks) {
 #pragma unroll 1
-    for (int i = 0; i < 64; ++i) acc = acc * 0.999f + 1.f;
+    for (int k = 0; k < 16; ++k)
+#pragma unroll
+      for (int i = 0; i < V; ++i) r[i] = r[i] * 0.999f + 1.f;
+    if (stop && __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
   }
-  if (acc == -1.f) sink[threadIdx.x] = lds[threadIdx.x];  // never true: keeps acc / lds live
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) acc += r[i];
+  if (acc == -1.f) sink[threadIdx.x] = lds[threadIdx.x];  // never true: keeps r / lds live
 }
-extern "C" int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, float* sink, hipStream_t st) {
+// stop flag for cu_hog: one vector (agent-scope atomic) store, ordered on the caller's stream
+__global__ void hog_stop_kernel(unsigned* stop, unsigned v) {
+  __hip_atomic_store(stop, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+extern "C" int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, int vgprs, const unsigned* stop, float* sink,
+                          hipStream_t st) {
   if (nblocks <= 0 || threads <= 0 || threads > 1024 || us <= 0 || us > 1e6) return -1;
-  hipLaunchKernelGGL(cu_hog_kernel, dim3(nblocks), dim3(threads), lds_bytes, st, (int64_t)(us * 100.0), sink);
+  const int64_t t = (int64_t)(us * 100.0);
+  if (vgprs <= 16) hipLaunchKernelGGL(cu_hog_kernel<8>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink);
+  else if (vgprs <= 64) hipLaunchKernelGGL(cu_hog_kernel<56>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink);
+  else hipLaunchKernelGGL(cu_hog_kernel<120>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink);
+  return (int)hipGetLastError();
+}
+extern "C" int dpe_hog_stop(unsigned* stop, unsigned v, hipStream_t st) {
+  hipLaunchKernelGGL(hog_stop_kernel, dim3(1), dim3(1), 0, st, stop, v);
   return (int)hipGetLastError();
 }

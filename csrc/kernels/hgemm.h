@@ -34,6 +34,8 @@ struct HgemmArgs {
   int group_m;              // tile rows per grouped-order band (L2 reuse per XCD); <= 0: row-major
   int a_dim, b_dim;         // load extents of A's M / B's N (>= M / N; 0 = M / N): loads may read the
                             // zero-padded columns of a padded operand, stores stay inside M x N
+  float* dbias;             // TN weight grads only: db[m] += alpha * sum_k A[k][m] (the bias gradient)
+  float* ws_bias;           // dbias with splits > 1: [splits][M] partial row sums (summed by hgemm_finalize)
 };
 
 // Tile configurations (BMxBN, waves WRxWC).

@@ -153,7 +153,11 @@ DPE_DEVICE float gelu_grad(float x) {
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
 }
 
-template <int BM, int BN, int WR, int WC, bool AK, bool BK, int EPI, int ACT>
+// BG (TN weight grads, A = dy^T M-contiguous): the same launch also produces the bias gradient
+// db[m] += alpha * sum_k A[k][m] -- the units of the first tile column sum the A fragments they
+// already hold in registers (wave wc takes fragment row-block wc, v_dot2 with ones: 8 VALU per half
+// image per K-tile), so dy is not streamed a second time by a column-sum kernel.
+template <int BM, int BN, int WR, int WC, bool AK, bool BK, int EPI, int ACT, bool BG = false>
 __global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
   using G = Geo<BM, BN, WR, WC>;
   constexpr int NW = G::NW, RH = G::RH, CH = G::CH, FMH = G::FMH, FNH = G::FNH, GA = G::GA, GB = G::GB;
@@ -244,6 +248,23 @@ __global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
 
   f32x4 acc[2 * FMH][2 * FNH];
   bf16x8 af[FMH][2], bfr[FNH][2];
+  static_assert(!BG || (!AK && FMH == WC), "bias-grad fusion: M-contiguous A, one fragment row-block per wave column");
+  float rsum[2] = {0.f, 0.f};  // BG: this lane's partial row sums (rows of half images 0 / 1)
+  bool bg_on = false;
+  const bf16x2_t ones2 = {(__bf16)1.f, (__bf16)1.f};
+#define BG_SUM(hh)                                                                           \
+  do {                                                                                       \
+    if (BG && bg_on) {                                                                       \
+      _Pragma("unroll") for (int i_ = 0; i_ < FMH; ++i_)                                     \
+        if (i_ == wc) {                                                                      \
+          _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_) {                                 \
+            const u32x4 q_ = __builtin_bit_cast(u32x4, af[i_][s_]);                          \
+            _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_)                                 \
+              rsum[hh] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, q_[e_]), ones2, rsum[hh], false); \
+          }                                                                                  \
+        }                                                                                    \
+    }                                                                                        \
+  } while (0)
 
 #define LOAD_A(buf, h)                                                                       \
   do {                                                                                       \
@@ -288,6 +309,10 @@ __global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
     for (int i = 0; i < 2 * FMH; ++i)
 #pragma unroll
       for (int j = 0; j < 2 * FNH; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (BG) {
+      bg_on = p.dbias != nullptr && n0 == 0;  // one tile column carries the row sums
+      rsum[0] = rsum[1] = 0.f;
+    }
     if (late) HG_BARRIER();
 
 #if HG_SCHED == 1
@@ -313,6 +338,7 @@ __global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       HG_BARRIER();
       MFMAQ(0, 1);
+      BG_SUM(0);  // A half 0 fragments: last used by this phase's MFMAs
       HG_BARRIER();
 
       LOAD_A(b, 1);
@@ -332,6 +358,7 @@ __global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       HG_BARRIER();
       MFMAQ(1, 0);
+      BG_SUM(1);  // A half 1 fragments
       HG_BARRIER();
     }
 #else
@@ -380,6 +407,23 @@ __global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
     const int rbase = m0 + wr * (BM / WR) + lm, cbase = n0 + wc * (BN / WC) + ln4;
     const int next = u + gridDim.x;
     const int cur_split = split;
+
+    // 0) bias gradient: the 4 lane groups hold k-slices of the same 16 rows
+    if constexpr (BG) {
+      if (bg_on) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          float v = rsum[hh];
+          v += __shfl_xor(v, 16, 64);
+          v += __shfl_xor(v, 32, 64);
+          const int row = m0 + wr * (BM / WR) + hh * RH + wc * 16 + lm;
+          if (lane < 16 && row < p.M) {
+            if (p.splits > 1) p.ws_bias[(int64_t)cur_split * p.M + row] = v;  // summed in split order by finalize
+            else p.dbias[row] += alpha * v;                                   // the row's only writer
+          }
+        }
+      }
+    }
 
     // 1) math (every global load of the epilogue happens here, before any DMA is in flight)
     u32x2 pk[2 * FMH][2 * FNH];
@@ -514,6 +558,7 @@ __global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
 #undef LOAD_B
 #undef QUAD
 #undef MFMAQ
+#undef BG_SUM
 }
 
 // sum of K-split partial slabs -> the real epilogue; one thread per 4 output columns
@@ -529,6 +574,11 @@ __global__ __launch_bounds__(256) void hgemm_finalize_kernel(HgemmArgs p) {
   for (int k = 1; k < p.splits; ++k) s += *(const f32x4*)(p.ws + k * plane + (int64_t)r * p.N + c);
   s *= alpha;
   if (p.bias) s += *(const f32x4*)(p.bias + c);
+  if (p.dbias && c == 0) {  // fused bias gradient: the units' partial row sums, in split order
+    float b = 0.f;
+    for (int k = 0; k < p.splits; ++k) b += p.ws_bias[(int64_t)k * p.M + r];
+    p.dbias[r] += alpha * b;
+  }
   const int64_t o = (int64_t)r * p.ldc + c;
   if constexpr (EPI == HE_BF16) {
     float v[4] = {s[0], s[1], s[2], s[3]};
@@ -565,6 +615,17 @@ namespace {
 template <int BM, int BN, int WR, int WC, bool AK, bool BK>
 int launch_epi(const HgemmArgs& p, int epi, int grid, hipStream_t st) {
   const dim3 g((unsigned)grid), b(WR * WC * 64);
+  if (p.dbias) {  // fused bias gradient: TN weight grads (raw slabs or fp32 accumulate) only
+    if constexpr (!AK && !BK && BM == 256 && BN == 256) {
+      if (p.act != ACT_NONE || (p.splits > 1 && !p.ws_bias)) return -3;
+      if (epi == HE_SLAB) hipLaunchKernelGGL((hg::hgemm_kernel<BM, BN, WR, WC, AK, BK, HE_SLAB, ACT_NONE, true>), g, b, 0, st, p);
+      else if (epi == HE_ACC_F32) hipLaunchKernelGGL((hg::hgemm_kernel<BM, BN, WR, WC, AK, BK, HE_ACC_F32, ACT_NONE, true>), g, b, 0, st, p);
+      else return -3;
+      return 0;
+    } else {
+      return -5;
+    }
+  }
 #define HL(E, A) hipLaunchKernelGGL((hg::hgemm_kernel<BM, BN, WR, WC, AK, BK, E, A>), g, b, 0, st, p)
   if (epi == HE_SLAB) {  // raw partials: the activation belongs to hgemm_finalize
     HL(HE_SLAB, ACT_NONE);

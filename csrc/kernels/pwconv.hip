@@ -337,6 +337,8 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
 
 using namespace dpe;
 
+extern "C" int dpe_cu_reserve();  // comm.cpp
+
 static int pw_wn(int K) { return K <= 128 ? 64 : 32; }
 
 // Every block carries the same number of tiles, so the grid must be exactly the resident
@@ -366,7 +368,8 @@ extern "C" int dpe_pw_rowgroups(int64_t M, int64_t N, int64_t K, int epi) {
   if (M * K * 2 >= (1ll << 31) - 4096 || M * N >= (1ll << 31)) return 0;
   const int64_t tiles = (M + pw::BM - 1) / pw::BM;
   const int64_t nbN = N / bnb;
-  const int cap = epi == PW_FWD ? pw_capacity<PW_FWD>((int)K) : pw_capacity<PW_DGRAD>((int)K);
+  // resident capacity minus the slots left to in-flight RCCL channel blocks (comm.cpp CU budget)
+  const int cap = (epi == PW_FWD ? pw_capacity<PW_FWD>((int)K) : pw_capacity<PW_DGRAD>((int)K)) - dpe_cu_reserve();
   int64_t rg = cap / nbN;  // one resident wave of blocks over the whole launch
   if (rg < 1) rg = 1;
   if (rg > tiles) rg = tiles;

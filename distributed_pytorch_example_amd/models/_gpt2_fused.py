@@ -15,7 +15,7 @@ forward  (x fp32 residual stream [B, T, D])
     h2 = LN2(x2) ; v = h2 W_fc^T + b ; u = gelu(v)   one GEMM: u and v from its epilogue
     y  = x2 + u W_p^T + b           fp32
 backward (g = dL/dy fp32, gb its bf16 copy)
-    dW_p += gb^T u ; db_p += colsum(gb) ; dv = gelu'(v) (gb W_p)   (GELU' in the GEMM epilogue)
+    dW_p += gb^T u , db_p += colsum(gb) (one launch) ; dv = gelu'(v) (gb W_p)   (GELU' in the GEMM epilogue)
     dW_fc += dv^T h2 ; db_fc ; dh2 = dv W_fc
     g2, g2b = g + LN2'(dh2)         one kernel: fp32 stream grad + bf16 copy
     dW_o += g2b^T a ; db_o ; da = g2b W_o ; dqkv = attn'(da)
@@ -110,13 +110,12 @@ class BlockFn(Function):
             grads[id(p)] = None if direct else buf
 
         def linear_bwd(lin, dyb, inp, want_dx=True, gelu_in=None):
-            """dW += dyb^T inp ; db += colsum(dyb) ; return dyb W (bf16), times gelu'(gelu_in) if given."""
+            """dW += dyb^T inp and db += colsum(dyb) in one GEMM launch ; return dyb W (bf16), times gelu'(gelu_in) if given."""
             buf, d = sink(lin.weight)
-            C.linear_wgrad(dyb, inp, buf, 1.0)
+            bb, bd = sink(lin.bias) if lin.bias is not None else (None, False)
+            C.linear_wgrad(dyb, inp, buf, 1.0, None, bb)  # bias grad from the same launch (row sums of dy^T)
             done(lin.weight, buf, d)
             if lin.bias is not None:
-                bb, bd = sink(lin.bias)
-                C.colsum(dyb, bb, True)
                 done(lin.bias, bb, bd)
             return C.linear_dgrad(dyb, shadow(lin.weight), None, None, gelu_in) if want_dx else None
 

@@ -107,9 +107,10 @@ def note_use(p: torch.Tensor) -> None:
 # is written either on the main stream or on this one; the reducers make the
 # RCCL stream wait on both before a bucket is reduced, and the end of backward
 # joins the side stream back into the main one (autograd engine callback).
-# Opt-in (DPE_WGRAD_STREAM=1): measured 2 % SLOWER on ResNet-50 / MI355X at batch 512
-# (46.6 vs 47.6 ms/step): the concurrent kernels contend more than they overlap.
-_WGRAD_STREAM_ON = __import__("os").environ.get("DPE_WGRAD_STREAM", "0") == "1"
+# Off: measured 2 % SLOWER on ResNet-50 / MI355X at batch 512 (46.6 vs 47.6 ms/step): the
+# concurrent kernels contend more than they overlap.  set_wgrad_stream(True) keeps the path
+# testable (tests/test_comm_gpu.py: the reducer waits on this stream too).
+_WGRAD_STREAM_ON = False
 
 
 def set_wgrad_stream(on: bool) -> bool:

@@ -665,12 +665,11 @@ class _LinearResidualFn(Function):
         dyb = dy.to(torch.bfloat16).contiguous()
         da = C.linear_dgrad(dyb, shadow(weight)) if ctx.needs_input_grad[0] else None
         buf, direct = grad_sink(weight)
-        C.linear_wgrad(dyb, ab, buf, 1.0)
+        bb, bd = grad_sink(bias) if bias is not None else (None, False)
+        C.linear_wgrad(dyb, ab, buf, 1.0, None, bb)  # bias grad: row sums of dy^T in the same launch
         grad_done(weight, direct)
         gb = None
         if bias is not None:
-            bb, bd = grad_sink(bias)
-            C.colsum(dy.contiguous(), bb, True)
             grad_done(bias, bd)
             gb = None if bd else bb
         return da, (None if direct else buf), gb, dy

@@ -57,6 +57,8 @@ def init_process_group(backend: str = "auto", timeout_s: float = 1800.0,
     backend = resolve_backend(backend)
     if comm_max_channels is None and os.environ.get("DPE_RCCL_MAX_CHANNELS"):
         comm_max_channels = int(os.environ["DPE_RCCL_MAX_CHANNELS"])
+    if comm_max_channels is None and backend == "rccl" and env.world_size > 1 and "NCCL_MAX_NCHANNELS" not in os.environ:
+        comm_max_channels = DEFAULT_MAX_CHANNELS
     if comm_max_channels:
         n = max(1, int(comm_max_channels))
         os.environ["NCCL_MAX_NCHANNELS"] = str(n)
@@ -72,9 +74,38 @@ def init_process_group(backend: str = "auto", timeout_s: float = 1800.0,
         torch.cuda.set_device(local_rank)
         _state["device"] = torch.device("cuda", local_rank)
         _state["comm"] = _make_comm(rank, world, local_rank)
+        set_cu_budget(cu_reserve_for(world, _state["max_channels"]))
     else:
         _state["device"] = torch.device("cpu")
     return rank, world, local_rank
+
+
+# RCCL channel cap at world > 1 (each channel = one workgroup resident on a CU while a bucket
+# all-reduce overlaps backward).  Bandwidth model behind 16: ResNet-50's 102 MB / GPT-2's 498 MB fp32
+# gradients need 2*7/8 of that per GPU over the ~25 / ~9 ms backward, i.e. < 100 GB/s of bus bandwidth
+# to stay hidden -- far below what 16 xGMI channels move -- while 16 blocks are 1.6-6 % of the
+# persistent kernels' slots (the compute side plans around them: cu_reserve_for).  A model, not a
+# measurement: no 8-GPU node was available to sweep it (bench.py --comm-max-channels does).
+DEFAULT_MAX_CHANNELS = 16
+
+
+def cu_reserve_for(world: int, channels: Optional[int]) -> int:
+    """Persistent-kernel slots left free while a bucket all-reduce is in flight: one per RCCL channel
+    block (a 256-thread RCCL workgroup displaces at most one block of ours per CU; measured footprint
+    in profiles/rccl_footprint_r3.txt).  ``DPE_CU_RESERVE`` overrides; 0 at world 1."""
+    if os.environ.get("DPE_CU_RESERVE"):
+        return max(0, int(os.environ["DPE_CU_RESERVE"]))
+    if world <= 1:
+        return 0
+    return int(channels) if channels else 32
+
+
+def set_cu_budget(slots: int) -> None:
+    """Slots the persistent compute kernels (hgemm, streaming pointwise convs) leave to RCCL while the
+    reducer has a collective in flight (csrc/comm/comm.cpp, CU budget)."""
+    from ..ops._ext import ext
+
+    ext().set_cu_reserve(int(slots))
 
 
 def _make_comm(rank: int, world: int, local_rank: int):
@@ -184,13 +215,33 @@ class Watchdog:
         self._stop = threading.Event()
         self._paused = 0
         self._grace = 0.0
+        self._pending: list = []  # (event, host time) of beats whose device work has not completed
+        self._lock = threading.Lock()
         self._on_fail = on_fail
         self.failure: Optional[str] = None
         self._thread = threading.Thread(target=self._run, name="dpe-watchdog", daemon=True)
         self._thread.start()
 
     def beat(self) -> None:
-        self._last = self._time.monotonic()
+        """A step finished on the host.  On a GPU job progress is what the DEVICE completes: the beat
+        records an event on the current stream and the heartbeat advances only when that event has
+        completed -- the host enqueues steps far ahead of a device that is stuck in a collective
+        whose peer died, so host-side beats alone would hide the stall until the next sync."""
+        now = self._time.monotonic()
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            ev = torch.cuda.Event()
+            ev.record()
+            with self._lock:
+                if len(self._pending) < 64:  # bounded: the oldest pending event is the one that matters
+                    self._pending.append((ev, now))
+            return
+        self._last = now
+
+    def _device_progress(self) -> None:
+        with self._lock:
+            while self._pending and self._pending[0][0].query():
+                self._pending.pop(0)
+                self._last = self._time.monotonic()
 
     def suspended(self):
         """Context: no stall check inside (checkpoint writes, the barrier behind them); RCCL async
@@ -231,22 +282,38 @@ class Watchdog:
         self._thread.join(timeout=5)
 
     def _run(self):
+        import threading
+
         while not self._stop.wait(self.interval_s):
             err = check_health()
+            self._device_progress()
             stalled = 0.0 if self._paused else self._time.monotonic() - self._last
             if err or stalled > self.timeout_s + self._grace:
                 self.failure = f"RCCL async error: {err}" if err else f"no progress for {stalled:.0f}s"
                 log.error(f"watchdog: {self.failure}; aborting communicator")
                 c = _state["comm"]
                 if c is not None:
-                    try:
-                        c.abort()
-                    except Exception:  # noqa: BLE001
-                        pass
+                    # ncclCommAbort releases ranks blocked in collectives; bounded, so an abort that
+                    # itself blocks cannot turn the failure into a hang
+                    t = threading.Thread(target=_try_abort, args=(c,), daemon=True)
+                    t.start()
+                    t.join(timeout=10.0)
                 if self._on_fail is not None:
                     self._on_fail(self.failure)
                     return
+                for h in log.handlers + __import__("logging").getLogger().handlers:
+                    try:
+                        h.flush()
+                    except Exception:  # noqa: BLE001
+                        pass
                 os._exit(1)
+
+
+def _try_abort(c) -> None:
+    try:
+        c.abort()
+    except Exception:  # noqa: BLE001
+        pass
 
 
 def start_watchdog(timeout_s: float = 600.0, interval_s: float = 2.0, on_fail=None) -> Watchdog:

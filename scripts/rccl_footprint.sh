@@ -20,17 +20,18 @@ f=$(find $R/gpurun_out/fp_trace -name "*kernel_trace.csv" | head -1)
 python3 - "$f" <<'EOF'
 import csv, sys, collections
 rows = list(csv.DictReader(open(sys.argv[1])))
-keys = ["Workgroup_Size", "Grid_Size", "LDS_Block_Size", "Arch_VGPR_Count", "Accum_VGPR_Count", "SGPR_Count", "Scratch_Size"]
+first = None
 seen = collections.OrderedDict()
 for r in rows:
     n = r["Kernel_Name"]
     if "nccl" in n.lower() or "rccl" in n.lower():
-        k = (n[:90],) + tuple(r.get(c, "?") for c in keys)
+        first = first or r
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        seen.setdefault(k, []).append(d)
-print("kernel | " + " | ".join(keys) + " | calls | median us")
-for k, ds in seen.items():
+        seen.setdefault(n[:90], []).append(d)
+if first:
+    print({k: v for k, v in first.items() if "Timestamp" not in k and "Id" not in k})
+for n, ds in seen.items():
     ds.sort()
-    print(" | ".join(k) + f" | {len(ds)} | {ds[len(ds) // 2]:.1f}")
+    print(f"{n} | calls {len(ds)} | median {ds[len(ds) // 2]:.1f} us")
 EOF
 rm -f $f

@@ -28,8 +28,7 @@ def _port():
     return p
 
 
-@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
-def test_native_reducer_world2_rccl():
+def _run_world2(args, extra_env=None, timeout=100):
     port = _port()
     procs = []
     for r in range(2):
@@ -39,18 +38,57 @@ def test_native_reducer_world2_rccl():
                     "NCCL_HOSTID": f"dpe-test-host-{r}", "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1",
                     "HSA_ENABLE_IPC_MODE_LEGACY": "0", "OMP_NUM_THREADS": "1",
                     "DPE_RCCL_MAX_CHANNELS": "4"})  # the CU cap for overlapped collectives, exercised
-        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "_rccl_world2_worker.py")],
-                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+        env.update(extra_env or {})
+        procs.append(subprocess.Popen([sys.executable, "-u", *args], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
     outs = []
     try:
         for p in procs:
-            outs.append(p.communicate(timeout=100)[0])
+            outs.append(p.communicate(timeout=timeout)[0])
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    codes = [p.returncode for p in procs]
+    return [p.returncode for p in procs], outs
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_native_reducer_world2_rccl():
+    codes, outs = _run_world2([os.path.join(ROOT, "tests", "_rccl_world2_worker.py")])
     assert codes == [0, 0], "\n".join(o[-3000:] for o in outs)
     assert all("ok: world-2 RCCL reducer" in o for o in outs)
     for o in outs:
         print([ln for ln in o.splitlines() if "ok: world-2" in ln][0])
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_native_reducer_world2_rccl_gpt2():
+    """The transformer path at world 2: tied wte written by two kernels, fused bias grads, rebuild,
+    no_sync (tests/_rccl_world2_worker.py main_gpt2)."""
+    codes, outs = _run_world2([os.path.join(ROOT, "tests", "_rccl_world2_worker.py"), "gpt2"])
+    assert codes == [0, 0], "\n".join(o[-3000:] for o in outs)
+    for o in outs:
+        print([ln for ln in o.splitlines() if "ok: world-2" in ln][0])
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_rank_death_mid_allreduce_aborts_survivor(tmp_path):
+    """Failure detection on the real RCCL path: rank 1 SIGKILLs itself at batch 3 of
+    epoch 0 (DPE_FAULT_INJECT) while rank 0 keeps issuing bucket all-reduces that can never complete.
+    Rank 0's watchdog (device-progress heartbeat + ncclCommGetAsyncError) must ncclCommAbort and exit
+    non-zero within its timeout instead of hanging; the launcher-level fail-fast is tested on gloo
+    (test_distributed_cpu.py::test_fault_injection_fails_fast)."""
+    import time
+
+    t0 = time.time()
+    codes, outs = _run_world2([os.path.join(ROOT, "train.py"), "--backend", "rccl", "--model", "resnet_tiny",
+                               "--image-size", "32", "--batch-size", "8", "--num-samples", "2048", "--epochs", "2",
+                               "--checkpoint-dir", str(tmp_path), "--watchdog-timeout", "15"],
+                              extra_env={"DPE_FAULT_INJECT": "1:0:3:kill"}, timeout=110)
+    dt = time.time() - t0
+    assert codes[1] == -9, outs[1][-2000:]                     # the injected death
+    assert codes[0] == 1, (codes, outs[0][-3000:])             # the survivor aborted, non-zero
+    assert "watchdog:" in outs[0] and "aborting communicator" in outs[0], outs[0][-3000:]
+    assert dt < 100, dt
+    print(f"survivor exited rc={codes[0]} after {dt:.1f}s: "
+          f"{[ln for ln in outs[0].splitlines() if 'watchdog:' in ln][0][-160:]}")

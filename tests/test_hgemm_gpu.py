@@ -102,3 +102,68 @@ def test_hgemm_plan_is_deterministic():
     a = [C.hgemm_plan(8192, n, k, True, True, True, 2) for n, k in ((2304, 768), (768, 3072), (50304, 768))]
     b = [C.hgemm_plan(8192, n, k, True, True, True, 2) for n, k in ((2304, 768), (768, 3072), (50304, 768))]
     assert a == b
+
+
+@pytest.mark.parametrize("splits", [1, 3, -1])
+def test_hgemm_tn_fused_bias_grad(splits):
+    """TN weight grad with the bias gradient from the same launch (hgemm BG: row sums of the A
+    fragments of the first tile column), raw and K-split (partials summed in split order by the
+    finalize), accumulated into existing fp32 buffers with alpha."""
+    C = ext()
+    g = torch.Generator(device=DEV).manual_seed(4)
+    M, N, K = 520, 776, 64 * 13  # M / N tails, uneven split
+    A, B, lda, ldb, ak, bk, ref = _ops(M, N, K, "tn", g)
+    acc = torch.randn(M, N, device=DEV, generator=g)
+    db0 = torch.randn(M, device=DEV, generator=g)
+    out, db = acc.clone(), db0.clone()
+    C.hgemm(A, B, out, M, N, K, lda, ldb, N, ak, bk, 2, 0, None, None, None, None, 0.5, 0, splits, 0, db)
+    torch.cuda.synchronize()
+    want = acc + 0.5 * ref
+    assert ((out - want).norm() / want.norm()).item() < 1e-5
+    dbw = db0 + 0.5 * A.float().sum(0)
+    assert ((db - dbw).norm() / dbw.norm()).item() < 1e-6, splits
+    # deterministic: the same launch twice gives the same bits
+    out2, db2 = acc.clone(), db0.clone()
+    C.hgemm(A, B, out2, M, N, K, lda, ldb, N, ak, bk, 2, 0, None, None, None, None, 0.5, 0, splits, 0, db2)
+    assert torch.equal(out, out2) and torch.equal(db, db2)
+
+
+def test_linear_wgrad_fused_bias_matches_colsum():
+    """linear_wgrad(dbias=...) (GPT-2 shapes: tokens % 64 == 0 -> hgemm BG) equals the separate
+    column-sum kernel it replaced, and the split the planner picks for 8192 tokens is exercised."""
+    C = ext()
+    g = torch.Generator(device=DEV).manual_seed(5)
+    T, fin, fout = 8192, 768, 2304
+    dy = torch.randn(T, fout, device=DEV, generator=g).bfloat16()
+    x = torch.randn(T, fin, device=DEV, generator=g).bfloat16()
+    dw, db = torch.zeros(fout, fin, device=DEV), torch.zeros(fout, device=DEV)
+    C.linear_wgrad(dy, x, dw, 1.0, None, db)
+    dbr = torch.zeros(fout, device=DEV)
+    C.colsum(dy, dbr, True)
+    torch.cuda.synchronize()
+    assert ((db - dbr).norm() / dbr.norm()).item() < 1e-5
+    ref = dy.float().t() @ x.float()
+    assert ((dw - ref).norm() / ref.norm()).item() < 1e-5
+
+
+def test_hgemm_plan_cu_budget():
+    """While a collective is marked in flight the planner leaves `reserve` slots free (grid <= CUs *
+    blocks per CU - reserve) and plans identically for identical state; idle: the full grid."""
+    C = ext()
+    shapes = [(8192, 2304, 768, True, True), (2304, 768, 8192, False, False), (8192, 768, 3072, True, False)]
+    free = [C.hgemm_plan(M, N, K, ak, bk, True, 2) for M, N, K, ak, bk in shapes]
+    C.set_cu_reserve(16)
+    try:
+        assert C.cu_reserve() == 0  # reserve applies only while comm is active
+        assert [C.hgemm_plan(M, N, K, ak, bk, True, 2) for M, N, K, ak, bk in shapes] == free
+        C.set_comm_active(True)
+        assert C.cu_reserve() == 16
+        busy = [C.hgemm_plan(M, N, K, ak, bk, True, 2) for M, N, K, ak, bk in shapes]
+        ncu = torch.cuda.get_device_properties(0).multi_processor_count
+        for (cfg, splits, kps, grid, est), (fcfg, *_rest) in zip(busy, free):
+            bpc = 2 if cfg == 3 else 1
+            assert grid <= ncu * bpc - 16
+        assert busy == [C.hgemm_plan(M, N, K, ak, bk, True, 2) for M, N, K, ak, bk in shapes]
+    finally:
+        C.set_comm_active(False)
+        C.set_cu_reserve(0)

@@ -1,0 +1,220 @@
+"""Full-scale numerical parity of the BASELINE models on the GPU (reference hot loop
+/root/reference/train.py:132-148: forward -> CE -> backward -> optimizer step, repeated).
+
+Full ResNet-50 v1.5 (batch 16 at 224^2, 15 SGD-momentum steps) and full GPT-2-small (batch 2 x 256
+tokens, 15 AdamW steps) on our kernels (bf16 compute, fp32 masters) are trained side by side with a
+plain-PyTorch twin of the same architecture -- identical initial weights, identical data -- whose
+ops are torch's own (F.conv2d / F.batch_norm / F.scaled_dot_product_attention / F.linear / torch
+optimizers), run twice on the same GPU: in fp32 (the oracle) and under torch.autocast(bfloat16).
+
+The bound is derived, not guessed: our per-step loss may deviate from the fp32 oracle by no more than
+2 % relative AND by no more than a small multiple of what PyTorch's own bf16 autocast deviates
+(+ an absolute floor); the final weights' distance to the oracle, relative to the oracle's own
+update, is bounded the same way.  Both tests print their curves.
+"""
+import copy
+import math
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from distributed_pytorch_example_amd.models import get_model  # noqa: E402
+from distributed_pytorch_example_amd.ops import functional as Fx  # noqa: E402
+from distributed_pytorch_example_amd.optim import SGD, AdamW  # noqa: E402
+
+DEV = torch.device("cuda")
+
+
+def _no_tf32():
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+
+
+# ----------------------------------------------------------------------------- ResNet-50 twin
+class _TConvBN(nn.Module):
+    def __init__(self, cb):
+        super().__init__()
+        c = cb.conv
+        self.conv = nn.Conv2d(c.in_channels, c.out_channels, c.kernel_size, c.stride, c.padding, bias=False)
+        self.bn = nn.BatchNorm2d(c.out_channels, eps=cb.bn.eps, momentum=cb.bn.momentum)
+        with torch.no_grad():
+            self.conv.weight.copy_(c.weight.detach().permute(0, 3, 1, 2))  # OHWI -> OIHW
+            self.bn.weight.copy_(cb.bn.weight.detach())
+            self.bn.bias.copy_(cb.bn.bias.detach())
+
+    def forward(self, x):
+        return self.bn(self.conv(x))
+
+
+class _TBottleneck(nn.Module):
+    def __init__(self, blk):
+        super().__init__()
+        self.c1, self.c2, self.c3 = _TConvBN(blk.c1), _TConvBN(blk.c2), _TConvBN(blk.c3)
+        self.down = _TConvBN(blk.down) if blk.down is not None else None
+
+    def forward(self, x):
+        idn = self.down(x) if self.down is not None else x
+        h = F.relu(self.c1(x))
+        h = F.relu(self.c2(h))
+        return F.relu(self.c3(h) + idn)
+
+
+class _TResNet(nn.Module):
+    def __init__(self, ours):
+        super().__init__()
+        self.stem = _TConvBN(ours.stem)
+        self.blocks = nn.Sequential(*[_TBottleneck(b) for b in ours.blocks])
+        self.fc = nn.Linear(ours.fc.in_features, ours.fc.out_features)
+        with torch.no_grad():
+            self.fc.weight.copy_(ours.fc.weight.detach())
+            self.fc.bias.copy_(ours.fc.bias.detach())
+
+    def forward(self, x):
+        h = F.max_pool2d(F.relu(self.stem(x)), 3, 2, 1)
+        h = self.blocks(h)
+        return self.fc(torch.flatten(F.adaptive_avg_pool2d(h, 1), 1))
+
+
+def _resnet_flat(m, ours: bool):
+    """Conv / BN / fc parameters in one canonical order, conv filters as OIHW."""
+    out = []
+    mods = [m.stem] + [c for b in m.blocks for c in (b.c1, b.c2, b.c3) + ((b.down,) if b.down is not None else ())]
+    for cb in mods:
+        w = cb.conv.weight.detach().float()
+        out += [w.permute(0, 3, 1, 2) if ours else w, cb.bn.weight.detach().float(), cb.bn.bias.detach().float()]
+    return out + [m.fc.weight.detach().float(), m.fc.bias.detach().float()]
+
+
+def _rel_dist(a, b, ref0):
+    num = sum(((x - y) ** 2).sum() for x, y in zip(a, b)).sqrt()
+    den = sum(((x - y) ** 2).sum() for x, y in zip(b, ref0)).sqrt()
+    return (num / den).item()
+
+
+def _check(name, ours, fp32, bf16, w_ours, w_bf16):
+    d_ours = [abs(a - b) / abs(b) for a, b in zip(ours, fp32)]
+    d_bf16 = [abs(a - b) / abs(b) for a, b in zip(bf16, fp32)]
+    print(f"\n{name}: step | ours (bf16 kernels) | torch fp32 | torch bf16-autocast | rel dev ours / torch-bf16")
+    for i, (a, b, c) in enumerate(zip(ours, fp32, bf16)):
+        print(f"  {i:2d} | {a:.5f} | {b:.5f} | {c:.5f} | {d_ours[i]:.2e} / {d_bf16[i]:.2e}")
+    print(f"  final weights, ||w - w_fp32|| / ||w_fp32 - w0||: ours {w_ours:.3e}, torch bf16 {w_bf16:.3e}")
+    bound = min(0.02, 4 * max(d_bf16) + 2e-3)
+    assert max(d_ours) <= bound, (name, max(d_ours), bound)
+    assert w_ours <= max(2 * w_bf16, 0.05), (name, w_ours, w_bf16)
+
+
+def test_resnet50_full_training_parity():
+    _no_tf32()
+    torch.manual_seed(0)
+    ours = get_model("resnet50").to(DEV)
+    twin = _TResNet(ours).to(DEV)
+    twin_bf = copy.deepcopy(twin)
+    w0 = _resnet_flat(twin, False)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    data = [(torch.randn(16, 3, 224, 224, device=DEV, generator=g), torch.randint(0, 1000, (16,), device=DEV, generator=g))
+            for _ in range(3)]
+    lr, mom, steps = 0.05, 0.9, 15
+    opt_o = SGD(ours.parameters(), lr=lr, momentum=mom)
+    opt_t = torch.optim.SGD(twin.parameters(), lr=lr, momentum=mom)
+    opt_b = torch.optim.SGD(twin_bf.parameters(), lr=lr, momentum=mom)
+    lo, lt, lb = [], [], []
+    for s in range(steps):
+        x, y = data[s % len(data)]
+        loss = Fx.cross_entropy(ours(x), y, 1000)
+        loss.backward()
+        opt_o.step()
+        opt_o.zero_grad()
+        lo.append(loss.item())
+        loss = F.cross_entropy(twin(x), y)
+        loss.backward()
+        opt_t.step()
+        opt_t.zero_grad()
+        lt.append(loss.item())
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(twin_bf(x), y)
+        loss.backward()
+        opt_b.step()
+        opt_b.zero_grad()
+        lb.append(loss.item())
+    assert all(math.isfinite(v) for v in lo) and lo[-1] < lo[0]
+    wt = _resnet_flat(twin, False)
+    _check("ResNet-50 bs16 224^2 SGD", lo, lt, lb, _rel_dist(_resnet_flat(ours, True), wt, w0),
+           _rel_dist(_resnet_flat(twin_bf, False), wt, w0))
+
+
+# ----------------------------------------------------------------------------- GPT-2 twin
+def _gpt2_twin_params(ours):
+    return {n: p.detach().clone().float().requires_grad_(True) for n, p in ours.named_parameters()}
+
+
+def _gpt2_twin_loss(P, cfg, idx, tgt):
+    B, T = idx.shape
+    H, d = cfg.n_head, cfg.n_embd
+    x = P["wte"][idx] + P["wpe"][:T]
+    for i in range(cfg.n_layer):
+        pre = f"h.{i}."
+        h = F.layer_norm(x, (d,), P[pre + "ln_1.weight"], P[pre + "ln_1.bias"], 1e-5)
+        qkv = F.linear(h, P[pre + "c_attn.weight"], P[pre + "c_attn.bias"])
+        q, k, v = qkv.view(B, T, 3, H, d // H).permute(2, 0, 3, 1, 4)
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True).transpose(1, 2).reshape(B, T, d)
+        x = x + F.linear(o, P[pre + "attn_proj.weight"], P[pre + "attn_proj.bias"])
+        h = F.layer_norm(x, (d,), P[pre + "ln_2.weight"], P[pre + "ln_2.bias"], 1e-5)
+        u = F.gelu(F.linear(h, P[pre + "c_fc.weight"], P[pre + "c_fc.bias"]), approximate="tanh")
+        x = x + F.linear(u, P[pre + "mlp_proj.weight"], P[pre + "mlp_proj.bias"])
+    x = F.layer_norm(x, (d,), P["ln_f.weight"], P["ln_f.bias"], 1e-5)
+    logits = F.linear(x, P["wte"])
+    return F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), tgt.reshape(-1))
+
+
+def test_gpt2_small_full_training_parity():
+    _no_tf32()
+    torch.manual_seed(0)
+    ours = get_model("gpt2").to(DEV)
+    with torch.no_grad():  # non-zero biases / LN affine: every parameter's gradient path is live
+        for n, p in ours.named_parameters():
+            if p.dim() == 1:
+                p.add_(torch.randn_like(p) * 0.02)
+    cfg = ours.cfg
+    names = [n for n, _ in ours.named_parameters()]
+    P = _gpt2_twin_params(ours)
+    Pb = _gpt2_twin_params(ours)
+    w0 = [P[n].detach().clone() for n in names]
+    g = torch.Generator(device=DEV).manual_seed(2)
+    T = 256
+    data = [(torch.randint(0, cfg.vocab_size, (2, T), device=DEV, generator=g),
+             torch.randint(0, cfg.vocab_size, (2, T), device=DEV, generator=g)) for _ in range(3)]
+    lr, steps = 3e-4, 15
+    opt_o = AdamW(ours.parameters(), lr=lr, weight_decay=0.0)
+    opt_t = torch.optim.AdamW([P[n] for n in names], lr=lr, weight_decay=0.0)
+    opt_b = torch.optim.AdamW([Pb[n] for n in names], lr=lr, weight_decay=0.0)
+    lo, lt, lb = [], [], []
+    for s in range(steps):
+        x, y = data[s % len(data)]
+        loss = ours(x, y)
+        loss.backward()
+        opt_o.step()
+        opt_o.zero_grad()
+        lo.append(loss.item())
+        loss = _gpt2_twin_loss(P, cfg, x, y)
+        loss.backward()
+        opt_t.step()
+        opt_t.zero_grad()
+        lt.append(loss.item())
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = _gpt2_twin_loss(Pb, cfg, x, y)
+        loss.backward()
+        opt_b.step()
+        opt_b.zero_grad()
+        lb.append(loss.item())
+    assert all(math.isfinite(v) for v in lo) and lo[-1] < lo[0]
+    wo = [p.detach().float() for p in ours.parameters()]
+    wt = [P[n].detach() for n in names]
+    wb = [Pb[n].detach() for n in names]
+    _check("GPT-2-small bs2 T256 AdamW", lo, lt, lb, _rel_dist(wo, wt, w0), _rel_dist(wb, wt, w0))
