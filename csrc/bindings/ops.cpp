@@ -89,6 +89,7 @@ int dpe_optim_step(int kind, const void* desc, const void* chunks, int nchunks, 
 int dpe_layernorm_fwd(const void* x, int x_bf16, const float* w, const float* b, uint16_t* y, float* mean, float* rstd,
                       int64_t rows, int D, float eps, hipStream_t st);
 int dpe_layernorm_bwd_nblocks(int64_t rows);
+int64_t dpe_layernorm_bwd_scratch(int64_t rows, int D);
 int dpe_layernorm_bwd(const uint16_t* dy, const void* x, int x_bf16, const float* w, const float* mean, const float* rstd,
                       void* dx, int dx_accumulate_f32, const float* res_in, uint16_t* dx_bf16, float* dw, float* db,
                       float* part, int64_t rows, int D, hipStream_t st);
@@ -1269,8 +1270,7 @@ Tensor layernorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const T
   } else {
     dx = at::empty_like(x);
   }
-  const int nb = dpe_layernorm_bwd_nblocks(rows);
-  Tensor part = at::empty({nb, 2, D}, x.options().dtype(at::kFloat));
+  Tensor part = at::empty({dpe_layernorm_bwd_scratch(rows, (int)D)}, x.options().dtype(at::kFloat));
   CHECK_RC(dpe_layernorm_bwd(bp(dy), x.data_ptr(), xb, fp(w), fp(mean), fp(rstd), dx.data_ptr(), acc ? 1 : 0, nullptr,
                              nullptr, fp(dw), fpom(db), fp(part), rows, (int)D, cur_stream()), "layernorm_bwd");
   return dx;
@@ -1289,8 +1289,7 @@ std::vector<Tensor> layernorm_bwd_residual(const Tensor& dy, const Tensor& x, co
   TORCH_CHECK(res_in.numel() == x.numel(), "layernorm_bwd_residual: res_in shape mismatch");
   Tensor dx = at::empty(x.sizes(), x.options().dtype(at::kFloat));
   Tensor dxb = at::empty(x.sizes(), x.options().dtype(at::kBFloat16));
-  const int nb = dpe_layernorm_bwd_nblocks(rows);
-  Tensor part = at::empty({nb, 2, D}, x.options().dtype(at::kFloat));
+  Tensor part = at::empty({dpe_layernorm_bwd_scratch(rows, (int)D)}, x.options().dtype(at::kFloat));
   CHECK_RC(dpe_layernorm_bwd(bp(dy), x.data_ptr(), xb, fp(w), fp(mean), fp(rstd), dx.data_ptr(), 1, fp(res_in), bpm(dxb),
                              fp(dw), fpom(db), fp(part), rows, (int)D, cur_stream()), "layernorm_bwd_residual");
   return {dx, dxb};

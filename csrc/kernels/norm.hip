@@ -73,23 +73,61 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
 }
 
-// D <= 2048: each lane owns at most 4 chunks (32 columns) for the dw/db partials.
-// dy and x of the row are loaded once and kept in registers for both passes.
+// Row sums of the LN backward for D > 2048 (one wave per row, the whole row):
+// rs[2 row] = sum(dy*w) / D, rs[2 row + 1] = sum(dy*w*xhat) / D.
+template <bool XBF>
+__global__ __launch_bounds__(256) void ln_bwd_rowsums_kernel(const uint16_t* __restrict__ dy, const void* __restrict__ x,
+                                                             const float* __restrict__ w, const float* __restrict__ mean_in,
+                                                             const float* __restrict__ rstd_in, float* __restrict__ rs,
+                                                             int64_t rows, int D) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t row = blockIdx.x * 4ll + wid;
+  if (row >= rows) return;
+  const int64_t base = row * D;
+  const float mean = mean_in[row], rstd = rstd_in[row];
+  float sg = 0.f, sgx = 0.f;
+  for (int c = lane; c < (D >> 3); c += 64) {
+    float d[8], f[8];
+    unpack8(*(const u32x4*)(dy + base + c * 8), d);
+    load8<XBF>(x, base + c * 8, f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float g = d[e] * w[c * 8 + e];
+      sg += g;
+      sgx += g * (f[e] - mean) * rstd;
+    }
+  }
+  sg = warp_sum(sg);
+  sgx = warp_sum(sgx);
+  if (lane == 0) {
+    rs[2 * row] = sg / (float)D;
+    rs[2 * row + 1] = sgx / (float)D;
+  }
+}
+
+// Columns [col0, col0 + D) of rows of width Dtot, D <= 2048: each lane owns at most 4 chunks (32 columns)
+// for the dw/db partials; dy and x of the row slice are loaded once and kept in registers for both
+// passes.  rsums == nullptr (D == Dtot): the row sums come from the registers; else from
+// ln_bwd_rowsums_kernel (rows wider than 2048: blockIdx.y walks the column chunks).
 template <bool XBF, int NJ>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict__ dy, const void* __restrict__ x,
                                                      const float* __restrict__ w, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, void* __restrict__ dx, int dx_acc,
                                                      const float* __restrict__ res_in, uint16_t* __restrict__ dx_bf16,
-                                                     float* __restrict__ part, int64_t rows, int D) {
+                                                     float* __restrict__ part, int64_t rows, int D, int Dtot,
+                                                     const float* __restrict__ rsums) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int CH = D >> 3;
+  const int col0 = blockIdx.y * D;  // this block's column slice
+  w += col0;
+  part += col0;
   float pw[NJ][8], pb[NJ][8];
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int e = 0; e < 8; ++e) { pw[j][e] = 0.f; pb[j][e] = 0.f; }
   for (int64_t row = blockIdx.x * 4ll + wid; row < rows; row += (int64_t)gridDim.x * 4) {
-    const int64_t base = row * D;
+    const int64_t base = row * Dtot + col0;
     const float mean = mean_in[row], rstd = rstd_in[row];
     float sg = 0.f, sgx = 0.f;
     float dd[NJ][8], xh[NJ][8];
@@ -111,8 +149,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
         }
       }
     }
-    sg = warp_sum(sg) / (float)D;
-    sgx = warp_sum(sgx) / (float)D;
+    if (rsums) {
+      sg = rsums[2 * row];
+      sgx = rsums[2 * row + 1];
+    } else {
+      sg = warp_sum(sg) / (float)D;
+      sgx = warp_sum(sgx) / (float)D;
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int c = lane + 64 * j;
@@ -156,8 +199,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
   }
   __syncthreads();
   for (int i = threadIdx.x; i < D; i += 256) {
-    part[(int64_t)blockIdx.x * 2 * D + i] = red0[i] + red0[D + i] + red0[2 * D + i] + red0[3 * D + i];
-    part[(int64_t)blockIdx.x * 2 * D + D + i] = red1[i] + red1[D + i] + red1[2 * D + i] + red1[3 * D + i];
+    part[(int64_t)blockIdx.x * 2 * Dtot + i] = red0[i] + red0[D + i] + red0[2 * D + i] + red0[3 * D + i];
+    part[(int64_t)blockIdx.x * 2 * Dtot + Dtot + i] = red1[i] + red1[D + i] + red1[2 * D + i] + red1[3 * D + i];
   }
 }
 
@@ -226,16 +269,34 @@ extern "C" int dpe_layernorm_bwd_nblocks(int64_t rows) {
   return (int)(nb < 1 ? 1 : (nb > 1024 ? 1024 : nb));
 }
 
+// Floats of the `part` scratch of dpe_layernorm_bwd: [nblocks][2][D] partials (+ [rows][2] row sums
+// when D > 2048).
+extern "C" int64_t dpe_layernorm_bwd_scratch(int64_t rows, int D) {
+  return (int64_t)dpe_layernorm_bwd_nblocks(rows) * 2 * D + (D > 2048 ? 2 * rows : 0);
+}
+
 extern "C" int dpe_layernorm_bwd(const uint16_t* dy, const void* x, int x_bf16, const float* w, const float* mean,
                                  const float* rstd, void* dx, int dx_acc, const float* res_in, uint16_t* dx_bf16, float* dw,
                                  float* db, float* part, int64_t rows, int D, hipStream_t st) {
-  if (D % 8 || D > 2048) return -1;
+  if (D % 8) return -1;
   const int nbc = dpe_layernorm_bwd_nblocks(rows);
-  const int nj = (D / 8 + 63) / 64;  // 16-B chunks per lane per row
-  const size_t lds = (size_t)2 * 4 * D * sizeof(float);
+  // rows wider than 2048: full-row sums first, then equal column slices of <= 2048 (blockIdx.y)
+  int nch = (D + 2047) / 2048;
+  while (D % nch || (D / nch) % 8) ++nch;  // terminates: nch = D / 8 always divides
+  const int Dc = D / nch;
+  float* rs = nullptr;
+  if (D > 2048) {
+    rs = part + (int64_t)nbc * 2 * D;
+    if (x_bf16) hipLaunchKernelGGL(ln_bwd_rowsums_kernel<true>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, dy, x, w,
+                                   mean, rstd, rs, rows, D);
+    else hipLaunchKernelGGL(ln_bwd_rowsums_kernel<false>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, dy, x, w, mean,
+                            rstd, rs, rows, D);
+  }
+  const int nj = (Dc / 8 + 63) / 64;  // 16-B chunks per lane per row slice
+  const size_t lds = (size_t)2 * 4 * Dc * sizeof(float);
 #define DPE_LNB(XB, NJ_) \
-  hipLaunchKernelGGL((ln_bwd_kernel<XB, NJ_>), dim3(nbc), dim3(256), lds, st, dy, x, w, mean, rstd, dx, dx_acc, res_in, \
-                     dx_bf16, part, rows, D)
+  hipLaunchKernelGGL((ln_bwd_kernel<XB, NJ_>), dim3(nbc, nch), dim3(256), lds, st, dy, x, w, mean, rstd, dx, dx_acc, \
+                     res_in, dx_bf16, part, rows, Dc, D, rs)
 #define DPE_LNB_J(XB) \
   if (nj == 1) DPE_LNB(XB, 1); else if (nj == 2) DPE_LNB(XB, 2); else if (nj == 3) DPE_LNB(XB, 3); else DPE_LNB(XB, 4)
   if (x_bf16) { DPE_LNB_J(true); } else { DPE_LNB_J(false); }

@@ -51,6 +51,11 @@ def _pad8(n: int) -> int:
 
 # ===================================================================== Linear
 class _LinearFn(Function):
+    """bf16 Linear on the MFMA GEMMs.  Output widths that are not a multiple of 8 (SimpleNet's
+    10-class head) run on the bf16 shadow padded to Np = pad8(N) rows: bias (zero-padded) and ReLU
+    stay in the GEMM epilogue, the backward pads dy once (F.pad, one kernel) and the weight grad
+    writes only the N real rows into the gradient buffer, with the bias grad from the same launch."""
+
     @staticmethod
     def forward(ctx, x, weight, bias, act: int, out_f32: bool):
         C = ext()
@@ -60,12 +65,8 @@ class _LinearFn(Function):
         xb = x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
         xb = xb.contiguous()
         if Np != N:
-            y = C.linear_fwd(xb, w16, None, 0, out_f32)[..., :N]
-            if bias is not None:
-                y = y + bias.to(y.dtype)
-            if act == ACT_RELU:
-                y = torch.relu(y)
-            y = y.contiguous()
+            bpad = F.pad(bias.detach(), (0, Np - N)) if bias is not None else None
+            y = C.linear_fwd(xb, w16, bpad, act, out_f32)[..., :N].contiguous()
         else:
             y = C.linear_fwd(xb, w16, bias.detach() if bias is not None else None, act, out_f32)
         ctx.save_for_backward(xb, y if act != ACT_NONE else None)
@@ -85,31 +86,25 @@ class _LinearFn(Function):
         if act == ACT_RELU:
             dy = C.act(dy.contiguous(), y.to(torch.bfloat16).contiguous() if y.dtype != torch.bfloat16 else y.contiguous(), 1)
         dy = dy.contiguous()
-        if Np != N:
-            dyp = torch.zeros((*dy.shape[:-1], Np), dtype=dy.dtype, device=dy.device)
-            dyp[..., :N] = dy
-        else:
-            dyp = dy
+        dyp = F.pad(dy, (0, Np - N)) if Np != N else dy  # zero pad columns: the GEMMs' 16-B rows
         dx = None
         if ctx.needs_input_grad[0]:
             dx = C.linear_dgrad(dyp, shadow(weight, Np - N))
             if ctx.x_dtype != torch.bfloat16:
                 dx = dx.to(ctx.x_dtype)
+        want_b = bias is not None and ctx.needs_input_grad[2]
+        bbuf, bdirect = grad_sink(bias) if want_b else (None, False)
         gw = None
         if ctx.needs_input_grad[1]:
             buf, direct = grad_sink(weight)
-            if Np != N:
-                tmp = torch.zeros((Np, weight.shape[1]), dtype=torch.float32, device=dy.device)
-                C.linear_wgrad(dyp, xb, tmp)
-                buf.add_(tmp[:N])
-            else:
-                C.linear_wgrad(dyp, xb, buf)
+            # column-padded dy: only the N real rows of dW (and of db) are written
+            C.linear_wgrad(dyp, xb, buf, 1.0, None, bbuf)
             grad_done(weight, direct)
             gw = None if direct else buf
-        gb = None
-        if bias is not None and ctx.needs_input_grad[2]:
-            bbuf, bdirect = grad_sink(bias)
+        elif want_b:
             C.colsum(dy, bbuf, True)
+        gb = None
+        if want_b:
             grad_done(bias, bdirect)
             gb = None if bdirect else bbuf
         return dx, gw, gb, None, None
