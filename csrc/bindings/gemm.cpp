@@ -11,6 +11,7 @@
 // measured single-shape throughputs of each tile (profiles/hgemm_*), relative
 // to the 256x256 tile.
 #include <torch/extension.h>
+#include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
@@ -116,7 +117,7 @@ Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int
 // head; 16-row bands worse everywhere.
 int group_rows(const Plan& pl) { return pl.grid >= 64 ? 4 : 1; }
 
-int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_bytes) {
+int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_bytes, hipStream_t fin_stream) {
   TORCH_CHECK(a.K % 64 == 0 && a.K > 0, "hgemm: K must be a positive multiple of 64 (got ", a.K, ")");
   const Plan pl = plan(a.M, a.N, a.K, ak, bk, allow_split, out_bytes);
   TORCH_CHECK(pl.cfg >= 0, "hgemm: no tile configuration for M=", a.M, " N=", a.N, " K=", a.K, " layout ", ak, bk);
@@ -133,7 +134,23 @@ int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_by
     const int rc = dpe_hgemm_launch(&a, pl.cfg, ak, bk, dpe::HE_SLAB, pl.grid, cur_stream());
     hipError_t e = hipGetLastError();
     TORCH_CHECK(rc == 0 && e == hipSuccess, "hgemm (split) launch failed rc=", rc, " ", hipGetErrorString(e));
-    const int rf = dpe_hgemm_finalize(&a, epi, cur_stream());
+    hipStream_t fs = cur_stream();
+    if (fin_stream && fin_stream != fs) {
+      // slabs -> side stream: event order, and the workspace stays allocated until the finalize ran
+      static thread_local hipEvent_t ev = [] {
+        hipEvent_t x = nullptr;
+        (void)hipEventCreateWithFlags(&x, hipEventDisableTiming);
+        return x;
+      }();
+      TORCH_CHECK(hipEventRecord(ev, fs) == hipSuccess && hipStreamWaitEvent(fin_stream, ev, 0) == hipSuccess,
+                  "hgemm: finalize stream ordering failed");
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      c10::hip::HIPCachingAllocator::recordStream(ws.storage().data_ptr(),
+                                                  c10::hip::getStreamFromExternal(fin_stream, (c10::DeviceIndex)dev));
+      fs = fin_stream;
+    }
+    const int rf = dpe_hgemm_finalize(&a, epi, fs);
     e = hipGetLastError();
     TORCH_CHECK(rf == 0 && e == hipSuccess, "hgemm finalize failed rc=", rf, " ", hipGetErrorString(e));
     return pl.cfg;

@@ -20,6 +20,9 @@ bool layout_ok(int cfg, int ak, int bk);
 Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int out_bytes, int force_cfg = -1,
           int force_splits = -1);
 // Plans, allocates the split workspace if any and launches; returns the tile configuration used.
-int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_bytes);
+// fin_stream (K-split plans only): the slab reduction (hgemm_finalize) runs there, ordered after the
+// slab kernel by an event -- a memory-bound pass co-resident with the next compute-bound GEMM on the
+// current stream.  The caller makes every consumer of C wait for fin_stream.
+int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_bytes, hipStream_t fin_stream = nullptr);
 
 }  // namespace dpe_gemm

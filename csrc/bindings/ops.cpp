@@ -421,7 +421,7 @@ dpe::ConvGeom geom(const Tensor& x, const Tensor& w, int64_t sh, int64_t sw, int
                    int64_t OH, int64_t OW);
 
 void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha, const c10::optional<Tensor>& alpha_t,
-                  const c10::optional<Tensor>& dbias) {
+                  const c10::optional<Tensor>& dbias, int64_t fin_stream) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(x); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
   const int64_t N = dw.size(0), K = dw.size(1), ldy = dy.size(-1);
   TORCH_CHECK(ldy >= N && x.size(-1) == K && dy.numel() / ldy == x.numel() / K, "linear_wgrad: shape mismatch");
@@ -442,7 +442,7 @@ void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha, c
       TORCH_CHECK(dbias->numel() == N, "linear_wgrad: dbias must have out_features elements");
       a.dbias = fp(*dbias);
     }
-    dpe_gemm::run(a, 0, 0, dpe::HE_ACC_F32, true, 4);
+    dpe_gemm::run(a, 0, 0, dpe::HE_ACC_F32, true, 4, (hipStream_t)(uintptr_t)fin_stream);
     return;
   }
   if (dbias.has_value() && dbias->defined()) {
@@ -624,7 +624,8 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
                                     const c10::optional<Tensor>& residual, const c10::optional<Tensor>& bn_x,
                                     const c10::optional<Tensor>& bn_coef, const Tensor* acc_into = nullptr,
                                     const c10::optional<Tensor>& bn_mask = c10::nullopt,
-                                    const c10::optional<Tensor>& residual_mask = c10::nullopt) {
+                                    const c10::optional<Tensor>& residual_mask = c10::nullopt,
+                                    bool res_stride2 = false) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(w); CHECK_CONTIG(dy); CHECK_CONTIG(w);
   // acc_into: dx += dgrad in place (the epilogue reads each element as its residual
   // right before overwriting it); parities no tap reaches are left untouched.
@@ -677,10 +678,20 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
   // write-heavy pointwise data grads (a bottleneck's conv1: K = Cout <= 256, N = Cin >= 2K), with the
   // residual / BN-backward epilogue: streaming kernel (pwconv.hip), BN partials per row group
   const int pw_rg = (pw_stream_on() && is_pointwise(g) && !acc_into) ? dpe_pw_rowgroups(a.M, a.N, a.K, dpe::PW_DGRAD) : 0;
+  if (res_stride2) {
+    // residual = the compact data grad of a downsample block's stride-2 1x1 conv ([N, H/2, W/2, C]),
+    // added at even (h, w) by the streaming kernel's epilogue
+    TORCH_CHECK(a.residual && !a.res_mask && pw_rg > 0 && g.H % 2 == 0 && g.W % 2 == 0,
+                "conv_dgrad: residual_stride2 needs the streaming pointwise data grad, even H / W, no residual mask");
+    TORCH_CHECK(residual->dim() == 4 && residual->size(0) == g.N && residual->size(1) == g.H / 2 &&
+                    residual->size(2) == g.W / 2 && residual->size(3) == g.C,
+                "conv_dgrad: residual_stride2 residual must be [N, H/2, W/2, C]");
+  }
   if (pw_rg > 0) {
     dpe::PwArgs pa{};
     pa.x = bp(dy); pa.w = bp(w); pa.y = bpm(dx);
     pa.residual = a.residual; pa.res_mask = a.res_mask;
+    if (res_stride2) { pa.res_h = g.H; pa.res_w = g.W; }
     pa.st_x = a.st_x; pa.st_coef = a.st_coef; pa.st_mask = a.st_mask;
     pa.M = a.M; pa.N = a.N; pa.K = a.K; pa.rg = pw_rg;
     if (want_bn) {
@@ -1331,7 +1342,9 @@ void register_ops(pybind11::module& m) {
   m.def("linear_dgrad", &linear_dgrad, py::arg("dy"), py::arg("w"), py::arg("residual") = py::none(),
         py::arg("alpha_t") = py::none(), py::arg("gelu_in") = py::none());
   m.def("linear_wgrad", &linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("alpha") = 1.0,
-        py::arg("alpha_t") = py::none(), py::arg("dbias") = py::none());
+        py::arg("alpha_t") = py::none(), py::arg("dbias") = py::none(), py::arg("fin_stream") = 0,
+        "dw (+)= alpha dy^T x (+ db += alpha colsum(dy)); fin_stream: run a K-split's slab reduction on that HIP "
+        "stream (the caller orders dw's consumers after it)");
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("want_stats") = false, py::arg("bias") = py::none(), py::arg("in_coef") = py::none());
   m.def("row_bn_on_load", [](std::vector<int64_t> xs, std::vector<int64_t> ws, std::vector<int64_t> stride,
@@ -1356,16 +1369,25 @@ void register_ops(pybind11::module& m) {
           return pw_stream_on() && (C == 64 || C == 128) && C <= cmax && cout % 8 == 0 && M % 32 == 0 &&
                  dpe_pw_rowgroups(M, cout, C, dpe::PW_FWD) > 0;
         }, py::arg("x_shape"), py::arg("cout"));
+  m.def("pw_dgrad_strided_residual_ok", [](std::vector<int64_t> xshape, int64_t k) {
+          // a downsample block's conv1 data grad (1x1, K = k -> N = xshape[3]) on the streaming kernel,
+          // which can take the stride-2 branch's compact data grad as its residual
+          if (xshape.size() != 4 || xshape[1] % 2 || xshape[2] % 2 || !pw_stream_on()) return false;
+          return dpe_pw_rowgroups(xshape[0] * xshape[1] * xshape[2], xshape[3], k, dpe::PW_DGRAD) > 0;
+        }, py::arg("xshape"), py::arg("k"));
   m.def("conv_dgrad_acc", &conv_dgrad_acc, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), "dx += data grad of conv(w) in place (parities without taps untouched)");
   m.def("conv_dgrad_bn", [](const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape, std::vector<int64_t> stride,
                             std::vector<int64_t> pad, std::vector<int64_t> dil, const c10::optional<Tensor>& residual,
                             const c10::optional<Tensor>& bn_x, const c10::optional<Tensor>& bn_coef,
-                            const c10::optional<Tensor>& bn_mask, const c10::optional<Tensor>& residual_mask) {
-          return conv_dgrad_impl(dy, w, xshape, stride, pad, dil, residual, bn_x, bn_coef, nullptr, bn_mask, residual_mask);
+                            const c10::optional<Tensor>& bn_mask, const c10::optional<Tensor>& residual_mask,
+                            bool residual_stride2) {
+          return conv_dgrad_impl(dy, w, xshape, stride, pad, dil, residual, bn_x, bn_coef, nullptr, bn_mask, residual_mask,
+                                 residual_stride2);
         }, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"),
         py::arg("pad"), py::arg("dil"), py::arg("residual") = py::none(), py::arg("bn_x") = py::none(),
         py::arg("bn_coef") = py::none(), py::arg("bn_mask") = py::none(), py::arg("residual_mask") = py::none(),
+        py::arg("residual_stride2") = false,
         "data grad; with bn_x/bn_coef also the BN-backward partials of the BN+ReLU that produced the conv input; "
         "with bn_mask (BN + residual + ReLU) the mask is bn_mask > 0 and dx is stored masked");
   m.def("bn_coef", &bn_coef, py::arg("stats"), py::arg("M"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),

@@ -23,6 +23,8 @@ struct PwArgs {
   int64_t M, N, K;
   int rg;                    // row groups (= partial columns), from dpe_pw_rowgroups
   const float* in_coef;      // PW_FWD: x is the pre-BN tensor; the operand is relu(x * in_coef[k] + in_coef[K + k])
+  int res_h, res_w;          // PW_DGRAD, > 0: y is an [*, res_h, res_w] image and the residual is the compact
+                             // [*, res_h/2, res_w/2] grid of a stride-2 1x1 conv's data grad, added at even (h, w) only
 };
 
 }  // namespace dpe

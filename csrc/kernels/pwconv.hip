@@ -138,6 +138,15 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
   float s[8], ss[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
+  // residual element offset of output row m (chunk nch); -1: no residual term at this row (the odd
+  // positions of a stride-2 downsample branch's compact data grad)
+  const int rh = a.res_h, rw = a.res_w;
+  auto res_off = [&](int m) -> int64_t {
+    if (rh <= 0) return (int64_t)m * N + nch;
+    const int hw = rh * rw, n = m / hw, r = m - n * hw, h = r / rw, w = r - h * rw;
+    if ((h | w) & 1) return -1;
+    return ((int64_t)(n * (rh >> 1) + (h >> 1)) * (rw >> 1) + (w >> 1)) * N + nch;
+  };
 
   if (EPI == PW_FWD && a.in_coef) {  // before the ring's first DMA (its counted waits start after this)
     for (int i = tid; i < 2 * K; i += 256) bnin[i] = a.in_coef[i];
@@ -179,7 +188,10 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
         for (int ps = 0; ps < HN; ++ps) {
           const int m = min(m0 + 32 * hf + ps * RPP + lane / CPRW, M - 1);
           const int64_t off = (int64_t)m * N + nch;
-          if (a.residual) hrv[hf][ps] = *(const u32x4*)(a.residual + off);
+          if (a.residual) {
+            const int64_t ro = res_off(m);
+            hrv[hf][ps] = ro >= 0 ? *(const u32x4*)(a.residual + ro) : u32x4{0u, 0u, 0u, 0u};
+          }
           hrmb[hf][ps] = a.res_mask ? (uint32_t)a.res_mask[off >> 3] : 0xffu;
           if (bnb) hxv[hf][ps] = *(const u32x4*)(a.st_x + off);
           hsmb[hf][ps] = (bnb && a.st_mask) ? (uint32_t)a.st_mask[off >> 3] : 0xffu;
@@ -242,7 +254,10 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
         for (int ps = 0; ps < NPS; ++ps) {
           const int m = min(m0 + 32 * hf + ps * RPP + lane / CPRW, M - 1);
           const int64_t off = (int64_t)m * N + nch;
-          if (a.residual) rv[ps] = *(const u32x4*)(a.residual + off);
+          if (a.residual) {
+            const int64_t ro = res_off(m);
+            rv[ps] = ro >= 0 ? *(const u32x4*)(a.residual + ro) : u32x4{0u, 0u, 0u, 0u};
+          }
           rmb[ps] = a.res_mask ? (uint32_t)a.res_mask[off >> 3] : 0xffu;
           if (bnb) xv[ps] = *(const u32x4*)(a.st_x + off);
           smb[ps] = (bnb && a.st_mask) ? (uint32_t)a.st_mask[off >> 3] : 0xffu;
@@ -381,6 +396,8 @@ extern "C" int dpe_pw_launch(const PwArgs* args, int epi, hipStream_t st) {
   if (a.rg <= 0 || a.rg != dpe_pw_rowgroups(a.M, a.N, a.K, epi)) return -1;
   if (epi == PW_FWD && (a.residual || a.st_x)) return -1;
   if (a.st_x && !a.st_coef) return -1;
+  if (a.res_h > 0 && (epi != PW_DGRAD || a.res_mask || a.res_h % 2 || a.res_w % 2 || a.M % ((int64_t)a.res_h * a.res_w)))
+    return -1;
   const int nbN = (int)(a.N / (4 * pw_wn((int)a.K)));
   const dim3 grid((unsigned)(a.rg * nbN)), block(256);
 #define PW_L(K_, WN_, NS_)                                                                              \

@@ -39,7 +39,7 @@ import torch
 from torch.autograd import Function
 
 from ..ops._ext import ext
-from ..ops._state import grad_done, grad_sink, note_use, shadow
+from ..ops._state import finalize_stream, grad_done, grad_sink, note_use, shadow
 
 # (fp32 grad, its bf16 copy, version) produced by the most recent block backward
 _carry: list = [None]
@@ -112,8 +112,11 @@ class BlockFn(Function):
         def linear_bwd(lin, dyb, inp, want_dx=True, gelu_in=None):
             """dW += dyb^T inp and db += colsum(dyb) in one GEMM launch ; return dyb W (bf16), times gelu'(gelu_in) if given."""
             buf, d = sink(lin.weight)
-            bb, bd = sink(lin.bias) if lin.bias is not None else (None, False)
-            C.linear_wgrad(dyb, inp, buf, 1.0, None, bb)  # bias grad from the same launch (row sums of dy^T)
+            bb, bd = sink(lin.bias) if lin.bias is not None else (None, True)
+            # bias grad from the same launch (row sums of dy^T); a K-split's slab reduction may run on the
+            # side stream when both gradients are bucket views (the reducer / backward join wait for it)
+            fs = finalize_stream(dyb.device) if (d and bd) else 0
+            C.linear_wgrad(dyb, inp, buf, 1.0, None, bb, fs)
             done(lin.weight, buf, d)
             if lin.bias is not None:
                 done(lin.bias, bb, bd)

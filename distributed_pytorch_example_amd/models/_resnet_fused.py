@@ -72,6 +72,8 @@ _BN_DUAL = os.environ.get("DPE_BN_DUAL", "1") != "0"
 _ROW_BNIN = _EPI_BNB and os.environ.get("DPE_ROW_BNIN", "1") != "0"
 # DPE_PW_BNIN=0: layer-1 a2 = relu(BN2(h2)) materialised by a bn_apply pass (A/B reference)
 _PW_BNIN = _EPI_BNB and os.environ.get("DPE_PW_BNIN", "1") != "0"
+# DPE_DOWN_CHAIN=0: the block before a downsample block runs its BN3 backward standalone (reduce + apply)
+_DOWN_CHAIN = _BN3_CHAIN and os.environ.get("DPE_DOWN_CHAIN", "1") != "0"
 
 
 def _out_hw(hw, conv):
@@ -152,9 +154,14 @@ class BottleneckFn(Function):
         else:
             out, bits = C.bn_apply(h3, c3, x, None, True, want_bits)
         ctx.save_for_backward(x, h1, a1, h2, a2, h3, out, hd, c1, c2, c3, cd)
-        # previous block's BN3 is fused into this block's first data grad (identity blocks only:
-        # a downsample block's dx is completed by a second, strided kernel)
-        ctx.link_in = (link_in if (link_in is not None and block.down is None and link_in.h3 is not None
+        # previous block's BN3 is fused into this block's first data grad.  A downsample block's dx also
+        # has the stride-2 branch's term: it is computed first as a compact [N, H/2, W/2, C] data grad
+        # and added at the even pixels by the streaming conv1 data grad's epilogue, which then applies
+        # the mask and emits the partials as for an identity block (layers 1 -> 2 and 2 -> 3).
+        strided_ok = block.down is not None and _DOWN_CHAIN and tuple(block.down.conv.stride) == (2, 2) and \
+            tuple(block.down.conv.kernel_size) == (1, 1) and tuple(convs[0].conv.stride) == (1, 1) and \
+            C.pw_dgrad_strided_residual_ok(list(x.shape), convs[0].conv.out_channels)
+        ctx.link_in = (link_in if (link_in is not None and (block.down is None or strided_ok) and link_in.h3 is not None
                                    and link_in.mask is not None) else None)
         ctx.link_out = link_out
         ctx.bits = bits  # ReLU mask of out as bits: the standalone BN3 backward reads these, not out
@@ -265,7 +272,17 @@ class BottleneckFn(Function):
         wgrad(0, dh1, x)
         dx = None
         if ctx.needs_input_grad[0]:
-            if has_down:
+            if has_down and ctx.link_in is not None:
+                if dhd is None:
+                    dhd, _ = bn_bwd(3, dz3, None, hd, cd, False)
+                wgrad(3, dhd, x)
+                li = ctx.link_in
+                n, hh, ww, cin = x.shape
+                dxd = C.conv_dgrad(dhd, ws[3], [n, hh // 2, ww // 2, cin], [1, 1], [0, 0], [1, 1])  # compact
+                s, p, d = _conv_conf(convs[0].conv)
+                dx, part = C.conv_dgrad_bn(dh1, ws[0], list(x.shape), s, p, d, dxd, li.h3, li.coef, li.mask, None, True)
+                li.part, li.dz_ptr, li.dz_shape = part, dx.data_ptr(), tuple(dx.shape)
+            elif has_down:
                 if dhd is None:
                     dhd, _ = bn_bwd(3, dz3, None, hd, cd, False)
                 wgrad(3, dhd, x)

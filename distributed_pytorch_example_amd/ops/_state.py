@@ -122,9 +122,21 @@ _aux_streams: dict = {}
 _aux_join_gen = [None]  # autograd graph task that already has a join queued
 
 
-def aux_stream(device: torch.device):
+# K-split weight-grad slab reductions (hgemm_finalize: memory-bound, ~13 us each, 48 per GPT-2 step)
+# on the side stream, co-resident with the next compute-bound GEMM on the main stream
+# (DPE_FINALIZE_STREAM=1 / set_finalize_stream; A/B in docs/perf_notes.md).
+_FIN_STREAM_ON = __import__("os").environ.get("DPE_FINALIZE_STREAM", "0") == "1"
+
+
+def set_finalize_stream(on: bool) -> bool:
+    global _FIN_STREAM_ON
+    prev, _FIN_STREAM_ON = _FIN_STREAM_ON, bool(on)
+    return prev
+
+
+def aux_stream(device: torch.device, force: bool = False):
     """The weight-grad side stream of ``device`` (None when disabled)."""
-    if not _WGRAD_STREAM_ON or device.type != "cuda":
+    if not (_WGRAD_STREAM_ON or force) or device.type != "cuda":
         return None
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _aux_streams.get(idx)
@@ -156,13 +168,28 @@ def run_on_aux(device: torch.device, fn, *tensors):
     for t in tensors:
         if t is not None:
             t.record_stream(s)
+    _queue_join()
+    return out
+
+
+def _queue_join():
     # one join per backward pass: keyed on the running graph task (a raised backward
     # cannot leave a stale "already queued" flag behind)
     gen = torch._C._current_graph_task_id() if hasattr(torch._C, "_current_graph_task_id") else None
     if gen is None or gen != _aux_join_gen[0]:
         _aux_join_gen[0] = gen
         torch.autograd.Variable._execution_engine.queue_callback(_join_aux)
-    return out
+
+
+def finalize_stream(device: torch.device) -> int:
+    """HIP stream handle for the slab reductions of K-split weight grads whose gradient lands in a
+    DDP bucket view (0: run them on the current stream).  The reducer waits for this stream before
+    a bucket's all-reduce and the end of backward joins it (so the optimizer sees the sums)."""
+    if not _FIN_STREAM_ON or device.type != "cuda":
+        return 0
+    s = aux_stream(device, force=True)
+    _queue_join()
+    return s.cuda_stream
 
 
 def aux_wait(device: torch.device) -> None:

@@ -853,6 +853,40 @@ def test_pw_stream_matches_igemm(C, N, H, W, Ci, Co):
             assert rel_err(s1.sum(-1), s2.sum(-1)) < 1e-4, i
 
 
+@pytest.mark.parametrize("N,H,W,Ci,Co,Cd", [(2, 8, 8, 256, 128, 512), (4, 28, 28, 256, 128, 512),
+                                            (3, 14, 14, 512, 256, 1024), (16, 56, 56, 256, 128, 512)])
+def test_pw_dgrad_strided_residual(C, N, H, W, Ci, Co, Cd):
+    """A downsample block's dx = conv1 data grad + the stride-2 branch's data grad: with
+    residual_stride2 the streaming kernel adds the branch's compact [N, H/2, W/2, Ci] data grad at the
+    even pixels, then masks with the previous block's ReLU bits and emits its BN3-backward partials.
+    Equals the two-kernel form (dgrad, then the strided data grad accumulated in place) followed by
+    the same mask / partials (bitwise output up to the order of two bf16 roundings; sums to 1e-4)."""
+    torch.manual_seed(41)
+    w1 = bf(torch.randn(Co, 1, 1, Ci, device=dev) / math.sqrt(Ci))   # conv1: Ci -> Co (stride 1)
+    wd = bf(torch.randn(Cd, 1, 1, Ci, device=dev) / math.sqrt(Ci))   # downsample: Ci -> Cd (stride 2)
+    dh1 = bf(torch.randn(N, H, W, Co, device=dev))
+    dhd = bf(torch.randn(N, H // 2, W // 2, Cd, device=dev))
+    h3, c3 = bf(torch.randn(N, H, W, Ci, device=dev)), _bn_coef(C, Ci)
+    _, bits = C.bn_apply(h3, c3, bf(torch.randn(N, H, W, Ci, device=dev)), None, True, True)
+    sh = [N, H, W, Ci]
+    z = [1, 1], [0, 0], [1, 1]
+    dxd = C.conv_dgrad(dhd, wd, [N, H // 2, W // 2, Ci], *z, None)
+    dx, part = C.conv_dgrad_bn(dh1, w1, sh, *z, dxd, h3, c3, bits, None, True)
+    # reference: dense two-kernel form, then mask + partials in fp32
+    full = C.conv_dgrad(dh1, w1, sh, *z, None)
+    C.conv_dgrad_acc(dhd, wd, full, [2, 2], [0, 0], [1, 1])
+    m = torch.zeros(N, H, W, Ci, dtype=torch.bool, device=dev)
+    ybits = bits.view(torch.uint8).reshape(N, H, W, Ci // 8)
+    for e in range(8):
+        m[..., e::8] = ((ybits >> e) & 1).bool()
+    dz = torch.where(m, full.float(), torch.zeros_like(full.float()))
+    assert rel_err(dx, dz) < 5e-3
+    hf = h3.float().reshape(-1, Ci)
+    ps = part.sum(-1)
+    assert rel_err(ps[0], dz.reshape(-1, Ci).sum(0)) < 2e-3
+    assert rel_err(ps[1], (dz.reshape(-1, Ci) * (hf - c3[2])).sum(0)) < 2e-3
+
+
 @pytest.mark.parametrize("N,H,W", [(2, 112, 112), (3, 112, 112), (1, 7, 100), (4, 3, 112)])
 def test_stem_kernel_matches_igemm(C, N, H, W):
     """The row-walking s2d stem kernel (stem.hip: filter in VGPRs, 5-row LDS ring, per-block BN
