@@ -815,7 +815,7 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape
 // dw [K,R,S,C] fp32 (+)= alpha * dy^T (x) im2col(x)
 // in_coef: as conv_fwd's (x pre-BN, BN+ReLU applied on load; row-walking 64-channel 3x3 kernel only)
 void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64_t> stride, std::vector<int64_t> pad,
-                std::vector<int64_t> dil, double alpha, const c10::optional<Tensor>& in_coef) {
+                std::vector<int64_t> dil, double alpha, const c10::optional<Tensor>& in_coef, int64_t fin_stream) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(x); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
   auto g = geom(x, dw, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], dy.size(1), dy.size(2));
   TORCH_CHECK(dy.size(3) == g.K && dy.size(0) == g.N, "conv_wgrad: dy shape mismatch");
@@ -865,7 +865,7 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64
     h.lda = g.K; h.ldb = g.C; h.ldc = g.C;
     h.a_dim = (int)((g.K + 7) / 8 * 8);
     h.alpha = (float)alpha;
-    dpe_gemm::run(h, 0, 0, dpe::HE_ACC_F32, true, 4);
+    dpe_gemm::run(h, 0, 0, dpe::HE_ACC_F32, true, 4, (hipStream_t)(uintptr_t)fin_stream);
     return;
   }
   run_igemm(a, dpe::A_DENSE_M, is_pointwise(g) ? dpe::B_DENSE_N : dpe::B_CONV_WGRAD, dpe::EPI_ATOMIC_F32, true, true);
@@ -1402,7 +1402,8 @@ void register_ops(pybind11::module& m) {
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), py::arg("residual") = py::none(), py::arg("residual_mask") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
-        py::arg("dil"), py::arg("alpha") = 1.0, py::arg("in_coef") = py::none());
+        py::arg("dil"), py::arg("alpha") = 1.0, py::arg("in_coef") = py::none(), py::arg("fin_stream") = 0,
+        "dw (+)= alpha dW; fin_stream: a K-split hgemm's slab reduction runs on that stream (caller orders consumers)");
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),
         py::arg("momentum"), py::arg("eps"), py::arg("relu"), py::arg("residual") = py::none(), py::arg("stats") = py::none());
   m.def("bn_fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),

@@ -60,7 +60,7 @@ import torch
 from torch.autograd import Function
 
 from ..ops._ext import ext
-from ..ops._state import grad_done, grad_sink, note_use, run_on_aux, shadow
+from ..ops._state import finalize_stream, grad_done, grad_sink, note_use, run_on_aux, shadow
 
 # DPE_BN_EPI=0: inner BN backward through the standalone reduce kernel (A/B reference)
 _EPI_BNB = os.environ.get("DPE_BN_EPI", "1") != "0"
@@ -210,7 +210,8 @@ class BottleneckFn(Function):
             s, p, d = _conv_conf(convs[i].conv)
             buf, direct = grad_sink(w)
             if direct:  # bucket view: on the weight-grad side stream (the reducers wait for it)
-                run_on_aux(dy.device, lambda: C.conv_wgrad(dy, inp, buf, s, p, d, 1.0, in_coef), dy, inp, in_coef)
+                fs = finalize_stream(dy.device)  # a K-split hgemm's slab reduction beside the next kernel
+                run_on_aux(dy.device, lambda: C.conv_wgrad(dy, inp, buf, s, p, d, 1.0, in_coef, fs), dy, inp, in_coef)
             else:
                 C.conv_wgrad(dy, inp, buf, s, p, d, 1.0, in_coef)
             grad_done(w, direct)
