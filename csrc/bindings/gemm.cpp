@@ -117,10 +117,50 @@ Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int
 // head; 16-row bands worse everywhere.
 int group_rows(const Plan& pl) { return pl.grid >= 64 ? 4 : 1; }
 
-int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_bytes, hipStream_t fin_stream) {
-  TORCH_CHECK(a.K % 64 == 0 && a.K > 0, "hgemm: K must be a positive multiple of 64 (got ", a.K, ")");
-  const Plan pl = plan(a.M, a.N, a.K, ak, bk, allow_split, out_bytes);
-  TORCH_CHECK(pl.cfg >= 0, "hgemm: no tile configuration for M=", a.M, " N=", a.N, " K=", a.K, " layout ", ak, bk);
+// Two-launch plans.  A GEMM whose tiles do not fill whole rounds of slots (GPT-2's QKV 8192x2304: 288
+// tiles of 256^2 on 256 CUs) spends its last round mostly idle.  Splitting the output into a main part
+// that fills whole rounds with one tile and a tail covered by a smaller tile (its own round) costs one
+// extra launch and removes most of that idle round.  The cut is along N (whole tile columns of the
+// main tile) or M (whole tile rows); both parts are planned by plan() and the split is taken only if
+// the modelled time improves by > 5 %.  Pure function of the shape, like plan().
+Plan2 plan2(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int out_bytes) {
+  Plan2 best;
+  best.main = plan(M, N, K, ak, bk, allow_split, out_bytes);
+  best.est_s = best.main.est_s;
+  if (best.main.cfg < 0 || g_force_cfg >= 0 || g_force_splits >= 0) return best;
+  const int ncu = num_cus();
+  const int reserve = dpe_cu_reserve();
+  for (const TileCfg& c : kTiles) {
+    if (!layout_ok(c.cfg, ak, bk)) continue;
+    const int64_t slots = std::max<int64_t>(c.bpc, (int64_t)ncu * c.bpc - reserve);
+    const int64_t tm = (M + c.bm - 1) / c.bm, tn = (N + c.bn - 1) / c.bn;
+    for (int axis = 0; axis < 2; ++axis) {  // 0: cut along N (main = leading columns), 1: along M
+      const int64_t lines = axis == 0 ? tn : tm, per = axis == 0 ? tm : tn;  // tiles per cut line
+      const int64_t rounds = lines * per / slots;
+      if (rounds < 1) continue;
+      const int64_t keep = rounds * slots / per;  // whole lines that fit in `rounds` full rounds
+      const int64_t at = keep * (axis == 0 ? c.bn : c.bm);
+      const int64_t rest = (axis == 0 ? N : M) - at;
+      if (keep < 1 || rest < 64) continue;
+      const Plan pm = axis == 0 ? plan(M, at, K, ak, bk, false, out_bytes, c.cfg, 1) : plan(at, N, K, ak, bk, false, out_bytes, c.cfg, 1);
+      const Plan pt = axis == 0 ? plan(M, rest, K, ak, bk, allow_split, out_bytes) : plan(rest, N, K, ak, bk, allow_split, out_bytes);
+      if (pm.cfg < 0 || pt.cfg < 0) continue;
+      const double t = pm.est_s + pt.est_s + kLaunch;
+      if (t < best.est_s * 0.95 && t < best.main.est_s * 0.95) {
+        best.main = pm;
+        best.tail = pt;
+        best.axis = axis;
+        best.at = (int)at;
+        best.est_s = t;
+      }
+    }
+  }
+  return best;
+}
+
+namespace {
+// one planned launch (+ its slab finalize when K-split)
+void launch_planned(dpe::HgemmArgs a, const Plan& pl, int ak, int bk, int epi, hipStream_t fin_stream) {
   a.splits = pl.splits;
   a.kps = pl.kps;
   if (a.group_m == 0) a.group_m = group_rows(pl);
@@ -153,12 +193,57 @@ int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_by
     const int rf = dpe_hgemm_finalize(&a, epi, fs);
     e = hipGetLastError();
     TORCH_CHECK(rf == 0 && e == hipSuccess, "hgemm finalize failed rc=", rf, " ", hipGetErrorString(e));
-    return pl.cfg;
+    return;
   }
   const int rc = dpe_hgemm_launch(&a, pl.cfg, ak, bk, epi, pl.grid, cur_stream());
   const hipError_t e = hipGetLastError();
   TORCH_CHECK(rc == 0 && e == hipSuccess, "hgemm launch failed rc=", rc, " ", hipGetErrorString(e));
-  return pl.cfg;
+}
+
+// the sub-GEMM of output rows [m1, M) or columns [n1, N): operand / output / epilogue pointers moved
+dpe::HgemmArgs part_args(const dpe::HgemmArgs& a, int ak, int bk, int out_bytes, int axis, int at) {
+  dpe::HgemmArgs b = a;
+  const int64_t eo = axis == 0 ? (int64_t)at : (int64_t)at * a.ldc;  // output element offset
+  b.C = (char*)a.C + eo * out_bytes;
+  if (a.residual_f32) b.residual_f32 = a.residual_f32 + eo;
+  if (a.aux_in) b.aux_in = a.aux_in + eo;
+  if (a.aux_out) b.aux_out = a.aux_out + eo;
+  if (axis == 0) {  // columns [at, N)
+    b.N = a.N - at;
+    b.B = bk ? a.B + (int64_t)at * a.ldb : a.B + at;
+    if (a.bias) b.bias = a.bias + at;
+    if (a.b_dim > 0) b.b_dim = a.b_dim - at;
+    b.dbias = nullptr;  // the row sums come from the first tile column, which is in the main part
+  } else {          // rows [at, M)
+    b.M = a.M - at;
+    b.A = ak ? a.A + (int64_t)at * a.lda : a.A + at;
+    if (a.a_dim > 0) b.a_dim = a.a_dim - at;
+    if (a.dbias) b.dbias = a.dbias + at;
+  }
+  return b;
+}
+}  // namespace
+
+int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_bytes, hipStream_t fin_stream) {
+  TORCH_CHECK(a.K % 64 == 0 && a.K > 0, "hgemm: K must be a positive multiple of 64 (got ", a.K, ")");
+  const Plan2 p2 = plan2(a.M, a.N, a.K, ak, bk, allow_split, out_bytes);
+  TORCH_CHECK(p2.main.cfg >= 0, "hgemm: no tile configuration for M=", a.M, " N=", a.N, " K=", a.K, " layout ", ak, bk);
+  if (p2.axis < 0) {
+    launch_planned(a, p2.main, ak, bk, epi, fin_stream);
+    return p2.main.cfg;
+  }
+  const int ob = (epi == dpe::HE_BF16) ? 2 : 4;
+  dpe::HgemmArgs m = a;
+  if (p2.axis == 0) {
+    m.N = p2.at;
+    if (m.b_dim > 0) m.b_dim = p2.at;
+  } else {
+    m.M = p2.at;
+    if (m.a_dim > 0) m.a_dim = p2.at;
+  }
+  launch_planned(m, p2.main, ak, bk, epi, fin_stream);
+  launch_planned(part_args(a, ak, bk, ob, p2.axis, p2.at), p2.tail, ak, bk, epi, fin_stream);
+  return p2.main.cfg;
 }
 
 }  // namespace dpe_gemm
@@ -292,6 +377,12 @@ void register_gemm(pybind11::module& m) {
           return std::make_tuple(p.cfg, p.splits, p.kps, p.grid, p.est_s * 1e6);
         }, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("a_k"), py::arg("b_k"), py::arg("allow_split") = true,
         py::arg("out_bytes") = 2, "the planner's (cfg, splits, k per split, grid, estimated us) for a GEMM");
+  m.def("hgemm_plan2", [](int64_t M, int64_t N, int64_t K, bool ak, bool bk, bool allow_split, int64_t out_bytes) {
+          const Plan2 p = plan2(M, N, K, ak, bk, allow_split, (int)out_bytes);
+          auto t = [](const Plan& q) { return std::make_tuple(q.cfg, q.splits, q.kps, q.grid, q.est_s * 1e6); };
+          return std::make_tuple(t(p.main), p.axis, p.at, t(p.tail), p.est_s * 1e6);
+        }, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("a_k"), py::arg("b_k"), py::arg("allow_split") = true,
+        py::arg("out_bytes") = 2, "(main plan, cut axis (-1 none, 0 N, 1 M), cut at, tail plan, estimated us)");
   m.def("linear32_fwd", &linear32_fwd, py::arg("x"), py::arg("w"), py::arg("bias") = py::none(), py::arg("relu") = false,
         py::arg("drop_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0,
         "fp32 Linear on the exact-f32 MFMA: dropout(relu(x w^T + b)), mask identical to dropout()");

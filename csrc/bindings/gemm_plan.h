@@ -14,11 +14,22 @@ struct Plan {
   double est_s;  // modelled time
 };
 
+// A plan in up to two launches: `main` over output rows/columns [0, at) and `tail` over the rest
+// (axis 0: columns, 1: rows; -1: a single launch, `main` covers everything).
+struct Plan2 {
+  Plan main{-1, 1, 0, 0, 1e30};
+  Plan tail{-1, 1, 0, 0, 0.0};
+  int axis = -1;
+  int at = 0;
+  double est_s = 1e30;
+};
+
 int num_cus();
 bool layout_ok(int cfg, int ak, int bk);
 // out_bytes: bytes per output element of the final epilogue (slab traffic estimate)
 Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int out_bytes, int force_cfg = -1,
           int force_splits = -1);
+Plan2 plan2(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int out_bytes);
 // Plans, allocates the split workspace if any and launches; returns the tile configuration used.
 // fin_stream (K-split plans only): the slab reduction (hgemm_finalize) runs there, ordered after the
 // slab kernel by an event -- a memory-bound pass co-resident with the next compute-bound GEMM on the

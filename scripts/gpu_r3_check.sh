@@ -6,3 +6,4 @@ case $rc in 124|134|137|139) echo "STOP rc=$rc"; exit $rc;; esac
 ARMS="DPE_FINALIZE_STREAM=1 -" MODEL=gpt2 ROUNDS=2 bash scripts/ab_bench.sh || exit 1
 ARMS="DPE_DOWN_CHAIN=0 - DPE_FINALIZE_STREAM=1" MODEL=resnet50 ROUNDS=2 bash scripts/ab_bench.sh || exit 1
 bash scripts/rccl_footprint.sh > gpurun_out/r3_fp.txt 2>&1; tail -4 gpurun_out/r3_fp.txt
+timeout -k 10 300 python scripts/bench_gemm_parts.py > gpurun_out/r3_gemm_parts.jsonl 2>&1; tail -12 gpurun_out/r3_gemm_parts.jsonl
