@@ -145,6 +145,11 @@ def main():
               last_bucket_mb="auto" if args.last_bucket_mb is None else (args.last_bucket_mb or None))
     if "bucket_mb" in cfg:
         cfg["bucket_mb"] = round(ddp.bucket_cap_bytes / 2**20, 2)
+    if world > 1:  # the RCCL channel cap and the compute side's CU budget while buckets are in flight
+        from distributed_pytorch_example_amd.ops import ext as _ext
+
+        cfg["rccl_max_channels"] = pdist.comm_max_channels()
+        cfg["cu_reserve_slots"] = _ext().cu_reserve_config() if dev.type == "cuda" else 0
     opt = build_optimizer(opt_name, model.parameters(), lr=lr, weight_decay=wd)
 
     def step(i):
