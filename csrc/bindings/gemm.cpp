@@ -127,7 +127,8 @@ Plan2 plan2(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, i
   Plan2 best;
   best.main = plan(M, N, K, ak, bk, allow_split, out_bytes);
   best.est_s = best.main.est_s;
-  if (best.main.cfg < 0 || g_force_cfg >= 0 || g_force_splits >= 0) return best;
+  static const bool on = [] { const char* e = getenv("DPE_HGEMM_PLAN2"); return !(e && e[0] == '0'); }();  // A/B
+  if (!on || best.main.cfg < 0 || g_force_cfg >= 0 || g_force_splits >= 0) return best;
   const int ncu = num_cus();
   const int reserve = dpe_cu_reserve();
   for (const TileCfg& c : kTiles) {
