@@ -255,6 +255,41 @@ def test_resnet_counts_batches_once_per_forward(C):
     assert counts and all(v == 2 for v in counts.values()), counts
 
 
+@pytest.mark.parametrize("reserve", [0, 16])
+def test_resnet_bn_statistics_bitwise_reproducible(C, reserve):
+    """BatchNorm statistics come from per-tile / per-row-group partials in fixed layouts and are summed
+    in a fixed order, so two identical training forwards give bitwise-equal running statistics and
+    BN-backward sums -- also while the CU budget is active (reserve > 0: the persistent kernels run
+    with fewer row groups, a different but equally fixed partial layout)."""
+    from distributed_pytorch_example_amd.models import get_model
+    from distributed_pytorch_example_amd.ops import functional as Fx
+
+    torch.manual_seed(13)
+    base = get_model("resnet50").to(dev)
+    x = torch.randn(16, 3, 224, 224, device=dev)
+    y = torch.randint(0, 1000, (16,), device=dev)
+    outs = []
+    C.set_cu_reserve(reserve)
+    try:
+        for _ in range(2):
+            m = copy.deepcopy(base)
+            C.set_comm_active(reserve > 0)
+            loss = Fx.cross_entropy(m(x), y, 1000)
+            loss.backward()
+            C.set_comm_active(False)
+            torch.cuda.synchronize()
+            stats = [b.detach().clone() for n, b in m.named_buffers() if "running" in n]
+            bn_grads = [p.grad.detach().clone() for n, p in m.named_parameters() if ".bn." in n]
+            outs.append((loss.item(), stats, bn_grads))
+    finally:
+        C.set_comm_active(False)
+        C.set_cu_reserve(0)
+    (l1, s1, g1), (l2, s2, g2) = outs
+    assert l1 == l2
+    assert len(s1) == 2 * 53 and all(torch.equal(a, b) for a, b in zip(s1, s2))
+    assert all(torch.equal(a, b) for a, b in zip(g1, g2))
+
+
 def test_graph_replayed_step_matches_eager(C):
     """A whole SimpleNet training step (forward, fused CE, backward, fused Adam with its device-side
     step counters and hyper-parameters) captured once in a HIP graph and replayed == the same steps
