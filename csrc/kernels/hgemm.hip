@@ -258,9 +258,11 @@ __global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
       _Pragma("unroll") for (int i_ = 0; i_ < FMH; ++i_)                                     \
         if (i_ == wc) {                                                                      \
           _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_) {                                 \
-            const u32x4 q_ = __builtin_bit_cast(u32x4, af[i_][s_]);                          \
-            _Pragma("unroll") for (int e_ = 0; e_ < 4; ++e_)                                 \
-              rsum[hh] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, q_[e_]), ones2, rsum[hh], false); \
+            const bf16x8 q_ = af[i_][s_];                                                    \
+            rsum[hh] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(q_, q_, 0, 1), ones2, rsum[hh], false); \
+            rsum[hh] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(q_, q_, 2, 3), ones2, rsum[hh], false); \
+            rsum[hh] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(q_, q_, 4, 5), ones2, rsum[hh], false); \
+            rsum[hh] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(q_, q_, 6, 7), ones2, rsum[hh], false); \
           }                                                                                  \
         }                                                                                    \
     }                                                                                        \

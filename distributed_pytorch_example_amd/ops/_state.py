@@ -95,8 +95,14 @@ def grad_done(p: torch.Tensor, direct: bool) -> None:
 
 
 def note_use(p: torch.Tensor) -> None:
-    """Forward-side use counter so a weight used k times is 'ready' after k backward writes."""
-    if getattr(p, "_dpe_direct", False) and torch.is_grad_enabled():
+    """Forward-side use counter so a weight used k times is 'ready' after k backward writes.
+
+    Called from autograd Functions' forward, which always runs with grad mode off -- so the counter
+    must not depend on torch.is_grad_enabled() (it did: every counter stayed 0 and a tied weight such
+    as GPT-2's wte was announced ready after its FIRST backward write, letting its bucket's all-reduce
+    start before the second write; caught by the world-2 RCCL GPT-2 test).  DDP.forward resets the
+    counters before every training forward, so counts left by no-grad (eval) forwards are harmless."""
+    if getattr(p, "_dpe_direct", False):
         p._dpe_uses = getattr(p, "_dpe_uses", 0) + 1
 
 

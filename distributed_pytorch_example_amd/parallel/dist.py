@@ -324,6 +324,7 @@ def destroy_process_group() -> None:
     if _state["comm"] is not None:
         torch.cuda.synchronize()
         _state["comm"] = None
+        set_cu_budget(0)
     if dist.is_initialized():
         dist.destroy_process_group()
     _state["backend"] = None

@@ -72,7 +72,9 @@ def ensure_single_process_env() -> None:
     os.environ.setdefault("WORLD_SIZE", "1")
     os.environ.setdefault("LOCAL_WORLD_SIZE", "1")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    # world 1: port 0 lets the TCPStore server bind an OS-assigned port (a probed "free" port can be
+    # taken by another socket before the bind: EADDRINUSE, seen between back-to-back bench runs)
+    os.environ.setdefault("MASTER_PORT", "0" if os.environ.get("WORLD_SIZE") == "1" else str(_free_port()))
 
 
 def _free_port() -> int:
