@@ -59,7 +59,7 @@ int dpe_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
 int dpe_act(const void* a, const void* b, void* out, int64_t n, int op, int bf16, hipStream_t st);
 int dpe_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset, int bf16, hipStream_t st);
 int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, int vgprs, const unsigned* stop, float* sink,
-               hipStream_t st);
+               int sleepy, hipStream_t st);
 int dpe_hog_stop(unsigned* stop, unsigned v, hipStream_t st);
 int dpe_conv3x3_rows_blocks(int N, int H, int W);
 int64_t dpe_wgrad3x3_rows_scratch(int N, int H, int W);
@@ -1439,17 +1439,18 @@ void register_ops(pybind11::module& m) {
         py::arg("dw"), py::arg("db") = py::none(), py::arg("dx_out") = py::none());
   m.def("set_pw_stream", &set_pw_stream, "streaming pointwise-conv kernel on/off (pwconv.hip)");
   m.def("cu_hog", [](int64_t nblocks, int64_t threads, int64_t lds_bytes, double us, int64_t vgprs,
-                     const c10::optional<Tensor>& stop) {
+                     const c10::optional<Tensor>& stop, bool sleepy) {
           static Tensor sink = at::empty({1024}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA));
           const unsigned* sp = nullptr;
           if (stop.has_value() && stop->defined()) {
             TORCH_CHECK(stop->is_cuda() && stop->scalar_type() == at::kInt && stop->numel() >= 1, "cu_hog: stop is an int32 GPU tensor");
             sp = (const unsigned*)stop->data_ptr();
           }
-          CHECK_RC(dpe_cu_hog((int)nblocks, (int)threads, (int)lds_bytes, us, (int)vgprs, sp, (float*)sink.data_ptr(), cur_stream()),
+          CHECK_RC(dpe_cu_hog((int)nblocks, (int)threads, (int)lds_bytes, us, (int)vgprs, sp, (float*)sink.data_ptr(),
+                              sleepy ? 1 : 0, cur_stream()),
                    "cu_hog");
         }, py::arg("nblocks"), py::arg("threads") = 256, py::arg("lds_bytes") = 0, py::arg("us") = 1000.0,
-        py::arg("vgprs") = 8, py::arg("stop") = py::none(),
+        py::arg("vgprs") = 8, py::arg("stop") = py::none(), py::arg("sleepy") = false,
         "occupancy probe: nblocks workgroups holding a CU slot (threads, LDS, ~vgprs per lane) until stop[0] != 0 or `us` "
         "microseconds pass (current stream)");
   m.def("hog_stop", [](Tensor& stop, int64_t v) {

@@ -374,17 +374,21 @@ extern "C" int dpe_embedding_bwd(const int64_t* idx, const float* dout, float* d
 // channel workgroups sharing the CUs with backward kernels (scripts/hog_probe.py).  Every wave leaves
 // at the deadline, so a stop flag that is never set cannot hang the device.
 template <int V>
-__global__ __launch_bounds__(256) void cu_hog_kernel(int64_t ticks, const unsigned* stop, float* sink) {
+__global__ __launch_bounds__(256) void cu_hog_kernel(int64_t ticks, const unsigned* stop, float* sink, int sleepy) {
   extern __shared__ float lds[];
   const int64_t t0 = wall_clock64();
   float r[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) r[i] = (float)(threadIdx.x + i);
   while (wall_clock64() - t0 < ticks) {
+    if (sleepy) {  // resident but idle: slot occupancy only (an RCCL block waiting on its peers)
+      __builtin_amdgcn_s_sleep(127);
+    } else {       // VALU-saturating: slot occupancy plus issue-cycle contention (worst case)
 #pragma unroll 1
-    for (int k = 0; k < 16; ++k)
+      for (int k = 0; k < 16; ++k)
 #pragma unroll
-      for (int i = 0; i < V; ++i) r[i] = r[i] * 0.999f + 1.f;
+        for (int i = 0; i < V; ++i) r[i] = r[i] * 0.999f + 1.f;
+    }
     if (stop && __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
   }
   float acc = 0.f;
@@ -397,13 +401,13 @@ __global__ void hog_stop_kernel(unsigned* stop, unsigned v) {
   __hip_atomic_store(stop, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 extern "C" int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, int vgprs, const unsigned* stop, float* sink,
-                          hipStream_t st) {
+                          int sleepy, hipStream_t st) {
   if (nblocks <= 0 || threads <= 0 || threads > 256 || us <= 0 || us > 1e6) return -1;  // RCCL-sized: 256 threads
   const int64_t t = (int64_t)(us * 100.0);
-  if (vgprs <= 16) hipLaunchKernelGGL(cu_hog_kernel<8>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink);
-  else if (vgprs <= 64) hipLaunchKernelGGL(cu_hog_kernel<56>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink);
-  else if (vgprs <= 128) hipLaunchKernelGGL(cu_hog_kernel<120>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink);
-  else hipLaunchKernelGGL(cu_hog_kernel<136>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink);  // RCCL: 140
+  if (vgprs <= 16) hipLaunchKernelGGL(cu_hog_kernel<8>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink, sleepy);
+  else if (vgprs <= 64) hipLaunchKernelGGL(cu_hog_kernel<56>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink, sleepy);
+  else if (vgprs <= 128) hipLaunchKernelGGL(cu_hog_kernel<120>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink, sleepy);
+  else hipLaunchKernelGGL(cu_hog_kernel<136>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink, sleepy);  // RCCL: 140
   return (int)hipGetLastError();
 }
 extern "C" int dpe_hog_stop(unsigned* stop, unsigned v, hipStream_t st) {
