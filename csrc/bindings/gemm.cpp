@@ -18,6 +18,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <mutex>
+#include <unordered_map>
 
 #include "../kernels/hgemm.h"
 #include "../kernels/igemm.h"
@@ -49,6 +51,36 @@ constexpr double kBw = 4.0e12;    // slab write + finalize read bandwidth
 constexpr double kLaunch = 3.0e-6;
 
 int g_force_cfg = -1, g_force_splits = -1;
+bool g_dynamic = [] { const char* e = getenv("DPE_HGEMM_DYNAMIC"); return !(e && e[0] == '0'); }();  // A/B
+
+// Dynamic-schedule state of the persistent GEMM (hgemm.hip: 8 per-XCD claim counters + exit
+// counters), one zeroed buffer per (device, stream): launches on one stream are ordered, and the last
+// block of each launch resets the counters, so the buffer is reused without a per-call memset.
+// Launches on different streams may overlap and get different buffers.  A stream first seen while
+// it is being captured into a graph gets none (its zeroing memset would only run at replay): such a
+// launch uses the static schedule.
+unsigned* sched_buffer(hipStream_t st) {
+  if (!g_dynamic) return nullptr;
+  static std::mutex mu;
+  static std::unordered_map<uint64_t, unsigned*> bufs;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const uint64_t key = (uint64_t)(uintptr_t)st * 64 + (uint64_t)dev;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = bufs.find(key);
+  if (it != bufs.end()) return it->second;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  unsigned* b = nullptr;
+  TORCH_CHECK(hipMalloc(&b, dpe::HGEMM_SCHED_BYTES) == hipSuccess &&
+                  hipMemsetAsync(b, 0, dpe::HGEMM_SCHED_BYTES, st) == hipSuccess,
+              "hgemm: schedule buffer allocation failed");
+  bufs.emplace(key, b);
+  return b;
+}
 }  // namespace
 
 int num_cus() {
@@ -165,6 +197,7 @@ void launch_planned(dpe::HgemmArgs a, const Plan& pl, int ak, int bk, int epi, h
   a.splits = pl.splits;
   a.kps = pl.kps;
   if (a.group_m == 0) a.group_m = group_rows(pl);
+  a.sched = sched_buffer(cur_stream());
   Tensor ws;
   if (pl.splits > 1) {
     // one allocation: [splits][M][N] partial slabs (+ [splits][M] bias-gradient partials)
@@ -346,6 +379,7 @@ Tensor hgemm_raw(const Tensor& A, const Tensor& B, Tensor C, int64_t M, int64_t 
   a.splits = pl.splits;
   a.kps = pl.kps;
   a.group_m = group_m != 0 ? (int)group_m : group_rows(pl);
+  a.sched = sched_buffer(cur_stream());
   Tensor ws;
   if (pl.splits > 1) {
     const int64_t slab = (int64_t)pl.splits * M * N;
@@ -393,6 +427,9 @@ void register_gemm(pybind11::module& m) {
         "fp32 dw += alpha dy^T x");
   m.def("set_hgemm_force", [](int64_t cfg, int64_t splits) { g_force_cfg = (int)cfg; g_force_splits = (int)splits; },
         py::arg("cfg") = -1, py::arg("splits") = -1, "pin the planner's tile / split (-1: free); A/B testing only");
+  m.def("set_hgemm_dynamic", [](bool on) { const bool was = g_dynamic; g_dynamic = on; return was; }, py::arg("on"),
+        "persistent GEMM: claim units beyond the grid at run time (default) or round-robin them statically; "
+        "returns the previous setting");
 }
 
 }  // namespace dpe_gemm

@@ -15,6 +15,8 @@ enum HEpi : int {
 // act values beyond igemm.h's Act: gelu backward, C = (alpha*acc) * gelu'(aux_in)
 constexpr int HACT_GELU_BWD = 3;
 
+constexpr int HGEMM_SCHED_BYTES = 17 * 1024;  // 17 counters, one 1 KB line each (hgemm.hip)
+
 struct HgemmArgs {
   const uint16_t* A;        // bf16, K-contiguous A[m][k] (lda) or M-contiguous A[k][m] (lda)
   const uint16_t* B;        // bf16, K-contiguous B[n][k] (ldb) or N-contiguous B[k][n] (ldb)
@@ -36,6 +38,8 @@ struct HgemmArgs {
                             // zero-padded columns of a padded operand, stores stay inside M x N
   float* dbias;             // TN weight grads only: db[m] += alpha * sum_k A[k][m] (the bias gradient)
   float* ws_bias;           // dbias with splits > 1: [splits][M] partial row sums (summed by hgemm_finalize)
+  unsigned* sched;          // dynamic unit claims (HGEMM_SCHED_BYTES zeroed, self-resetting; one per stream),
+                            // or nullptr: static round-robin over the persistent grid
 };
 
 // Tile configurations (BMxBN, waves WRxWC).

@@ -53,6 +53,7 @@ constexpr int TK = 64;
 #ifndef HG_SCHED
 #define HG_SCHED 1
 #endif
+#define HG_SCHED_LINE 256  // words between two dynamic-schedule counters (hgemm.h HGEMM_SCHED_BYTES)
 
 template <int BM, int BN, int WR, int WC>
 struct Geo {
@@ -158,13 +159,16 @@ DPE_DEVICE float gelu_grad(float x) {
 // already hold in registers (wave wc takes fragment row-block wc, v_dot2 with ones: 8 VALU per half
 // image per K-tile), so dy is not streamed a second time by a column-sum kernel.
 template <int BM, int BN, int WR, int WC, bool AK, bool BK, int EPI, int ACT, bool BG = false>
-__global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
+// (4-wave tiles run 2 blocks per CU: 2 waves per SIMD, so at most 256 VGPRs + AGPRs per wave)
+__global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kernel(HgemmArgs p) {
   using G = Geo<BM, BN, WR, WC>;
   constexpr int NW = G::NW, RH = G::RH, CH = G::CH, FMH = G::FMH, FNH = G::FNH, GA = G::GA, GB = G::GB;
   constexpr int AHB = G::AHB, BHB = G::BHB;
   static_assert(AK || BM == 256, "M-contiguous A needs 128-column half images (BM = 256)");
   static_assert(BK || BN == 256, "N-contiguous B needs 128-column half images (BN = 256)");
-  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+  // + 16 B: the next-unit slot of the dynamic schedule (in the one LDS array: a second __shared__
+  // object can make the compiler drain vmcnt before the main loop's ds_reads)
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS + 16];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -172,9 +176,88 @@ __global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
   const bool late = NW == 8 && wid >= 4;  // second-dispatched half runs one barrier behind
   const int tilesM = (p.M + BM - 1) / BM, tilesN = (p.N + BN - 1) / BN;
   const int ntile = tilesM * tilesN, nunits = ntile * p.splits;
-  int u = xcd_remap(blockIdx.x, gridDim.x);
-  if (u >= nunits) return;
   const float alpha = p.alpha * (p.alpha_ptr ? *p.alpha_ptr : 1.f);
+
+  // Schedule.  Without p.sched (or with one round of units) block b computes units
+  // xcd_remap(b), +grid, +2 grid, ...  With p.sched and more units than blocks, the leading 7/8 of
+  // the grid start on static units (no claim latency at launch) and every other unit is claimed at
+  // run time from 8 per-XCD queues (umap below), stealing from the other queues when its own is
+  // empty.  So a block whose CU is shared with foreign work (RCCL channel blocks, another
+  // stream's kernel) computes fewer units, and the grid's tail -- the blocks the dispatcher cannot
+  // place while foreign workgroups hold slots -- holds no unit hostage: by the time it is placed the
+  // queues are usually drained and it exits at once.  The claim for a block's next unit is issued
+  // during the current unit's third-to-last K-tile and consumed after its main loop, so its latency
+  // overlaps MFMA work.  No unit depends on which block computes it (no cross-unit reduction): outputs are
+  // bitwise independent of the schedule.
+  const int G0 = gridDim.x;
+  const bool dsched = p.sched != nullptr && nunits > G0;
+  const int S = dsched ? (G0 - G0 / 8) & ~7 : G0;  // blocks [0, S) start on a static unit
+  const int dyn = dsched ? nunits - S : 0;         // units [S, nunits) are claimed
+  const int xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;  // hwreg(HW_REG_XCC_ID, 0, 4)
+  // counters, each on a 1 KB line of its own (HG_SCHED_LINE words apart): [0, 8) claim queues,
+  // [8, 16) exit counts per block group b % 8, 16 the groups done.  (Packed in one cache line, all
+  // claims of the chip serialise on one memory-side atomic unit.)
+  auto ctr = [&](int k) { return p.sched + k * HG_SCHED_LINE; };
+  // queue q's j-th ticket: chunk (j / CK) * 8 + q of CK = grid/8 consecutive claimed units -- XCD q
+  // takes the q-th eighth of every grid-sized stretch of the grouped unit order, as under the static
+  // round-robin (its blocks in flight share A rows / B columns in its L2)
+  const unsigned CK = (unsigned)max(1, G0 >> 3);
+  auto umap = [&](int q, unsigned j) -> int64_t { return S + ((int64_t)(j / CK) * 8 + q) * CK + (j % CK); };
+  int claim_v = 0;  // wave 0 lane 0: the in-flight fetch_add of its own queue
+  const int claimer = dyn > 0 && wid == 0 && lane == 0;
+  int* const slot = (int*)(smem + G::LDS);
+  // wave 0: the unit for own-queue ticket c0, else one stolen from another queue, else -1
+  auto resolve = [&](int c0) -> int {
+    if (umap(xcc, (unsigned)c0) < nunits) return (int)umap(xcc, (unsigned)c0);
+    // (the opaque copy keeps the lane-dependent values below from being hoisted out of the unit
+    // loop, where they would stay live -- and spill -- across every unit's main loop)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    while (true) {  // each pass either claims or sees every queue drained
+      const int q = (xcc + ln) & 7;
+      unsigned c = 0xffffffffu;
+      if (ln < 8) c = __hip_atomic_load(ctr(q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t has = __ballot(ln < 8 && umap(q, c) < nunits);
+      if (!has) return -1;
+      const int pick = (xcc + (int)__builtin_ctzll(has)) & 7;
+      int w = 0;
+      if (ln == 0) w = (int)__hip_atomic_fetch_add(ctr(pick), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      w = __builtin_amdgcn_readfirstlane(w);
+      if (umap(pick, (unsigned)w) < nunits) return (int)umap(pick, (unsigned)w);
+    }
+  };
+  // the last block out resets every counter for the next launch on this stream (every block's final,
+  // failed claim precedes its exit count, so no claim can follow the reset).  Exits are counted per
+  // block group b % 8 (sizes known exactly, whatever the placement), then per group.
+  auto sched_exit = [&]() {
+    if (dyn > 0 && wid == 0 && lane == 0) {
+      const int g = blockIdx.x & 7;
+      const unsigned in_g = (unsigned)(G0 - g + 7) / 8u;
+      if (__hip_atomic_fetch_add(ctr(8 + g), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_g - 1u &&
+          __hip_atomic_fetch_add(ctr(16), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)min(G0, 8) - 1u)
+        for (int k = 0; k <= 16; ++k) __hip_atomic_store(ctr(k), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+
+  int u;
+  if ((int)blockIdx.x < S) {
+    u = xcd_remap(blockIdx.x, S);
+    if (u >= nunits) return;  // (the planner's grid never exceeds the unit count)
+  } else {
+    if (wid == 0) {
+      int c0 = 0;
+      if (lane == 0) c0 = (int)__hip_atomic_fetch_add(ctr(xcc), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int nx = resolve(__builtin_amdgcn_readfirstlane(c0));
+      if (lane == 0) *slot = nx;
+    }
+    __syncthreads();
+    u = __builtin_amdgcn_readfirstlane(*slot);
+    __syncthreads();  // the slot is rewritten before this unit's epilogue
+    if (u < 0) {
+      sched_exit();
+      return;
+    }
+  }
 
   const char* const Ab = (const char*)p.A;
   const char* const Bb = (const char*)p.B;
@@ -337,6 +420,17 @@ __global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
 
       LOAD_B(b, 1);
       if (h2) STAGE_A(0, b, t + 2);
+      {
+        // the next unit's claim, consumed after the main loop: issued behind A0(t+2), fewer DMAs than
+        // this tile's counted wait keeps in flight are younger than it, so it may stay in flight until
+        // the drain (wait_vm<0>) of tile nt-2 -- about six phases (claimer goes through an empty asm
+        // every iteration: the loop must not be unswitched on it, a second loop copy for wave 0
+        // would double the hot loop's instruction footprint)
+        int cl = claimer;
+        asm volatile("" : "+v"(cl));
+        if (t == (nt >= 3 ? nt - 3 : 0) && cl)
+          claim_v = (int)__hip_atomic_fetch_add(ctr(xcc), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       HG_BARRIER();
       MFMAQ(0, 1);
@@ -401,13 +495,22 @@ __global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
       HG_BARRIER();
     }
 #endif
+    // resolve the next unit (wave 0; its result reaches the other waves through the LDS slot and the
+    // barrier below: the late waves' last loop barrier pairs with this rebalance barrier)
+    if (dyn > 0 && wid == 0) {
+      const int nx = resolve(__builtin_amdgcn_readfirstlane(claim_v));  // lane 0 (the wave is whole here)
+      if (lane == 0) *slot = nx;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // s_barrier does not wait for the ds_write
+    }
     if (!late) HG_BARRIER();  // rebalance the stagger: every wave is past its last LDS read
 
     // ------------------------------------------------------------ epilogue
     // acc[i][j][e]: row m0 + wr*(BM/WR) + (i/FMH)*RH + (i%FMH)*16 + lm,
     //               col n0 + wc*(BN/WC) + (j/FNH)*CH + (j%FNH)*16 + ln4 + e
     const int rbase = m0 + wr * (BM / WR) + lm, cbase = n0 + wc * (BN / WC) + ln4;
-    const int next = u + gridDim.x;
+    // (readfirstlane: the value is uniform; keeping it scalar keeps the tile indexing in SGPRs)
+    const int next = dyn > 0 ? __builtin_amdgcn_readfirstlane(*slot)
+                             : (u + (int)gridDim.x < nunits ? u + (int)gridDim.x : -1);
     const int cur_split = split;
 
     // 0) bias gradient: the 4 lane groups hold k-slices of the same 16 rows
@@ -504,7 +607,7 @@ __global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
     }
 
     // 2) the next unit's prologue DMA (LDS is free: every wave passed the rebalance barrier)
-    if (next < nunits) {
+    if (next >= 0) {
       u = next;
       decode(u);
       PROLOGUE();
@@ -549,10 +652,11 @@ __global__ __launch_bounds__(WR * WC * 64) void hgemm_kernel(HgemmArgs p) {
         }
       }
     }
-    if (next >= nunits) break;
+    if (next < 0) break;
     wait_vm<0>();
     HG_BARRIER();
   }
+  sched_exit();
 #undef STAGE_A
 #undef STAGE_B
 #undef PROLOGUE

@@ -31,7 +31,11 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 # single-issue VALU (no NaN-quieting canonicalisation v_max before each fmaxf, no SLP packing into
 # v_pk_*_f32, which costs extra issue cycles beside MFMAs) -- without inline asm, whose
 # operands would miss the compiler's hazard wait states.  NaN inputs are not honoured there.
-FILE_FLAGS = {"attn.hip": ["-fno-slp-vectorize", "-fno-honor-nans"]}
+# hgemm.hip: the schedule's claim atomics are issued by one lane and consumed phases later; the
+# atomic optimizer rewrites a uniform-address add into a wave-wide add plus a per-lane offset
+# (readfirstlane of the result), which puts a vmcnt(0) wait right behind the atomic.
+FILE_FLAGS = {"attn.hip": ["-fno-slp-vectorize", "-fno-honor-nans"],
+              "hgemm.hip": ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]}
 
 
 def _torch_dirs():

@@ -167,3 +167,92 @@ def test_hgemm_plan_cu_budget():
     finally:
         C.set_comm_active(False)
         C.set_cu_reserve(0)
+
+
+def _nt(C, A, B, out, M, N, K, splits=1):
+    C.hgemm(A, B, out, M, N, K, K, K, N, True, True, 1, 0, None, None, None, None, 1.0, -1, splits)
+
+
+@pytest.mark.parametrize("splits", [1, 3])
+def test_hgemm_dynamic_schedule_bitwise_equals_static(splits):
+    """Units beyond the persistent grid are claimed at run time from per-XCD queues (hgemm.hip).  A
+    unit's result does not depend on the block that computes it, so the dynamic and the static
+    round-robin schedule give identical bits -- with the full grid, with a CU budget (more rounds),
+    for repeated launches on one stream (the counters reset themselves), for two streams at once, and
+    for a graph replay."""
+    C = ext()
+    g = torch.Generator(device=DEV).manual_seed(6)
+    M, N, K = 8192, 2304, 768  # 288 tiles of 256^2: more units than slots
+    A = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    B = torch.randn(N, K, device=DEV, generator=g).bfloat16()
+    ref = torch.empty(M, N, device=DEV)
+    was = C.set_hgemm_dynamic(False)
+    try:
+        _nt(C, A, B, ref, M, N, K, splits)
+        C.set_hgemm_dynamic(True)
+        for reserve in (0, 64):
+            C.set_cu_reserve(reserve)
+            C.set_comm_active(reserve > 0)
+            for _ in range(4):
+                out = torch.full((M, N), float("nan"), device=DEV)
+                _nt(C, A, B, out, M, N, K, splits)
+                assert torch.equal(out, ref), reserve
+        C.set_comm_active(False)
+        C.set_cu_reserve(0)
+        # two streams at once (each has its own claim counters)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        o1, o2 = torch.empty_like(ref), torch.empty_like(ref)
+        torch.cuda.synchronize()
+        for _ in range(3):
+            with torch.cuda.stream(s1):
+                _nt(C, A, B, o1, M, N, K, splits)
+            with torch.cuda.stream(s2):
+                _nt(C, A, B, o2, M, N, K, splits)
+        torch.cuda.synchronize()
+        assert torch.equal(o1, ref) and torch.equal(o2, ref)
+        # graph capture on a stream that already has its counters: replays reuse them
+        gs = torch.cuda.Stream()
+        og = torch.empty_like(ref)
+        with torch.cuda.stream(gs):
+            _nt(C, A, B, og, M, N, K, splits)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=gs):
+            _nt(C, A, B, og, M, N, K, splits)
+        for _ in range(3):
+            og.fill_(float("nan"))
+            graph.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(og, ref)
+    finally:
+        C.set_comm_active(False)
+        C.set_cu_reserve(0)
+        C.set_hgemm_dynamic(was)
+
+
+def test_hgemm_dynamic_schedule_with_resident_foreign_blocks():
+    """Foreign workgroups (the RCCL-sized hog of scripts/hog_probe.py) occupy CU slots while a
+    multi-round GEMM runs: the blocks that share a CU claim fewer units; the result is unchanged."""
+    C = ext()
+    g = torch.Generator(device=DEV).manual_seed(7)
+    M, N, K = 8192, 3072, 768
+    A = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    B = torch.randn(N, K, device=DEV, generator=g).bfloat16()
+    ref = torch.empty(M, N, device=DEV)
+    was = C.set_hgemm_dynamic(False)
+    try:
+        _nt(C, A, B, ref, M, N, K)
+        C.set_hgemm_dynamic(True)
+        stop = torch.zeros(1, dtype=torch.int32, device=DEV)
+        side = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(side):
+            C.cu_hog(32, 256, 19968, 200000.0, 136, stop, False)  # bounded: 200 ms
+        out = torch.empty_like(ref)
+        for _ in range(3):
+            _nt(C, A, B, out, M, N, K)
+        C.hog_stop(stop, 1)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+    finally:
+        C.set_hgemm_dynamic(was)
