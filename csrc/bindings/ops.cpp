@@ -62,11 +62,12 @@ int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, int vgprs, co
                int sleepy, hipStream_t st);
 int dpe_hog_stop(unsigned* stop, unsigned v, hipStream_t st);
 int dpe_conv3x3_rows_blocks(int N, int H, int W);
-int64_t dpe_wgrad3x3_rows_scratch(int N, int H, int W);
-int dpe_wgrad3x3_rows_launch(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H, int W,
+int dpe_wgrad3x3_rows_blocks(int N, int H, int W);
+int64_t dpe_wgrad3x3_rows_scratch(int nb);
+int dpe_wgrad3x3_rows_launch(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H, int W, int nb,
                              float alpha, const float* in_coef, hipStream_t st);
 int dpe_conv3x3_rows_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* st_x,
-                            const float* st_coef, int N, int H, int W, int bnb, const float* in_coef, hipStream_t st);
+                            const float* st_coef, int N, int H, int W, int nb, int bnb, const float* in_coef, hipStream_t st);
 int dpe_stem_blocks(int N, int H, int W);
 int64_t dpe_stem_wgrad_scratch(int N, int H, int W);
 int dpe_stem_wgrad_launch(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H, int W,
@@ -577,7 +578,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
     const int nb = dpe_conv3x3_rows_blocks(g.N, g.H, g.W);
     if (want_stats) stats = at::empty({2, g.K, nb}, x.options().dtype(at::kFloat));
     CHECK_RC(dpe_conv3x3_rows_launch(bp(x), bp(w), bpm(y), want_stats ? fp(stats) : nullptr, nullptr, nullptr, g.N, g.H,
-                                     g.W, 0, icoef, cur_stream()),
+                                     g.W, nb, 0, icoef, cur_stream()),
              "conv3x3 rows fwd");
     return {y, stats};
   }
@@ -714,7 +715,7 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
       const int nb = dpe_conv3x3_rows_blocks(f.N, f.H, f.W);
       if (want_bn) part = at::empty({2, g.C, nb}, dy.options().dtype(at::kFloat));
       CHECK_RC(dpe_conv3x3_rows_launch(bp(dy), bp(wt), bpm(dx), want_bn ? fp(part) : nullptr, a.st_x, a.st_coef, f.N, f.H,
-                                       f.W, want_bn ? 1 : 0, nullptr, cur_stream()),
+                                       f.W, nb, want_bn ? 1 : 0, nullptr, cur_stream()),
                "conv3x3 rows dgrad");
       return {dx, part};
     }
@@ -827,7 +828,8 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64
   a.alpha = (float)alpha;
   // 64 -> 64 3x3 (ResNet layer 1): the row-walking weight-grad kernel (rowconv.hip)
   const float* icoef = fpo(in_coef);
-  const bool row = rowconv_geom(g) && dpe_wgrad3x3_rows_scratch(g.N, g.H, g.W) > 0;
+  const int row_nb = rowconv_geom(g) ? dpe_wgrad3x3_rows_blocks(g.N, g.H, g.W) : 0;  // (depends on the CU budget)
+  const bool row = row_nb > 0;
   if (icoef && !row) {
     // 1x1 weight grad over a pre-BN input: the LDS-DMA weight-grad kernel applies BN + ReLU to its
     // B fragments (b_coef); outside that kernel's envelope there is no such path
@@ -837,8 +839,8 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64
     return;
   }
   if (row && (row_wgrad_on() || icoef)) {
-    auto scratch = at::empty({dpe_wgrad3x3_rows_scratch(g.N, g.H, g.W)}, dw.options());
-    CHECK_RC(dpe_wgrad3x3_rows_launch(bp(x), bp(dy), fp(dw), fp(scratch), g.N, g.H, g.W, (float)alpha, icoef,
+    auto scratch = at::empty({dpe_wgrad3x3_rows_scratch(row_nb)}, dw.options());
+    CHECK_RC(dpe_wgrad3x3_rows_launch(bp(x), bp(dy), fp(dw), fp(scratch), g.N, g.H, g.W, row_nb, (float)alpha, icoef,
                                       cur_stream()),
              "wgrad3x3_rows");
     return;
@@ -1358,7 +1360,7 @@ void register_ops(pybind11::module& m) {
           g.dh = (int)dil[0]; g.dw = (int)dil[1];
           g.OH = (g.H + 2 * g.ph - g.dh * (g.R - 1) - 1) / g.sh + 1;
           g.OW = (g.W + 2 * g.pw - g.dw * (g.S - 1) - 1) / g.sw + 1;
-          return ws[3] == xs[3] && rowconv_geom(g) && dpe_wgrad3x3_rows_scratch(g.N, g.H, g.W) > 0;
+          return ws[3] == xs[3] && rowconv_geom(g) && dpe_wgrad3x3_rows_blocks(g.N, g.H, g.W) > 0;
         }, py::arg("x_shape"), py::arg("w_shape"), py::arg("stride"), py::arg("pad"), py::arg("dil"));
   m.def("pw_bn_on_load", [](std::vector<int64_t> xs, int64_t cout) {
           // a 1x1 / stride-1 conv over a pre-BN input [N, H, W, C]: the streaming pointwise forward and the

@@ -7,7 +7,8 @@
 // 72 KiB filter (profiles/pmc_conv3_r2.txt).  A tile-local halo in LDS (the filter in LDS too)
 // measured slower: > 80 KiB per block left one block per CU with no overlap (docs/perf_notes.md).
 // Here, as in the stem kernel (stem.hip):
-//   * a block owns consecutive output rows of one image; wave (mh, nh) holds output channels
+//   * a block owns a contiguous range of the N*H output rows (one segment per image it touches; one
+//     block per resident slot, rows_grid below); wave (mh, nh) holds output channels
 //     32 nh .. +31 of the filter in VGPRs (18 K-steps x 2 fragments, 144 VGPRs) for the whole block;
 //   * the three input rows an output row needs sit in a 4-slot LDS ring ([W + 2][64 ch], 16-B
 //     chunks XOR-swizzled by pixel, zero pixels at both ends); each input row is read from HBM once
@@ -18,6 +19,8 @@
 //     coefficients), accumulated per thread and reduced once per block ([2][64][blocks]).
 // One barrier per output row.  Same K order as the implicit GEMM (tap-major, 32-channel halves), so
 // the stored output is bitwise identical to it.
+#include <algorithm>
+
 #include "common.h"
 
 namespace dpe {
@@ -51,7 +54,7 @@ struct RowArgs {
   float* stats;           // [2][64][blocks] or nullptr
   const uint16_t* st_x;   // BNB: pre-BN input [N][H][W][64]
   const float* st_coef;   // BNB: [4][64] scale, shift, mean, invstd
-  int N, H, W, parts;
+  int N, H, W;
   const float* in_coef;   // INBN: x is the pre-BN tensor; the operand is relu(x * in_coef[c] + in_coef[64 + c])
 };
 
@@ -65,8 +68,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_rows_kernel(RowArgs p) {
   const int mh = wid & 1, nh = wid >> 1;  // pixels 32 mh .. +31, channels 32 nh .. +31
   const int H = p.H, W = p.W;
   const int blk = blockIdx.x;
-  const int n = blk / p.parts, part = blk - n * p.parts;
-  const int oh_beg = (int)((int64_t)H * part / p.parts), oh_end = (int)((int64_t)H * (part + 1) / p.parts);
   const int lm = lane & 15, kc = lane >> 4;
 
   // filter fragments: output channel 32 nh + 16 j + lm, K elements 32 ks + 8 kc .. +7
@@ -80,7 +81,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_rows_kernel(RowArgs p) {
   for (int i = tid; i < NSLOT * SLOT / 16; i += 256) *(u32x4*)(ring + i * 16) = zero16();
 
   // one input row = W pixels x 8 chunks (<= 512): thread t owns chunks t and t + 256
-  const int64_t img = (int64_t)n * H * W * 64;
+  int n = 0;
+  int64_t img = 0;
   const int nch = W * 8;
   auto load_row = [&](int ih, u32x4 (&v)[2]) {
 #pragma unroll
@@ -113,21 +115,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_rows_kernel(RowArgs p) {
       }
     }
   };
-  __syncthreads();
-  {
-    u32x4 t0[2], t1[2], t2[2];
-    load_row(oh_beg - 1, t0);
-    load_row(oh_beg, t1);
-    load_row(oh_beg + 1, t2);
-    write_row(oh_beg - 1, t0);
-    write_row(oh_beg, t1);
-    write_row(oh_beg + 1, t2);
-  }
-  u32x4 pf0[2], pf1[2];
-  load_row(oh_beg + 2, pf0);
-  load_row(oh_beg + 3, pf1);
-  __syncthreads();
-
   // store-phase channel chunk of this thread and its BN coefficients
   const int sc = tid & 7;
   float s[8], ss[8], bsc[8], bsh[8], bmu[8];
@@ -143,6 +130,32 @@ __global__ __launch_bounds__(256, 2) void conv3x3_rows_kernel(RowArgs p) {
   }
   // this wave's pixel fragments: 32 mh + 16 i + lm (rows >= W compute on zero pixels, never stored)
   const int nfr = min(2, max(0, (W - 32 * mh + 15) / 16));
+
+  // The block owns output rows [r0, r1) of the N*H rows (image-major), one segment per image it
+  // touches; the ring's zero pixels persist, every data pixel of a slot is rewritten per row.
+  const int64_t T = (int64_t)p.N * H;
+  int64_t r0 = T * blk / gridDim.x;
+  const int64_t r1 = T * (blk + 1) / gridDim.x;
+  for (; r0 < r1;) {
+  n = (int)(r0 / H);
+  img = (int64_t)n * H * W * 64;
+  const int oh_beg = (int)(r0 - (int64_t)n * H);
+  const int oh_end = (int)min<int64_t>(H, oh_beg + (r1 - r0));
+  r0 += oh_end - oh_beg;
+  __syncthreads();  // the previous segment's last stores have read the output buffers
+  {
+    u32x4 t0[2], t1[2], t2[2];
+    load_row(oh_beg - 1, t0);
+    load_row(oh_beg, t1);
+    load_row(oh_beg + 1, t2);
+    write_row(oh_beg - 1, t0);
+    write_row(oh_beg, t1);
+    write_row(oh_beg + 1, t2);
+  }
+  u32x4 pf0[2], pf1[2];
+  load_row(oh_beg + 2, pf0);
+  load_row(oh_beg + 3, pf1);
+  __syncthreads();
 
   for (int oh = oh_beg; oh < oh_end; ++oh) {
     f32x4 acc[2][2];
@@ -218,6 +231,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_rows_kernel(RowArgs p) {
       }
     }
   }
+  }  // segments
   if (p.stats) {
 #pragma unroll
     for (int e = 0; e < 8; ++e)
@@ -252,13 +266,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_rows_kernel(RowArgs p) {
 // for the same 64 -> 64 3x3 / stride-1 / pad-1 layer.  As a GEMM this is M = 64, N = 576 (9 taps x
 // 64), K = the 1.6 M output pixels at batch 512; the im2col weight-grad tile (igemm_wgrad_dma,
 // 64x128) reads every activation once per tap through L2 and ran at ~320 TF (365 us).  Here a
-// block walks the output rows of one image and keeps the whole 64 x 576 gradient of that image in
-// registers: wave w owns input channels 16 w .. +15 for all 9 taps and all 64 output channels
+// block walks a contiguous range of output rows (a slot's share of the N*H rows) and keeps the
+// whole 64 x 576 gradient of its rows in registers: wave w owns input channels 16 w .. +15 for all 9 taps and all 64 output channels
 // (4 x 9 accumulator tiles, 144 VGPRs).  Per output row the dy row (K = pixels, M = co) and the three
 // x rows (K = pixels shifted by the tap column, N = ci) are LDS images read with the transposing
 // ds_read_b64_tr_b16, so each input row is read from HBM once per block.  The block's gradient is
 // stored as one coalesced fp32 partial ([blocks][64 x 576], in accumulator order) and a second
-// kernel sums the partials into dW (fp32 atomics across 16 partial groups).
+// kernel sums the partials into dW in a fixed order (16 group sums, then their sum).
 namespace wg {
 constexpr int XSLOT = 66 * 128;              // x row: zero pixel, W (<= 64) pixels, zero pixels
 constexpr int DSLOT = 64 * 128;              // dy row: W pixels, zero rows up to 64
@@ -290,15 +304,14 @@ DPE_DEVICE bf16x8 trfrag(const char* img, int row0, int c0) {
 template <bool INBN>
 __global__ __launch_bounds__(256, 2) void wgrad3x3_rows_kernel(const uint16_t* __restrict__ x,
                                                                const uint16_t* __restrict__ dy,
-                                                               float* __restrict__ part, int H, int W,
+                                                               float* __restrict__ part, int N, int H, int W,
                                                                const float* __restrict__ in_coef) {
   __shared__ __attribute__((aligned(16))) char smem[LDS];
   char* const ring = smem;                     // x rows: input row ih in slot (ih + 1) % 4
   char* const dbuf = smem + NSLOT * XSLOT;     // dy rows: output row oh in slot oh & 1
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // input channels 16 w .. +15
-  const int n = blockIdx.x;
-  const int64_t img = (int64_t)n * H * W * 64;
+  int64_t img = 0;
   const int nch = W * 8;
 
   for (int i = tid; i < LDS / 16; i += 256) *(u32x4*)(smem + i * 16) = zero16();
@@ -337,31 +350,13 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_rows_kernel(const uint16_t* _
     }
     put(xslot(ih), 1, v);
   };
-  __syncthreads();
-  {
-    u32x4 t0[2], t1[2], t2[2];
-    load(x, -1, t0);
-    load(x, 0, t1);
-    load(dy, 0, t2);
-    putx(-1, t0);
-    putx(0, t1);
-    put(dbuf, 0, t2);
-    load(x, 1, t0);
-    putx(1, t0);
-  }
-  u32x4 px0[2], px1[2], pd0[2], pd1[2];  // prefetch: x rows oh + 2, oh + 3; dy rows oh + 1, oh + 2
-  load(x, 2, px0);
-  load(x, 3, px1);
-  load(dy, 1, pd0);
-  load(dy, 2, pd1);
-  __syncthreads();
-
   f32x4 acc[4][9];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nks = W > 32 ? 2 : 1;  // 32-pixel K-steps per row (pixels >= W are zero rows of dy)
+  u32x4 px0[2], px1[2], pd0[2], pd1[2];  // prefetch: x rows oh + 2, oh + 3; dy rows oh + 1, oh + 2
 
   // one output row; pxA / pdA hold x row oh + 2 / dy row oh + 1 and are refilled in place with rows
   // oh + 4 / oh + 3 (two rows per loop trip with two buffer sets: a prefetch is first waited on two
@@ -388,22 +383,57 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_rows_kernel(const uint16_t* _
     load(dy, oh + 3, pdA);
     __syncthreads();
   };
-  for (int oh = 0; oh < H; oh += 2) {
-    step(oh, px0, pd0);
-    if (oh + 1 < H) step(oh + 1, px1, pd1);
+  // The block owns output rows [r0, r1) of the N*H rows (image-major), one segment per image it
+  // touches (dy rows outside the segment are never stepped on, so no row is counted twice).
+  const int64_t T = (int64_t)N * H;
+  int64_t r0 = T * blockIdx.x / gridDim.x;
+  const int64_t r1 = T * (blockIdx.x + 1) / gridDim.x;
+  while (r0 < r1) {
+    const int n = (int)(r0 / H);
+    img = (int64_t)n * H * W * 64;
+    const int oh_beg = (int)(r0 - (int64_t)n * H);
+    const int oh_end = (int)min<int64_t>(H, oh_beg + (r1 - r0));
+    r0 += oh_end - oh_beg;
+    __syncthreads();  // every wave is done with the previous segment's slots
+    {
+      u32x4 t0[2], t1[2], t2[2];
+      load(x, oh_beg - 1, t0);
+      load(x, oh_beg, t1);
+      load(dy, oh_beg, t2);
+      putx(oh_beg - 1, t0);
+      putx(oh_beg, t1);
+      put(dbuf + (oh_beg & 1) * DSLOT, 0, t2);
+      load(x, oh_beg + 1, t0);
+      putx(oh_beg + 1, t0);
+    }
+    load(x, oh_beg + 2, px0);
+    load(x, oh_beg + 3, px1);
+    load(dy, oh_beg + 1, pd0);
+    load(dy, oh_beg + 2, pd1);
+    __syncthreads();
+    for (int oh = oh_beg; oh < oh_end; oh += 2) {
+      step(oh, px0, pd0);
+      if (oh + 1 < oh_end) step(oh + 1, px1, pd1);
+    }
   }
   // acc[m][t][e]: co = 16 m + (lane & 15), ci = 16 w + 4 (lane >> 4) + e, tap t
-  float* pb = part + (int64_t)n * PART;
+  float* pb = part + (int64_t)blockIdx.x * PART;
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int t = 0; t < 9; ++t) *(f32x4*)(pb + (((m * 9 + t) * 4 + w) * 64 + lane) * 4) = acc[m][t];
 }
 
-// dW [64][3][3][64] += alpha * sum of the partials; grid (PART / 1024, groups), 256 threads: one
-// float4 of accumulator order per thread over nparts / groups partials
-__global__ __launch_bounds__(256) void wgrad3x3_rows_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw,
-                                                                   int nparts, int per, float alpha) {
+// dW [64][3][3][64] += alpha * sum of the block partials, in a fixed order (bitwise reproducible):
+// stage 1, grid (PART / 1024, groups): group g sums partials [g * per, (g + 1) * per) into gsum[g]
+// (or, with one group, straight into dW); stage 2, grid PART / 1024: dW += alpha * sum_g gsum[g].
+// One thread per float4 of accumulator order; every dW element has one writer.
+DPE_DEVICE float* dw_elem(float* dw, int q) {
+  const int lane = q & 63, w = (q >> 6) & 3, mt = q >> 8, t = mt % 9, m = mt / 9;
+  return dw + (16 * m + (lane & 15)) * 576 + t * 64 + 16 * w + 4 * (lane >> 4);
+}
+__global__ __launch_bounds__(256) void wgrad3x3_rows_reduce_kernel(const float* __restrict__ part, float* __restrict__ gsum,
+                                                                   float* __restrict__ dw, int nparts, int per, float alpha) {
   const int q = blockIdx.x * 256 + threadIdx.x;  // float4 index, < PART / 4
   const int b0 = blockIdx.y * per, b1 = min(nparts, b0 + per);
   f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0;
@@ -415,52 +445,99 @@ __global__ __launch_bounds__(256) void wgrad3x3_rows_reduce_kernel(const float* 
   }
   if (b < b1) s0 += src[(int64_t)b * (PART / 4)];
   s0 += s1;
-  const int lane = q & 63, w = (q >> 6) & 3, mt = q >> 8, t = mt % 9, m = mt / 9;
-  float* d = dw + (16 * m + (lane & 15)) * 576 + t * 64 + 16 * w + 4 * (lane >> 4);
+  if (gridDim.y > 1) {
+    ((f32x4*)gsum)[(int64_t)blockIdx.y * (PART / 4) + q] = s0;
+    return;
+  }
+  float* d = dw_elem(dw, q);
 #pragma unroll
-  for (int e = 0; e < 4; ++e) atomicAdd(d + e, alpha * s0[e]);
+  for (int e = 0; e < 4; ++e) d[e] += alpha * s0[e];
+}
+__global__ __launch_bounds__(256) void wgrad3x3_rows_sum_kernel(const float* __restrict__ gsum, float* __restrict__ dw,
+                                                                int groups, float alpha) {
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  f32x4 s = ((const f32x4*)gsum)[q];
+  for (int g = 1; g < groups; ++g) s += ((const f32x4*)gsum)[(int64_t)g * (PART / 4) + q];
+  float* d = dw_elem(dw, q);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) d[e] += alpha * s[e];
 }
 }  // namespace wg
 }  // namespace rowconv
 }  // namespace dpe
 
-// Blocks of the launch for an [N, H, W, 64] input (0: outside the kernel's envelope).
+extern "C" int dpe_cu_reserve();  // comm.cpp: slots left to in-flight collectives
+
+namespace {
+int rows_slots() {  // resident blocks of the row-walking kernels (2 per CU), minus the CU budget
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+      (void)hipGetLastError();
+      n = 256;
+    }
+    return n > 0 ? n : 256;
+  }();
+  return max(2, 2 * ncu - dpe_cu_reserve());
+}
+// One block per resident slot, each owning a contiguous range of the N*H output rows (>= 16 rows):
+// a single wave of blocks whatever the CU budget -- a fixed N*2 grid went from exactly 2 waves to
+// 2 + a sliver when RCCL channel blocks held 16 slots (x1.4-1.6, profiles/cu_hog_probe_r3.txt).
+int rows_grid(int N, int H) { return (int)std::max<int64_t>(1, std::min<int64_t>(rows_slots(), (int64_t)N * H / 16)); }
+}  // namespace
+
+// Blocks of the launch for an [N, H, W, 64] input (0: outside the kernel's envelope).  Depends on the
+// CU budget in force: compute it once per launch and pass it to dpe_conv3x3_rows_launch.
 extern "C" int dpe_conv3x3_rows_blocks(int N, int H, int W) {
   if (N <= 0 || H < 2 || W < 1 || W > 64) return 0;
-  return N * 2;
+  return rows_grid(N, H);
 }
 
-// y = conv3x3(x, w) (stride 1, pad 1, 64 -> 64 channels); bnb: stats are the BN-backward partials
-// of the BN with pre-BN input st_x and coefficients st_coef, else the BN-forward sums of y.
-// in_coef (forward only, not with bnb): x is the pre-BN tensor of a BatchNorm+ReLU, applied on load.
+// y = conv3x3(x, w) (stride 1, pad 1, 64 -> 64 channels) on nb blocks (dpe_conv3x3_rows_blocks); bnb:
+// stats ([2][64][nb]) are the BN-backward partials of the BN with pre-BN input st_x and coefficients
+// st_coef, else the BN-forward sums of y.  in_coef (forward only, not with bnb): x is the pre-BN
+// tensor of a BatchNorm+ReLU, applied on load.
 extern "C" int dpe_conv3x3_rows_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* st_x,
-                                       const float* st_coef, int N, int H, int W, int bnb, const float* in_coef,
+                                       const float* st_coef, int N, int H, int W, int nb, int bnb, const float* in_coef,
                                        hipStream_t st) {
-  const int nb = dpe_conv3x3_rows_blocks(N, H, W);
-  if (nb <= 0 || (bnb && (!stats || !st_x || !st_coef)) || (bnb && in_coef)) return -1;
-  dpe::rowconv::RowArgs a{x, w, y, stats, st_x, st_coef, N, H, W, 2, in_coef};
+  if (nb <= 0 || N <= 0 || H < 2 || W < 1 || W > 64 || (bnb && (!stats || !st_x || !st_coef)) || (bnb && in_coef)) return -1;
+  dpe::rowconv::RowArgs a{x, w, y, stats, st_x, st_coef, N, H, W, in_coef};
   if (bnb) hipLaunchKernelGGL(dpe::rowconv::conv3x3_rows_kernel<true>, dim3(nb), dim3(256), 0, st, a);
   else if (in_coef) hipLaunchKernelGGL((dpe::rowconv::conv3x3_rows_kernel<false, true>), dim3(nb), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(dpe::rowconv::conv3x3_rows_kernel<false>, dim3(nb), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 
-// Scratch floats of the weight-grad launch (the per-image partials), 0: outside the envelope.
-extern "C" int64_t dpe_wgrad3x3_rows_scratch(int N, int H, int W) {
+// Blocks of the weight-grad launch (0: outside the envelope); as dpe_conv3x3_rows_blocks.
+extern "C" int dpe_wgrad3x3_rows_blocks(int N, int H, int W) {
   if (N <= 0 || H < 1 || W < 1 || W > 64) return 0;
-  return (int64_t)N * dpe::rowconv::wg::PART;
+  return rows_grid(N, H);
+}
+namespace {
+int rows_groups(int nb) { return nb >= 64 ? 16 : 1; }
+}  // namespace
+
+// Scratch floats of the weight-grad launch on nb blocks: the block partials + the group sums.
+extern "C" int64_t dpe_wgrad3x3_rows_scratch(int nb) {
+  if (nb <= 0) return 0;
+  const int groups = rows_groups(nb);
+  return (int64_t)(nb + (groups > 1 ? groups : 0)) * dpe::rowconv::wg::PART;
 }
 
-// dw (+)= alpha * dW of conv3x3(x) w.r.t. its filter, given dy (64 -> 64, stride 1, pad 1).
-// in_coef: x is the pre-BN tensor of a BatchNorm+ReLU ([scale | shift] of 64 channels), applied on load.
+// dw (+)= alpha * dW of conv3x3(x) w.r.t. its filter, given dy (64 -> 64, stride 1, pad 1), on nb
+// blocks (dpe_wgrad3x3_rows_blocks).  in_coef: x is the pre-BN tensor of a BatchNorm+ReLU ([scale |
+// shift] of 64 channels), applied on load.
 extern "C" int dpe_wgrad3x3_rows_launch(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H,
-                                        int W, float alpha, const float* in_coef, hipStream_t st) {
-  if (dpe_wgrad3x3_rows_scratch(N, H, W) <= 0 || !scratch) return -1;
+                                        int W, int nb, float alpha, const float* in_coef, hipStream_t st) {
+  if (nb <= 0 || N <= 0 || H < 1 || W < 1 || W > 64 || !scratch) return -1;
   using namespace dpe::rowconv::wg;
-  if (in_coef) hipLaunchKernelGGL(wgrad3x3_rows_kernel<true>, dim3(N), dim3(256), 0, st, x, dy, scratch, H, W, in_coef);
-  else hipLaunchKernelGGL(wgrad3x3_rows_kernel<false>, dim3(N), dim3(256), 0, st, x, dy, scratch, H, W, in_coef);
-  const int groups = N >= 64 ? 16 : 1;
-  const int per = (N + groups - 1) / groups;
-  hipLaunchKernelGGL(wgrad3x3_rows_reduce_kernel, dim3(PART / 1024, groups), dim3(256), 0, st, scratch, dw, N, per, alpha);
+  if (in_coef) hipLaunchKernelGGL(wgrad3x3_rows_kernel<true>, dim3(nb), dim3(256), 0, st, x, dy, scratch, N, H, W, in_coef);
+  else hipLaunchKernelGGL(wgrad3x3_rows_kernel<false>, dim3(nb), dim3(256), 0, st, x, dy, scratch, N, H, W, in_coef);
+  const int groups = rows_groups(nb);
+  const int per = (nb + groups - 1) / groups;
+  float* gsum = scratch + (int64_t)nb * PART;
+  hipLaunchKernelGGL(wgrad3x3_rows_reduce_kernel, dim3(PART / 1024, groups), dim3(256), 0, st, scratch, gsum, dw, nb, per,
+                     alpha);
+  if (groups > 1) hipLaunchKernelGGL(wgrad3x3_rows_sum_kernel, dim3(PART / 1024), dim3(256), 0, st, gsum, dw, groups, alpha);
   return (int)hipGetLastError();
 }
