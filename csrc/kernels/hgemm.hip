@@ -84,8 +84,17 @@ DPE_DEVICE void wait_vm() {
   asm volatile("" ::: "memory");
 }
 
+// LDS-DMA of one 16-B chunk per lane to dst + 16 * lane (dst wave-uniform).  Issued through inline
+// asm on purpose: after a compiler-visible LDS-DMA, hipcc (ROCm 7.2) puts s_waitcnt vmcnt(0) in
+// front of every ds_read_b64_tr_b16 (not of ds_read_b128) -- in the M- / N-contiguous layouts that
+// drained the whole prefetch pipeline four times per K-tile (TN ran at 885 TF vs NT 1334,
+// scripts/gpu_pmc_hgemm.sh: equal LDS-array cycles, 2.3x the LDS-wait).  The kernel's own counted
+// wait_vm<N> calls are what order the DMA against the LDS reads; a VMEM op the compiler does not
+// see can only make its own vmcnt waits stricter, never wrong.  No other code in these kernels
+// uses M0.
 DPE_DEVICE void glds(const char* src, char* dst) {
-  __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst, 16, 0, 0);
+  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)dst);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory");
 }
 
 // K-image fragment read, rows r0 + [0,16), k-step s
