@@ -42,9 +42,10 @@ constexpr TileCfg kTiles[] = {
     {dpe::HC_256x128, 256, 128, 1, 0.70},
     {dpe::HC_128x128, 128, 128, 2, 0.75},
 };
-// per-CU main-loop rate of the 256x256 tile by operand layout (random bf16, 8192^3:
-// NT 1334 / NN 1047 / TN 885 TF on 256 CUs)
-double layout_rate(int ak, int bk) { return ak && bk ? 5.2e12 : (ak ? 4.1e12 : 3.5e12); }
+// per-CU main-loop rate of the 256x256 tile by operand layout (random bf16, 4096^3 / 8192^3 on 256
+// CUs: NT 1318 / 1196, NN 1262 / 1274, TN 1187 / 1222 TF, scripts/bench_hgemm_layouts.py; before the
+// LDS-DMA moved into inline asm the transposed-read layouts ran at NN 1047 / TN 885)
+double layout_rate(int ak, int bk) { return ak && bk ? 5.2e12 : (ak ? 5.0e12 : 4.7e12); }
 constexpr double kEpi = 5.0e-11;  // s per output byte per CU: the store tail is issue-bound (~20 GB/s per CU)
 constexpr double kFix = 2.0e-6;   // first prologue + launch
 constexpr double kBw = 4.0e12;    // slab write + finalize read bandwidth
