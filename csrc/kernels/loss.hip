@@ -62,8 +62,8 @@ __global__ __launch_bounds__(1024) void ce_kernel(const TIn* __restrict__ logits
   const float zy = s_zy;  // published by the barriers inside block_sum
   const float li = ignored ? 0.f : lse - zy;
   if (threadIdx.x == 0) {
-    if (loss_rows) loss_rows[row] = li;
-    if (loss_sum) atomicAdd(loss_sum, li);
+    if (loss_rows) loss_rows[row] = li;                 // summed in row order by ce_sum_kernel
+    else if (loss_sum) atomicAdd(loss_sum, li);
     if (correct && !ignored) atomicAdd(correct, (am == label) ? 1.f : 0.f);
   }
   if (dlogits) {
@@ -200,8 +200,8 @@ __global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 1) void ce_vec_kernel(const TI
   const float lse = m + __logf(s);
   const float li = ignored ? 0.f : lse - zy;
   if (tid == 0) {
-    if (loss_rows) loss_rows[row] = li;
-    if (loss_sum) atomicAdd(loss_sum, li);
+    if (loss_rows) loss_rows[row] = li;                 // summed in row order by ce_sum_kernel
+    else if (loss_sum) atomicAdd(loss_sum, li);
     if (correct && !ignored) atomicAdd(correct, (am == label) ? 1.f : 0.f);
   }
   if (dlogits) {
@@ -229,6 +229,22 @@ __global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 1) void ce_vec_kernel(const TI
       }
     }
   }
+}
+
+// loss_sum[0] += sum of the B per-row losses in a fixed order (thread t takes rows t, t + 256, ...,
+// then a fixed-shape tree): the reported loss is bitwise reproducible, unlike a float atomicAdd per
+// row whose order follows the block schedule.
+__global__ __launch_bounds__(256) void ce_sum_kernel(const float* __restrict__ rows, int B, float* __restrict__ out) {
+  __shared__ float sh[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < B; i += 256) s += rows[i];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] += sh[0];
 }
 
 template <typename TIn, typename TOut>
@@ -259,11 +275,24 @@ bool ce_vec_launch(const TIn* logits, const int64_t* labels, int B, int V, int64
 
 using namespace dpe;
 
+static int dpe_cross_entropy_rows(const void* logits, int in_bf16, const int64_t* labels, int B, int V, int64_t ld,
+                                  float grad_scale, void* dlogits, int out_bf16, float* loss_rows, float* loss_sum,
+                                  float* correct, int ignore_index, hipStream_t st);
+
 // in_bf16 / out_bf16 select dtypes; dlogits may be null (eval)
 extern "C" int dpe_cross_entropy(const void* logits, int in_bf16, const int64_t* labels, int B, int V, int64_t ld,
                                  float grad_scale, void* dlogits, int out_bf16, float* loss_rows, float* loss_sum,
                                  float* correct, int ignore_index, hipStream_t st) {
   if (dlogits == logits && in_bf16 != out_bf16) return -2;  // in-place needs equal dtypes
+  const int rc = dpe_cross_entropy_rows(logits, in_bf16, labels, B, V, ld, grad_scale, dlogits, out_bf16, loss_rows, loss_sum,
+                                        correct, ignore_index, st);
+  if (rc == 0 && loss_rows && loss_sum) hipLaunchKernelGGL(ce_sum_kernel, dim3(1), dim3(256), 0, st, loss_rows, B, loss_sum);
+  return rc;
+}
+
+static int dpe_cross_entropy_rows(const void* logits, int in_bf16, const int64_t* labels, int B, int V, int64_t ld,
+                                  float grad_scale, void* dlogits, int out_bf16, float* loss_rows, float* loss_sum,
+                                  float* correct, int ignore_index, hipStream_t st) {
   if (in_bf16 ? (out_bf16 ? ce_vec_launch((const uint16_t*)logits, labels, B, V, ld, grad_scale, (uint16_t*)dlogits,
                                            loss_rows, loss_sum, correct, ignore_index, st)
                            : ce_vec_launch((const uint16_t*)logits, labels, B, V, ld, grad_scale, (float*)dlogits,

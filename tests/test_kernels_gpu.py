@@ -339,6 +339,18 @@ def test_cross_entropy(C, B, V, ld, in_bf):
     assert torch.equal(d2, d)
 
 
+def test_cross_entropy_loss_sum_bitwise_reproducible(C):
+    """The loss sum is a fixed-order reduction of the per-row losses (no float atomics): identical
+    inputs give identical bits on every call, and it equals the rows' sum in that order's tolerance."""
+    torch.manual_seed(11)
+    z = bf(torch.randn(4096, 1000, device=dev) * 3)
+    y = torch.randint(0, 1000, (4096,), device=dev)
+    sums = [C.cross_entropy(z, y, 1000, 1.0, False, True, -100)[1].item() for _ in range(8)]
+    assert len(set(sums)) == 1, sums
+    rows = C.cross_entropy(z, y, 1000, 1.0, False, True, -100)[0]
+    assert abs(rows.double().sum().item() - sums[0]) <= 1e-5 * abs(sums[0])
+
+
 # ---------------------------------------------------------------- eltwise
 def test_cast_act_dropout(C):
     x = torch.randn(1000003, device=dev)
