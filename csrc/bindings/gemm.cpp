@@ -34,13 +34,16 @@ namespace dpe_gemm {
 namespace {
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
-struct TileCfg { int cfg, bm, bn, bpc; double eff; };
-// eff: per-CU throughput relative to the 256x256 tile with the CU fully occupied
+struct TileCfg { int cfg, bm, bn, bpc; double eff, eff_alone; };
+// eff: per-CU throughput relative to the 256x256 tile with the CU fully occupied (bpc blocks);
+// eff_alone: the same for ONE block of a 2-per-CU tile holding a CU by itself (a launch with no
+// more units than CUs): 128x128 x 768 units ran in ~10 us alone vs 16.2 us two to a CU
+// (scripts/bench_gemm_parts.py two-launch tails, GPT-2 shapes)
 constexpr TileCfg kTiles[] = {
-    {dpe::HC_256x256, 256, 256, 1, 1.00},
-    {dpe::HC_128x256, 128, 256, 1, 0.70},
-    {dpe::HC_256x128, 256, 128, 1, 0.70},
-    {dpe::HC_128x128, 128, 128, 2, 0.75},
+    {dpe::HC_256x256, 256, 256, 1, 1.00, 1.00},
+    {dpe::HC_128x256, 128, 256, 1, 0.70, 0.70},
+    {dpe::HC_256x128, 256, 128, 1, 0.70, 0.70},
+    {dpe::HC_128x128, 128, 128, 2, 0.75, 0.65},
 };
 // per-CU main-loop rate of the 256x256 tile by operand layout (random bf16, 4096^3 / 8192^3 on 256
 // CUs: NT 1318 / 1196, NN 1262 / 1274, TN 1187 / 1222 TF, scripts/bench_hgemm_layouts.py; before the
@@ -132,8 +135,12 @@ Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int
       if (s > 1 && (kt < 4 || (double)s * M * N * 4 > 2.0e9)) continue;
       const int64_t units = tiles * s;
       const int64_t rounds = (units + slots - 1) / slots;
-      const double t_unit = 2.0 * c.bm * c.bn * kt * 64 / (layout_rate(ak, bk) * c.eff / c.bpc) +
-                            kEpi * c.bm * c.bn * (s > 1 ? 4 : out_bytes) * c.bpc;
+      // blocks sharing a CU (bpc) each get 1/bpc of its rate; with no more units than CUs every
+      // block has a CU to itself
+      const bool alone = c.bpc > 1 && units <= (int64_t)ncu - (reserve + c.bpc - 1) / c.bpc;
+      const double rate_blk = alone ? layout_rate(ak, bk) * c.eff_alone : layout_rate(ak, bk) * c.eff / c.bpc;
+      const double t_unit = 2.0 * c.bm * c.bn * kt * 64 / rate_blk + kEpi * c.bm * c.bn * (s > 1 ? 4 : out_bytes) *
+                                                                          (alone ? 1 : c.bpc);
       double t = rounds * t_unit + kFix;
       if (s > 1) t += ((double)s * M * N * 4 * 2 + (double)M * N * out_bytes) / kBw + kLaunch;
       if (t < best.est_s * 0.995) best = Plan{c.cfg, s, (int)(kt * 64), (int)std::min<int64_t>(units, slots), t};
