@@ -421,8 +421,10 @@ Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const c10::optional<Tenso
 dpe::ConvGeom geom(const Tensor& x, const Tensor& w, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
                    int64_t OH, int64_t OW);
 
+// overwrite: dw = alpha dy^T x instead of dw += (the step's first writer of a gradient whose stale
+// contents were not zeroed, ops/_state.py grad_fresh); the bias gradient always accumulates.
 void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha, const c10::optional<Tensor>& alpha_t,
-                  const c10::optional<Tensor>& dbias, int64_t fin_stream) {
+                  const c10::optional<Tensor>& dbias, int64_t fin_stream, bool overwrite) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(x); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
   const int64_t N = dw.size(0), K = dw.size(1), ldy = dy.size(-1);
   TORCH_CHECK(ldy >= N && x.size(-1) == K && dy.numel() / ldy == x.numel() / K, "linear_wgrad: shape mismatch");
@@ -443,9 +445,10 @@ void linear_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, double alpha, c
       TORCH_CHECK(dbias->numel() == N, "linear_wgrad: dbias must have out_features elements");
       a.dbias = fp(*dbias);
     }
-    dpe_gemm::run(a, 0, 0, dpe::HE_ACC_F32, true, 4, (hipStream_t)(uintptr_t)fin_stream);
+    dpe_gemm::run(a, 0, 0, overwrite ? dpe::HE_F32 : dpe::HE_ACC_F32, true, 4, (hipStream_t)(uintptr_t)fin_stream);
     return;
   }
+  if (overwrite) dw.zero_();  // the split-K fallback below accumulates with atomics
   if (dbias.has_value() && dbias->defined()) {
     CHECK_F32((*dbias)); CHECK_CONTIG((*dbias));
     TORCH_CHECK(dbias->numel() == N, "linear_wgrad: dbias must have out_features elements");
@@ -1345,8 +1348,9 @@ void register_ops(pybind11::module& m) {
         py::arg("alpha_t") = py::none(), py::arg("gelu_in") = py::none());
   m.def("linear_wgrad", &linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("alpha") = 1.0,
         py::arg("alpha_t") = py::none(), py::arg("dbias") = py::none(), py::arg("fin_stream") = 0,
+        py::arg("overwrite") = false,
         "dw (+)= alpha dy^T x (+ db += alpha colsum(dy)); fin_stream: run a K-split's slab reduction on that HIP "
-        "stream (the caller orders dw's consumers after it)");
+        "stream (the caller orders dw's consumers after it); overwrite: dw = instead of dw +=");
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("want_stats") = false, py::arg("bias") = py::none(), py::arg("in_coef") = py::none());
   m.def("row_bn_on_load", [](std::vector<int64_t> xs, std::vector<int64_t> ws, std::vector<int64_t> stride,

@@ -730,11 +730,13 @@ namespace {
 template <int BM, int BN, int WR, int WC, bool AK, bool BK>
 int launch_epi(const HgemmArgs& p, int epi, int grid, hipStream_t st) {
   const dim3 g((unsigned)grid), b(WR * WC * 64);
-  if (p.dbias) {  // fused bias gradient: TN weight grads (raw slabs or fp32 accumulate) only
+  if (p.dbias) {  // fused bias gradient: TN weight grads (raw slabs, fp32 accumulate or overwrite) only
     if constexpr (!AK && !BK && BM == 256 && BN == 256) {
       if (p.act != ACT_NONE || (p.splits > 1 && !p.ws_bias)) return -3;
       if (epi == HE_SLAB) hipLaunchKernelGGL((hg::hgemm_kernel<BM, BN, WR, WC, AK, BK, HE_SLAB, ACT_NONE, true>), g, b, 0, st, p);
       else if (epi == HE_ACC_F32) hipLaunchKernelGGL((hg::hgemm_kernel<BM, BN, WR, WC, AK, BK, HE_ACC_F32, ACT_NONE, true>), g, b, 0, st, p);
+      else if (epi == HE_F32 && !p.bias && !p.residual_f32)  // overwrite (the gradient's first writer of the step)
+        hipLaunchKernelGGL((hg::hgemm_kernel<BM, BN, WR, WC, AK, BK, HE_F32, ACT_NONE, true>), g, b, 0, st, p);
       else return -3;
       return 0;
     } else {

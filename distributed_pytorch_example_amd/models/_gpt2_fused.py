@@ -39,7 +39,7 @@ import torch
 from torch.autograd import Function
 
 from ..ops._ext import ext
-from ..ops._state import finalize_stream, grad_done, grad_sink, note_use, shadow
+from ..ops._state import finalize_stream, grad_done, grad_fresh, grad_sink, note_use, shadow
 
 # (fp32 grad, its bf16 copy, version) produced by the most recent block backward
 _carry: list = [None]
@@ -116,7 +116,7 @@ class BlockFn(Function):
             # bias grad from the same launch (row sums of dy^T); a K-split's slab reduction may run on the
             # side stream when both gradients are bucket views (the reducer / backward join wait for it)
             fs = finalize_stream(dyb.device) if (d and bd) else 0
-            C.linear_wgrad(dyb, inp, buf, 1.0, None, bb, fs)
+            C.linear_wgrad(dyb, inp, buf, 1.0, None, bb, fs, d and grad_fresh(lin.weight))
             done(lin.weight, buf, d)
             if lin.bias is not None:
                 done(lin.bias, bb, bd)
@@ -147,3 +147,4 @@ class BlockFn(Function):
 
 def block_forward(blk, x):
     return BlockFn.apply(x, blk, *block_params(blk))
+

@@ -58,6 +58,10 @@ class Block(nn.Module):
         self.c_fc = Linear(d, 4 * d, bias=cfg.bias)
         self.mlp_proj = Linear(4 * d, d, bias=cfg.bias)
         self.fused = _FUSED
+        # every backward writes these through one weight-grad GEMM that honours grad_fresh (fused
+        # and per-op paths alike): DDP may leave them out of the gradient re-zero (ops/_state.py)
+        for lin in (self.c_attn, self.attn_proj, self.c_fc, self.mlp_proj):
+            lin.weight._dpe_overwrite_ok = True
 
     def forward(self, x):
         if x.is_cuda and self.fused and torch.is_grad_enabled():
@@ -81,6 +85,9 @@ class GPT2(nn.Module):
         self.wpe = nn.Parameter(torch.empty(cfg.block_size, cfg.n_embd))
         self.h = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layer)])
         self.ln_f = LayerNorm(cfg.n_embd, bias=cfg.bias)
+        # tied LM head / embedding: the LM-head weight grad (first writer) overwrites when fresh, the
+        # embedding scatter-add accumulates after it
+        self.wte._dpe_overwrite_ok = True
         self._init()
 
     def _init(self):

@@ -82,6 +82,22 @@ def grad_sink(p: torch.Tensor):
     return torch.zeros_like(p, dtype=torch.float32), False
 
 
+def grad_fresh(p: torch.Tensor) -> bool:
+    """True (once) when ``p.grad`` holds stale values this step's first writer must overwrite.
+
+    DDP re-zeroes the gradient buckets at the first forward after ``zero_grad(set_to_none=True)``;
+    parameters marked ``_dpe_overwrite_ok`` (every backward writes them through a kernel that honours
+    this flag, the first writer overwriting) are left out of that fill -- for GPT-2-small that is
+    497 MB of fp32 zeros per step plus the read of them by the weight-grad GEMMs' accumulate
+    epilogues.  The flag is cleared by the first query, so later writers (a tied weight's second
+    use, gradient-accumulation micro-steps) accumulate.  DDP zeroes any parameter still fresh at the
+    end of backward (an unused one) before its bucket is reduced."""
+    if getattr(p, "_dpe_fresh", False):
+        p._dpe_fresh = False
+        return True
+    return False
+
+
 def grad_done(p: torch.Tensor, direct: bool) -> None:
     if not direct:
         return

@@ -16,7 +16,7 @@ import torch.nn.functional as F
 from torch.autograd import Function
 
 from ._ext import ext
-from ._state import grad_done, grad_sink, note_use, shadow
+from ._state import grad_done, grad_fresh, grad_sink, note_use, shadow
 
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 
@@ -98,7 +98,7 @@ class _LinearFn(Function):
         if ctx.needs_input_grad[1]:
             buf, direct = grad_sink(weight)
             # column-padded dy: only the N real rows of dW (and of db) are written
-            C.linear_wgrad(dyp, xb, buf, 1.0, None, bbuf)
+            C.linear_wgrad(dyp, xb, buf, 1.0, None, bbuf, 0, direct and grad_fresh(weight))
             grad_done(weight, direct)
             gw = None if direct else buf
         elif want_b:
@@ -561,6 +561,9 @@ class _EmbFn(Function):
         (idx,) = ctx.saved_tensors
         tb, td = grad_sink(ctx.wte)
         pb, pd = grad_sink(ctx.wpe) if ctx.wpe is not None else (None, False)
+        for p, buf, d in ((ctx.wte, tb, td), (ctx.wpe, pb, pd)):  # the scatter-add needs a zeroed start
+            if p is not None and d and grad_fresh(p):
+                buf.zero_()
         ext().embedding_bwd(idx, dout.contiguous().float(), tb, pb)
         grad_done(ctx.wte, td)
         if ctx.wpe is not None:
@@ -661,7 +664,7 @@ class _LinearResidualFn(Function):
         da = C.linear_dgrad(dyb, shadow(weight)) if ctx.needs_input_grad[0] else None
         buf, direct = grad_sink(weight)
         bb, bd = grad_sink(bias) if bias is not None else (None, False)
-        C.linear_wgrad(dyb, ab, buf, 1.0, None, bb)  # bias grad: row sums of dy^T in the same launch
+        C.linear_wgrad(dyb, ab, buf, 1.0, None, bb, 0, direct and grad_fresh(weight))  # bias grad: row sums of dy^T in the same launch
         grad_done(weight, direct)
         gb = None
         if bias is not None:
@@ -701,7 +704,7 @@ class _LMHeadFn(Function):
         d = dlogits.to(torch.bfloat16).contiguous()
         dx = C.linear_dgrad(d, shadow(ctx.wte, ctx.pad))
         buf, direct = grad_sink(ctx.wte)
-        C.linear_wgrad(d, xb, buf, 1.0)  # padded leading dim, only the V real rows are produced
+        C.linear_wgrad(d, xb, buf, 1.0, None, None, 0, direct and grad_fresh(ctx.wte))  # padded leading dim, only the V real rows are produced
         grad_done(ctx.wte, direct)
         return dx, (None if direct else buf), None
 
@@ -738,7 +741,7 @@ class _LMHeadCEFn(Function):
         scale = (g.float() / n).reshape(1).contiguous()
         dx = C.linear_dgrad(d, shadow(ctx.wte, ctx.pad), None, scale)
         buf, direct = grad_sink(ctx.wte)
-        C.linear_wgrad(d, xb, buf, 1.0, scale)
+        C.linear_wgrad(d, xb, buf, 1.0, scale, None, 0, direct and grad_fresh(ctx.wte))
         grad_done(ctx.wte, direct)
         return dx.reshape(ctx.xshape), (None if direct else buf), None, None, None
 

@@ -73,6 +73,10 @@ def _has_ext() -> bool:
 _DEFAULT_FIRST_BUCKET_BYTES = 1024 * 1024
 
 
+
+# DPE_GRAD_FRESH=0: re-zero every gradient bucket (A/B arm of the overwrite-first-write protocol)
+_GRAD_FRESH = os.environ.get("DPE_GRAD_FRESH", "1") != "0"
+
 class _PyReducer:
     """Python reducer: gloo backend, or any backend with a user comm hook.
 
@@ -370,9 +374,18 @@ class DistributedDataParallel(nn.Module):
                     p.grad = v
                     reattached = True
         if zero or reattached:
-            # set_to_none=True zero_grad dropped the views: grads restart from zero (all buckets in
-            # one multi-tensor launch)
-            torch._foreach_zero_(list(self.buckets))
+            # set_to_none=True zero_grad dropped the views: grads restart from zero (one multi-tensor
+            # launch).  Parameters whose first backward writer overwrites (ops/_state.py grad_fresh)
+            # are marked fresh instead of filled.
+            # (GPU only: there every writer of such a parameter is one of our kernels; on the CPU
+            # autograd's AccumulateGrad adds into .grad)
+            ow = [getattr(p, "_dpe_overwrite_ok", False) and p.is_cuda and _GRAD_FRESH for p in self._params]
+            if any(ow):
+                for p, o in zip(self._params, ow):
+                    p._dpe_fresh = o
+                torch._foreach_zero_([self._views[i] for i, o in enumerate(ow) if not o])
+            else:
+                torch._foreach_zero_(list(self.buckets))
 
     # ---------------------------------------------------------- per-step
     def _on_ready(self, p):
@@ -390,6 +403,10 @@ class DistributedDataParallel(nn.Module):
 
     def _finalize(self):
         self._queued = False
+        for i, p in enumerate(self._params):  # fresh but never written this step: zero, as stock
+            if getattr(p, "_dpe_fresh", False):
+                p._dpe_fresh = False
+                self._views[i].zero_()
         self.reducer.finalize()
         if self._record_order:
             self._record_order = False

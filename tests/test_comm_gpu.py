@@ -2,6 +2,7 @@
 host a world of 1, so the reducer runs in `force` mode (collectives issued
 even at world 1; ncclAvg over one rank is the identity): this exercises the
 real comm stream, events, bucket ordering and finalize on hardware."""
+import contextlib
 import copy
 
 import pytest
@@ -169,3 +170,47 @@ def test_bucket_registration_world1(C, comm):
     for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
         assert ((a.grad - b.grad).norm() / (a.grad.norm() + 1e-12)).item() < 2e-2, n
     print(f"registered {ddp.reducer.registered_buffers}/{ddp.num_buckets()} buckets")
+
+
+def test_gpt2_fresh_gradients_equal_zeroed(C):
+    """DDP leaves the GPT-2 Linear and tied-embedding gradients out of the bucket re-zero after
+    zero_grad(set_to_none=True): their first backward writer overwrites (ops/_state.py grad_fresh).
+    Gradients over several steps -- including a 2-micro-step no_sync accumulation and a step where
+    the buckets still hold the previous step's values -- are bitwise those of the same run with
+    every gradient zeroed (the tied embedding's to its scatter-add's atomic-order noise)."""
+    from distributed_pytorch_example_amd.models import get_model
+    from distributed_pytorch_example_amd.parallel import DDP
+
+    torch.manual_seed(6)
+    base = get_model("gpt2", n_layer=2).to(dev)
+    idx = [torch.randint(0, 50257, (2, 256), device=dev) for _ in range(3)]
+    tgt = [torch.randint(0, 50257, (2, 256), device=dev) for _ in range(3)]
+
+    def run(fresh_ok):
+        m = copy.deepcopy(base)
+        for p in m.parameters():
+            if getattr(p, "_dpe_overwrite_ok", False):
+                p._dpe_overwrite_ok = fresh_ok
+        ddp = DDP(m, bucket_cap_mb=8)
+        out = []
+        for step in range(3):
+            for p in m.parameters():
+                p.grad = None
+            micro = 2 if step == 1 else 1
+            for a in range(micro):
+                ctx = ddp.no_sync() if a + 1 < micro else contextlib.nullcontext()
+                with ctx:
+                    ddp(idx[(step + a) % 3], tgt[(step + a) % 3]).backward()
+            torch.cuda.synchronize()
+            out.append([p.grad.clone() for p in m.parameters()])
+        return out
+
+    ref, got = run(False), run(True)
+    assert any(getattr(p, "_dpe_overwrite_ok", False) for p in base.parameters())
+    names = [n for n, _ in base.named_parameters()]
+    for s, (a, b) in enumerate(zip(ref, got)):
+        for n, x, y in zip(names, a, b):
+            if n in ("wte", "wpe"):  # the embedding scatter-add uses float atomics: run-to-run last bits
+                assert ((x - y).norm() / x.norm()).item() < 1e-6, (s, n)
+            else:
+                assert torch.equal(x, y), (s, n)
