@@ -354,7 +354,11 @@ using namespace dpe;
 
 extern "C" int dpe_cu_reserve();  // comm.cpp
 
-static int pw_wn(int K) { return K <= 128 ? 64 : 32; }
+// columns per wave.  The data grads at K = 128 use 32 (like K = 256) so that the epilogue operands
+// (residual, pre-BN input, masks) can be hoisted ahead of the tile's MFMAs: with 64 columns per wave
+// they were loaded in the epilogue and each half-tile stalled a full HBM round trip (layer-2 conv1
+// data grads ran at ~61 % of their HBM roofline).
+static int pw_wn(int K, int epi) { return K == 64 || (K == 128 && epi == PW_FWD) ? 64 : 32; }
 
 // Every block carries the same number of tiles, so the grid must be exactly the resident
 // capacity (blocks per CU from the occupancy API x CUs): a grid that lets the dispatcher put
@@ -372,13 +376,15 @@ static int pw_slots() {
 }
 template <int EPI>
 static int pw_capacity(int K) {
-  return K == 64 ? pw_slots<64, 64, 4, EPI>() : K == 128 ? pw_slots<128, 64, 3, EPI>() : pw_slots<256, 32, 2, EPI>();
+  if (K == 64) return pw_slots<64, 64, 4, EPI>();
+  if (K == 128) return EPI == PW_FWD ? pw_slots<128, 64, 3, EPI>() : pw_slots<128, 32, 3, EPI>();
+  return pw_slots<256, 32, 2, EPI>();
 }
 
 extern "C" int dpe_pw_rowgroups(int64_t M, int64_t N, int64_t K, int epi) {
   if (K != 64 && K != 128 && K != 256) return 0;
   if (epi != PW_FWD && epi != PW_DGRAD) return 0;
-  const int bnb = 4 * pw_wn((int)K);
+  const int bnb = 4 * pw_wn((int)K, epi);
   if (N % bnb || N < 2 * K) return 0;  // write-heavy shapes only (N >= 2K)
   if (M * K * 2 >= (1ll << 31) - 4096 || M * N >= (1ll << 31)) return 0;
   const int64_t tiles = (M + pw::BM - 1) / pw::BM;
@@ -398,7 +404,7 @@ extern "C" int dpe_pw_launch(const PwArgs* args, int epi, hipStream_t st) {
   if (a.st_x && !a.st_coef) return -1;
   if (a.res_h > 0 && (epi != PW_DGRAD || a.res_mask || a.res_h % 2 || a.res_w % 2 || a.M % ((int64_t)a.res_h * a.res_w)))
     return -1;
-  const int nbN = (int)(a.N / (4 * pw_wn((int)a.K)));
+  const int nbN = (int)(a.N / (4 * pw_wn((int)a.K, epi)));
   const dim3 grid((unsigned)(a.rg * nbN)), block(256);
 #define PW_L(K_, WN_, NS_)                                                                              \
   if (a.K == K_) {                                                                                      \
@@ -407,6 +413,10 @@ extern "C" int dpe_pw_launch(const PwArgs* args, int epi, hipStream_t st) {
     return 0;                                                                                           \
   }
   PW_L(64, 64, 4)
+  if (a.K == 128 && epi == PW_DGRAD) {
+    hipLaunchKernelGGL((pw::pw_stream_kernel<128, 32, 3, PW_DGRAD>), grid, block, 0, st, a);
+    return 0;
+  }
   PW_L(128, 64, 3)
   PW_L(256, 32, 2)
 #undef PW_L
