@@ -8,8 +8,7 @@ ops are torch's own (F.conv2d / F.batch_norm / F.scaled_dot_product_attention / 
 optimizers), run twice on the same GPU: in fp32 (the oracle) and under torch.autocast(bfloat16).
 
 The bound is derived, not guessed: our per-step loss may deviate from the fp32 oracle by no more than
-2 % relative AND by no more than a small multiple of what PyTorch's own bf16 autocast deviates
-(+ an absolute floor); the final weights' distance to the oracle, relative to the oracle's own
+twice what PyTorch's own bf16 autocast deviates (+ a small floor); the final weights' distance to the oracle, relative to the oracle's own
 update, is bounded the same way.  Both tests print their curves.
 """
 import copy
@@ -105,7 +104,9 @@ def _check(name, ours, fp32, bf16, w_ours, w_bf16):
     for i, (a, b, c) in enumerate(zip(ours, fp32, bf16)):
         print(f"  {i:2d} | {a:.5f} | {b:.5f} | {c:.5f} | {d_ours[i]:.2e} / {d_bf16[i]:.2e}")
     print(f"  final weights, ||w - w_fp32|| / ||w_fp32 - w0||: ours {w_ours:.3e}, torch bf16 {w_bf16:.3e}")
-    bound = min(0.02, 4 * max(d_bf16) + 2e-3)
+    # at most twice what PyTorch's own bf16 autocast deviates (+ a floor).  No fixed 2 % cap: past a
+    # loss spike both bf16 runs leave the fp32 oracle by 3-4 % (GPT-2 step 12) while tracking each other
+    bound = 2 * max(d_bf16) + 2e-3
     assert max(d_ours) <= bound, (name, max(d_ours), bound)
     assert w_ours <= max(2 * w_bf16, 0.05), (name, w_ours, w_bf16)
 
@@ -120,7 +121,9 @@ def test_resnet50_full_training_parity():
     g = torch.Generator(device=DEV).manual_seed(1)
     data = [(torch.randn(16, 3, 224, 224, device=DEV, generator=g), torch.randint(0, 1000, (16,), device=DEV, generator=g))
             for _ in range(3)]
-    lr, mom, steps = 0.05, 0.9, 15
+    # lr 0.05 made even the fp32 oracle diverge (loss 7 -> 66 by step 6: a chaotic trajectory that no
+    # two implementations follow); at 0.003 the fp32 loss falls smoothly 7.1 -> 3.8 over the 15 steps
+    lr, mom, steps = 0.003, 0.9, 15
     opt_o = SGD(ours.parameters(), lr=lr, momentum=mom)
     opt_t = torch.optim.SGD(twin.parameters(), lr=lr, momentum=mom)
     opt_b = torch.optim.SGD(twin_bf.parameters(), lr=lr, momentum=mom)
