@@ -989,6 +989,98 @@ Tensor bn_bwd_partials(const Tensor& dy, const Tensor& x, const c10::optional<Te
   return dx;
 }
 
+// BatchNorm-backward coefficients [3][C] (dx = a*dz + b*x + c) from the (sum dz, sum dz*(x-mean))
+// partials, without the apply pass (its consumer applies it on load: conv1x1_bnin_dgrad).
+// dgamma/dbeta accumulate.
+Tensor bn_bwd_coef(const Tensor& partials, int64_t M, const c10::optional<Tensor>& gamma, const Tensor& coef,
+                   const c10::optional<Tensor>& dgamma, const c10::optional<Tensor>& dbeta) {
+  CHECK_GPU(partials); CHECK_F32(partials);
+  TORCH_CHECK(partials.dim() == 3 && partials.size(0) == 2, "partials must be [2][C][nb]");
+  const int64_t C = partials.size(1);
+  Tensor bcoef = at::empty({3, C}, partials.options());
+  CHECK_RC(dpe_bn_bwd_finalize(fp(partials), (int)partials.size(2), (int)C, M, fpo(gamma), fp(coef), fpom(dgamma),
+                               fpom(dbeta), fp(bcoef), cur_stream()), "bn_bwd_finalize");
+  return bcoef;
+}
+
+// 1x1 stride-1 convolutions over a BatchNorm output that is never written by a pass of its own
+// (igemm.h AXform): the LDS-DMA kernel computes the operand from two tensors on its fragments and
+// stores it once as a by-product (x_out [+ x_bits]), so the consumer's own read of it disappears.
+//
+// forward: y = x . W^T,  x = relu(h * scale + shift + res)           (res_coef absent)
+//                         x = relu(h * scale + shift + bf16(res * scale_d + shift_d))   (downsample identity)
+// with the BN-forward partials of y when want_stats.  tile_m: 128 or 256 (N = 64 only).
+std::vector<Tensor> conv1x1_bnin_fwd(const Tensor& h, const Tensor& res, const Tensor& coef,
+                                     const c10::optional<Tensor>& res_coef, const Tensor& w, Tensor& x_out,
+                                     Tensor& x_bits, bool want_stats, int64_t tile_m) {
+  CHECK_GPU(h); CHECK_BF16(h); CHECK_BF16(res); CHECK_BF16(w); CHECK_BF16(x_out);
+  CHECK_CONTIG(h); CHECK_CONTIG(res); CHECK_CONTIG(w); CHECK_CONTIG(x_out); CHECK_CONTIG(x_bits);
+  CHECK_F32(coef);
+  TORCH_CHECK(h.dim() == 4 && w.dim() == 4 && w.size(1) == 1 && w.size(2) == 1 && w.size(3) == h.size(3),
+              "conv1x1_bnin_fwd: NHWC h / [K,1,1,C] w shape mismatch");
+  TORCH_CHECK(res.sizes() == h.sizes() && x_out.sizes() == h.sizes(), "conv1x1_bnin_fwd: res / x_out must have h's shape");
+  TORCH_CHECK(x_bits.scalar_type() == at::kByte && x_bits.numel() * 8 == h.numel(), "conv1x1_bnin_fwd: x_bits [.., C/8] u8");
+  const int64_t C = h.size(3), K = w.size(0);
+  TORCH_CHECK(coef.numel() == 4 * C && (!res_coef.has_value() || res_coef->numel() == 4 * C), "coef must be [4][C]");
+  TORCH_CHECK(C % 32 == 0 && C <= 2048 && K % 8 == 0, "conv1x1_bnin_fwd: C % 32 == 0, C <= 2048");
+  Tensor y = at::empty({h.size(0), h.size(1), h.size(2), K}, h.options());
+  auto a = base_args();
+  a.g = geom(h, w, 1, 1, 0, 0, 1, 1, h.size(1), h.size(2));
+  a.A = bp(h); a.B = bp(w); a.C = y.data_ptr();
+  a.M = (int)(h.numel() / C); a.N = (int)K; a.K = (int)C;
+  a.lda = C; a.ldb = C; a.ldc = K;
+  a.k_split = a.K;
+  a.a_mode = (res_coef.has_value() && res_coef->defined()) ? dpe::AX_BN_RES2 : dpe::AX_BN_RES;
+  a.a2 = bp(res); a.a_coef = fp(coef); a.a_coef2 = fpo(res_coef);
+  a.a_out = bpm(x_out); a.a_bits = (uint8_t*)x_bits.data_ptr();
+  Tensor stats;
+  if (want_stats) {  // per-128-row partials: the layout every conv path produces (BN finalize is tile-agnostic)
+    stats = at::empty({2, K, (a.M + 127) / 128}, h.options().dtype(at::kFloat));
+    a.col_stats = fp(stats);
+  }
+  const int bm = (K == 64 && tile_m == 256) ? 256 : 128, bn = K <= 64 ? 64 : 128;
+  CHECK_RC(dpe_igemm_dma_launch(&a, bm, bn, dpe::A_DENSE_K, dpe::B_DENSE_K, dpe::EPI_BF16, cur_stream()),
+           "conv1x1_bnin_fwd");
+  return {y, stats};
+}
+
+// data grad: dx = dh . W  with  dh = a * dz + b * h + c  (BN backward applied on load, dh stored as a
+// by-product for the weight grad), plus the BN-backward partials of the BN + ReLU that produced this
+// conv's input (bn_x, bn_coef: ReLU mask recomputed from bn_x), as conv_dgrad_bn.
+std::vector<Tensor> conv1x1_bnin_dgrad(const Tensor& dz, const Tensor& h, const Tensor& bcoef, const Tensor& w,
+                                       Tensor& dh_out, const Tensor& bn_x, const Tensor& bn_coef) {
+  CHECK_GPU(dz); CHECK_BF16(dz); CHECK_BF16(h); CHECK_BF16(w); CHECK_BF16(dh_out); CHECK_BF16(bn_x);
+  CHECK_CONTIG(dz); CHECK_CONTIG(h); CHECK_CONTIG(w); CHECK_CONTIG(dh_out); CHECK_CONTIG(bn_x);
+  CHECK_F32(bcoef); CHECK_F32(bn_coef);
+  TORCH_CHECK(dz.dim() == 4 && w.dim() == 4 && w.size(1) == 1 && w.size(2) == 1 && w.size(0) == dz.size(3),
+              "conv1x1_bnin_dgrad: NHWC dz / [K,1,1,C] w shape mismatch");
+  TORCH_CHECK(h.sizes() == dz.sizes() && dh_out.sizes() == dz.sizes(), "conv1x1_bnin_dgrad: h / dh_out must have dz's shape");
+  const int64_t K = dz.size(3), C = w.size(3);
+  TORCH_CHECK(bcoef.numel() == 3 * K, "bcoef must be [3][K]");
+  TORCH_CHECK(K % 32 == 0 && K <= 2048 && C % 8 == 0, "conv1x1_bnin_dgrad: K % 32 == 0, K <= 2048");
+  TORCH_CHECK(bn_x.dim() == 4 && bn_x.size(0) == dz.size(0) && bn_x.size(1) == dz.size(1) && bn_x.size(2) == dz.size(2) &&
+                  bn_x.size(3) == C && bn_coef.numel() == 4 * C,
+              "conv1x1_bnin_dgrad: bn_x must be [N,H,W,C], bn_coef [4][C]");
+  Tensor dx = at::empty_like(bn_x);
+  auto a = base_args();
+  a.g = geom(dx, w, 1, 1, 0, 0, 1, 1, dz.size(1), dz.size(2));
+  a.A = bp(dz); a.B = bp(w); a.C = dx.data_ptr();
+  a.M = (int)(dz.numel() / K); a.N = (int)C; a.K = (int)K;
+  a.lda = K; a.ldb = C; a.ldc = C;
+  a.k_split = a.K;
+  a.a_mode = dpe::AX_BN_BWD;
+  a.a2 = bp(h); a.a_coef = fp(bcoef); a.a_out = bpm(dh_out);
+  a.st_x = bp(bn_x); a.st_coef = fp(bn_coef);
+  const int64_t tiles_m = (a.M + 127) / 128;
+  Tensor part = at::empty({2, C, tiles_m}, dz.options().dtype(at::kFloat));
+  a.col_stats = fp(part);
+  a.stats_ld = (int)tiles_m;
+  const int bn = C <= 64 ? 64 : 128;
+  CHECK_RC(dpe_igemm_dma_launch(&a, 128, bn, dpe::A_DENSE_K, dpe::B_DENSE_N, dpe::EPI_BF16_BNB, cur_stream()),
+           "conv1x1_bnin_dgrad");
+  return {dx, part};
+}
+
 // Two BatchNorms fed by the same dz (a downsample bottleneck: BN3 and BN_d both see dz3):
 // BN3's backward from its epilogue partials, BN_d's reduce fused into BN3's apply pass
 // (dz read once for both), then BN_d's apply.  Returns (dx, dx2).
@@ -1396,6 +1488,15 @@ void register_ops(pybind11::module& m) {
         py::arg("residual_stride2") = false,
         "data grad; with bn_x/bn_coef also the BN-backward partials of the BN+ReLU that produced the conv input; "
         "with bn_mask (BN + residual + ReLU) the mask is bn_mask > 0 and dx is stored masked");
+  m.def("bn_bwd_coef", &bn_bwd_coef, py::arg("partials"), py::arg("M"), py::arg("gamma"), py::arg("coef"),
+        py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none(),
+        "BN-backward coefficients [3][C] from the dgrad-epilogue partials (no apply pass); dgamma/dbeta +=");
+  m.def("conv1x1_bnin_fwd", &conv1x1_bnin_fwd, py::arg("h"), py::arg("res"), py::arg("coef"), py::arg("res_coef"),
+        py::arg("w"), py::arg("x_out"), py::arg("x_bits"), py::arg("want_stats") = true, py::arg("tile_m") = 128,
+        "1x1 conv over x = relu(BN(h) + res [BN_d]) computed on load; x (+ ReLU bits) stored as a by-product");
+  m.def("conv1x1_bnin_dgrad", &conv1x1_bnin_dgrad, py::arg("dz"), py::arg("h"), py::arg("bcoef"), py::arg("w"),
+        py::arg("dh_out"), py::arg("bn_x"), py::arg("bn_coef"),
+        "1x1 data grad over dh = a*dz + b*h + c computed on load (dh stored as a by-product) + BN-backward partials");
   m.def("bn_coef", &bn_coef, py::arg("stats"), py::arg("M"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("momentum"), py::arg("eps"));
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("coef"), py::arg("residual") = py::none(),

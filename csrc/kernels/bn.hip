@@ -19,17 +19,7 @@ namespace dpe {
 
 constexpr int BN_T = 256;
 
-// ReLU-mask bits of 8 packed bf16 outputs: bit e = (y[e] > 0), i.e. sign clear and nonzero
-DPE_DEVICE uint8_t mask_byte(const u32x4& pk) {
-  uint32_t b = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t lo = pk[j] & 0xffffu, hi = pk[j] >> 16;
-    b |= (uint32_t)(lo != 0 && !(lo & 0x8000u)) << (2 * j);
-    b |= (uint32_t)(hi != 0 && !(hi & 0x8000u)) << (2 * j + 1);
-  }
-  return (uint8_t)b;
-}
+DPE_DEVICE uint8_t mask_byte(const u32x4& pk) { return relu_mask_byte(pk); }
 
 // Thread layout for a [rows][C] pass: chunk c = tid % CPR (8 channels), row phase tid / CPR.
 __global__ __launch_bounds__(BN_T) void bn_stats_partial_kernel(const uint16_t* __restrict__ x, int64_t M, int C,

@@ -49,6 +49,18 @@ DPE_DEVICE u32x4 pack8(const float* f) {
   return r;
 }
 
+// ReLU-mask bits of 8 packed bf16 values: bit e = (v[e] > 0), i.e. sign clear and nonzero
+DPE_DEVICE uint8_t relu_mask_byte(const u32x4& pk) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t lo = pk[j] & 0xffffu, hi = pk[j] >> 16;
+    b |= (uint32_t)(lo != 0 && !(lo & 0x8000u)) << (2 * j);
+    b |= (uint32_t)(hi != 0 && !(hi & 0x8000u)) << (2 * j + 1);
+  }
+  return (uint8_t)b;
+}
+
 DPE_DEVICE float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -26,6 +26,15 @@ enum Epi : int {
   EPI_BF16_BNB = 3,    // EPI_BF16 + BatchNorm-backward partials of dL/dy in the epilogue (data-grad of a BN+ReLU input)
 };
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
+// LDS-DMA conv kernel, dense A: the A operand is the output of a BatchNorm pass that is never run
+// on its own -- computed on the fragments from two bf16 tensors (A, a2) and per-K-channel
+// coefficients, and stored once as a by-product (a_out, a_bits) by the blocks of the first N tile.
+enum AXform : int {
+  AX_NONE = 0,
+  AX_BN_RES = 1,   // relu(A * s[k] + t[k] + a2)                  a_coef = [scale | shift] (BN forward coef [4][K])
+  AX_BN_RES2 = 2,  // relu(A * s[k] + t[k] + bf16(a2 * s2[k] + t2[k]))   + a_coef2 (the downsample BN's)
+  AX_BN_BWD = 3,   // a[k] * A + b[k] * a2 + c[k]                  a_coef = [a | b | c] (BN backward coef [3][K])
+};
 
 struct ConvGeom {
   int N, H, W, C;      // input  NHWC
@@ -72,6 +81,13 @@ struct IgemmArgs {
   ConvGeom g;
   const float* b_coef;  // LDS-DMA weight grad, B_DENSE_N: B is a pre-BN tensor; the operand is
                         //   relu(B * b_coef[n] + b_coef[N + n]) (the BN output is never stored)
+  // A on-load transform (AXform; LDS-DMA kernel, A_DENSE_K only)
+  int a_mode;
+  const uint16_t* a2;       // [M][lda] second operand of the transform
+  const float* a_coef;      // per-K coefficients (see AXform)
+  const float* a_coef2;     // AX_BN_RES2: the second BatchNorm's forward coefficients [4][K]
+  uint16_t* a_out;          // [M][lda] the transformed A, written by the tn == 0 blocks (required)
+  uint8_t* a_bits;          // [M][lda/8] ReLU-mask bits of a_out (AX_BN_RES / _RES2), or nullptr
 };
 
 }  // namespace dpe

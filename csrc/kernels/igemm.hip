@@ -691,8 +691,21 @@ constexpr int DSTAGES = 3;
 DPE_DEVICE __amdgpu_buffer_rsrc_t dma_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
+// LDS-DMA of one 16-B chunk per lane to wave_dst + 16 * lane.  Issued through inline asm: after a
+// compiler-visible LDS-DMA, hipcc (ROCm 7.2) puts s_waitcnt vmcnt(0) in front of LDS reads it cannot
+// prove disjoint from the DMA's destination (ds_read_b64_tr_b16 fragments, the A-transform's
+// coefficient table), which drained the ring every K-step in the data-grad (B_DENSE_N) and the
+// A-transform kernels.  The kernels' own counted wait_vm<N> calls order the DMA against the LDS
+// reads; a VMEM op the compiler does not see can only make its own vmcnt waits stricter.  M0 is
+// used by nothing else in these kernels.  (-DDPE_DMA_BUILTIN: the builtin, for A/B.)
 DPE_DEVICE void dma16(__amdgpu_buffer_rsrc_t r, char* wave_dst, uint32_t voff, uint32_t soff) {
+#ifdef DPE_DMA_BUILTIN
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)wave_dst, 16, voff, soff, 0, 0);
+#else
+  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)wave_dst);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               ::"s"(m0), "v"(voff), "s"(r), "s"(soff) : "memory");
+#endif
 }
 
 template <int N>
@@ -711,13 +724,22 @@ DPE_DEVICE void wait_vm() {
 #define DPE_DMA_OCC4 1  // hold the 4-wave tiles to 128 VGPRs: 4 blocks per CU even with the BN epilogue
                         // (a few epilogue spills; measured 44.2 -> 43.9 ms/step)
 #endif
-template <int BM, int BN, int WGM, int WGN, int BL, int EPI, int NS = DSTAGES>
+//
+// AX != AX_NONE (dense A only, 2-stage ring): the A operand is the output of a BatchNorm pass that
+// is never launched on its own (AXform, igemm.h) -- a second A tensor (a2) streams into the stage
+// beside A, the per-K-channel coefficients are staged in LDS once, and the transformed fragments
+// feed the MFMAs.  The waves of the first N tile whose columns start at 0 (exactly one wave per A row)
+// also store the transformed A (and its ReLU-mask bits): the standalone pass that wrote it before
+// read the same two tensors, so the consumer's own read of it is what disappears.
+template <int BM, int BN, int WGM, int WGN, int BL, int EPI, int NS = DSTAGES, int AX = AX_NONE>
 __global__ __launch_bounds__(64 * WGM * WGN, ((BM == 256 && BN == 128) || (DPE_DMA_OCC4 && WGM * WGN == 4)) ? 4 : 1)
 void igemm_dma_kernel(IgemmArgs p, int a_dense) {
   constexpr int NTH = 64 * WGM * WGN, NW = WGM * WGN;
   constexpr bool BKc = (BL == B_DENSE_K);
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int A2_BYTES = AX ? A_BYTES : 0;
+  static_assert(AX == AX_NONE || NS == 2, "A transform: 2-stage ring");
+  constexpr int STAGE = A_BYTES + A2_BYTES + B_BYTES;
   constexpr int CROW = BN * 2 + 16;
   constexpr int LDS_MAIN = (NS == 4 ? 3 : NS) * STAGE;
   constexpr int LDS_C = BM * CROW + 2 * NW * BN * 4;
@@ -774,6 +796,7 @@ void igemm_dma_kernel(IgemmArgs p, int a_dense) {
   const int64_t apre = a_dense ? 0 : ((int64_t)g.ph * g.W + g.pw) * g.C;
   const int64_t abytes = a_dense ? (int64_t)p.M * p.lda * 2 : ((int64_t)g.N * g.H * g.W * g.C + apre) * 2;
   const __amdgpu_buffer_rsrc_t ar = dma_rsrc(p.A - apre, (uint32_t)abytes);
+  const __amdgpu_buffer_rsrc_t ar2 = dma_rsrc(AX ? p.a2 : p.A, (uint32_t)abytes);
 
   // ---- B: per-piece offsets, fixed for the loop (validity never changes along K)
   uint32_t boff[PB];
@@ -829,10 +852,11 @@ void igemm_dma_kernel(IgemmArgs p, int a_dense) {
       for (int i = 0; i < PA; ++i) {
         const uint32_t v = ((amask[i] >> tap) & 1u) ? aoff[i] : DMA_OOB;
         dma16(ar, st + (wid * PA + i) * 1024, v, tapoff + ci * 2);
+        if constexpr (AX != AX_NONE) dma16(ar2, st + A_BYTES + (wid * PA + i) * 1024, v, tapoff + ci * 2);
       }
     }
 #pragma unroll
-    for (int i = 0; i < PB; ++i) dma16(br, st + A_BYTES + (wid * PB + i) * 1024, boff[i], kbo);
+    for (int i = 0; i < PB; ++i) dma16(br, st + A_BYTES + A2_BYTES + (wid * PB + i) * 1024, boff[i], kbo);
     kbo += bstep;
     if (c16) {
       next_tap();
@@ -852,9 +876,76 @@ void igemm_dma_kernel(IgemmArgs p, int a_dense) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // A transform: the per-K-channel coefficient tables sit in (dynamic) LDS for the whole launch,
+  // [NXC][K] floats (K <= 2048: <= 32 KiB, and the big-K shapes are the small-M ones); the lane
+  // reads the 8 channels 32 t + 8 g .. +7 of each table per K-step (broadcast reads)
+  constexpr int NXC = AX == AX_BN_RES ? 2 : AX == AX_BN_BWD ? 3 : 4;
+  extern __shared__ __attribute__((aligned(16))) float ax_coef[];
+  const int xg = (lane >> 4) * 8;
+  // the waves holding output columns [0, BN/WGN) of the first N tile store the transformed A
+  const bool ax_store = AX != AX_NONE && tn == 0 && wn == 0;
+  const __amdgpu_buffer_rsrc_t aout_r = dma_rsrc(AX ? (const void*)p.a_out : p.A, (uint32_t)((int64_t)p.M * p.lda * 2));
+  const __amdgpu_buffer_rsrc_t bits_r = dma_rsrc(AX ? (const void*)p.a_bits : p.A, (uint32_t)((int64_t)p.M * p.lda / 8));
+  auto xform = [&](int t, bf16x8 (&a)[RM], const bf16x8 (&a2)[RM]) {
+    if constexpr (AX != AX_NONE) {
+      const int k = t * BK + xg;
+      float c[NXC][8];
+#pragma unroll
+      for (int q = 0; q < NXC; ++q) {
+        const f32x4 lo = *(const f32x4*)(ax_coef + q * p.K + k), hi = *(const f32x4*)(ax_coef + q * p.K + k + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { c[q][e] = lo[e]; c[q][e + 4] = hi[e]; }
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        float f[8], g[8];
+        unpack8(__builtin_bit_cast(u32x4, a[i]), f);
+        unpack8(__builtin_bit_cast(u32x4, a2[i]), g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if constexpr (AX == AX_BN_RES) {
+            f[e] = fmaxf(fmaf(f[e], c[0][e], c[1][e]) + g[e], 0.f);
+          } else if constexpr (AX == AX_BN_RES2) {  // the residual rounded to bf16 first, as bn_apply2
+            f[e] = fmaxf(fmaf(f[e], c[0][e], c[1][e]) + bf2f(f2bf(fmaf(g[e], c[2 % NXC][e], c[3 % NXC][e]))), 0.f);
+          } else {
+            f[e] = fmaf(c[0][e], f[e], fmaf(c[1 % NXC][e], g[e], c[2 % NXC][e]));
+          }
+        }
+        const u32x4 pk = pack8(f);
+        a[i] = __builtin_bit_cast(bf16x8, pk);
+        if (ax_store) {
+          // buffer stores, issued unconditionally (rows past M get an out-of-range offset and are
+          // dropped by the buffer unit), so every storing wave has exactly AX_ST stores per K-step
+          // behind the next stage's DMA -- the counted wait at the next step leaves them in flight
+          const int m = m0 + wm + 16 * i + (lane & 15);
+          const uint32_t off = (uint32_t)m * (uint32_t)p.lda + (uint32_t)k;  // elements (< 2^30: checked on the host)
+          const bool ok = m < p.M;
+          __builtin_amdgcn_raw_buffer_store_b128(pk, aout_r, ok ? off * 2u : DMA_OOB, 0, 0);
+          if constexpr (AX != AX_BN_BWD) {
+            // the row's 4 mask bytes of this K-step (lanes li, li+16, li+32, li+48) as one dword
+            const uint32_t b = relu_mask_byte(pk), li = lane & 15;
+            const uint32_t w = b | ((uint32_t)__shfl(b, li + 16, 64) << 8) | ((uint32_t)__shfl(b, li + 32, 64) << 16) |
+                               ((uint32_t)__shfl(b, li + 48, 64) << 24);
+            __builtin_amdgcn_raw_buffer_store_b32(w, bits_r, (ok && lane < 16) ? off >> 3 : DMA_OOB, 0, 0);
+          }
+        }
+      }
+    }
+  };
+  // stores per K-step of a storing wave (the counted wait below)
+  constexpr int AX_ST = AX == AX_NONE ? 0 : AX == AX_BN_BWD ? RM : 2 * RM;
+  if constexpr (AX != AX_NONE) {
+    // tables: AX_BN_RES [scale | shift] = a_coef rows 0-1; AX_BN_BWD [a | b | c]; AX_BN_RES2 + a_coef2 rows 0-1
+    for (int i = tid; i < NXC * p.K; i += NTH) {
+      const int q = i / p.K, kk = i - q * p.K;
+      ax_coef[i] = (AX == AX_BN_RES2 && q >= 2) ? p.a_coef2[(q - 2) * p.K + kk] : p.a_coef[q * p.K + kk];
+    }
+    __syncthreads();
+  }
+
   auto read_frags = [&](int buf, bf16x8 (&a)[RM], bf16x8 (&b)[RN]) {
     const char* As = smem + buf * STAGE;
-    const char* Bs = As + A_BYTES;
+    const char* Bs = As + A_BYTES + A2_BYTES;
 #pragma unroll
     for (int i = 0; i < RM; ++i) a[i] = kfrag(As, wm + 16 * i);
 #pragma unroll
@@ -883,11 +974,20 @@ void igemm_dma_kernel(IgemmArgs p, int a_dense) {
     if (nt > 0) issue(0);
     if (NS == 3 && nt > 1) issue(1);
     for (int t = 0; t < nt; ++t) {
-      if (NS == 3 && t + 1 < nt) wait_vm<PA + PB>(); else wait_vm<0>();
+      if (NS == 3 && t + 1 < nt) wait_vm<PA + PB>();
+      else if (AX != AX_NONE && ax_store && t > 0) wait_vm<AX_ST>();  // the previous step's by-product stores stay in flight
+      else wait_vm<0>();
       barrier();
       if (t + NS - 1 < nt) issue((t + NS - 1) % NS);
       bf16x8 af[RM], bfr[RN];
       read_frags(t % NS, af, bfr);
+      if constexpr (AX != AX_NONE) {
+        bf16x8 a2f[RM];
+        const char* A2s = smem + (t % NS) * STAGE + A_BYTES;
+#pragma unroll
+        for (int i = 0; i < RM; ++i) a2f[i] = kfrag(A2s, wm + 16 * i);
+        xform(t, af, a2f);
+      }
       mfmas(af, bfr);
     }
   }
@@ -1140,6 +1240,33 @@ extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int a
   if (abytes >= lim || bbytes >= lim) return -1;
   const int tiles = ((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
   const int dn = dense ? 1 : 0;
+  if (a.a_mode != AX_NONE) {
+    // A on-load transform: dense A with lda == K (the by-product is a whole [M][K] tensor)
+    if (!dense || a.lda != a.K || !a.a2 || !a.a_coef || !a.a_out) return -1;
+    if (a.a_mode == AX_BN_RES2 && !a.a_coef2) return -1;
+    const int ncoef = a.a_mode == AX_BN_RES ? 2 : a.a_mode == AX_BN_BWD ? 3 : 4;
+    if (a.K > 2048) return -1;  // coefficient tables <= 32 KiB of LDS
+    if (a.a_mode != AX_BN_BWD && !a.a_bits) return -1;
+    if ((int64_t)a.M * a.lda >= (1ll << 30)) return -1;  // 32-bit buffer offsets of the by-product
+#define DPE_DMA_AX(BM_, BN_, WGM_, WGN_, BL_, EP_, AX_)                                                     \
+  if (bm == BM_ && bn == BN_ && bload == BL_ && epi == EP_ && a.a_mode == AX_) {                            \
+    hipLaunchKernelGGL((igemm_dma_kernel<BM_, BN_, WGM_, WGN_, BL_, EP_, 2, AX_>), dim3(tiles),             \
+                       dim3(64 * WGM_ * WGN_), (size_t)ncoef * a.K * 4, st, a, dn);                         \
+    return 0;                                                                                               \
+  }
+    // forward: the next block's conv1 over relu(BN3(h3) + identity) of the block before it
+    DPE_DMA_AX(128, 64, 2, 2, B_DENSE_K, EPI_BF16, AX_BN_RES)
+    DPE_DMA_AX(128, 128, 2, 2, B_DENSE_K, EPI_BF16, AX_BN_RES)
+    DPE_DMA_AX(256, 64, 4, 1, B_DENSE_K, EPI_BF16, AX_BN_RES)
+    DPE_DMA_AX(128, 64, 2, 2, B_DENSE_K, EPI_BF16, AX_BN_RES2)
+    DPE_DMA_AX(128, 128, 2, 2, B_DENSE_K, EPI_BF16, AX_BN_RES2)
+    DPE_DMA_AX(256, 64, 4, 1, B_DENSE_K, EPI_BF16, AX_BN_RES2)
+    // backward: conv3's data grad over BN3's backward apply (dh3 = a dz3 + b h3 + c)
+    DPE_DMA_AX(128, 64, 2, 2, B_DENSE_N, EPI_BF16_BNB, AX_BN_BWD)
+    DPE_DMA_AX(128, 128, 2, 2, B_DENSE_N, EPI_BF16_BNB, AX_BN_BWD)
+#undef DPE_DMA_AX
+    return -1;
+  }
 // 4-wave tiles: a 2-stage ring keeps 4 blocks/CU; tiles up to DPE_DMA_NS3_MAX elements take the
 // 3-stage ring (two K-steps in flight)
 #ifndef DPE_DMA_NS3_MAX

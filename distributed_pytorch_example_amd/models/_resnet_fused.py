@@ -47,6 +47,17 @@ ReLU mask from h1.  Likewise a2 (DPE_PW_BNIN=1, default): the streaming
 pointwise conv3 forward and its LDS-DMA weight grad apply relu(BN2(h2)) to
 their operand fragments.)
 
+Block outputs and BN3 backward applies on load (DPE_AX_FWD=1 / DPE_AX_BWD=1): block i's
+output out_i = relu(BN3(h3_i) + idn_i) is not written by a bn_apply pass of its own.  Block i+1's
+conv1 (1x1, stride 1) computes it on its A fragments from (h3_i, idn_i) and BN3_i's coefficients
+and stores it once as a by-product (with its ReLU-mask bits) for the consumers that need it later
+(block i+1's identity / downsample conv, its conv1 weight grad, the backward masks): the pass that
+wrote out_i read the same two tensors, so conv1's own read of out_i is what disappears.  In
+backward, block i's dh3 = a*dz3 + b*h3 + c is likewise computed on the A fragments of conv3's data
+grad and stored once for conv3's weight grad (conv1x1_bnin_fwd / conv1x1_bnin_dgrad, igemm.hip
+AXform).  That removes one full read of each such tensor.  Measured: the backward form pays in
+layers 1-2 (default there), the forward form does not (off by default; see the flags below).
+
 Weight gradients are accumulated straight into the DDP bucket views and each
 parameter is announced to the reducer as soon as its gradient is final, in
 reverse-forward order, so bucket all-reduces start while earlier blocks are
@@ -74,6 +85,33 @@ _ROW_BNIN = _EPI_BNB and os.environ.get("DPE_ROW_BNIN", "1") != "0"
 _PW_BNIN = _EPI_BNB and os.environ.get("DPE_PW_BNIN", "1") != "0"
 # DPE_DOWN_CHAIN=0: the block before a downsample block runs its BN3 backward standalone (reduce + apply)
 _DOWN_CHAIN = _BN3_CHAIN and os.environ.get("DPE_DOWN_CHAIN", "1") != "0"
+# DPE_AX_FWD=1: block outputs written by the next block's conv1 instead of a bn_apply pass.  Off:
+# measured slower at every ResNet-50 shape (scripts/bench_bnin.py, profiles/bnin_r3.jsonl: layer 1
+# 654 vs 635 us, layers 3-4 +20-80 %) -- the by-product leaves the K-loop in 64-B row segments
+# (one 32-deep K-step per row per store), which the memory system absorbs at ~3 TB/s where the
+# streaming pass writes whole 1-KiB runs at ~6 TB/s.
+_AX_FWD = _BN3_CHAIN and os.environ.get("DPE_AX_FWD", "0") == "1"
+# DPE_AX_BWD=1: every chained block's dh3 (of at most DPE_AX_BWD_MAXC channels) computed on conv3's
+# data-grad fragments instead of a bn_bwd_apply pass.  Per op: layer 2 -11 %, layer 1 -1.5 %,
+# layers 3-4 +1-19 % (profiles/bnin_r3.jsonl); on the ResNet-50 step within noise (37.99-38.15 vs
+# 37.99-38.11 ms, 3 alternating rounds), so off by default -- kept as a tested building block.
+_AX_BWD = _BN3_CHAIN and os.environ.get("DPE_AX_BWD", "0") == "1"
+_AX_BWD_MAXC = int(os.environ.get("DPE_AX_BWD_MAXC", "512"))
+# row tile of the on-load forward at 64 output channels (128: 4 blocks/CU, 256: 2; the
+# downsample-identity form spills at 128)
+_AX_TILE = int(os.environ.get("DPE_AX_TILE", "256"))
+
+
+def _ax_ok(conv, cin) -> bool:
+    """A 1x1 stride-1 conv whose input channels the on-load transform kernel takes."""
+    return (tuple(conv.kernel_size) == (1, 1) and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (0, 0)
+            and cin % 32 == 0 and cin <= 2048)
+
+
+def can_materialise_input(block) -> bool:
+    """True when ``block``'s conv1 can compute (and store) its input from the previous block's
+    pre-BN3 tensors, so the previous block may defer its output (DPE_AX_FWD)."""
+    return _AX_FWD and block.fused and _ax_ok(block.c1.conv, block.c1.conv.in_channels)
 
 
 def _out_hw(hw, conv):
@@ -86,11 +124,14 @@ class _BN3Link:
     fused-epilogue result (BN3_i partials, identity of the masked dz3_i)
     handed back to block i's backward."""
 
-    __slots__ = ("h3", "coef", "mask", "part", "dz_ptr", "dz_shape")
+    __slots__ = ("h3", "coef", "mask", "part", "dz_ptr", "dz_shape", "pending")
 
     def __init__(self):
         self.h3 = self.coef = self.mask = self.part = None
         self.dz_ptr, self.dz_shape = 0, None
+        # (h3, coef3, idn, idn_coef, out, bits): block i's output, allocated but not yet written --
+        # block i+1's conv1 writes it (conv1x1_bnin_fwd)
+        self.pending = None
 
 
 def _conv_conf(conv):
@@ -99,15 +140,28 @@ def _conv_conf(conv):
 
 class BottleneckFn(Function):
     @staticmethod
-    def forward(ctx, x, block, link_in, link_out, *params):
+    def forward(ctx, x, block, link_in, link_out, defer_out, *params):
         C = ext()
         convs = [block.c1, block.c2, block.c3] + ([block.down] if block.down is not None else [])
         ws = [shadow(cb.conv.weight) for cb in convs]
+        pend = link_in.pending if link_in is not None else None
+        if pend is not None:
+            # x is the previous block's output, not yet written: conv1 computes it on load from
+            # (h3, identity) and BN3's coefficients and stores it (+ its ReLU bits) as a by-product
+            ph3, pc3, pidn, pcd, pout, pbits = pend
+            assert pout is x, "deferred block output consumed by a different tensor"
+            link_in.pending = None
+            h1_st = C.conv1x1_bnin_fwd(ph3, pidn, pc3, pcd, ws[0], x, pbits, True, _AX_TILE)
+        else:
+            h1_st = None
 
         def convbn(i, inp, relu, residual=None):
             cb = convs[i]
             s, p, d = _conv_conf(cb.conv)
-            h, st = C.conv_fwd(inp, ws[i], s, p, d, True, None)  # BN stats partials from the epilogue
+            if i == 0 and h1_st is not None:
+                h, st = h1_st
+            else:
+                h, st = C.conv_fwd(inp, ws[i], s, p, d, True, None)  # BN stats partials from the epilogue
             bn = cb.bn
             y, coef = C.bn_fwd_train(h, bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var,
                                      bn.momentum, bn.eps, relu, residual, st)
@@ -116,17 +170,20 @@ class BottleneckFn(Function):
         def conv_coef(i, inp, in_coef=None):
             cb = convs[i]
             s, p, d = _conv_conf(cb.conv)
-            h, st = C.conv_fwd(inp, ws[i], s, p, d, True, None, in_coef)
+            if i == 0 and h1_st is not None:
+                h, st = h1_st
+            else:
+                h, st = C.conv_fwd(inp, ws[i], s, p, d, True, None, in_coef)
             bn = cb.bn
             M = h.numel() // h.shape[-1]
             return h, C.bn_coef(st, M, bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var, bn.momentum,
                                 bn.eps)
 
-        if block.down is not None:
+        c1conv, c2conv = convs[0].conv, convs[1].conv
+        if h1_st is None and block.down is not None:
             hd, cd = conv_coef(3, x)  # BN_d is applied inside BN3's pass (bn_apply with residual_coef)
         else:
-            hd, cd = None, None
-        c1conv, c2conv = convs[0].conv, convs[1].conv
+            hd, cd = None, None  # (x still pending: after conv1 has written it)
         h1_shape = [x.shape[0], _out_hw(x.shape[1], c1conv), _out_hw(x.shape[2], c1conv), c1conv.out_channels]
         if _ROW_BNIN and C.row_bn_on_load(h1_shape, list(ws[1].shape), *_conv_conf(c2conv)):
             # a1 never materialised: conv2 applies relu(BN1(h1)) to its input rows on load
@@ -136,6 +193,8 @@ class BottleneckFn(Function):
         else:
             h1, a1, c1 = convbn(0, x, True)
             h2, st2 = C.conv_fwd(a1, ws[1], *_conv_conf(c2conv), True, None)
+        if h1_st is not None and block.down is not None:
+            hd, cd = conv_coef(3, x)  # x written by conv1 above
         bn2 = convs[1].bn
         if _PW_BNIN and C.pw_bn_on_load(list(h2.shape), convs[2].conv.out_channels):
             # a2 never materialised: the streaming conv3 forward and its LDS-DMA weight grad apply
@@ -149,7 +208,12 @@ class BottleneckFn(Function):
         # the next block's fused data-grad epilogue reads this output's ReLU mask as bits
         want_bits = True  # 1/16 of out: read by the next block's fused epilogue or by this block's BN3 backward
         h3, c3 = conv_coef(2, h2, c2) if a2 is None else conv_coef(2, a2)
-        if block.down is not None:
+        if defer_out and link_out is not None:
+            # written later by the next block's conv1 (conv1x1_bnin_fwd): no bn_apply pass
+            out = torch.empty_like(h3)
+            bits = torch.empty(*h3.shape[:-1], h3.shape[-1] // 8, dtype=torch.uint8, device=h3.device)
+            link_out.pending = (h3, c3, hd, cd, out, bits) if block.down is not None else (h3, c3, x, None, out, bits)
+        elif block.down is not None:
             out, bits = C.bn_apply(h3, c3, hd, cd, True, want_bits)
         else:
             out, bits = C.bn_apply(h3, c3, x, None, True, want_bits)
@@ -186,6 +250,7 @@ class BottleneckFn(Function):
         grads = {}
         res_mask = None  # set when dz3 is represented as (dout, ReLU bits of out)
         dhd = None  # downsample BN's dL/dhd, when computed together with BN3's (bn_bwd_dual)
+        dh3_coef = None  # set when dh3 is computed on load by conv3's data grad
 
         def bn_sinks(i):
             bn = convs[i].bn
@@ -246,6 +311,9 @@ class BottleneckFn(Function):
                 dh3, dhd = C.bn_bwd_dual(dz3, h3, bn.weight.detach(), c3, lk.part, gb, bb, hd, bnd.weight.detach(), cd,
                                          gbd, bbd)
                 bn_done(bnd, gbd, gdd, bbd, bdd)
+            elif _AX_BWD and _EPI_BNB and h3.shape[-1] <= _AX_BWD_MAXC and _ax_ok(convs[2].conv, h3.shape[-1]):
+                # dh3 = a*dz3 + b*h3 + c computed on conv3's data-grad fragments (below), no apply pass
+                dh3_coef = C.bn_bwd_coef(lk.part, h3.numel() // h3.shape[-1], bn.weight.detach(), c3, gb, bb)
             else:
                 dh3 = C.bn_bwd_partials(dz3, h3, bn.weight.detach(), c3, lk.part, gb, bb, relu_mask=False)
             bn_done(bn, gb, gd, bb, bd)
@@ -260,11 +328,23 @@ class BottleneckFn(Function):
         ctx.bits = None
         if lk is not None:
             lk.h3 = lk.coef = lk.mask = None
-        if a2 is None:  # a2 = relu(BN2(h2)) recomputed on the weight grad's B fragments
-            wgrad(2, dh3, h2, c2)
+        if dh3_coef is not None:
+            # conv3's data grad over dh3 = a*dz3 + b*h3 + c (on load), dh3 stored for the weight grad
+            dh3 = torch.empty_like(h3)
+            da2, part2 = C.conv1x1_bnin_dgrad(dz3, h3, dh3_coef, ws[2], dh3, h2, c2)
+            bn, gb, gd, bb, bd = bn_sinks(1)
+            dh2 = C.bn_bwd_partials(da2, h2, bn.weight.detach(), c2, part2, gb, bb)
+            bn_done(bn, gb, gd, bb, bd)
+            if a2 is None:
+                wgrad(2, dh3, h2, c2)
+            else:
+                wgrad(2, dh3, a2)
         else:
-            wgrad(2, dh3, a2)
-        dh2 = dgrad_bnb(2, dh3, 1, a2, h2, c2)  # (a2 unused: _EPI_BNB recomputes the mask from h2)
+            if a2 is None:  # a2 = relu(BN2(h2)) recomputed on the weight grad's B fragments
+                wgrad(2, dh3, h2, c2)
+            else:
+                wgrad(2, dh3, a2)
+            dh2 = dgrad_bnb(2, dh3, 1, a2, h2, c2)  # (a2 unused: _EPI_BNB recomputes the mask from h2)
         if a1 is None:  # a1 = relu(BN1(h1)) recomputed on load by the row-walking weight grad
             wgrad(1, dh2, h1, c1)
         else:
@@ -305,19 +385,22 @@ class BottleneckFn(Function):
                 dhd, _ = bn_bwd(3, dz3, None, hd, cd, False)
             wgrad(3, dhd, x)
         pgrads = [grads.get(id(p)) for p in ctx.block._fused_params]
-        return (dx, None, None, None, *pgrads)
+        return (dx, None, None, None, None, *pgrads)
 
 
-def bottleneck_forward(block, x, link_in=None, chain=False, count_batches=True):
+def bottleneck_forward(block, x, link_in=None, chain=False, count_batches=True, defer_out=False):
     """Fused block forward.  ``chain=True`` (the ResNet's own block loop, where
     this block's output feeds only the next block) returns ``(out, link)`` for
     the next block's ``link_in``.  ``count_batches=False``: the ResNet advanced
-    every block's num_batches_tracked in one launch already."""
+    every block's num_batches_tracked in one launch already.  ``defer_out`` (with
+    ``chain``; the next block passes ``can_materialise_input``): the returned
+    output is written by the next block's conv1, which MUST be called next."""
     params = block._fused_params
     if count_batches:
         nbt = [cb.bn.num_batches_tracked
                for cb in [block.c1, block.c2, block.c3] + ([block.down] if block.down is not None else [])]
         torch._foreach_add_(nbt, 1)
     link_out = _BN3Link() if (chain and _BN3_CHAIN) else None
-    out = BottleneckFn.apply(x, block, link_in if _BN3_CHAIN else None, link_out, *params)
+    out = BottleneckFn.apply(x, block, link_in if _BN3_CHAIN else None, link_out, bool(defer_out and link_out is not None),
+                             *params)
     return (out, link_out) if chain else out

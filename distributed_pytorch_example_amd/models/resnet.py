@@ -59,14 +59,15 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         return self.forward_chained(x, None, chain=False)
 
-    def forward_chained(self, x, link=None, chain=True, count_batches=True):
+    def forward_chained(self, x, link=None, chain=True, count_batches=True, defer_out=False):
         """``chain=True``: returns (out, link); the link lets the next block's
         backward fuse this block's BN3 backward (``_resnet_fused``).
-        ``count_batches=False``: the caller already advanced the BNs' num_batches_tracked."""
+        ``count_batches=False``: the caller already advanced the BNs' num_batches_tracked.
+        ``defer_out``: the output is written by the next block's conv1 (called next)."""
         if x.is_cuda and self.training and self.fused:
             from ._resnet_fused import bottleneck_forward
 
-            return bottleneck_forward(self, x, link, chain, count_batches)
+            return bottleneck_forward(self, x, link, chain, count_batches, defer_out)
         out = self._forward_per_op(x)
         return (out, None) if chain else out
 
@@ -129,8 +130,15 @@ class ResNet(nn.Module):
         if any(fused):
             torch._foreach_add_([m.num_batches_tracked for b, f in zip(self.blocks, fused) if f for m in b.modules()
                                  if getattr(m, "num_batches_tracked", None) is not None], 1)
-        for blk, f in zip(self.blocks, fused):  # each block's output feeds only the next block
-            h, link = blk.forward_chained(h, link, count_batches=not f)
+        # a block's output may be left to the next block's conv1 to write (on-load BN3 apply)
+        defer = [False] * len(fused)
+        if any(fused):
+            from ._resnet_fused import can_materialise_input
+
+            defer = [f and i + 1 < len(fused) and fused[i + 1] and can_materialise_input(self.blocks[i + 1])
+                     for i, f in enumerate(fused)]
+        for blk, f, d in zip(self.blocks, fused, defer):  # each block's output feeds only the next block
+            h, link = blk.forward_chained(h, link, count_batches=not f, defer_out=d)
         h = Fx.global_avg_pool_nhwc(h)
         return self.fc(h)
 

@@ -1,0 +1,120 @@
+"""BatchNorm applies computed on the A operand of the 1x1 LDS-DMA conv (igemm.hip AXform,
+ops conv1x1_bnin_fwd / conv1x1_bnin_dgrad), against the standalone passes they replace:
+
+* forward: out = relu(BN3(h3) + idn) [idn = BN_d(hd) for a downsample block] stored as a
+  by-product is bitwise the bn_apply output (and its ReLU bits); the conv over it matches the
+  conv over the materialised tensor, and so do the BN partials of its output;
+* backward: dh3 = a*dz3 + b*h3 + c stored as a by-product is bitwise bn_bwd_partials' output;
+  the data grad and its BN2-backward partials match conv_dgrad_bn over the materialised dh3.
+
+ResNet-50 shapes at reduced batch (every layer's K / N), plus an M tail (243 rows).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+dev = torch.device("cuda")
+
+
+def bf(t):
+    return t.to(torch.bfloat16).contiguous()
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+def _bn_coef(Cc, g=None):
+    scale = torch.rand(Cc, device=dev, generator=g) + 0.5
+    shift = torch.randn(Cc, device=dev, generator=g) * 0.5
+    mean = torch.randn(Cc, device=dev, generator=g) * 0.3
+    invstd = torch.rand(Cc, device=dev, generator=g) + 0.5
+    return torch.stack([scale, shift, mean, invstd]).contiguous()
+
+
+FWD_SHAPES = [(4, 56, 256, 64, 128), (4, 56, 256, 64, 256), (4, 28, 512, 128, 128), (8, 14, 1024, 256, 128),
+              (8, 7, 2048, 512, 128), (3, 9, 256, 64, 128), (3, 9, 256, 64, 256)]
+
+
+@pytest.mark.parametrize("N,H,Ci,Co,tile", FWD_SHAPES)
+@pytest.mark.parametrize("down", [False, True])
+def test_conv1x1_bnin_fwd_matches_bn_apply_then_conv(C, N, H, Ci, Co, tile, down):
+    g = torch.Generator(device=dev).manual_seed(Ci + Co + H + int(down))
+    h = bf(torch.randn(N, H, H, Ci, device=dev, generator=g))
+    res = bf(torch.randn(N, H, H, Ci, device=dev, generator=g))
+    coef = _bn_coef(Ci, g)
+    rc = _bn_coef(Ci, g) if down else None
+    w = bf(torch.randn(Co, 1, 1, Ci, device=dev, generator=g) / math.sqrt(Ci))
+    x_ref, bits_ref = C.bn_apply(h, coef, res, rc, True, True)
+    y_ref, st_ref = C.conv_fwd(x_ref, w, [1, 1], [0, 0], [1, 1], True, None)
+    x = torch.full_like(h, float("nan"))
+    bits = torch.full((N, H, H, Ci // 8), 0xA5, dtype=torch.uint8, device=dev)
+    y, st = C.conv1x1_bnin_fwd(h, res, coef, rc, w, x, bits, True, tile)
+    torch.cuda.synchronize()
+    assert torch.equal(x, x_ref), "by-product differs from bn_apply"
+    assert torch.equal(bits, bits_ref), "ReLU bits differ from bn_apply's"
+    assert rel_err(y, y_ref) < 2e-3
+    assert rel_err(st.sum(-1), st_ref.sum(-1)) < 1e-3
+
+
+BWD_SHAPES = [(4, 56, 64, 256), (4, 28, 128, 512), (8, 14, 256, 1024), (8, 7, 512, 2048), (3, 9, 64, 256)]
+
+
+@pytest.mark.parametrize("N,H,Cm,Co", BWD_SHAPES)
+def test_conv1x1_bnin_dgrad_matches_bn_bwd_then_dgrad(C, N, H, Cm, Co):
+    g = torch.Generator(device=dev).manual_seed(Cm + Co + H)
+    M = N * H * H
+    dz = bf(torch.randn(N, H, H, Co, device=dev, generator=g))
+    h3 = bf(torch.randn(N, H, H, Co, device=dev, generator=g))
+    c3 = _bn_coef(Co, g)
+    gamma = torch.rand(Co, device=dev, generator=g) + 0.5
+    part = torch.randn(2, Co, 7, device=dev, generator=g) * math.sqrt(M)
+    w = bf(torch.randn(Co, 1, 1, Cm, device=dev, generator=g) / math.sqrt(Co))  # conv3: Cm -> Co
+    h2 = bf(torch.randn(N, H, H, Cm, device=dev, generator=g))
+    c2 = _bn_coef(Cm, g)
+    dg_ref, db_ref = torch.zeros(Co, device=dev), torch.zeros(Co, device=dev)
+    dh_ref = C.bn_bwd_partials(dz, h3, gamma, c3, part, dg_ref, db_ref, relu_mask=False)
+    da_ref, p_ref = C.conv_dgrad_bn(dh_ref, w, [N, H, H, Cm], [1, 1], [0, 0], [1, 1], None, h2, c2)
+    dg, db = torch.zeros(Co, device=dev), torch.zeros(Co, device=dev)
+    bcoef = C.bn_bwd_coef(part, M, gamma, c3, dg, db)
+    dh = torch.full_like(h3, float("nan"))
+    da, p = C.conv1x1_bnin_dgrad(dz, h3, bcoef, w, dh, h2, c2)
+    torch.cuda.synchronize()
+    assert torch.equal(dg, dg_ref) and torch.equal(db, db_ref)
+    assert torch.equal(dh, dh_ref), "by-product differs from bn_bwd_apply"
+    assert rel_err(da, da_ref) < 2e-3
+    assert rel_err(p.sum(-1), p_ref.sum(-1)) < 2e-3
+
+
+def test_resnet_step_with_on_load_bn_matches_default(C):
+    """Model level: a ResNet whose blocks chain through identity blocks, trained one step with the
+    on-load forward / backward BN applies (DPE_AX_FWD / DPE_AX_BWD) and without: same loss and
+    gradients (the by-products are bitwise; only the conv1 tile's accumulation order may differ)."""
+    from distributed_pytorch_example_amd.models import _resnet_fused as RF
+    from distributed_pytorch_example_amd.models.resnet import ResNet
+    from distributed_pytorch_example_amd.ops import functional as Fx
+
+    torch.manual_seed(3)
+    model = ResNet((2, 2, 2, 1), num_classes=10).to(dev)
+    x = torch.randn(8, 3, 64, 64, device=dev)
+    y = torch.randint(0, 10, (8,), device=dev)
+    saved = RF._AX_FWD, RF._AX_BWD, RF._AX_BWD_MAXC
+    runs = []
+    try:
+        for fwd, bwd in ((False, False), (True, True)):
+            RF._AX_FWD, RF._AX_BWD, RF._AX_BWD_MAXC = fwd, bwd, 2048
+            model.zero_grad(set_to_none=True)
+            loss = Fx.cross_entropy(model(x), y, 10)
+            loss.backward()
+            torch.cuda.synchronize()
+            runs.append((loss.item(), [p.grad.detach().float().clone() for p in model.parameters()]))
+    finally:
+        RF._AX_FWD, RF._AX_BWD, RF._AX_BWD_MAXC = saved
+    (l0, g0), (l1, g1) = runs
+    assert abs(l0 - l1) <= 1e-3 * abs(l0)
+    for a, b in zip(g0, g1):
+        assert rel_err(b, a) < 2e-2

@@ -117,7 +117,7 @@ def test_resnet50_full_training_parity():
     ours = get_model("resnet50").to(DEV)
     twin = _TResNet(ours).to(DEV)
     twin_bf = copy.deepcopy(twin)
-    w0 = _resnet_flat(twin, False)
+    w0 = [t.clone() for t in _resnet_flat(twin, False)]  # (.float() of an fp32 tensor aliases it)
     g = torch.Generator(device=DEV).manual_seed(1)
     data = [(torch.randn(16, 3, 224, 224, device=DEV, generator=g), torch.randint(0, 1000, (16,), device=DEV, generator=g))
             for _ in range(3)]
