@@ -185,7 +185,10 @@ int g_dma_tile = 0;
 int dma_tile_mode() { return g_dma_tile; }
 
 void dma_tile(const dpe::IgemmArgs& a, int aload, int bload, int& bm, int& bn) {
-  if (bm != 128 || bload != dpe::B_DENSE_K) return;
+  if (bm != 128) return;
+  // (1x1 data grads, N-contiguous weights: the 256x128 8-wave tile measured slower at K >= 1024,
+  // ResNet-50 37.77-37.82 vs 37.63-37.67 ms: they stay on the 128-row tiles)
+  if (bload != dpe::B_DENSE_K) return;
   int mode = dma_tile_mode();
   const bool taps = aload == dpe::A_CONV_FWD && a.g.R * a.g.S > 1;
   if (a.N <= 64) {

@@ -157,6 +157,8 @@ CONV_CASES = [
     (3, 7, 7, 128, 512, 1, 1, 0),
     (2, 9, 9, 256, 1024, 1, 1, 0),
     (4, 30, 30, 64, 512, 1, 1, 0),
+    # 1x1 data grad with K = 2048, M tail (588 rows)
+    (3, 14, 14, 512, 2048, 1, 1, 0),
     # C = 16 (s2d stem form): two filter taps per 32-wide K-step on the LDS-DMA kernel
     (2, 12, 12, 16, 64, 4, 1, 2),
     (2, 9, 9, 16, 48, 2, 2, 0),
