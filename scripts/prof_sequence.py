@@ -17,11 +17,18 @@ rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]
 marks = [r for r in rows if marker in r["Kernel_Name"]]
 t0, t1 = int(marks[skip - 1]["End_Timestamp"]), int(marks[skip]["End_Timestamp"])
 sel = [r for r in rows if t0 < int(r["Start_Timestamp"]) <= t1]
-tot = 0.0
+tot, prev_end, gaps = 0.0, t0, []
 for i, r in enumerate(sel):
-    us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    us = (en - st) / 1e3
+    gap = max(0, st - prev_end) / 1e3  # idle time before this launch (ns -> us)
+    prev_end = max(prev_end, en)
     tot += us
     grid = r.get("Grid_Size", r.get("Grid_Size_X", "?"))
     wg = r.get("Workgroup_Size", r.get("Workgroup_Size_X", "?"))
     name = re.sub(r"\(.*", "", r["Kernel_Name"])[:90]
-    print(f"{i:4d} {us:8.1f}us cum={tot / 1e3:7.3f}ms grid={grid:>8} wg={wg:>5} {name}")
+    gaps.append((gap, i, name))
+    print(f"{i:4d} {us:8.1f}us gap={gap:6.1f}us cum={tot / 1e3:7.3f}ms grid={grid:>8} wg={wg:>5} {name}")
+print(f"# idle between launches: {sum(g for g, _, _ in gaps) / 1e3:.3f} ms over {len(gaps)} launches; largest:")
+for g, i, n in sorted(gaps, reverse=True)[:12]:
+    print(f"#   {g:7.1f}us before #{i} {n}")
