@@ -354,11 +354,17 @@ using namespace dpe;
 
 extern "C" int dpe_cu_reserve();  // comm.cpp
 
-// columns per wave.  The data grads at K = 128 use 32 (like K = 256) so that the epilogue operands
+// columns per wave.  The data grads at K = 64 / 128 use 32 (like K = 256) so that the epilogue operands
 // (residual, pre-BN input, masks) can be hoisted ahead of the tile's MFMAs: with 64 columns per wave
 // they were loaded in the epilogue and each half-tile stalled a full HBM round trip (layer-2 conv1
 // data grads ran at ~61 % of their HBM roofline).
-static int pw_wn(int K, int epi) { return K == 64 || (K == 128 && epi == PW_FWD) ? 64 : 32; }
+#ifndef DPE_PW64_DGRAD_WN
+#define DPE_PW64_DGRAD_WN 32  // (64: the previous layout, for A/B)
+#endif
+static int pw_wn(int K, int epi) {
+  if (K == 64 && epi == PW_DGRAD) return DPE_PW64_DGRAD_WN;
+  return (K == 64 || K == 128) && epi == PW_FWD ? 64 : 32;
+}
 
 // Every block carries the same number of tiles, so the grid must be exactly the resident
 // capacity (blocks per CU from the occupancy API x CUs): a grid that lets the dispatcher put
@@ -376,7 +382,7 @@ static int pw_slots() {
 }
 template <int EPI>
 static int pw_capacity(int K) {
-  if (K == 64) return pw_slots<64, 64, 4, EPI>();
+  if (K == 64) return EPI == PW_FWD ? pw_slots<64, 64, 4, EPI>() : pw_slots<64, DPE_PW64_DGRAD_WN, 4, EPI>();
   if (K == 128) return EPI == PW_FWD ? pw_slots<128, 64, 3, EPI>() : pw_slots<128, 32, 3, EPI>();
   return pw_slots<256, 32, 2, EPI>();
 }
@@ -411,6 +417,10 @@ extern "C" int dpe_pw_launch(const PwArgs* args, int epi, hipStream_t st) {
     if (epi == PW_FWD) hipLaunchKernelGGL((pw::pw_stream_kernel<K_, WN_, NS_, PW_FWD>), grid, block, 0, st, a); \
     else hipLaunchKernelGGL((pw::pw_stream_kernel<K_, WN_, NS_, PW_DGRAD>), grid, block, 0, st, a);    \
     return 0;                                                                                           \
+  }
+  if (a.K == 64 && epi == PW_DGRAD) {
+    hipLaunchKernelGGL((pw::pw_stream_kernel<64, DPE_PW64_DGRAD_WN, 4, PW_DGRAD>), grid, block, 0, st, a);
+    return 0;
   }
   PW_L(64, 64, 4)
   if (a.K == 128 && epi == PW_DGRAD) {
