@@ -361,9 +361,19 @@ extern "C" int dpe_cu_reserve();  // comm.cpp
 #ifndef DPE_PW64_DGRAD_WN
 #define DPE_PW64_DGRAD_WN 32  // (64: the previous layout, for A/B)
 #endif
+// The forward (stats-only epilogue, no operand loads) keeps 64 columns per wave: 32 measured slower
+// at K = 64 and 128 (ResNet-50 +0.1-0.2 ms/step: each row tile's DMA and BN-on-load transform then
+// run in twice as many blocks); the defines are the compile-time A/B arms.
+#ifndef DPE_PW64_FWD_WN
+#define DPE_PW64_FWD_WN 64
+#endif
+#ifndef DPE_PW128_FWD_WN
+#define DPE_PW128_FWD_WN 64
+#endif
 static int pw_wn(int K, int epi) {
-  if (K == 64 && epi == PW_DGRAD) return DPE_PW64_DGRAD_WN;
-  return (K == 64 || K == 128) && epi == PW_FWD ? 64 : 32;
+  if (K == 64) return epi == PW_DGRAD ? DPE_PW64_DGRAD_WN : DPE_PW64_FWD_WN;
+  if (K == 128) return epi == PW_FWD ? DPE_PW128_FWD_WN : 32;
+  return 32;
 }
 
 // Every block carries the same number of tiles, so the grid must be exactly the resident
@@ -382,8 +392,8 @@ static int pw_slots() {
 }
 template <int EPI>
 static int pw_capacity(int K) {
-  if (K == 64) return EPI == PW_FWD ? pw_slots<64, 64, 4, EPI>() : pw_slots<64, DPE_PW64_DGRAD_WN, 4, EPI>();
-  if (K == 128) return EPI == PW_FWD ? pw_slots<128, 64, 3, EPI>() : pw_slots<128, 32, 3, EPI>();
+  if (K == 64) return EPI == PW_FWD ? pw_slots<64, DPE_PW64_FWD_WN, 4, EPI>() : pw_slots<64, DPE_PW64_DGRAD_WN, 4, EPI>();
+  if (K == 128) return EPI == PW_FWD ? pw_slots<128, DPE_PW128_FWD_WN, 3, EPI>() : pw_slots<128, 32, 3, EPI>();
   return pw_slots<256, 32, 2, EPI>();
 }
 
@@ -422,12 +432,18 @@ extern "C" int dpe_pw_launch(const PwArgs* args, int epi, hipStream_t st) {
     hipLaunchKernelGGL((pw::pw_stream_kernel<64, DPE_PW64_DGRAD_WN, 4, PW_DGRAD>), grid, block, 0, st, a);
     return 0;
   }
-  PW_L(64, 64, 4)
+  if (a.K == 64) {
+    hipLaunchKernelGGL((pw::pw_stream_kernel<64, DPE_PW64_FWD_WN, 4, PW_FWD>), grid, block, 0, st, a);
+    return 0;
+  }
   if (a.K == 128 && epi == PW_DGRAD) {
     hipLaunchKernelGGL((pw::pw_stream_kernel<128, 32, 3, PW_DGRAD>), grid, block, 0, st, a);
     return 0;
   }
-  PW_L(128, 64, 3)
+  if (a.K == 128) {
+    hipLaunchKernelGGL((pw::pw_stream_kernel<128, DPE_PW128_FWD_WN, 3, PW_FWD>), grid, block, 0, st, a);
+    return 0;
+  }
   PW_L(256, 32, 2)
 #undef PW_L
   return -1;
