@@ -204,34 +204,36 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
   }
 }
 
-// Column-parallel reduction of the [nb][2][D] partials: block = 64 columns x
-// 16 waves splitting the nb rows (coalesced 256-B row reads, 4 independent
-// accumulators per lane), blockIdx.y picks dw (0) or db (1).
-constexpr int LNF_W = 16;
+// Column-parallel reduction of the [nb][2][D] partials: block = 16 columns x 64 row stripes
+// (16 waves, each lane one (column, stripe); 64-B row segments), 4 independent accumulators per
+// lane, fixed-order tree over the stripes; blockIdx.y picks dw (0) or db (1).  96 blocks at D = 768
+// (64 columns per block gave 24 blocks on 24 CUs: ~8 us, latency-bound, 25 calls per GPT-2 step).
+constexpr int LNF_W = 16, LNF_C = 16, LNF_S = LNF_W * (64 / LNF_C);
 __global__ __launch_bounds__(64 * LNF_W) void ln_bwd_finalize_kernel(const float* __restrict__ part, int nb, int D,
                                                                      float* __restrict__ dw, float* __restrict__ db) {
-  __shared__ float red[LNF_W][64];
+  __shared__ float red[LNF_S][LNF_C];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int cl = lane % LNF_C, stripe = wid * (64 / LNF_C) + lane / LNF_C;
   const int which = blockIdx.y;
-  const int col = blockIdx.x * 64 + lane;
+  const int col = blockIdx.x * LNF_C + cl;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (col < D) {
     const float* src = part + (int64_t)which * D + col;
-    int k = wid;
-    for (; k + 3 * LNF_W < nb; k += 4 * LNF_W) {
+    int k = stripe;
+    for (; k + 3 * LNF_S < nb; k += 4 * LNF_S) {
       a0 += src[(int64_t)k * 2 * D];
-      a1 += src[(int64_t)(k + LNF_W) * 2 * D];
-      a2 += src[(int64_t)(k + 2 * LNF_W) * 2 * D];
-      a3 += src[(int64_t)(k + 3 * LNF_W) * 2 * D];
+      a1 += src[(int64_t)(k + LNF_S) * 2 * D];
+      a2 += src[(int64_t)(k + 2 * LNF_S) * 2 * D];
+      a3 += src[(int64_t)(k + 3 * LNF_S) * 2 * D];
     }
-    for (; k < nb; k += LNF_W) a0 += src[(int64_t)k * 2 * D];
+    for (; k < nb; k += LNF_S) a0 += src[(int64_t)k * 2 * D];
   }
-  red[wid][lane] = (a0 + a1) + (a2 + a3);
+  red[stripe][cl] = (a0 + a1) + (a2 + a3);
   __syncthreads();
-  if (wid == 0 && col < D) {
+  if (threadIdx.x < LNF_C && col < D) {
     float t = 0.f;
-#pragma unroll
-    for (int w = 0; w < LNF_W; ++w) t += red[w][lane];
+#pragma unroll 8
+    for (int w = 0; w < LNF_S; ++w) t += red[w][cl];
     if (which == 0) dw[col] += t;
     else if (db) db[col] += t;
   }
@@ -302,6 +304,7 @@ extern "C" int dpe_layernorm_bwd(const uint16_t* dy, const void* x, int x_bf16, 
   if (x_bf16) { DPE_LNB_J(true); } else { DPE_LNB_J(false); }
 #undef DPE_LNB_J
 #undef DPE_LNB
-  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 63) / 64, db ? 2 : 1), dim3(64 * LNF_W), 0, st, part, nbc, D, dw, db);
+  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + LNF_C - 1) / LNF_C, db ? 2 : 1), dim3(64 * LNF_W), 0, st, part, nbc, D,
+                     dw, db);
   return 0;
 }
