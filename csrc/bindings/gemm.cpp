@@ -289,6 +289,22 @@ int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_by
   return p2.main.cfg;
 }
 
+Plan plan_bnb(int64_t M, int64_t N, int64_t K, int ak, int bk, int* partial_cols) {
+  const Plan pl = plan(M, N, K, ak, bk, false, 2);
+  int bm = 0, wr = 0;
+  for (const TileCfg& c : kTiles)
+    if (c.cfg == pl.cfg) bm = c.bm;
+  wr = pl.cfg == dpe::HC_256x128 ? 4 : 2;  // wave rows of the configuration (hgemm.h HCfg)
+  *partial_cols = pl.cfg >= 0 ? (int)((M + bm - 1) / bm) * wr : 0;
+  return pl;
+}
+
+void run_bnb(dpe::HgemmArgs& a, const Plan& pl, int ak, int bk) {
+  TORCH_CHECK(pl.cfg >= 0 && pl.splits == 1 && a.col_stats && a.st_x && a.st_coef, "hgemm BN-backward epilogue: bad plan");
+  a.act = dpe::HACT_BNB;
+  launch_planned(a, pl, ak, bk, dpe::HE_BF16, nullptr);
+}
+
 }  // namespace dpe_gemm
 
 extern "C" int dpe_gemm_f32(const float* A, const float* B, float* C, int64_t sam, int64_t sak, int64_t sbk, int64_t sbn,

@@ -35,5 +35,9 @@ Plan2 plan2(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, i
 // slab kernel by an event -- a memory-bound pass co-resident with the next compute-bound GEMM on the
 // current stream.  The caller makes every consumer of C wait for fin_stream.
 int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_bytes, hipStream_t fin_stream = nullptr);
+// The BN-backward-partials GEMM (HE_BF16 + HACT_BNB): one launch, no K split.  plan_bnb returns the
+// plan and the number of partial columns it writes (tile rows x wave rows); run_bnb launches it.
+Plan plan_bnb(int64_t M, int64_t N, int64_t K, int ak, int bk, int* partial_cols);
+void run_bnb(dpe::HgemmArgs& a, const Plan& pl, int ak, int bk);
 
 }  // namespace dpe_gemm

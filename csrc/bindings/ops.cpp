@@ -620,6 +620,12 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
 // dx NHWC [N,H,W,C] = conv_transpose(dy, w); optional residual added into dx.
 // With bn_x/bn_coef (dx is dL/d relu(BN(bn_x))), the epilogue also emits the
 // BatchNorm-backward partials [2][C][tiles] (sum dz, sum dz*(x-mean)).
+// DPE_HGEMM_DGRAD=0: 1x1 data grads with K >= 1024 stay on the implicit-GEMM kernel (A/B reference)
+bool hgemm_dgrad_on() {
+  static const bool on = [] { const char* e = getenv("DPE_HGEMM_DGRAD"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 // DPE_DGRAD_FWD=0: stride-1 data grads on the transposed-filter loaders (A/B reference)
 bool dgrad_as_fwd() {
   static const bool on = [] { const char* e = getenv("DPE_DGRAD_FWD"); return !(e && e[0] == '0'); }();
@@ -707,6 +713,25 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
     }
     CHECK_RC(dpe_pw_launch(&pa, dpe::PW_DGRAD, cur_stream()), "pw_stream dgrad");
     return {dx, part};
+  }
+  // 1x1 data grads at depth >= 1024 (layers 3-4: conv3's) with the plain BN-backward epilogue: the
+  // persistent GEMM (NN layout, hgemm.hip HACT_BNB) -- its GEMM alone 73 vs 112-118 us for layer 3's conv3
+  // data grad (profiles/pw_vs_hgemm_r3.jsonl); ResNet-50 37.73-37.76 vs 37.81-37.88 ms/step.  At K = 512
+  // (layer 2) it measured +0.3 ms/step, so that depth stays on the implicit GEMM.
+  if (is_pointwise(g) && !a.residual && !a.res_mask && !a.st_mask && !acc_into && !res_stride2 && want_bn &&
+      hgemm_dgrad_on() && a.K >= 1024 && a.K % 64 == 0 && g.C % 8 == 0) {
+    int pcols = 0;
+    const auto pl = dpe_gemm::plan_bnb(a.M, g.C, a.K, 1, 0, &pcols);
+    if (pl.cfg >= 0 && pcols > 0) {
+      part = at::empty({2, g.C, pcols}, dy.options().dtype(at::kFloat));
+      auto h = hargs();
+      h.A = bp(dy); h.B = bp(w); h.C = dx.data_ptr();
+      h.M = a.M; h.N = g.C; h.K = a.K;
+      h.lda = g.K; h.ldb = g.C; h.ldc = g.C;
+      h.col_stats = fp(part); h.st_x = a.st_x; h.st_coef = a.st_coef; h.stats_ld = pcols;
+      dpe_gemm::run_bnb(h, pl, 1, 0);
+      return {dx, part};
+    }
   }
   auto tiles_of = [&](int64_t M, int64_t K) { const Cfg c = pick_cfg(M, g.C, K, false); return (M + c.bm - 1) / c.bm; };
   if (!is_pointwise(g) && g.sh == 1 && g.sw == 1 && g.dh == 1 && g.dw == 1 && dgrad_as_fwd()) {

@@ -554,7 +554,9 @@ def _bn_relu(h, coef):
 
 
 @pytest.mark.parametrize("N,H,W,Ci,Co,k,s,p", [(2, 14, 14, 64, 128, 3, 1, 1), (2, 14, 14, 64, 128, 3, 2, 1),
-                                               (4, 7, 7, 256, 64, 1, 1, 0), (2, 28, 28, 128, 128, 3, 2, 1)])
+                                               (4, 7, 7, 256, 64, 1, 1, 0), (2, 28, 28, 128, 128, 3, 2, 1),
+                                               # 1x1 at depth >= 1024: the persistent GEMM's BN-backward epilogue
+                                               (2, 7, 7, 256, 1024, 1, 1, 0), (3, 14, 14, 512, 2048, 1, 1, 0)])
 def test_dgrad_bn_backward_partials(C, N, H, W, Ci, Co, k, s, p):
     """dgrad epilogue partials + bn_bwd_partials == the standalone BN backward (mask from y)."""
     torch.manual_seed(13)
@@ -565,7 +567,11 @@ def test_dgrad_bn_backward_partials(C, N, H, W, Ci, Co, k, s, p):
     dy = bf(torch.randn(N, OH, OH, Co, device=dev))
     da_ref = C.conv_dgrad(dy, w, [N, H, W, Ci], [s, s], [p, p], [1, 1], None)
     da, part = C.conv_dgrad_bn(dy, w, [N, H, W, Ci], [s, s], [p, p], [1, 1], None, h, coef)
-    assert torch.equal(da, da_ref)
+    if k == 1 and Co >= 1024:  # different kernels (persistent GEMM vs implicit GEMM): same math, rounding may differ
+        ref32 = (dy.float().reshape(-1, Co) @ w.float().reshape(Co, Ci)).reshape(da.shape)
+        assert rel_err(da, ref32) < 1e-2 and rel_err(da, da_ref) < 1e-2
+    else:
+        assert torch.equal(da, da_ref)
     df = da.float().reshape(-1, Ci)
     hf = h.float().reshape(-1, Ci)
     dz = torch.where(hf * coef[0] + coef[1] > 0, df, torch.zeros_like(df))
