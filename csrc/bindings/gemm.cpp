@@ -300,8 +300,9 @@ Plan plan_bnb(int64_t M, int64_t N, int64_t K, int ak, int bk, int* partial_cols
 }
 
 void run_bnb(dpe::HgemmArgs& a, const Plan& pl, int ak, int bk) {
-  TORCH_CHECK(pl.cfg >= 0 && pl.splits == 1 && a.col_stats && a.st_x && a.st_coef, "hgemm BN-backward epilogue: bad plan");
-  a.act = dpe::HACT_BNB;
+  if (a.act != dpe::HACT_BNF) a.act = dpe::HACT_BNB;
+  TORCH_CHECK(pl.cfg >= 0 && pl.splits == 1 && a.col_stats && (a.act == dpe::HACT_BNF || (a.st_x && a.st_coef)),
+              "hgemm BN-statistics epilogue: bad plan / arguments");
   launch_planned(a, pl, ak, bk, dpe::HE_BF16, nullptr);
 }
 

@@ -38,6 +38,6 @@ int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_by
 // The BN-backward-partials GEMM (HE_BF16 + HACT_BNB): one launch, no K split.  plan_bnb returns the
 // plan and the number of partial columns it writes (tile rows x wave rows); run_bnb launches it.
 Plan plan_bnb(int64_t M, int64_t N, int64_t K, int ak, int bk, int* partial_cols);
-void run_bnb(dpe::HgemmArgs& a, const Plan& pl, int ak, int bk);
+void run_bnb(dpe::HgemmArgs& a, const Plan& pl, int ak, int bk);  // a.act: HACT_BNB (default) or HACT_BNF
 
 }  // namespace dpe_gemm

@@ -542,6 +542,13 @@ bool wgrad_hgemm_on() {
 }
 void set_wgrad_hgemm(bool on) { g_wgrad_hgemm = on ? 1 : 0; }
 
+// DPE_HGEMM_DGRAD=0: 1x1 convs (data grads, and forwards with BN statistics) with K >= 1024 stay on the
+// implicit-GEMM kernel (A/B reference)
+bool hgemm_dgrad_on() {
+  static const bool on = [] { const char* e = getenv("DPE_HGEMM_DGRAD"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 bool is_pointwise(const dpe::ConvGeom& g) {
   return g.R == 1 && g.S == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0;
 }
@@ -606,6 +613,25 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
     CHECK_RC(dpe_pw_launch(&pa, dpe::PW_FWD, cur_stream()), "pw_stream fwd");
     return {y, stats};
   }
+  // 1x1 stride-1 forward at depth >= 1024 (layers 3-4 conv1) with BN statistics: the persistent GEMM's
+  // BN-forward-partials epilogue (hgemm.hip HACT_BNF; its GEMM alone 60-71 vs 79-89 us,
+  // profiles/pw_vs_hgemm_r3.jsonl)
+  if (want_stats && is_pointwise(g) && !a.bias && !icoef && hgemm_dgrad_on() && a.K >= 1024 && a.K % 64 == 0 &&
+      a.N % 8 == 0) {
+    int pcols = 0;
+    const auto pl = dpe_gemm::plan_bnb(a.M, a.N, a.K, 1, 1, &pcols);
+    if (pl.cfg >= 0 && pcols > 0) {
+      stats = at::empty({2, g.K, pcols}, x.options().dtype(at::kFloat));
+      auto h = hargs();
+      h.A = bp(x); h.B = bp(w); h.C = y.data_ptr();
+      h.M = a.M; h.N = a.N; h.K = a.K;
+      h.lda = a.K; h.ldb = a.K; h.ldc = a.N;
+      h.act = dpe::HACT_BNF;
+      h.col_stats = fp(stats); h.stats_ld = pcols;
+      dpe_gemm::run_bnb(h, pl, 1, 1);
+      return {y, stats};
+    }
+  }
   if (want_stats) {
     // [2][K][tilesM] partial (sum, sumsq) per output channel and M-tile, reduced by bn_fwd_train
     const Cfg c = pick_cfg(a.M, a.N, a.K, false);
@@ -620,11 +646,6 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
 // dx NHWC [N,H,W,C] = conv_transpose(dy, w); optional residual added into dx.
 // With bn_x/bn_coef (dx is dL/d relu(BN(bn_x))), the epilogue also emits the
 // BatchNorm-backward partials [2][C][tiles] (sum dz, sum dz*(x-mean)).
-// DPE_HGEMM_DGRAD=0: 1x1 data grads with K >= 1024 stay on the implicit-GEMM kernel (A/B reference)
-bool hgemm_dgrad_on() {
-  static const bool on = [] { const char* e = getenv("DPE_HGEMM_DGRAD"); return !(e && e[0] == '0'); }();
-  return on;
-}
 
 // DPE_DGRAD_FWD=0: stride-1 data grads on the transposed-filter loaders (A/B reference)
 bool dgrad_as_fwd() {

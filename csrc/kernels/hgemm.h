@@ -18,6 +18,8 @@ constexpr int HACT_GELU_BWD = 3;
 // output y = relu(BN(st_x))): per column (sum dz, sum dz*(st_x - mean)), dz = v * [st_x*scale+shift > 0],
 // written to col_stats[2][N][stats_ld] at column stats_off + (m0 / BM) * WR + wave row (no atomics)
 constexpr int HACT_BNB = 4;
+// HE_BF16 + the BatchNorm-forward partials of the stored values (sum v, sum v^2), same layout as HACT_BNB
+constexpr int HACT_BNF = 5;
 
 constexpr int HGEMM_SCHED_BYTES = 17 * 1024;  // 17 counters, one 1 KB line each (hgemm.hip)
 
@@ -44,7 +46,7 @@ struct HgemmArgs {
   float* ws_bias;           // dbias with splits > 1: [splits][M] partial row sums (summed by hgemm_finalize)
   unsigned* sched;          // dynamic unit claims (HGEMM_SCHED_BYTES zeroed, self-resetting; one per stream),
                             // or nullptr: static round-robin over the persistent grid
-  // HACT_BNB (no K split): BN-backward partials
+  // HACT_BNB / HACT_BNF (no K split): BN-backward / BN-forward partials
   float* col_stats;         // [2][N][stats_ld]
   const uint16_t* st_x;     // bf16 [M][ldc] pre-BN input of the BN whose output this GEMM's result is the gradient of
   const float* st_coef;     // [4][N]: scale, shift, mean, invstd

@@ -578,7 +578,7 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
         }
         if constexpr (ACT == HACT_GELU_BWD) __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (ACT == HACT_BNB) {
+      if constexpr (ACT == HACT_BNB || ACT == HACT_BNF) {
         // BN-backward partials of the stored (rounded) values over this wave's rows of the tile: per
         // column j-fragment, sum over the row fragments in registers, then over the 16 lanes (lm) that
         // hold the same 4 columns; lane lm == 0 writes the wave row's partial column
@@ -587,23 +587,35 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
           const int c = cbase + (j / FNH) * CH + (j % FNH) * 16;
           const bool cv = c < p.N;
           const int cc = cv ? c : 0;
-          const f32x4 sc = *(const f32x4*)(p.st_coef + cc), sh = *(const f32x4*)(p.st_coef + p.N + cc);
-          const f32x4 mu = *(const f32x4*)(p.st_coef + 2 * p.N + cc);
+          f32x4 sc{}, sh{}, mu{};
+          if constexpr (ACT == HACT_BNB) {
+            sc = *(const f32x4*)(p.st_coef + cc);
+            sh = *(const f32x4*)(p.st_coef + p.N + cc);
+            mu = *(const f32x4*)(p.st_coef + 2 * p.N + cc);
+          }
           f32x4 s1 = f32x4{0.f, 0.f, 0.f, 0.f}, s2 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int i = 0; i < 2 * FMH; ++i) {
             const int r = rbase + (i / FMH) * RH + (i % FMH) * 16;
             if (r < p.M && cv) {
-              const u32x2 xr = *(const u32x2*)(p.st_x + (int64_t)r * p.ldc + c);
-              const float x4[4] = {__uint_as_float(xr[0] << 16), __uint_as_float(xr[0] & 0xffff0000u),
-                                   __uint_as_float(xr[1] << 16), __uint_as_float(xr[1] & 0xffff0000u)};
               const float v4[4] = {__uint_as_float(pk[i][j][0] << 16), __uint_as_float(pk[i][j][0] & 0xffff0000u),
                                    __uint_as_float(pk[i][j][1] << 16), __uint_as_float(pk[i][j][1] & 0xffff0000u)};
+              if constexpr (ACT == HACT_BNB) {
+                const u32x2 xr = *(const u32x2*)(p.st_x + (int64_t)r * p.ldc + c);
+                const float x4[4] = {__uint_as_float(xr[0] << 16), __uint_as_float(xr[0] & 0xffff0000u),
+                                     __uint_as_float(xr[1] << 16), __uint_as_float(xr[1] & 0xffff0000u)};
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float dz = fmaf(x4[e], sc[e], sh[e]) > 0.f ? v4[e] : 0.f;
-                s1[e] += dz;
-                s2[e] = fmaf(dz, x4[e] - mu[e], s2[e]);
+                for (int e = 0; e < 4; ++e) {
+                  const float dz = fmaf(x4[e], sc[e], sh[e]) > 0.f ? v4[e] : 0.f;
+                  s1[e] += dz;
+                  s2[e] = fmaf(dz, x4[e] - mu[e], s2[e]);
+                }
+              } else {  // forward statistics of the stored values
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  s1[e] += v4[e];
+                  s2[e] = fmaf(v4[e], v4[e], s2[e]);
+                }
               }
             }
           }
@@ -811,6 +823,7 @@ int launch_epi(const HgemmArgs& p, int epi, int grid, hipStream_t st) {
     else if (p.act == HACT_GELU_BWD) HL(HE_BF16, HACT_GELU_BWD);
     else if (p.act == ACT_RELU) HL(HE_BF16, ACT_RELU);
     else if (p.act == HACT_BNB && AK && !BK && p.splits == 1 && p.col_stats && p.st_x && p.st_coef) HL(HE_BF16, HACT_BNB);
+    else if (p.act == HACT_BNF && AK && BK && p.splits == 1 && p.col_stats && !p.bias) HL(HE_BF16, HACT_BNF);
     else return -3;
   } else if (p.act != ACT_NONE) {
     return -3;

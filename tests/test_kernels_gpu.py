@@ -159,6 +159,9 @@ CONV_CASES = [
     (4, 30, 30, 64, 512, 1, 1, 0),
     # 1x1 data grad with K = 2048, M tail (588 rows)
     (3, 14, 14, 512, 2048, 1, 1, 0),
+    # 1x1 forwards at depth >= 1024 (persistent GEMM with the BN-forward statistics epilogue), M tails
+    (2, 7, 7, 1024, 256, 1, 1, 0),
+    (3, 9, 9, 2048, 512, 1, 1, 0),
     # C = 16 (s2d stem form): two filter taps per 32-wide K-step on the LDS-DMA kernel
     (2, 12, 12, 16, 64, 4, 1, 2),
     (2, 9, 9, 16, 48, 2, 2, 0),
