@@ -283,6 +283,190 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
   }
 }
 
+// Forward, VALU-lean form of attn_fwd_kernel.  The forward is VALU-throughput-bound per SIMD (three
+// waves share one VALU; ~166 VALU vs 32 MFMA per 64-key tile and wave), so:
+//  * the softmax row sum l comes from the MFMA unit: a constant all-ones A operand against the same
+//    bf16 P fragments (4 extra MFMAs per tile) replaces 32 fp32 adds and the final cross-lane sum --
+//    l is then the sum of exactly the rounded P that O accumulated;
+//  * K/V go global -> LDS by LDS-DMA (no staging registers or ds_writes; the 8 accumulator registers
+//    of l fit in 3 waves per SIMD).  Each lane fetches the chunk that the swizzled image places at its
+//    slot (the XOR swizzles are involutions).
+// (A software-pipelined variant -- next tile's S MFMAs issued under this tile's softmax, three LDS
+// buffers -- measured 26.0 vs 26.2 us: the MFMA unit is not what the softmax waits on.)
+typedef __attribute__((address_space(3))) void alds_void_t;
+// LDS-DMA of one 16-B chunk per lane to wave_dst + 16 * lane, issued through inline asm so the
+// compiler puts no vmcnt(0) drain in front of the LDS reads it cannot prove disjoint (as igemm.hip's
+// dma16); the kernel orders it with its own vmcnt(0) before the step's barrier.  M0 is used by
+// nothing else here.
+DPE_DEVICE void attn_dma16(__amdgpu_buffer_rsrc_t r, char* wave_dst, uint32_t voff, uint32_t soff) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(alds_void_t*)wave_dst);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               ::"s"(m0), "v"(voff), "s"(r), "s"(soff) : "memory");
+}
+DPE_DEVICE void attn_vm_drain() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8));  // vmcnt(0) only
+  asm volatile("" ::: "memory");
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void attn_fwd_dma_kernel(
+    const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out, float* __restrict__ lse2, int B, int T, int H,
+    float sl2) {
+  constexpr int KB = 2 * AKV * 64, STG = KB + AKV * 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int nq = (T + FQ - 1) / FQ, BH = B * H;
+  const int qt = nq - 1 - (int)(blockIdx.x / BH);
+  const int bh = blockIdx.x % BH, b = bh / H, h = bh % H;
+  const int64_t RS = 3LL * H * AD;
+  const uint16_t* qb = qkv + (int64_t)b * T * RS + (int64_t)h * AD;
+  const uint16_t* kb = qb + H * AD;
+  const int q0w = qt * FQ + 32 * w;
+  const bool live = q0w < T;
+  const int ktw = live ? (q0w + 31) / AKV : -1;
+  const int nkt = min((qt * FQ + FQ - 1) / AKV, T / AKV - 1) + 1;
+
+  bf16x8 qf[2][2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      qf[r][kk] = live ? __builtin_bit_cast(bf16x8, *(const u32x4*)(qb + (int64_t)(q0w + 16 * r + li) * RS + 32 * kk + 8 * g))
+                       : bf16x8{};
+
+  // the sequence's qkv rows from K of head h on: one buffer resource, tile advance in soffset
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(kb), (short)0, (int)(T * RS * 2), 0x00020000);
+  uint32_t voff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int o = (w + 4 * i) * 1024 + lane * 16;  // this lane's byte slot in the 16 KiB tile image
+    int key, dc, vo;
+    if (i < 2) {  // K halves: kimg(key, c) = key * 64 + ((c ^ sw(key)) << 4), half dc >> 2
+      const int dh = o >> 12, oo = o & 4095;
+      key = oo >> 6;
+      dc = 4 * dh + (((oo >> 4) & 3) ^ ((0x78 >> (((key >> 2) & 3) << 1)) & 3));
+      vo = 0;
+    } else {      // V: pimg(key, c) = key * 128 + ((c ^ h(key)) << 4)
+      const int oo = o - KB;
+      key = oo >> 7;
+      dc = ((oo >> 4) & 7) ^ (((key >> 1) & 3) << 1);
+      vo = H * AD;
+    }
+    voff[i] = (uint32_t)(((int64_t)key * RS + vo + dc * 8) * 2);
+  }
+  auto dma_tile = [&](int kt, char* s) {
+    const uint32_t so = (uint32_t)((int64_t)kt * AKV * RS * 2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) attn_dma16(rs, s + (w + 4 * i) * 1024, voff[i], so);
+  };
+
+  f32x4 acc[2][4], accl[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    accl[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc[r][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  float m[2] = {-INFINITY, -INFINITY};
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
+  const int kd = (q0w + 1) / AKV;
+
+  auto compute = [&](int kt, const char* s, auto maskc) {
+    constexpr bool MASK = decltype(maskc)::value;
+    f32x4 sc[2][4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const bf16x8 k0 = kfrag64(s, 16 * nt), k1 = kfrag64(s + AKV * 64, 16 * nt);
+#pragma unroll
+      for (int r = 0; r < 2; ++r) sc[r][nt] = MFMA(k1, qf[r][1], MFMA(k0, qf[r][0], zero));
+    }
+    float mc[2];
+    bool need[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      if constexpr (MASK) {
+        const int lim = q0w + 16 * r + li - kt * AKV - 4 * g;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (16 * nt + e > lim) sc[r][nt][e] = -INFINITY;
+      }
+      float mx = sc[r][0][0];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int e = (nt == 0); e < 4; ++e) mx = fmaxf(mx, sc[r][nt][e]);
+      mc[r] = rowmax4(mx) * sl2;
+      need[r] = mc[r] > m[r] + RESCALE_TH;
+    }
+    if (__builtin_amdgcn_ballot_w64(need[0] || need[1])) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const float alpha = need[r] ? __builtin_amdgcn_exp2f(m[r] - mc[r]) : 1.f;
+        m[r] = need[r] ? mc[r] : m[r];
+        accl[r] *= alpha;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) acc[r][d] *= alpha;
+      }
+    }
+    bf16x8 pk[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const float nm = -m[r];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sc[r][nt][e] = __builtin_amdgcn_exp2f(fmaf(sc[r][nt][e], sl2, nm));
+      pk[r][0] = pack_frag(sc[r][0], sc[r][1]);
+      pk[r][1] = pack_frag(sc[r][2], sc[r][3]);
+      accl[r] = MFMA(ones, pk[r][1], MFMA(ones, pk[r][0], accl[r]));
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const bf16x8 v0 = trfrag(s + KB, 0, 16 * d), v1 = trfrag(s + KB, 32, 16 * d);
+#pragma unroll
+      for (int r = 0; r < 2; ++r) acc[r][d] = MFMA(v1, pk[r][1], MFMA(v0, pk[r][0], acc[r][d]));
+    }
+  };
+
+  dma_tile(0, smem);
+  attn_vm_drain();
+  __syncthreads();
+  // the tile loop unrolled by two: each step's LDS buffer is a compile-time constant
+  auto step = [&](int kt, auto bufc) {
+    constexpr int cur = decltype(bufc)::value;
+    const bool more = kt + 1 < nkt;
+    if (more) dma_tile(kt + 1, smem + (cur ^ 1) * STG);  // read last in step kt - 1, before its barrier
+    if (kt < kd) compute(kt, smem + cur * STG, std::false_type{});
+    else if (kt <= ktw) compute(kt, smem + cur * STG, std::true_type{});
+    if (more) attn_vm_drain();
+    __syncthreads();
+  };
+  for (int kt = 0; kt < nkt; kt += 2) {
+    step(kt, std::integral_constant<int, 0>{});
+    if (kt + 1 < nkt) step(kt + 1, std::integral_constant<int, 1>{});
+  }
+  if (!live) return;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int myq = q0w + 16 * r + li;
+    const float l = accl[r][0];  // every row of the all-ones product is the sum over keys for query li
+    const float inv = 1.f / l;
+    uint16_t* o = out + ((int64_t)(b * T + myq) * H + h) * AD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      u32x2 pk2;
+      pk2[0] = pack_bf2(acc[r][d][0] * inv, acc[r][d][1] * inv);
+      pk2[1] = pack_bf2(acc[r][d][2] * inv, acc[r][d][3] * inv);
+      *(u32x2*)(o + 16 * d + 4 * g) = pk2;
+    }
+    if (g == 0) lse2[(int64_t)bh * T + myq] = m[r] + __log2f(l);
+  }
+}
+
 // ======================================================================= bwd
 // dK / dV: one workgroup = 128 keys of one (b, h), 4 waves x 32 keys, looping over the
 // 64-query tiles at or after the key tile.  The query tile's Q / dO images are double-
@@ -601,7 +785,16 @@ extern "C" int dpe_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int 
                             hipStream_t st) {
   if (D != AD || T % AKV != 0 || !causal) return -1;
   const float sl2 = scale * 1.4426950408889634f;
+#ifdef DPE_ATTN_FWD_STAGED
   hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * H * ((T + FQ - 1) / FQ)), dim3(256), 0, st, qkv, out, lse, B, T, H, sl2);
+#else
+  // one sequence's qkv rows must fit the DMA kernel's 32-bit buffer range
+  if ((int64_t)T * 3 * H * AD * 2 < (1LL << 31))
+    hipLaunchKernelGGL(attn_fwd_dma_kernel, dim3(B * H * ((T + FQ - 1) / FQ)), dim3(256), 0, st, qkv, out, lse, B, T, H,
+                       sl2);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * H * ((T + FQ - 1) / FQ)), dim3(256), 0, st, qkv, out, lse, B, T, H, sl2);
+#endif
   return 0;
 }
 
