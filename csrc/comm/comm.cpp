@@ -182,6 +182,7 @@ void Communicator::abort() {
     ncclCommAbort(comm_);
     aborted_ = true;
   }
+  set_comm_active(false);  // no collective of this communicator is in flight any more
 }
 
 // ------------------------------------------------ CU budget while collectives overlap compute
@@ -277,6 +278,7 @@ void Reducer::init_tracking(int64_t nparams) {
 
 Reducer::~Reducer() {
   if (host_launch_) return;  // no HIP objects in host-transport mode
+  set_comm_active(false);  // a backward that raised after its first launch never reached finalize()
   if (comm_) {
     // the last step's all-reduces may still be running on the comm stream (finalize only makes the
     // compute stream wait): drain them before their buffers are deregistered / released and a
@@ -292,6 +294,9 @@ Reducer::~Reducer() {
 }
 
 void Reducer::prepare() {
+  // a new step: clear a flag left set by a backward that raised after its first bucket launch (no
+  // finalize ran), so compute kernels until this step's first launch plan with every slot
+  if (!host_launch_) set_comm_active(false);
   pending_ = expected_;
   std::fill(ready_.begin(), ready_.end(), 0);
   std::fill(seen_.begin(), seen_.end(), 0);

@@ -199,7 +199,13 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
   // overlaps MFMA work.  No unit depends on which block computes it (no cross-unit reduction): outputs are
   // bitwise independent of the schedule.
   const int G0 = gridDim.x;
+#if HG_SCHED == 1
   const bool dsched = p.sched != nullptr && nunits > G0;
+#else
+  // only the HG_SCHED == 1 main loop issues the next-unit claim: any other build runs the static
+  // schedule (a dynamic one would re-resolve the same unit forever)
+  const bool dsched = false;
+#endif
   const int S = dsched ? (G0 - G0 / 8) & ~7 : G0;  // blocks [0, S) start on a static unit
   const int dyn = dsched ? nunits - S : 0;         // units [S, nunits) are claimed
   const int xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;  // hwreg(HW_REG_XCC_ID, 0, 4)

@@ -252,10 +252,12 @@ class DistributedDataParallel(nn.Module):
         self._build_buckets(None)
         self._queued = False
         self._hooks = []
-        for p in self._params:
+        for i, p in enumerate(self._params):
             p._dpe_direct = True
             p._dpe_ready = self._on_ready
             self._hooks.append(p.register_post_accumulate_grad_hook(self._on_ready))
+            if getattr(p, "_dpe_overwrite_ok", False):
+                self._hooks.append(p.register_hook(self._fresh_guard(i)))
 
     # --------------------------------------------------------------- setup
     @torch.no_grad()
@@ -386,6 +388,20 @@ class DistributedDataParallel(nn.Module):
                 torch._foreach_zero_([self._views[i] for i, o in enumerate(ow) if not o])
             else:
                 torch._foreach_zero_(list(self.buckets))
+
+    def _fresh_guard(self, i: int):
+        """Tensor hook of a ``_dpe_overwrite_ok`` parameter: it runs when autograd is about to
+        accumulate a gradient for it (a writer other than our kernels, which write the bucket view
+        directly and hand autograd no tensor).  If the view still holds last step's values (fresh, no
+        kernel has overwritten it yet), zero it first so AccumulateGrad adds into zeros, not stale data."""
+        def hook(grad):
+            p = self._params[i]
+            if getattr(p, "_dpe_fresh", False):
+                p._dpe_fresh = False
+                self._views[i].zero_()
+            return grad
+
+        return hook
 
     # ---------------------------------------------------------- per-step
     def _on_ready(self, p):

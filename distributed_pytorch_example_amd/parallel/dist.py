@@ -57,8 +57,10 @@ def init_process_group(backend: str = "auto", timeout_s: float = 1800.0,
     backend = resolve_backend(backend)
     if comm_max_channels is None and os.environ.get("DPE_RCCL_MAX_CHANNELS"):
         comm_max_channels = int(os.environ["DPE_RCCL_MAX_CHANNELS"])
-    if comm_max_channels is None and backend == "rccl" and env.world_size > 1 and "NCCL_MAX_NCHANNELS" not in os.environ:
-        comm_max_channels = DEFAULT_MAX_CHANNELS
+    _state["max_channels"] = None
+    if comm_max_channels is None and os.environ.get("NCCL_MAX_NCHANNELS", "").strip().isdigit():
+        # a cap the user set for RCCL directly: the CU budget follows it
+        _state["max_channels"] = max(1, int(os.environ["NCCL_MAX_NCHANNELS"]))
     if comm_max_channels:
         n = max(1, int(comm_max_channels))
         os.environ["NCCL_MAX_NCHANNELS"] = str(n)
@@ -80,13 +82,14 @@ def init_process_group(backend: str = "auto", timeout_s: float = 1800.0,
     return rank, world, local_rank
 
 
-# RCCL channel cap at world > 1 (each channel = one workgroup resident on a CU while a bucket
-# all-reduce overlaps backward).  Bandwidth model behind 16: ResNet-50's 102 MB / GPT-2's 498 MB fp32
-# gradients need 2*7/8 of that per GPU over the ~25 / ~9 ms backward, i.e. < 100 GB/s of bus bandwidth
-# to stay hidden -- far below what 16 xGMI channels move -- while 16 blocks are 1.6-6 % of the
-# persistent kernels' slots (the compute side plans around them: cu_reserve_for).  A model, not a
-# measurement: no 8-GPU node was available to sweep it (bench.py --comm-max-channels does).
-DEFAULT_MAX_CHANNELS = 16
+# RCCL channel cap (each channel = one workgroup resident on a CU while a bucket all-reduce overlaps
+# backward).  OPT-IN: without --comm-max-channels / DPE_RCCL_MAX_CHANNELS / NCCL_MAX_NCHANNELS, RCCL
+# keeps its own topology-tuned channel count.  Suggested value 16 (bandwidth model: ResNet-50's 102 MB
+# / GPT-2's 498 MB fp32 gradients need 2*7/8 of that per GPU over the ~25 / ~9 ms backward, i.e.
+# < 100 GB/s of bus bandwidth to stay hidden, while 16 blocks are 1.6-6 % of the persistent kernels'
+# slots) -- a model, not a measurement, so it is not the default until an 8-GPU sweep
+# (bench.py --comm-max-channels) backs it.
+SUGGESTED_MAX_CHANNELS = 16
 
 
 def cu_reserve_for(world: int, channels: Optional[int]) -> int:
@@ -97,6 +100,7 @@ def cu_reserve_for(world: int, channels: Optional[int]) -> int:
         return max(0, int(os.environ["DPE_CU_RESERVE"]))
     if world <= 1:
         return 0
+    # RCCL's own channel count is not queryable: assume 32 resident channel blocks when uncapped
     return int(channels) if channels else 32
 
 
@@ -231,11 +235,19 @@ class Watchdog:
         if torch.cuda.is_available() and torch.cuda.is_initialized():
             ev = torch.cuda.Event()
             ev.record()
-            with self._lock:
-                if len(self._pending) < 64:  # bounded: the oldest pending event is the one that matters
-                    self._pending.append((ev, now))
+            self._push(ev, now)
             return
         self._last = now
+
+    def _push(self, ev, now: float) -> None:
+        with self._lock:
+            # bounded: keep the oldest pending events (they gate progress) and always the newest beat --
+            # a full list replaces its last entry, so the most recent step keeps an event and the
+            # heartbeat advances as soon as the device reaches it
+            if len(self._pending) >= 64:
+                self._pending[-1] = (ev, now)
+            else:
+                self._pending.append((ev, now))
 
     def _device_progress(self) -> None:
         with self._lock:
@@ -316,6 +328,20 @@ def _try_abort(c) -> None:
         pass
 
 
+# The reference's collectives run on gloo, whose process group times out after 30 min
+# ($TORCH/distributed/constants.py:12).  On the rccl backend every tensor collective is RCCL, which has
+# no timeout of its own: the watchdog is that bound, on by default at world > 1.
+DEFAULT_COLLECTIVE_TIMEOUT_S = 1800.0
+
+
+def default_watchdog_timeout(requested: Optional[float], backend_name: Optional[str], world: int) -> float:
+    """Watchdog stall timeout in seconds (0 = off).  An explicit value wins (``0`` is the opt-out);
+    otherwise 1800 s on the rccl backend at world > 1, off elsewhere (gloo keeps its own timeout)."""
+    if requested is not None:
+        return max(0.0, float(requested))
+    return DEFAULT_COLLECTIVE_TIMEOUT_S if (backend_name == "rccl" and world > 1) else 0.0
+
+
 def start_watchdog(timeout_s: float = 600.0, interval_s: float = 2.0, on_fail=None) -> Watchdog:
     return Watchdog(timeout_s, interval_s, on_fail)
 
@@ -328,6 +354,7 @@ def destroy_process_group() -> None:
     if dist.is_initialized():
         dist.destroy_process_group()
     _state["backend"] = None
+    _state["max_channels"] = None
 
 
 def get_device(local_rank: int) -> torch.device:

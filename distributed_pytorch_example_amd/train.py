@@ -72,9 +72,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--gradient-compression", default="none", choices=["none", "bf16"],
                    help="all-reduce bf16 copies of the fp32 gradient buckets")
     p.add_argument("--ddp-debug", action="store_true", help="cross-rank bucket-layout check + per-bucket stream sync")
-    p.add_argument("--watchdog-timeout", type=float, default=0.0,
+    p.add_argument("--watchdog-timeout", type=float, default=None,
                    help="abort the job when no training step completes for this many seconds or RCCL reports an "
-                        "async error (0 = off)")
+                        "async error (0 = off; default: 1800 s -- the reference's gloo collective timeout -- on the "
+                        "rccl backend at world > 1, off otherwise)")
     p.add_argument("--watchdog-checkpoint-grace", type=float, default=600.0,
                    help="extra seconds the watchdog allows in the end-of-epoch barrier (rank 0 writes checkpoints)")
     return p
@@ -182,7 +183,8 @@ def main(argv=None):
                 debug=args.ddp_debug or None)
     if args.roctx:
         tracing.enable(True)
-    watchdog = pdist.start_watchdog(args.watchdog_timeout) if args.watchdog_timeout > 0 else None
+    wd_timeout = pdist.default_watchdog_timeout(args.watchdog_timeout, pdist.backend(), world_size)
+    watchdog = pdist.start_watchdog(wd_timeout) if wd_timeout > 0 else None
     logger.info(f"Model parameters: {sum(p.numel() for p in model.parameters()):,}")
 
     train_dataset, val_dataset, num_classes = _datasets(args, device)

@@ -1,8 +1,10 @@
-"""One rank of the 2-process native-reducer test (tests/test_ddp_rccl_world2_gpu.py).
+"""One rank of the N-process native-reducer tests (tests/test_ddp_rccl_world2_gpu.py; N = 2 or 4).
 
-Both ranks share GPU 0; each process gets its own NCCL_HOSTID so RCCL treats them
-as two hosts and connects them through its socket transport -- the C++ Reducer
-then issues real world-2 RCCL all-reduces (Reducer::launch with world() == 2).
+All ranks share GPU 0; each process gets its own NCCL_HOSTID so RCCL treats them
+as N hosts and connects them through its socket transport -- the C++ Reducer
+then issues real world-N RCCL all-reduces (Reducer::launch with world() == N).  At
+N = 4 the rank-0 bucket-order broadcast reaches three peers and RCCL runs a
+multi-peer ring, which world 2 (a degenerate ring) never exercises.
 """
 import copy
 import os
@@ -46,7 +48,7 @@ def main():
     m = resnet18_like(num_classes=10).to(dev)
     ref = copy.deepcopy(m)  # plain-autograd twin (copied before DDP attaches bucket views / hooks)
     ddp = DDP(m, bucket_cap_mb=1, first_bucket_mb=0.25)
-    assert ddp._native and ddp.reducer.world == 2, "native RCCL reducer expected at world 2"
+    assert ddp._native and ddp.reducer.world == world, f"native RCCL reducer expected at world {world}"
     ref.load_state_dict(m.state_dict())  # rank 0's weights after the init broadcast
     for p in m.parameters():  # init sync over RCCL
         q = p.detach().float().cpu()
@@ -64,7 +66,13 @@ def main():
         torch.cuda.synchronize()
         assert ddp.reducer.launch_order() == list(range(ddp.num_buckets()))
         checks.append(max(rel(p.grad, w) for p, w in zip(m.parameters(), want)))
+        if step == 1:
+            layout_after_rebuild = ddp.layout_fingerprint()
     assert ddp.bucket_rebuilds == 1
+    # the rebuilt layout (rank 0's observed order, broadcast) is identical on every rank
+    fps = [None] * world
+    dist.all_gather_object(fps, layout_after_rebuild)
+    assert len(set(fps)) == 1, fps
     assert max(checks) < 1e-4, checks
     # no_sync: two local micro-steps + one synced == rank average of the summed grads
     for p in m.parameters():
@@ -102,10 +110,10 @@ def main():
     # metric all-reduce + barrier over RCCL (reference C7 / C8)
     t = torch.tensor([float(rank + 1)], device=dev)
     pdist.all_reduce(t)
-    assert t.item() == 3.0
+    assert t.item() == world * (world + 1) / 2
     pdist.barrier()
     assert pdist.check_health() == ""
-    print(f"rank {rank} ok: world-2 RCCL reducer, max rel err {max(checks):.2e}, "
+    print(f"rank {rank} ok: world-{world} RCCL reducer, max rel err {max(checks):.2e}, "
           f"{ddp.reducer.registered_buffers}/{ddp.num_buckets()} bucket buffers ncclCommRegister'ed", flush=True)
     pdist.destroy_process_group()
 
@@ -127,7 +135,7 @@ def main_gpt2():
                 p.normal_(0, 0.05)
     ref = copy.deepcopy(m)
     ddp = DDP(m, bucket_cap_mb=0.25, first_bucket_mb=0.05)
-    assert ddp._native and ddp.reducer.world == 2
+    assert ddp._native and ddp.reducer.world == world
     ref.load_state_dict(m.state_dict())
     V, T = m.cfg.vocab_size, 64
 
@@ -175,7 +183,7 @@ def main_gpt2():
         g = r.grad.detach().float().cpu()
         dist.all_reduce(g)
         assert rel(p.grad, (g / world).to(dev)) < 1e-4
-    print(f"rank {rank} ok: world-2 RCCL reducer gpt2-tiny, max rel err {max(checks):.2e}, "
+    print(f"rank {rank} ok: world-{world} RCCL reducer gpt2-tiny, max rel err {max(checks):.2e}, "
           f"{ddp.num_buckets()} buckets", flush=True)
     pdist.destroy_process_group()
 

@@ -214,3 +214,39 @@ def test_gpt2_fresh_gradients_equal_zeroed(C):
                 assert ((x - y).norm() / x.norm()).item() < 1e-6, (s, n)
             else:
                 assert torch.equal(x, y), (s, n)
+
+
+def test_gpt2_fresh_gradients_with_foreign_writer(C):
+    """a stock-torch writer of an overwrite-tagged parameter (an auxiliary loss on the tied
+    embedding, through autograd's AccumulateGrad) must not add into last step's stale bucket values:
+    DDP's tensor hook zeroes a still-fresh view before the accumulation.  Gradients equal the run
+    with every bucket zeroed (to the embedding scatter-add's atomic-order noise)."""
+    from distributed_pytorch_example_amd.models import get_model
+    from distributed_pytorch_example_amd.parallel import DDP
+
+    torch.manual_seed(7)
+    base = get_model("gpt2", n_layer=1).to(dev)
+    idx = [torch.randint(0, 50257, (2, 128), device=dev) for _ in range(3)]
+    tgt = [torch.randint(0, 50257, (2, 128), device=dev) for _ in range(3)]
+
+    def run(fresh_ok):
+        m = copy.deepcopy(base)
+        for p in m.parameters():
+            if getattr(p, "_dpe_overwrite_ok", False):
+                p._dpe_overwrite_ok = fresh_ok
+        ddp = DDP(m, bucket_cap_mb=8)
+        out = []
+        for step in range(3):
+            for p in m.parameters():
+                p.grad = None
+            loss = ddp(idx[step], tgt[step]) + 1e-3 * (m.wte.float() ** 2).sum()  # foreign writer of wte
+            loss.backward()
+            torch.cuda.synchronize()
+            out.append([p.grad.clone() for p in m.parameters()])
+        return out
+
+    ref, got = run(False), run(True)
+    names = [n for n, _ in base.named_parameters()]
+    for s, (a, b) in enumerate(zip(ref, got)):
+        for n, x, y in zip(names, a, b):
+            assert ((x - y).norm() / (x.norm() + 1e-12)).item() < 1e-6, (s, n)

@@ -1,11 +1,13 @@
-"""The native C++ Reducer at world 2 over real RCCL collectives, on a 1-GPU box.
+"""The native C++ Reducer at world 2 and 4 over real RCCL collectives, on a 1-GPU box.
 
-Two processes share GPU 0.  Each gets its own NCCL_HOSTID, so RCCL sees two
-hosts (no duplicate-GPU refusal) and connects them with its socket transport
-over loopback: Reducer::launch runs with world() == 2, the buckets are really
-all-reduced (ncclAvg), the bucket rebuild, no_sync accumulation and the bf16
-compression path are checked against rank-averaged plain-backward gradients
-(tests/_rccl_world2_worker.py).  On an 8-GPU node the same code runs over xGMI.
+N processes share GPU 0.  Each gets its own NCCL_HOSTID, so RCCL sees N hosts
+(no duplicate-GPU refusal) and connects them with its socket transport over
+loopback: Reducer::launch runs with world() == N, the buckets are really
+all-reduced (ncclAvg), the bucket rebuild (rank 0's order broadcast to N-1 peers),
+no_sync accumulation and the bf16 compression path are checked against
+rank-averaged plain-backward gradients (tests/_rccl_world2_worker.py), and a rank
+killed mid-epoch must take every survivor down through its watchdog.  On an
+8-GPU node the same code runs over xGMI.
 """
 import os
 import socket
@@ -28,12 +30,12 @@ def _port():
     return p
 
 
-def _run_world2(args, extra_env=None, timeout=100):
+def _run_world(n, args, extra_env=None, timeout=100):
     port = _port()
     procs = []
-    for r in range(2):
+    for r in range(n):
         env = dict(os.environ)
-        env.update({"RANK": str(r), "WORLD_SIZE": "2", "LOCAL_RANK": "0", "LOCAL_WORLD_SIZE": "2",
+        env.update({"RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_RANK": "0", "LOCAL_WORLD_SIZE": str(n),
                     "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "PYTHONPATH": ROOT,
                     "NCCL_HOSTID": f"dpe-test-host-{r}", "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1",
                     "HSA_ENABLE_IPC_MODE_LEGACY": "0", "OMP_NUM_THREADS": "1",
@@ -50,6 +52,10 @@ def _run_world2(args, extra_env=None, timeout=100):
             if p.poll() is None:
                 p.kill()
     return [p.returncode for p in procs], outs
+
+
+def _run_world2(args, extra_env=None, timeout=100):
+    return _run_world(2, args, extra_env, timeout)
 
 
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
@@ -92,3 +98,42 @@ def test_rank_death_mid_allreduce_aborts_survivor(tmp_path):
     assert dt < 100, dt
     print(f"survivor exited rc={codes[0]} after {dt:.1f}s: "
           f"{[ln for ln in outs[0].splitlines() if 'watchdog:' in ln][0][-160:]}")
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_native_reducer_world4_rccl():
+    """world 4 -- RCCL's multi-peer ring, rank 0's bucket order broadcast to three
+    peers, one rebuild, no_sync, registration and the bf16 hook, against rank-averaged grads."""
+    codes, outs = _run_world(4, [os.path.join(ROOT, "tests", "_rccl_world2_worker.py")], timeout=170)
+    assert codes == [0] * 4, "\n".join(o[-2000:] for o in outs)
+    for o in outs:
+        print([ln for ln in o.splitlines() if "ok: world-4" in ln][0])
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_native_reducer_world4_rccl_gpt2():
+    codes, outs = _run_world(4, [os.path.join(ROOT, "tests", "_rccl_world2_worker.py"), "gpt2"], timeout=170)
+    assert codes == [0] * 4, "\n".join(o[-2000:] for o in outs)
+    for o in outs:
+        print([ln for ln in o.splitlines() if "ok: world-4" in ln][0])
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_rank_death_world4_aborts_every_survivor(tmp_path):
+    """Rank 2 SIGKILLs itself at batch 3 of epoch 0; ranks 0, 1 and 3 are blocked in bucket
+    all-reduces of a 4-rank ring that can never complete.  Each survivor's watchdog must abort its
+    communicator and exit non-zero within the timeout (several peers blocked at once)."""
+    import time
+
+    t0 = time.time()
+    codes, outs = _run_world(4, [os.path.join(ROOT, "train.py"), "--backend", "rccl", "--model", "resnet_tiny",
+                                 "--image-size", "32", "--batch-size", "8", "--num-samples", "2048", "--epochs", "2",
+                                 "--checkpoint-dir", str(tmp_path), "--watchdog-timeout", "15"],
+                             extra_env={"DPE_FAULT_INJECT": "2:0:3:kill"}, timeout=150)
+    dt = time.time() - t0
+    assert codes[2] == -9, outs[2][-2000:]
+    for r in (0, 1, 3):
+        assert codes[r] not in (0, None) and codes[r] != -9, (r, codes, outs[r][-2000:])
+        assert "watchdog:" in outs[r] and "aborting communicator" in outs[r], (r, outs[r][-2000:])
+    assert dt < 140, dt
+    print(f"survivors rc={[codes[r] for r in (0, 1, 3)]} after {dt:.1f}s")

@@ -108,7 +108,27 @@ def _check(name, ours, fp32, bf16, w_ours, w_bf16):
     # loss spike both bf16 runs leave the fp32 oracle by 3-4 % (GPT-2 step 12) while tracking each other
     bound = 2 * max(d_bf16) + 2e-3
     assert max(d_ours) <= bound, (name, max(d_ours), bound)
-    assert w_ours <= max(2 * w_bf16, 0.05), (name, w_ours, w_bf16)
+    # final-weight distance: within 25 % of torch-bf16's own (+ 0.01).  (Was max(2x, 0.05): vacuous
+    # for ResNet-50, where both bf16 runs sit at ~1.39 of the oracle's own update.)
+    assert w_ours <= 1.25 * w_bf16 + 0.01, (name, w_ours, w_bf16)
+
+
+def _grad_check(name, names, g_ours, g_fp32, g_bf16, floor=2e-3):
+    """Step-0 per-parameter gradient parity: ||g - g_fp32|| / ||g_fp32|| of every tensor must be at
+    most twice torch-bf16-autocast's error for that same tensor, plus ``floor``.  Prints the five
+    tensors closest to their bound."""
+    rows = []
+    for n, a, b, c in zip(names, g_ours, g_fp32, g_bf16):
+        den = b.norm().item() + 1e-30
+        e_o = (a - b).norm().item() / den
+        e_b = (c - b).norm().item() / den
+        rows.append((e_o / (2 * e_b + floor), n, e_o, e_b))
+    rows.sort(reverse=True)
+    print(f"\n{name}: step-0 gradients, {len(rows)} tensors; worst five (ours / torch-bf16 rel err, bound 2x+{floor:g}):")
+    for r, n, e_o, e_b in rows[:5]:
+        print(f"  {n:40s} {e_o:.3e} / {e_b:.3e}  ({100 * r:.0f} % of bound)")
+    bad = [(n, e_o, e_b) for r, n, e_o, e_b in rows if r > 1.0]
+    assert not bad, (name, bad[:8])
 
 
 def test_resnet50_full_training_parity():
@@ -152,6 +172,69 @@ def test_resnet50_full_training_parity():
     assert all(math.isfinite(v) for v in lo) and lo[-1] < lo[0]
     _check("ResNet-50 bs16 224^2 SGD", lo, lt, lb, _rel_dist(_resnet_flat(ours, True), wt, w0),
            _rel_dist(_resnet_flat(twin_bf, False), wt, w0))
+
+
+def _resnet_flat_grads(m, ours: bool):
+    out, names = [], []
+    mods = [("stem", m.stem)] + [(f"b{i}.{k}", cb) for i, b in enumerate(m.blocks)
+                                 for k, cb in zip(("c1", "c2", "c3", "down"), (b.c1, b.c2, b.c3, b.down)) if cb is not None]
+    for nm, cb in mods:
+        g = cb.conv.weight.grad.detach().float()
+        out += [g.permute(0, 3, 1, 2) if ours else g, cb.bn.weight.grad.detach().float(), cb.bn.bias.grad.detach().float()]
+        names += [nm + ".conv.weight", nm + ".bn.weight", nm + ".bn.bias"]
+    return out + [m.fc.weight.grad.detach().float(), m.fc.bias.grad.detach().float()], names + ["fc.weight", "fc.bias"]
+
+
+def test_resnet50_step0_gradient_parity():
+    """every one of ResNet-50's 161 parameter gradients at step 0 (batch 16,
+    224^2, the bench's image size), against the fp32 torch oracle, bounded per tensor by twice torch's
+    own bf16-autocast error on that tensor."""
+    _no_tf32()
+    torch.manual_seed(3)
+    ours = get_model("resnet50").to(DEV)
+    twin = _TResNet(ours).to(DEV)
+    twin_bf = copy.deepcopy(twin)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = torch.randn(16, 3, 224, 224, device=DEV, generator=g)
+    y = torch.randint(0, 1000, (16,), device=DEV, generator=g)
+    Fx.cross_entropy(ours(x), y, 1000).backward()
+    F.cross_entropy(twin(x), y).backward()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        loss = F.cross_entropy(twin_bf(x), y)
+    loss.backward()
+    go, names = _resnet_flat_grads(ours, True)
+    gt, _ = _resnet_flat_grads(twin, False)
+    gb, _ = _resnet_flat_grads(twin_bf, False)
+    assert len(go) == 161
+    _grad_check("ResNet-50 bs16 224^2", names, go, gt, gb)
+
+
+def test_gpt2_small_step0_gradient_parity_T1024():
+    """every GPT-2-small parameter gradient at step 0 at the bench's sequence
+    length T = 1024 (batch 1), against the fp32 torch oracle (SDPA, F.linear, F.layer_norm), bounded
+    per tensor by twice torch's bf16-autocast error on that tensor."""
+    _no_tf32()
+    torch.manual_seed(5)
+    ours = get_model("gpt2").to(DEV)
+    with torch.no_grad():  # non-zero biases / LN affine: every gradient path carries signal
+        for n, p in ours.named_parameters():
+            if p.dim() == 1:
+                p.add_(torch.randn_like(p) * 0.02)
+    cfg = ours.cfg
+    names = [n for n, _ in ours.named_parameters()]
+    P = _gpt2_twin_params(ours)
+    Pb = _gpt2_twin_params(ours)
+    g = torch.Generator(device=DEV).manual_seed(6)
+    T = 1024
+    x = torch.randint(0, cfg.vocab_size, (1, T), device=DEV, generator=g)
+    y = torch.randint(0, cfg.vocab_size, (1, T), device=DEV, generator=g)
+    ours(x, y).backward()
+    _gpt2_twin_loss(P, cfg, x, y).backward()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        loss = _gpt2_twin_loss(Pb, cfg, x, y)
+    loss.backward()
+    go = [p.grad.detach().float() for p in ours.parameters()]
+    _grad_check("GPT-2-small bs1 T1024", names, go, [P[n].grad for n in names], [Pb[n].grad for n in names])
 
 
 # ----------------------------------------------------------------------------- GPT-2 twin
