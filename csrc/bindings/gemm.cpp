@@ -423,9 +423,68 @@ Tensor hgemm_raw(const Tensor& A, const Tensor& B, Tensor C, int64_t M, int64_t 
   return C;
 }
 
+// Grouped TN weight gradients (hgemm.hip HE_GROUP): dw_g (+)= dy_g^T x_g and db_g += colsum(dy_g) for up to
+// HGEMM_MAX_GROUP problems sharing the token count K, in ONE persistent launch of whole-K 256x256 tiles.
+// A transformer layer's weight-gradient GEMMs have few output tiles (GPT-2-small: 27 + 9 + 36 + 36 per
+// layer at d = 768) over K = B*T = 8192 tokens: alone, each needs an 8-9-way K split to fill the chip,
+// whose fp32 partial slabs (as many bytes as the GEMM's whole operand traffic) and finalize launch
+// dominate.  Two layers' problems together are 216 tiles, one round on 256 CUs with no split.
+void linear_wgrad_group(const std::vector<Tensor>& dys, const std::vector<Tensor>& xs, const std::vector<Tensor>& dws,
+                        const std::vector<Tensor>& dbs, const std::vector<bool>& overwrite) {
+  const size_t n = dys.size();
+  TORCH_CHECK(n >= 1 && n <= (size_t)dpe::HGEMM_MAX_GROUP && xs.size() == n && dws.size() == n && dbs.size() == n &&
+                  overwrite.size() == n, "linear_wgrad_group: 1..", dpe::HGEMM_MAX_GROUP, " problems, equal list lengths");
+  dpe::HgemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.alpha = 1.f;
+  a.splits = 1;
+  a.ngroup = (int)n;
+  int64_t K = -1;
+  int tiles = 0;
+  for (size_t g = 0; g < n; ++g) {
+    const Tensor &dy = dys[g], &x = xs[g], &dw = dws[g], &db = dbs[g];
+    TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dw.is_cuda(), "linear_wgrad_group: GPU tensors");
+    TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && dy.is_contiguous() && x.is_contiguous(),
+                "linear_wgrad_group: dy / x must be contiguous bf16");
+    TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.is_contiguous() && dw.dim() == 2, "linear_wgrad_group: dw contiguous fp32 [out, in]");
+    const int64_t N = dw.size(0), Kin = dw.size(1), ldy = dy.size(-1);
+    TORCH_CHECK(ldy >= N && ldy % 8 == 0 && N % 8 == 0 && Kin % 8 == 0 && x.size(-1) == Kin, "linear_wgrad_group: shapes");
+    const int64_t T = dy.numel() / ldy;
+    TORCH_CHECK(x.numel() / Kin == T && T % 64 == 0, "linear_wgrad_group: token counts (multiple of 64)");
+    TORCH_CHECK(K < 0 || K == T, "linear_wgrad_group: every problem must have the same token count");
+    K = T;
+    dpe::HgemmProblem& q = a.grp[g];
+    q.A = (const uint16_t*)dy.data_ptr();
+    q.B = (const uint16_t*)x.data_ptr();
+    q.C = (float*)dw.data_ptr();
+    q.M = (int)N; q.N = (int)Kin; q.a_dim = (int)N;
+    q.lda = ldy; q.ldb = Kin; q.ldc = Kin;
+    q.overwrite = overwrite[g] ? 1 : 0;
+    if (db.defined() && db.numel() > 0) {
+      TORCH_CHECK(db.is_cuda() && db.scalar_type() == at::kFloat && db.is_contiguous() && db.numel() == N,
+                  "linear_wgrad_group: db contiguous fp32 [out]");
+      q.dbias = (float*)db.data_ptr();
+    }
+    tiles += (int)(((N + 255) / 256) * ((Kin + 255) / 256));
+    q.tile_end = tiles;
+  }
+  a.K = (int)K;
+  a.kps = (int)K;
+  a.group_m = 4;
+  const int slots = std::max(1, num_cus() - dpe_cu_reserve());
+  a.sched = sched_buffer(cur_stream());
+  const int rc = dpe_hgemm_group_launch(&a, std::min(tiles, slots), cur_stream());
+  const hipError_t e = hipGetLastError();
+  TORCH_CHECK(rc == 0 && e == hipSuccess, "hgemm group launch failed rc=", rc, " ", hipGetErrorString(e));
+}
+
 }  // namespace
 
 void register_gemm(pybind11::module& m) {
+  m.def("linear_wgrad_group", &linear_wgrad_group, pybind11::arg("dys"), pybind11::arg("xs"), pybind11::arg("dws"),
+        pybind11::arg("dbs"), pybind11::arg("overwrite"),
+        "grouped TN weight grads in one launch: dws[g] (+)= dys[g]^T xs[g], dbs[g] += colsum(dys[g]) "
+        "(dbs[g] empty: none; overwrite[g]: the gradient's first writer)");
   namespace py = pybind11;
   m.def("hgemm", &hgemm_raw, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("a_k"), py::arg("b_k"), py::arg("epi") = 0,

@@ -11,7 +11,23 @@ enum HEpi : int {
   HE_F32 = 1,     // C f32  = alpha*acc + bias (+ residual_f32)
   HE_ACC_F32 = 2, // C f32 += alpha*acc                       (weight grads into fp32 buckets; no K split)
   HE_SLAB = 3,    // ws[split] f32 = acc (K-split partial; hgemm_finalize applies the real epilogue)
+  HE_GROUP = 4,   // grouped TN weight grads: per problem g, C_g f32 (+)= alpha*acc (+ the fused bias grad)
 };
+
+// One problem of a grouped launch (HE_GROUP): several independent TN weight-gradient GEMMs sharing K
+// (the token count), the 256x256 tile, no K split.  Units [tile_end of the previous problem,
+// tile_end) are this problem's output tiles.
+struct HgemmProblem {
+  const uint16_t* A;  // dy, M-contiguous A[k][m] (lda)
+  const uint16_t* B;  // x, N-contiguous B[k][n] (ldb)
+  float* C;           // the fp32 weight gradient [M][ldc]
+  float* dbias;       // [M] bias gradient (+= row sums of dy^T) or nullptr
+  int64_t lda, ldb, ldc;
+  int M, N, a_dim;    // a_dim: load extent of A's M (>= M; 0 = M)
+  int tile_end;       // cumulative 256x256 tile count through this problem
+  int overwrite;      // 1: C = alpha*acc (the gradient's first writer of the step), 0: C += alpha*acc
+};
+constexpr int HGEMM_MAX_GROUP = 8;
 // act values beyond igemm.h's Act: gelu backward, C = (alpha*acc) * gelu'(aux_in)
 constexpr int HACT_GELU_BWD = 3;
 // HE_BF16 + the BatchNorm-backward partials of the stored values (a conv data grad dL/dy of a BN + ReLU
@@ -51,6 +67,9 @@ struct HgemmArgs {
   const uint16_t* st_x;     // bf16 [M][ldc] pre-BN input of the BN whose output this GEMM's result is the gradient of
   const float* st_coef;     // [4][N]: scale, shift, mean, invstd
   int stats_ld;
+  // HE_GROUP: the problems (A, B, C, M, N, lda, ldb, ldc, a_dim, dbias above are ignored)
+  int ngroup;
+  HgemmProblem grp[HGEMM_MAX_GROUP];
 };
 
 // Tile configurations (BMxBN, waves WRxWC).
@@ -67,5 +86,7 @@ enum HCfg : int {
 // Returns 0, or < 0 when the configuration is outside the kernel's envelope.
 extern "C" int dpe_hgemm_launch(const dpe::HgemmArgs* args, int cfg, int a_k, int b_k, int epi, int grid,
                                 hipStream_t stream);
+// Grouped TN weight grads (HE_GROUP): args->ngroup problems, 256x256 tile, no K split.
+extern "C" int dpe_hgemm_group_launch(const dpe::HgemmArgs* args, int grid, hipStream_t stream);
 // Sum of `splits` f32 partial slabs [M][N] -> the real epilogue (bias, act, residual, bf16/f32 out).
 extern "C" int dpe_hgemm_finalize(const dpe::HgemmArgs* args, int epi, hipStream_t stream);

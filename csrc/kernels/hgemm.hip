@@ -179,12 +179,23 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
   // object can make the compiler drain vmcnt before the main loop's ds_reads)
   __shared__ __attribute__((aligned(16))) char smem[G::LDS + 16];
 
+  // Grouped launch (HE_GROUP): several TN weight-grad problems share one persistent grid; decode()
+  // switches these per unit.  Otherwise they are the launch's single problem.
+  constexpr bool GRP = EPI == HE_GROUP;
+  const void* qA = p.A;
+  const void* qB = p.B;
+  void* qC = p.C;
+  float* qdbias = p.dbias;
+  int qM = p.M, qN = p.N, qadim = p.a_dim, qover = 0;
+  int64_t qlda = p.lda, qldb = p.ldb, qldc = p.ldc;
+
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid / WC, wc = wid % WC;
   const bool late = NW == 8 && wid >= 4;  // second-dispatched half runs one barrier behind
-  const int tilesM = (p.M + BM - 1) / BM, tilesN = (p.N + BN - 1) / BN;
-  const int ntile = tilesM * tilesN, nunits = ntile * p.splits;
+  int tilesM = (qM + BM - 1) / BM, tilesN = (qN + BN - 1) / BN;
+  int ntile = tilesM * tilesN;
+  const int nunits = GRP ? p.grp[p.ngroup - 1].tile_end : ntile * p.splits;
   const float alpha = p.alpha * (p.alpha_ptr ? *p.alpha_ptr : 1.f);
 
   // Schedule.  Without p.sched (or with one round of units) block b computes units
@@ -274,10 +285,10 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
     }
   }
 
-  const char* const Ab = (const char*)p.A;
-  const char* const Bb = (const char*)p.B;
-  const int64_t astep = AK ? (int64_t)TK * 2 : (int64_t)TK * p.lda * 2;
-  const int64_t bstep = BK ? (int64_t)TK * 2 : (int64_t)TK * p.ldb * 2;
+  const char* Ab = (const char*)qA;
+  const char* Bb = (const char*)qB;
+  int64_t astep = AK ? (int64_t)TK * 2 : (int64_t)TK * qlda * 2;
+  int64_t bstep = BK ? (int64_t)TK * 2 : (int64_t)TK * qldb * 2;
   char* const wdA = smem + wid * GA * 1024;             // this wave's pieces in every A half image
   char* const wdB = smem + G::B_REGION + wid * GB * 1024;
 
@@ -301,8 +312,25 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
   // shares only A: L2 hit rate 50 % on 8192^3, measured -- profiles/hgemm_pmc_r2.txt).
   const int gm_rows = p.group_m > 0 ? p.group_m : 1;
   auto decode = [&](int uu) {
-    const int tile = uu % ntile;
-    split = uu / ntile;
+    int tile;
+    if constexpr (GRP) {
+      int g = 0;  // (wave-uniform: a few scalar compares)
+      while (g + 1 < p.ngroup && uu >= p.grp[g].tile_end) ++g;
+      const HgemmProblem& q = p.grp[g];
+      qA = q.A; qB = q.B; qC = q.C; qdbias = q.dbias;
+      qM = q.M; qN = q.N; qadim = q.a_dim; qover = q.overwrite;
+      qlda = q.lda; qldb = q.ldb; qldc = q.ldc;
+      Ab = (const char*)qA;
+      Bb = (const char*)qB;
+      tilesM = (qM + BM - 1) / BM;
+      tilesN = (qN + BN - 1) / BN;
+      ntile = tilesM * tilesN;
+      tile = uu - (g > 0 ? p.grp[g - 1].tile_end : 0);
+      split = 0;
+    } else {
+      tile = uu % ntile;
+      split = uu / ntile;
+    }
     const int gsz = gm_rows * tilesN;
     const int g0 = (tile / gsz) * gm_rows;
     const int grows = min(tilesM - g0, gm_rows);
@@ -311,10 +339,14 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
     n0 = (in / grows) * BN;
     kb = split * p.kps;
     nt = (min(p.K, kb + p.kps) - kb) / TK;
-    stage_setup<BM, WR, RH, GA, AK>(p.lda, p.a_dim > 0 ? p.a_dim : p.M, m0, AK ? kb : 0, ga);
-    stage_setup<BN, WC, CH, GB, BK>(p.ldb, p.b_dim > 0 ? p.b_dim : p.N, n0, BK ? kb : 0, gb);
-    if constexpr (!AK) { for (int h = 0; h < 2; ++h) for (int i = 0; i < GA; ++i) ga[h][i] += (uint32_t)((int64_t)kb * p.lda * 2); }
-    if constexpr (!BK) { for (int h = 0; h < 2; ++h) for (int i = 0; i < GB; ++i) gb[h][i] += (uint32_t)((int64_t)kb * p.ldb * 2); }
+    stage_setup<BM, WR, RH, GA, AK>(qlda, qadim > 0 ? qadim : qM, m0, AK ? kb : 0, ga);
+    stage_setup<BN, WC, CH, GB, BK>(qldb, p.b_dim > 0 ? p.b_dim : qN, n0, BK ? kb : 0, gb);
+    if constexpr (GRP) {
+      astep = AK ? (int64_t)TK * 2 : (int64_t)TK * qlda * 2;
+      bstep = BK ? (int64_t)TK * 2 : (int64_t)TK * qldb * 2;
+    }
+    if constexpr (!AK) { for (int h = 0; h < 2; ++h) for (int i = 0; i < GA; ++i) ga[h][i] += (uint32_t)((int64_t)kb * qlda * 2); }
+    if constexpr (!BK) { for (int h = 0; h < 2; ++h) for (int i = 0; i < GB; ++i) gb[h][i] += (uint32_t)((int64_t)kb * qldb * 2); }
   };
 
 #define STAGE_A(h, buf, t)                                                                   \
@@ -410,7 +442,7 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
 #pragma unroll
       for (int j = 0; j < 2 * FNH; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (BG) {
-      bg_on = p.dbias != nullptr && n0 == 0;  // one tile column carries the row sums
+      bg_on = qdbias != nullptr && n0 == 0;  // one tile column carries the row sums
       rsum[0] = rsum[1] = 0.f;
     }
     if (late) HG_BARRIER();
@@ -537,9 +569,9 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
           v += __shfl_xor(v, 16, 64);
           v += __shfl_xor(v, 32, 64);
           const int row = m0 + wr * (BM / WR) + hh * RH + wc * 16 + lm;
-          if (lane < 16 && row < p.M) {
-            if (p.splits > 1) p.ws_bias[(int64_t)cur_split * p.M + row] = v;  // summed in split order by finalize
-            else p.dbias[row] += alpha * v;                                   // the row's only writer
+          if (lane < 16 && row < qM) {
+            if (p.splits > 1) p.ws_bias[(int64_t)cur_split * qM + row] = v;  // summed in split order by finalize
+            else qdbias[row] += alpha * v;                                   // the row's only writer
           }
         }
       }
@@ -553,11 +585,11 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
 #pragma unroll
       for (int j = 0; j < 2 * FNH; ++j) {
         const int c = cbase + (j / FNH) * CH + (j % FNH) * 16;
-        bias[j] = (p.bias && c < p.N) ? *(const f32x4*)(p.bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        bias[j] = (p.bias && c < qN) ? *(const f32x4*)(p.bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
       for (int i = 0; i < 2 * FMH; ++i) {
-        const int r = min(rbase + (i / FMH) * RH + (i % FMH) * 16, p.M - 1);
+        const int r = min(rbase + (i / FMH) * RH + (i % FMH) * 16, qM - 1);
 #pragma unroll
         for (int j = 0; j < 2 * FNH; ++j) {
           const int c = cbase + (j / FNH) * CH + (j % FNH) * 16;
@@ -570,7 +602,7 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = gelu_fwd(v[e]);
           } else if constexpr (ACT == HACT_GELU_BWD) {
-            const u32x2 a = c < p.N ? *(const u32x2*)(p.aux_in + (int64_t)r * p.ldc + c) : u32x2{0u, 0u};
+            const u32x2 a = c < qN ? *(const u32x2*)(p.aux_in + (int64_t)r * qldc + c) : u32x2{0u, 0u};
             v[0] *= gelu_grad(__uint_as_float(a[0] << 16));
             v[1] *= gelu_grad(__uint_as_float(a[0] & 0xffff0000u));
             v[2] *= gelu_grad(__uint_as_float(a[1] << 16));
@@ -591,23 +623,23 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
 #pragma unroll
         for (int j = 0; j < 2 * FNH; ++j) {
           const int c = cbase + (j / FNH) * CH + (j % FNH) * 16;
-          const bool cv = c < p.N;
+          const bool cv = c < qN;
           const int cc = cv ? c : 0;
           f32x4 sc{}, sh{}, mu{};
           if constexpr (ACT == HACT_BNB) {
             sc = *(const f32x4*)(p.st_coef + cc);
-            sh = *(const f32x4*)(p.st_coef + p.N + cc);
-            mu = *(const f32x4*)(p.st_coef + 2 * p.N + cc);
+            sh = *(const f32x4*)(p.st_coef + qN + cc);
+            mu = *(const f32x4*)(p.st_coef + 2 * qN + cc);
           }
           f32x4 s1 = f32x4{0.f, 0.f, 0.f, 0.f}, s2 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int i = 0; i < 2 * FMH; ++i) {
             const int r = rbase + (i / FMH) * RH + (i % FMH) * 16;
-            if (r < p.M && cv) {
+            if (r < qM && cv) {
               const float v4[4] = {__uint_as_float(pk[i][j][0] << 16), __uint_as_float(pk[i][j][0] & 0xffff0000u),
                                    __uint_as_float(pk[i][j][1] << 16), __uint_as_float(pk[i][j][1] & 0xffff0000u)};
               if constexpr (ACT == HACT_BNB) {
-                const u32x2 xr = *(const u32x2*)(p.st_x + (int64_t)r * p.ldc + c);
+                const u32x2 xr = *(const u32x2*)(p.st_x + (int64_t)r * qldc + c);
                 const float x4[4] = {__uint_as_float(xr[0] << 16), __uint_as_float(xr[0] & 0xffff0000u),
                                      __uint_as_float(xr[1] << 16), __uint_as_float(xr[1] & 0xffff0000u)};
 #pragma unroll
@@ -638,7 +670,7 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               p.col_stats[(int64_t)(c + e) * p.stats_ld + col] = s1[e];
-              p.col_stats[(int64_t)(p.N + c + e) * p.stats_ld + col] = s2[e];
+              p.col_stats[(int64_t)(qN + c + e) * p.stats_ld + col] = s2[e];
             }
           }
         }
@@ -648,33 +680,33 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
 #pragma unroll
       for (int j = 0; j < 2 * FNH; ++j) {
         const int c = cbase + (j / FNH) * CH + (j % FNH) * 16;
-        bias[j] = (p.bias && c < p.N) ? *(const f32x4*)(p.bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        bias[j] = (p.bias && c < qN) ? *(const f32x4*)(p.bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
       for (int i = 0; i < 2 * FMH; ++i) {
-        const int r = min(rbase + (i / FMH) * RH + (i % FMH) * 16, p.M - 1);
+        const int r = min(rbase + (i / FMH) * RH + (i % FMH) * 16, qM - 1);
 #pragma unroll
         for (int j = 0; j < 2 * FNH; ++j) {
           const int c = cbase + (j / FNH) * CH + (j % FNH) * 16;
           f32x4 res = f32x4{0.f, 0.f, 0.f, 0.f};
-          if (p.residual_f32 && c < p.N) res = *(const f32x4*)(p.residual_f32 + (int64_t)r * p.ldc + c);
+          if (p.residual_f32 && c < qN) res = *(const f32x4*)(p.residual_f32 + (int64_t)r * qldc + c);
           // stored right away (holding 128 fp32 results across the next prologue spills)
-          if (c < p.N && rbase + (i / FMH) * RH + (i % FMH) * 16 < p.M)
-            *(f32x4*)((float*)p.C + (int64_t)r * p.ldc + c) = acc[i][j] * alpha + bias[j] + res;
+          if (c < qN && rbase + (i / FMH) * RH + (i % FMH) * 16 < qM)
+            *(f32x4*)((float*)qC + (int64_t)r * qldc + c) = acc[i][j] * alpha + bias[j] + res;
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-    } else if constexpr (EPI == HE_ACC_F32) {
+    } else if constexpr (EPI == HE_ACC_F32 || EPI == HE_GROUP) {
 #pragma unroll
       for (int i = 0; i < 2 * FMH; ++i) {
-        const int r = min(rbase + (i / FMH) * RH + (i % FMH) * 16, p.M - 1);
+        const int r = min(rbase + (i / FMH) * RH + (i % FMH) * 16, qM - 1);
 #pragma unroll
         for (int j = 0; j < 2 * FNH; ++j) {
           const int c = cbase + (j / FNH) * CH + (j % FNH) * 16;
           f32x4 old = f32x4{0.f, 0.f, 0.f, 0.f};
-          if (c < p.N) old = *(const f32x4*)((const float*)p.C + (int64_t)r * p.ldc + c);
-          if (c < p.N && rbase + (i / FMH) * RH + (i % FMH) * 16 < p.M)
-            *(f32x4*)((float*)p.C + (int64_t)r * p.ldc + c) = acc[i][j] * alpha + old;
+          if (c < qN && !(GRP && qover)) old = *(const f32x4*)((const float*)qC + (int64_t)r * qldc + c);
+          if (c < qN && rbase + (i / FMH) * RH + (i % FMH) * 16 < qM)
+            *(f32x4*)((float*)qC + (int64_t)r * qldc + c) = acc[i][j] * alpha + old;
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -704,13 +736,13 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
           u32x2 a = pk[i][j], b = pk[i + 1][j];
           auto x = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
           auto y = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
-          if (r < p.M && c < p.N) *(u32x4*)((uint16_t*)p.C + (int64_t)r * p.ldc + c) = u32x4{x[0], y[0], x[1], y[1]};
+          if (r < qM && c < qN) *(u32x4*)((uint16_t*)qC + (int64_t)r * qldc + c) = u32x4{x[0], y[0], x[1], y[1]};
           if constexpr (ACT == ACT_GELU) {
             u32x2 va = pv[i][j], vb = pv[i + 1][j];
             auto vx = __builtin_amdgcn_permlane16_swap(va[0], vb[0], false, false);
             auto vy = __builtin_amdgcn_permlane16_swap(va[1], vb[1], false, false);
-            if (p.aux_out && r < p.M && c < p.N)
-              *(u32x4*)(p.aux_out + (int64_t)r * p.ldc + c) = u32x4{vx[0], vy[0], vx[1], vy[1]};
+            if (p.aux_out && r < qM && c < qN)
+              *(u32x4*)(p.aux_out + (int64_t)r * qldc + c) = u32x4{vx[0], vy[0], vx[1], vy[1]};
           }
         }
       }
@@ -718,11 +750,11 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
 #pragma unroll
       for (int i = 0; i < 2 * FMH; ++i) {
         const int r = rbase + (i / FMH) * RH + (i % FMH) * 16;
-        if (r >= p.M) continue;
+        if (r >= qM) continue;
 #pragma unroll
         for (int j = 0; j < 2 * FNH; ++j) {
           const int c = cbase + (j / FNH) * CH + (j % FNH) * 16;
-          if (c < p.N) *(f32x4*)(p.ws + ((int64_t)cur_split * p.M + r) * p.N + c) = acc[i][j];
+          if (c < qN) *(f32x4*)(p.ws + ((int64_t)cur_split * qM + r) * qN + c) = acc[i][j];
         }
       }
     }
@@ -878,6 +910,26 @@ extern "C" int dpe_hgemm_launch(const HgemmArgs* a, int cfg, int a_k, int b_k, i
     case HC_128x128: return launch_layout<128, 128, 2, 2>(p, a_k, b_k, epi, grid, st);
     default: return -1;
   }
+}
+
+extern "C" int dpe_hgemm_group_launch(const HgemmArgs* a, int grid, hipStream_t st) {
+  const HgemmArgs& p = *a;
+  if (p.ngroup < 1 || p.ngroup > HGEMM_MAX_GROUP || p.K % 64 || p.K <= 0 || grid <= 0) return -1;
+  if (p.splits != 1 || p.kps != p.K || p.act != ACT_NONE) return -1;
+  int prev = 0;
+  for (int g = 0; g < p.ngroup; ++g) {
+    const HgemmProblem& q = p.grp[g];
+    const int adim = q.a_dim > 0 ? q.a_dim : q.M;
+    if (!q.A || !q.B || !q.C || q.M <= 0 || q.N <= 0 || q.N % 8 || adim < q.M || adim % 8) return -1;
+    if (q.lda < adim || q.ldb < q.N || q.lda % 8 || q.ldb % 8 || q.ldc < q.N) return -1;
+    if ((int64_t)p.K * q.lda * 2 >= (1ll << 32) || (int64_t)p.K * q.ldb * 2 >= (1ll << 32)) return -4;
+    const int tiles = ((q.M + 255) / 256) * ((q.N + 255) / 256);
+    if (q.tile_end != prev + tiles) return -1;  // host and kernel agree on the unit -> problem map
+    prev = q.tile_end;
+  }
+  hipLaunchKernelGGL((hg::hgemm_kernel<256, 256, 2, 4, false, false, HE_GROUP, ACT_NONE, true>), dim3((unsigned)grid),
+                     dim3(512), 0, st, p);
+  return 0;
 }
 
 extern "C" int dpe_hgemm_finalize(const HgemmArgs* a, int epi, hipStream_t st) {

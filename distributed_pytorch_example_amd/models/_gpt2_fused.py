@@ -34,6 +34,7 @@ BASELINE.json config 4 -- same math as ``models/gpt2.py:Block``.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 from torch.autograd import Function
@@ -43,6 +44,42 @@ from ..ops._state import finalize_stream, grad_done, grad_fresh, grad_sink, note
 
 # (fp32 grad, its bf16 copy, version) produced by the most recent block backward
 _carry: list = [None]
+
+# Grouped weight gradients.  Alone, a layer's four weight-grad GEMMs (dW = dy^T x over K = B*T tokens;
+# 27 / 9 / 36 / 36 output tiles of 256x256 at d = 768) need an 8-9-way K split each to fill 256 CUs,
+# and the split's fp32 partial slabs plus their finalize launch cost about as much as the GEMM itself.
+# Deferred here and launched together (C.linear_wgrad_group, hgemm HE_GROUP), DPE_GPT2_WGRAD_GROUP layers
+# at a time (default 2: 216 whole-K tiles, one round of the persistent grid, no slabs).  Only gradients
+# that live in DDP bucket views are deferred (the reducer is told when the group has been written; a
+# gradient autograd would receive from this node must be complete when backward returns).  0 = off.
+_WG_GROUP = int(os.environ.get("DPE_GPT2_WGRAD_GROUP", "2"))
+_wq: list = []  # (dy, x, dw, db | None, overwrite, weight param, bias param | None)
+
+
+def reset_wgrad_queue() -> None:
+    """Drop deferred work of a backward that raised (called at every forward)."""
+    _wq.clear()
+
+
+def flush_wgrad_queue() -> None:
+    """Launch the queued weight gradients (groups of at most 8 problems) and announce them."""
+    if not _wq:
+        return
+    C = ext()
+    items = list(_wq)
+    _wq.clear()
+    for i in range(0, len(items), 8):
+        chunk = items[i:i + 8]
+        C.linear_wgrad_group([q[0] for q in chunk], [q[1] for q in chunk], [q[2] for q in chunk],
+                             [q[3] if q[3] is not None else _EMPTY(q[2]) for q in chunk], [q[4] for q in chunk])
+    for q in items:
+        grad_done(q[5], True)
+        if q[6] is not None:
+            grad_done(q[6], True)
+
+
+def _EMPTY(like):
+    return like.new_empty(0)
 
 
 def _bf16_of(g: torch.Tensor) -> torch.Tensor:
@@ -100,6 +137,8 @@ class BlockFn(Function):
         g = g.contiguous()
         gb = _bf16_of(g)
         grads = {}
+        T = g.numel() // g.shape[-1]
+        group = _WG_GROUP > 0 and T % 64 == 0 and g.shape[-1] % 8 == 0
 
         def sink(p):
             buf, direct = grad_sink(p)
@@ -113,6 +152,10 @@ class BlockFn(Function):
             """dW += dyb^T inp and db += colsum(dyb) in one GEMM launch ; return dyb W (bf16), times gelu'(gelu_in) if given."""
             buf, d = sink(lin.weight)
             bb, bd = sink(lin.bias) if lin.bias is not None else (None, True)
+            if group and d and bd:
+                # deferred to the grouped launch at the end of this block's (or the next one's) backward
+                _wq.append((dyb, inp, buf, bb, grad_fresh(lin.weight), lin.weight, lin.bias))
+                return C.linear_dgrad(dyb, shadow(lin.weight), None, None, gelu_in) if want_dx else None
             # bias grad from the same launch (row sums of dy^T); a K-split's slab reduction may run on the
             # side stream when both gradients are bucket views (the reducer / backward join wait for it)
             fs = finalize_stream(dyb.device) if (d and bd) else 0
@@ -140,6 +183,8 @@ class BlockFn(Function):
         dqkv = dqkv.view(a.shape[0], a.shape[1], -1)
         dh1 = linear_bwd(blk.c_attn, dqkv, h1)
         g1, g1b = ln_bwd(blk.ln_1, dh1, x, m1, r1, g2)
+        if _wq and (len(_wq) >= 4 * _WG_GROUP or getattr(blk, "_dpe_layer", 0) == 0 or not group):
+            flush_wgrad_queue()  # every _WG_GROUP layers, and always at the first block (end of backward)
         _carry[0] = (g1, g1b, g1._version)
         pgrads = [grads.get(id(p)) for p in block_params(blk)]
         return (g1, None, *pgrads)

@@ -84,6 +84,8 @@ class GPT2(nn.Module):
         self.wte = nn.Parameter(torch.empty(cfg.vocab_size, cfg.n_embd))
         self.wpe = nn.Parameter(torch.empty(cfg.block_size, cfg.n_embd))
         self.h = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layer)])
+        for i, blk in enumerate(self.h):
+            blk._dpe_layer = i  # the fused backward flushes deferred weight grads at layer 0 (end of backward)
         self.ln_f = LayerNorm(cfg.n_embd, bias=cfg.bias)
         # tied LM head / embedding: the LM-head weight grad (first writer) overwrites when fresh, the
         # embedding scatter-add accumulates after it
@@ -112,6 +114,10 @@ class GPT2(nn.Module):
         outside it)."""
         B, T = idx.shape
         assert T <= self.cfg.block_size, "sequence longer than block_size"
+        if _FUSED and idx.is_cuda:
+            from ._gpt2_fused import reset_wgrad_queue
+
+            reset_wgrad_queue()
         x = Fx.embedding(idx, self.wte, self.wpe[:T] if not idx.is_cuda else self.wpe)
         for blk in self.h:
             x = blk(x)
