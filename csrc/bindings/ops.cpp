@@ -18,6 +18,16 @@
 using at::Tensor;
 
 extern "C" {
+int dpe_cu_reserve();  // comm.cpp: slots to leave to in-flight collectives
+int dpe_gram_blocks(int64_t M, int C);
+int64_t dpe_gram_ws_floats(int64_t M, int C);
+int dpe_gram(const uint16_t* x, const float* coef, int64_t M, int C, float* ws, float* G, float* s, hipStream_t st);
+int dpe_gram_coef(const float* G, const float* s, const uint16_t* w, int Cin, int Cout, int64_t M, const float* gamma,
+                  const float* beta, float* rmean, float* rvar, float momentum, float eps, float* coef, float* u,
+                  hipStream_t st);
+int dpe_gram_bwd(const float* part, int rg, const float* P, const uint16_t* w, const float* u, const float* s,
+                 const float* coef3, const float* gamma, int Cin, int Cout, int64_t M, float* dgamma, float* dbeta,
+                 float* dw, uint16_t* bcat, float* abc, float* ebias, hipStream_t st);
 int dpe_bn_stats_nblocks(int64_t M, int C);
 
 int dpe_bn_stats(const uint16_t* x, int64_t M, int C, int nb, float* part, hipStream_t st);
@@ -138,8 +148,11 @@ Cfg pick_cfg(int64_t M, int64_t N, int64_t K, bool allow_split) {
     const int64_t ksteps = (K + 31) / 32;
     // register-staged weight-grad tiles (1x1 with 128 channels): 512 blocks (768 / 1024 / 1536 measured
     // worse, docs/perf_notes.md); the LDS-DMA im2col weight-grad kernel re-derives its split (run_igemm)
-    constexpr int64_t target_blocks = 512;
-    int64_t splits = std::max<int64_t>(1, std::min<int64_t>((target_blocks + t - 1) / t, ksteps / 8));
+    // (at the CU budget -- an overlapped RCCL collective holding `reserve` slots -- a slot fewer per
+    // reserved workgroup, so the split still fits one resident wave: SURVEY §5.8 item 7)
+    const int64_t target_blocks = std::max<int64_t>(64, 2 * (int64_t)dpe_gemm::num_cus() - dpe_cu_reserve());
+    const int64_t per = dpe_cu_reserve() > 0 ? target_blocks / t : (target_blocks + t - 1) / t;
+    int64_t splits = std::max<int64_t>(1, std::min<int64_t>(per, ksteps / 8));
     const int64_t kps = (ksteps + splits - 1) / splits;
     c.k_split = (int)(kps * 32);
     c.splits = (int)((ksteps + kps - 1) / kps);
@@ -224,9 +237,14 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
       // (profiles/wgrad_blocks_ab_r2.txt, all split-K weight grads at one target): 256 -8 %, 384 -2.4 %,
       // 512 0, 768 +1.4-1.8 %, 1024 -0.5 %, 1536 -0.5 %, 2048 -1 %; 704-768 best of 640-896.  The
       // register-staged 1x1 tiles measured best at 512 and keep pick_cfg's split.
-      constexpr int64_t dma_target = 768;
+      // 3 per CU (768 on 256 CUs), less the slots an overlapped RCCL collective holds (CU budget,
+      // comm.cpp): a split that needs more blocks than fit beside the collective's workgroups runs a
+      // second, nearly empty wave (x1.56-1.60 per kernel next to 16 RCCL-sized workgroups,
+      // profiles/cu_hog_probe_r3.txt).  Rounded down, so tiles x splits <= the target.
+      const int64_t dma_target = std::max<int64_t>(64, 3 * (int64_t)dpe_gemm::num_cus() - dpe_cu_reserve());
       const int64_t t = (int64_t)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn), ksteps = (a.K + 31) / 32;
-      const int64_t sp = std::max<int64_t>(1, std::min<int64_t>((dma_target + t - 1) / t, ksteps / 8));
+      const int64_t rs = dpe_cu_reserve() > 0 ? dma_target / t : (dma_target + t - 1) / t;  // (unchanged at no reserve)
+      const int64_t sp = std::max<int64_t>(1, std::min<int64_t>(rs, ksteps / 8));
       const int64_t kps = (ksteps + sp - 1) / sp;
       a.k_split = (int)(kps * 32);
       splits = (int)((ksteps + kps - 1) / kps);
@@ -659,7 +677,7 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
                                     const c10::optional<Tensor>& bn_coef, const Tensor* acc_into = nullptr,
                                     const c10::optional<Tensor>& bn_mask = c10::nullopt,
                                     const c10::optional<Tensor>& residual_mask = c10::nullopt,
-                                    bool res_stride2 = false) {
+                                    bool res_stride2 = false, const c10::optional<Tensor>& sum_mask = c10::nullopt) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(w); CHECK_CONTIG(dy); CHECK_CONTIG(w);
   // acc_into: dx += dgrad in place (the epilogue reads each element as its residual
   // right before overwriting it); parities no tap reaches are left untouched.
@@ -715,11 +733,32 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
   if (res_stride2) {
     // residual = the compact data grad of a downsample block's stride-2 1x1 conv ([N, H/2, W/2, C]),
     // added at even (h, w) by the streaming kernel's epilogue
-    TORCH_CHECK(a.residual && !a.res_mask && pw_rg > 0 && g.H % 2 == 0 && g.W % 2 == 0,
+    TORCH_CHECK(a.residual && !a.res_mask && (pw_rg > 0 || (sum_mask.has_value() && sum_mask->defined())) &&
+                    g.H % 2 == 0 && g.W % 2 == 0,
                 "conv_dgrad: residual_stride2 needs the streaming pointwise data grad, even H / W, no residual mask");
     TORCH_CHECK(residual->dim() == 4 && residual->size(0) == g.N && residual->size(1) == g.H / 2 &&
                     residual->size(2) == g.W / 2 && residual->size(3) == g.C,
                 "conv_dgrad: residual_stride2 residual must be [N, H/2, W/2, C]");
+  }
+  if (sum_mask.has_value() && sum_mask->defined()) {
+    // BN + residual + ReLU backward partials WITHOUT the pre-BN input (Gram algebra, bngram.hip): dx stored
+    // masked by the output's bits, partials row 0 = sum dz (row 1 unwritten); streaming kernel only
+    TORCH_CHECK(!want_bn && !acc_into && is_pointwise(g), "conv_dgrad: sum_mask excludes bn_x / accumulate");
+    CHECK_CONTIG((*sum_mask));
+    TORCH_CHECK(sum_mask->scalar_type() == at::kByte && sum_mask->numel() * 8 == dx.numel() && g.C % 8 == 0,
+                "conv_dgrad: sum_mask must be uint8 mask bits [N,H,W,C/8] of dx's shape");
+    const int rg = pw_stream_on() ? dpe_pw_rowgroups(a.M, a.N, a.K, dpe::PW_DSUM) : 0;
+    TORCH_CHECK(rg > 0, "conv_dgrad: sum_mask needs the streaming pointwise data grad");
+    dpe::PwArgs pa{};
+    pa.x = bp(dy); pa.w = bp(w); pa.y = bpm(dx);
+    pa.residual = a.residual; pa.res_mask = a.res_mask;
+    if (res_stride2) { pa.res_h = g.H; pa.res_w = g.W; }
+    pa.st_mask = (const uint8_t*)sum_mask->data_ptr();
+    pa.M = a.M; pa.N = a.N; pa.K = a.K; pa.rg = rg;
+    part = at::empty({2, g.C, rg}, dy.options().dtype(at::kFloat));
+    pa.stats = fp(part);
+    CHECK_RC(dpe_pw_launch(&pa, dpe::PW_DSUM, cur_stream()), "pw_stream dgrad (sum dz)");
+    return {dx, part};
   }
   if (pw_rg > 0) {
     dpe::PwArgs pa{};
@@ -1001,6 +1040,120 @@ std::vector<Tensor> bn_bwd(const Tensor& dy, const c10::optional<Tensor>& y, con
   CHECK_RC(dpe_bn_bwd_apply(bp(dy), yp, yb, bp(x), fp(bcoef), bpm(dx), want_dz ? bpm(dz) : nullptr, M, (int)C, nullptr, st),
            "bn_bwd_apply");
   return {dx, dz};
+}
+
+// ------------------------------------------------------------ BN3 by Gram algebra (bngram.hip)
+// G = a2^T a2 [C][C] and s = colsum(a2) [C] of a2 = relu(x * coef[0] + coef[1]) (coef: the BN's [4][C]) or x.
+std::vector<Tensor> bn_gram(const Tensor& x, const c10::optional<Tensor>& coef) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x);
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(C == 64 || C == 128 || C == 256, "bn_gram: C must be 64, 128 or 256");
+  if (coef.has_value() && coef->defined()) {
+    CHECK_F32((*coef));
+    TORCH_CHECK(coef->numel() >= 2 * C, "bn_gram: coef must be the BN's [4][C] coefficients");
+  }
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor ws = at::empty({dpe_gram_ws_floats(M, (int)C)}, fo);
+  Tensor G = at::empty({C, C}, fo), sv = at::empty({C}, fo);
+  CHECK_RC(dpe_gram(bp(x), fpo(coef), M, (int)C, fp(ws), fp(G), fp(sv), cur_stream()), "bn_gram");
+  return {G, sv};
+}
+
+// BN coefficients [4][Cout] of h = a2 W^T (never computed) from G, s: mean = w.s / M, E[h^2] = w^T G w / M;
+// running stats updated as bn_coef.  Also returns u = W G [Cout][Cin] (fp32) for the backward.
+std::vector<Tensor> bn_gram_coef(const Tensor& G, const Tensor& sv, const Tensor& w, int64_t M,
+                                 const c10::optional<Tensor>& gamma, const c10::optional<Tensor>& beta,
+                                 const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar, double momentum,
+                                 double eps) {
+  CHECK_GPU(G); CHECK_F32(G); CHECK_F32(sv); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(G);
+  const int64_t Cin = G.size(0), Cout = w.size(0);
+  TORCH_CHECK(w.numel() == Cout * Cin && sv.numel() == Cin, "bn_gram_coef: shapes");
+  Tensor coef = at::empty({4, Cout}, G.options()), u = at::empty({Cout, Cin}, G.options());
+  CHECK_RC(dpe_gram_coef(fp(G), fp(sv), bp(w), (int)Cin, (int)Cout, M, fpo(gamma), fpo(beta), fpom(rmean), fpom(rvar),
+                         (float)momentum, (float)eps, fp(coef), fp(u), cur_stream()), "bn_gram_coef");
+  return {coef, u};
+}
+
+// y = relu(BN(x' W^T) + residual) of a 1x1 conv (x' = relu(x * in_coef) or x), with the BN's coefficients known
+// in advance (bn_gram_coef): streaming pointwise kernel, PW_APPLY.  res_coef: the residual is the pre-BN
+// output of a downsample conv, BN'd (and rounded) on the fly.  Returns (y, ReLU bits of y).
+std::vector<Tensor> conv1x1_apply(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& in_coef,
+                                  const Tensor& out_coef, const Tensor& residual, const c10::optional<Tensor>& res_coef) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_F32(out_coef);
+  CHECK_BF16(residual); CHECK_CONTIG(residual);
+  const int64_t K = x.size(-1), M = x.numel() / K, N = w.size(0);
+  TORCH_CHECK(w.numel() == N * K && out_coef.numel() == 4 * N, "conv1x1_apply: shapes");
+  auto ysz = x.sizes().vec();
+  ysz.back() = N;
+  TORCH_CHECK(residual.sizes().vec() == ysz, "conv1x1_apply: residual must have the output's shape");
+  const int rg = pw_stream_on() ? dpe_pw_rowgroups(M, N, K, dpe::PW_APPLY) : 0;
+  TORCH_CHECK(rg > 0, "conv1x1_apply: outside the streaming pointwise kernel's envelope");
+  Tensor y = at::empty(ysz, x.options());
+  auto bsz = ysz;
+  bsz.back() = N / 8;
+  Tensor bits = at::empty(bsz, x.options().dtype(at::kByte));
+  dpe::PwArgs pa{};
+  pa.x = bp(x); pa.w = bp(w); pa.y = bpm(y);
+  pa.in_coef = fpo(in_coef);
+  pa.out_coef = fp(out_coef);
+  pa.residual = bp(residual);
+  pa.res_coef = fpo(res_coef);
+  pa.out_bits = (uint8_t*)bits.data_ptr();
+  pa.M = M; pa.N = N; pa.K = K; pa.rg = rg;
+  CHECK_RC(dpe_pw_launch(&pa, dpe::PW_APPLY, cur_stream()), "pw_stream apply");
+  return {y, bits};
+}
+
+// BN3 backward by Gram algebra: from part (row 0: sum dz partials, [2][Cout][rg]), P = dz^T a2 [Cout][Cin], W,
+// u = W G, s, the forward coef: dgamma / dbeta / dw accumulate; returns the data grad's B operand
+// [Cout + Cin][Cin] bf16 (= [diag(a) W ; W^T diag(b) W]) and its bias c^T W [Cin].
+std::vector<Tensor> bn_gram_bwd(const Tensor& part, const Tensor& P, const Tensor& w, const Tensor& u, const Tensor& sv,
+                                const Tensor& coef, const c10::optional<Tensor>& gamma, int64_t M,
+                                const c10::optional<Tensor>& dgamma, const c10::optional<Tensor>& dbeta, Tensor& dw) {
+  CHECK_GPU(part); CHECK_F32(part); CHECK_F32(P); CHECK_F32(u); CHECK_F32(sv); CHECK_F32(coef); CHECK_F32(dw);
+  CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(P); CHECK_CONTIG(dw); CHECK_CONTIG(part);
+  const int64_t Cout = w.size(0), Cin = w.numel() / Cout;
+  TORCH_CHECK(part.dim() == 3 && part.size(1) == Cout && P.numel() == Cout * Cin && u.numel() == Cout * Cin &&
+                  dw.numel() == Cout * Cin && sv.numel() == Cin && coef.numel() == 4 * Cout,
+              "bn_gram_bwd: shapes");
+  auto fo = P.options();
+  Tensor bcat = at::empty({Cout + Cin, Cin}, w.options()), abc = at::empty({3, Cout}, fo), e = at::empty({Cin}, fo);
+  CHECK_RC(dpe_gram_bwd(fp(part), (int)part.size(2), fp(P), bp(w), fp(u), fp(sv), fp(coef), fpo(gamma), (int)Cin,
+                        (int)Cout, M, fpom(dgamma), fpom(dbeta), fp(dw), bpm(bcat), fp(abc), fp(e), cur_stream()),
+           "bn_gram_bwd");
+  return {bcat, e};
+}
+
+// da2 = [dz | a2] x bcat + e with the BN-backward partials of the BN + ReLU that produced a2 (bn_x, bn_coef):
+// the concatenated-K data grad of the Gram-algebra BN3 backward (igemm AX_CAT).  a2 = relu(a2src * a2_coef)
+// when a2_coef is given (a2 never materialised), else a2src itself.  Returns (da2, partials).
+std::vector<Tensor> conv1x1_dgrad_cat(const Tensor& dz, const Tensor& a2src, const c10::optional<Tensor>& a2_coef,
+                                      const Tensor& bcat, const Tensor& e, const Tensor& bn_x, const Tensor& bn_coef) {
+  CHECK_GPU(dz); CHECK_BF16(dz); CHECK_CONTIG(dz); CHECK_BF16(a2src); CHECK_CONTIG(a2src); CHECK_BF16(bcat);
+  CHECK_CONTIG(bcat); CHECK_F32(e); CHECK_BF16(bn_x); CHECK_CONTIG(bn_x); CHECK_F32(bn_coef);
+  const int64_t K1 = dz.size(-1), M = dz.numel() / K1, C = a2src.size(-1);
+  TORCH_CHECK(a2src.numel() == M * C && bcat.size(0) == K1 + C && bcat.size(1) == C && e.numel() == C &&
+                  bn_x.sizes() == a2src.sizes() && bn_coef.numel() == 4 * C && K1 % 32 == 0 && C % 32 == 0,
+              "conv1x1_dgrad_cat: shapes");
+  Tensor dx = at::empty_like(bn_x);
+  auto a = base_args();
+  a.A = bp(dz); a.B = bp(bcat); a.C = dx.data_ptr();
+  a.M = (int)M; a.N = (int)C; a.K = (int)(K1 + C);
+  a.lda = K1; a.ldb = C; a.ldc = C;
+  a.k_split = a.K;
+  a.bias = fp(e);
+  a.a_mode = dpe::AX_CAT;
+  a.a2 = bp(a2src); a.lda2 = C; a.k1 = (int)K1;
+  a.a_coef = fpo(a2_coef);
+  a.st_x = bp(bn_x); a.st_coef = fp(bn_coef);
+  const int bm = 128, bn = C <= 64 ? 64 : 128;
+  const int64_t tilesM = (M + bm - 1) / bm;
+  Tensor part = at::empty({2, C, tilesM}, dz.options().dtype(at::kFloat));
+  a.col_stats = fp(part);
+  a.stats_ld = (int)tilesM;
+  const int rc = dpe_igemm_dma_launch(&a, bm, bn, dpe::A_DENSE_K, dpe::B_DENSE_N, dpe::EPI_BF16_BNB, cur_stream());
+  CHECK_RC(rc, "igemm_dma AX_CAT data grad");
+  return {dx, part};
 }
 
 // BatchNorm coefficients [4][C] (scale, shift, mean, invstd) from conv-epilogue
@@ -1516,6 +1669,18 @@ void register_ops(pybind11::module& m) {
           return pw_stream_on() && (C == 64 || C == 128) && C <= cmax && cout % 8 == 0 && M % 32 == 0 &&
                  dpe_pw_rowgroups(M, cout, C, dpe::PW_FWD) > 0;
         }, py::arg("x_shape"), py::arg("cout"));
+  m.def("gram_ok", [](std::vector<int64_t> h2shape, int64_t cout3, int64_t next_width) {
+          // BN3 by Gram algebra for a bottleneck whose conv3 input is h2 [N, H, W, C2] (bngram.hip): conv3's
+          // forward with the BN3 + residual + ReLU epilogue on the streaming kernel (PW_APPLY), its data
+          // grad as the concatenated-K LDS-DMA GEMM, and the next block's conv1 data grad (K = next_width ->
+          // cout3) emitting the sum-dz partials (PW_DSUM)
+          if (h2shape.size() != 4 || !pw_stream_on()) return false;
+          const int64_t M = h2shape[0] * h2shape[1] * h2shape[2], C2 = h2shape[3];
+          if (C2 != 64 && C2 != 128 && C2 != 256) return false;
+          if (cout3 % 128 || M % 32) return false;
+          return dpe_pw_rowgroups(M, cout3, C2, dpe::PW_APPLY) > 0 &&
+                 dpe_pw_rowgroups(M, cout3, next_width, dpe::PW_DSUM) > 0;
+        }, py::arg("h2_shape"), py::arg("cout3"), py::arg("next_width"));
   m.def("pw_dgrad_strided_residual_ok", [](std::vector<int64_t> xshape, int64_t k) {
           // a downsample block's conv1 data grad (1x1, K = k -> N = xshape[3]) on the streaming kernel,
           // which can take the stride-2 branch's compact data grad as its residual
@@ -1528,15 +1693,29 @@ void register_ops(pybind11::module& m) {
                             std::vector<int64_t> pad, std::vector<int64_t> dil, const c10::optional<Tensor>& residual,
                             const c10::optional<Tensor>& bn_x, const c10::optional<Tensor>& bn_coef,
                             const c10::optional<Tensor>& bn_mask, const c10::optional<Tensor>& residual_mask,
-                            bool residual_stride2) {
+                            bool residual_stride2, const c10::optional<Tensor>& sum_mask) {
           return conv_dgrad_impl(dy, w, xshape, stride, pad, dil, residual, bn_x, bn_coef, nullptr, bn_mask, residual_mask,
-                                 residual_stride2);
+                                 residual_stride2, sum_mask);
         }, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"),
         py::arg("pad"), py::arg("dil"), py::arg("residual") = py::none(), py::arg("bn_x") = py::none(),
         py::arg("bn_coef") = py::none(), py::arg("bn_mask") = py::none(), py::arg("residual_mask") = py::none(),
-        py::arg("residual_stride2") = false,
+        py::arg("residual_stride2") = false, py::arg("sum_mask") = py::none(),
         "data grad; with bn_x/bn_coef also the BN-backward partials of the BN+ReLU that produced the conv input; "
         "with bn_mask (BN + residual + ReLU) the mask is bn_mask > 0 and dx is stored masked");
+  m.def("bn_gram", &bn_gram, py::arg("x"), py::arg("coef") = py::none(),
+        "(G = a2^T a2, s = colsum(a2)) of a2 = relu(x * coef[0] + coef[1]) (or x), fp32, deterministic");
+  m.def("bn_gram_coef", &bn_gram_coef, py::arg("G"), py::arg("s"), py::arg("w"), py::arg("M"), py::arg("gamma"),
+        py::arg("beta"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
+        "BN coefficients [4][Cout] of the never-computed h = a2 W^T from (G, s), and u = W G");
+  m.def("conv1x1_apply", &conv1x1_apply, py::arg("x"), py::arg("w"), py::arg("in_coef"), py::arg("out_coef"),
+        py::arg("residual"), py::arg("res_coef") = py::none(),
+        "y = relu(BN(x' W^T) + residual [BN_d]) and its ReLU bits (pre-BN tensor never stored)");
+  m.def("bn_gram_bwd", &bn_gram_bwd, py::arg("part"), py::arg("P"), py::arg("w"), py::arg("u"), py::arg("s"),
+        py::arg("coef"), py::arg("gamma"), py::arg("M"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dw"),
+        "BN3 backward from (sum dz partials, P = dz^T a2): dgamma/dbeta/dw +=, returns (B_cat bf16, bias)");
+  m.def("conv1x1_dgrad_cat", &conv1x1_dgrad_cat, py::arg("dz"), py::arg("a2src"), py::arg("a2_coef"), py::arg("bcat"),
+        py::arg("e"), py::arg("bn_x"), py::arg("bn_coef"),
+        "[dz | a2] x bcat + e with the BN2-backward partials (concatenated-K data grad)");
   m.def("bn_bwd_coef", &bn_bwd_coef, py::arg("partials"), py::arg("M"), py::arg("gamma"), py::arg("coef"),
         py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none(),
         "BN-backward coefficients [3][C] from the dgrad-epilogue partials (no apply pass); dgamma/dbeta +=");

@@ -34,6 +34,9 @@ enum AXform : int {
   AX_BN_RES = 1,   // relu(A * s[k] + t[k] + a2)                  a_coef = [scale | shift] (BN forward coef [4][K])
   AX_BN_RES2 = 2,  // relu(A * s[k] + t[k] + bf16(a2 * s2[k] + t2[k]))   + a_coef2 (the downsample BN's)
   AX_BN_BWD = 3,   // a[k] * A + b[k] * a2 + c[k]                  a_coef = [a | b | c] (BN backward coef [3][K])
+  AX_CAT = 4,      // concatenated K: columns [0, k1) of A are A[m][k] (lda), columns [k1, K) are
+                   // a2[m][k - k1] (lda2), relu(a2 * s[k-k1] + t[k-k1]) when a_coef = [s | t] is given
+                   // (nothing stored; the Gram-algebra data grad [dz3 | a2] x [diag(a) W3 ; Q], bngram.hip)
 };
 
 struct ConvGeom {
@@ -88,6 +91,8 @@ struct IgemmArgs {
   const float* a_coef2;     // AX_BN_RES2: the second BatchNorm's forward coefficients [4][K]
   uint16_t* a_out;          // [M][lda] the transformed A, written by the tn == 0 blocks (required)
   uint8_t* a_bits;          // [M][lda/8] ReLU-mask bits of a_out (AX_BN_RES / _RES2), or nullptr
+  int k1;                   // AX_CAT: K of the first segment (multiple of 32)
+  int64_t lda2;             // AX_CAT: row stride of a2
 };
 
 }  // namespace dpe

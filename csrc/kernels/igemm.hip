@@ -732,12 +732,15 @@ DPE_DEVICE void wait_vm() {
 // also store the transformed A (and its ReLU-mask bits): the standalone pass that wrote it before
 // read the same two tensors, so the consumer's own read of it is what disappears.
 template <int BM, int BN, int WGM, int WGN, int BL, int EPI, int NS = DSTAGES, int AX = AX_NONE>
-__global__ __launch_bounds__(64 * WGM * WGN, ((BM == 256 && BN == 128) || (DPE_DMA_OCC4 && WGM * WGN == 4)) ? 4 : 1)
+// (AX_CAT 128x128: 3 blocks per CU -- at 128 VGPRs its two-segment loader spilled 27 registers)
+__global__ __launch_bounds__(64 * WGM * WGN, ((BM == 256 && BN == 128) || (DPE_DMA_OCC4 && WGM * WGN == 4))
+                                                 ? ((AX == AX_CAT && BN == 128) ? 3 : 4) : 1)
 void igemm_dma_kernel(IgemmArgs p, int a_dense) {
   constexpr int NTH = 64 * WGM * WGN, NW = WGM * WGN;
   constexpr bool BKc = (BL == B_DENSE_K);
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  constexpr int A2_BYTES = AX ? A_BYTES : 0;
+  constexpr bool CAT = AX == AX_CAT;
+  constexpr int A2_BYTES = (AX && !CAT) ? A_BYTES : 0;
   static_assert(AX == AX_NONE || NS == 2, "A transform: 2-stage ring");
   constexpr int STAGE = A_BYTES + A2_BYTES + B_BYTES;
   constexpr int CROW = BN * 2 + 16;
@@ -796,7 +799,19 @@ void igemm_dma_kernel(IgemmArgs p, int a_dense) {
   const int64_t apre = a_dense ? 0 : ((int64_t)g.ph * g.W + g.pw) * g.C;
   const int64_t abytes = a_dense ? (int64_t)p.M * p.lda * 2 : ((int64_t)g.N * g.H * g.W * g.C + apre) * 2;
   const __amdgpu_buffer_rsrc_t ar = dma_rsrc(p.A - apre, (uint32_t)abytes);
-  const __amdgpu_buffer_rsrc_t ar2 = dma_rsrc(AX ? p.a2 : p.A, (uint32_t)abytes);
+  const __amdgpu_buffer_rsrc_t ar2 =
+      CAT ? dma_rsrc(p.a2, (uint32_t)((int64_t)p.M * p.lda2 * 2)) : dma_rsrc(AX ? p.a2 : p.A, (uint32_t)abytes);
+  // AX_CAT: the second segment's per-piece row offsets (dense rows, lda2)
+  uint32_t aoff2[CAT ? PA : 1];
+  if constexpr (CAT) {
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const int row = (wid * PA + i) * 16 + (lane >> 2);
+      const int lc = (lane & 3) ^ ((0x78 >> (((row >> 2) & 3) << 1)) & 3);
+      const int m = m0 + row;
+      aoff2[i] = m < p.M ? (uint32_t)m * (uint32_t)p.lda2 * 2u + lc * 16 : DMA_OOB;
+    }
+  }
 
   // ---- B: per-piece offsets, fixed for the loop (validity never changes along K)
   uint32_t boff[PB];
@@ -851,8 +866,13 @@ void igemm_dma_kernel(IgemmArgs p, int a_dense) {
 #pragma unroll
       for (int i = 0; i < PA; ++i) {
         const uint32_t v = ((amask[i] >> tap) & 1u) ? aoff[i] : DMA_OOB;
-        dma16(ar, st + (wid * PA + i) * 1024, v, tapoff + ci * 2);
-        if constexpr (AX != AX_NONE) dma16(ar2, st + A_BYTES + (wid * PA + i) * 1024, v, tapoff + ci * 2);
+        if constexpr (CAT) {
+          if (ci < p.k1) dma16(ar, st + (wid * PA + i) * 1024, v, ci * 2);
+          else dma16(ar2, st + (wid * PA + i) * 1024, aoff2[i], (ci - p.k1) * 2);
+        } else {
+          dma16(ar, st + (wid * PA + i) * 1024, v, tapoff + ci * 2);
+          if constexpr (AX != AX_NONE) dma16(ar2, st + A_BYTES + (wid * PA + i) * 1024, v, tapoff + ci * 2);
+        }
       }
     }
 #pragma unroll
@@ -879,15 +899,35 @@ void igemm_dma_kernel(IgemmArgs p, int a_dense) {
   // A transform: the per-K-channel coefficient tables sit in (dynamic) LDS for the whole launch,
   // [NXC][K] floats (K <= 2048: <= 32 KiB, and the big-K shapes are the small-M ones); the lane
   // reads the 8 channels 32 t + 8 g .. +7 of each table per K-step (broadcast reads)
-  constexpr int NXC = AX == AX_BN_RES ? 2 : AX == AX_BN_BWD ? 3 : 4;
+  constexpr int NXC = (AX == AX_BN_RES || CAT) ? 2 : AX == AX_BN_BWD ? 3 : 4;
+  const int KT = CAT ? p.K - p.k1 : p.K;  // coefficient table length
   extern __shared__ __attribute__((aligned(16))) float ax_coef[];
   const int xg = (lane >> 4) * 8;
   // the waves holding output columns [0, BN/WGN) of the first N tile store the transformed A
-  const bool ax_store = AX != AX_NONE && tn == 0 && wn == 0;
+  const bool ax_store = AX != AX_NONE && !CAT && tn == 0 && wn == 0;
   const __amdgpu_buffer_rsrc_t aout_r = dma_rsrc(AX ? (const void*)p.a_out : p.A, (uint32_t)((int64_t)p.M * p.lda * 2));
   const __amdgpu_buffer_rsrc_t bits_r = dma_rsrc(AX ? (const void*)p.a_bits : p.A, (uint32_t)((int64_t)p.M * p.lda / 8));
+  auto xform_cat = [&](int t, bf16x8 (&a)[RM]) {
+    // second segment, BN + ReLU on load: relu(a2 * s[k - k1] + t[k - k1])
+    const int k = t * BK + xg - p.k1;
+    float c[2][8];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const f32x4 lo = *(const f32x4*)(ax_coef + q * KT + k), hi = *(const f32x4*)(ax_coef + q * KT + k + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { c[q][e] = lo[e]; c[q][e + 4] = hi[e]; }
+    }
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      float f[8];
+      unpack8(__builtin_bit_cast(u32x4, a[i]), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], c[0][e], c[1][e]), 0.f);
+      a[i] = __builtin_bit_cast(bf16x8, pack8(f));
+    }
+  };
   auto xform = [&](int t, bf16x8 (&a)[RM], const bf16x8 (&a2)[RM]) {
-    if constexpr (AX != AX_NONE) {
+    if constexpr (AX != AX_NONE && !CAT) {
       const int k = t * BK + xg;
       float c[NXC][8];
 #pragma unroll
@@ -933,14 +973,17 @@ void igemm_dma_kernel(IgemmArgs p, int a_dense) {
     }
   };
   // stores per K-step of a storing wave (the counted wait below)
-  constexpr int AX_ST = AX == AX_NONE ? 0 : AX == AX_BN_BWD ? RM : 2 * RM;
+  constexpr int AX_ST = (AX == AX_NONE || CAT) ? 0 : AX == AX_BN_BWD ? RM : 2 * RM;
   if constexpr (AX != AX_NONE) {
-    // tables: AX_BN_RES [scale | shift] = a_coef rows 0-1; AX_BN_BWD [a | b | c]; AX_BN_RES2 + a_coef2 rows 0-1
-    for (int i = tid; i < NXC * p.K; i += NTH) {
-      const int q = i / p.K, kk = i - q * p.K;
-      ax_coef[i] = (AX == AX_BN_RES2 && q >= 2) ? p.a_coef2[(q - 2) * p.K + kk] : p.a_coef[q * p.K + kk];
+    // tables: AX_BN_RES [scale | shift] = a_coef rows 0-1; AX_BN_BWD [a | b | c]; AX_BN_RES2 + a_coef2 rows 0-1;
+    // AX_CAT [scale | shift] of the second segment's K - k1 channels (rows 0-1 of its [4][K - k1] BN coef)
+    if (!CAT || p.a_coef) {
+      for (int i = tid; i < NXC * KT; i += NTH) {
+        const int q = i / KT, kk = i - q * KT;
+        ax_coef[i] = (AX == AX_BN_RES2 && q >= 2) ? p.a_coef2[(q - 2) * KT + kk] : p.a_coef[q * KT + kk];
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 
   auto read_frags = [&](int buf, bf16x8 (&a)[RM], bf16x8 (&b)[RN]) {
@@ -981,7 +1024,9 @@ void igemm_dma_kernel(IgemmArgs p, int a_dense) {
       if (t + NS - 1 < nt) issue((t + NS - 1) % NS);
       bf16x8 af[RM], bfr[RN];
       read_frags(t % NS, af, bfr);
-      if constexpr (AX != AX_NONE) {
+      if constexpr (CAT) {
+        if (p.a_coef && t * BK >= p.k1) xform_cat(t, af);
+      } else if constexpr (AX != AX_NONE) {
         bf16x8 a2f[RM];
         const char* A2s = smem + (t % NS) * STAGE + A_BYTES;
 #pragma unroll
@@ -1240,6 +1285,24 @@ extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int a
   if (abytes >= lim || bbytes >= lim) return -1;
   const int tiles = ((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
   const int dn = dense ? 1 : 0;
+  if (a.a_mode == AX_CAT) {
+    // concatenated-K data grad: A segments dense, K1 = k1 from A (lda), K - k1 from a2 (lda2)
+    if (!dense || !a.a2 || a.k1 <= 0 || a.k1 % 32 || a.k1 >= a.K || a.lda < a.k1 || a.lda2 < a.K - a.k1 ||
+        a.lda2 % 8 || (int64_t)a.M * a.lda2 * 2 >= lim || a.K - a.k1 > 2048)
+      return -1;
+#define DPE_DMA_CAT(BM_, BN_, WGM_, WGN_, BL_, EP_)                                                         \
+  if (bm == BM_ && bn == BN_ && bload == BL_ && epi == EP_) {                                               \
+    hipLaunchKernelGGL((igemm_dma_kernel<BM_, BN_, WGM_, WGN_, BL_, EP_, 2, AX_CAT>), dim3(tiles),          \
+                       dim3(64 * WGM_ * WGN_), a.a_coef ? (size_t)2 * (a.K - a.k1) * 4 : 0, st, a, dn);     \
+    return 0;                                                                                               \
+  }
+    DPE_DMA_CAT(128, 64, 2, 2, B_DENSE_N, EPI_BF16_BNB)
+    DPE_DMA_CAT(128, 128, 2, 2, B_DENSE_N, EPI_BF16_BNB)
+    DPE_DMA_CAT(128, 64, 2, 2, B_DENSE_N, EPI_BF16)
+    DPE_DMA_CAT(128, 128, 2, 2, B_DENSE_N, EPI_BF16)
+#undef DPE_DMA_CAT
+    return -1;
+  }
   if (a.a_mode != AX_NONE) {
     // A on-load transform: dense A with lda == K (the by-product is a whole [M][K] tensor)
     if (!dense || a.lda != a.K || !a.a2 || !a.a_coef || !a.a_out) return -1;

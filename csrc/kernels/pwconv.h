@@ -8,6 +8,9 @@ namespace dpe {
 enum PwEpi : int {
   PW_FWD = 0,    // y = x . W^T; stats = BatchNorm-forward (sum, sum of squares) of the stored y
   PW_DGRAD = 1,  // y = x . W (+ residual [masked]); stats = BatchNorm-backward (sum dz, sum dz*(st_x - mean))
+  PW_APPLY = 2,  // y = relu(BN(x . W^T) + residual): out_coef = the BN's [4][N] coefficients, known before the
+                 // conv (Gram algebra, bngram.hip); the pre-BN tensor is never stored; out_bits = ReLU bits of y
+  PW_DSUM = 3,   // PW_DGRAD with st_mask and no st_x: stats row 0 = sum dz only (row 1 left unwritten)
 };
 
 struct PwArgs {
@@ -25,6 +28,9 @@ struct PwArgs {
   const float* in_coef;      // PW_FWD: x is the pre-BN tensor; the operand is relu(x * in_coef[k] + in_coef[K + k])
   int res_h, res_w;          // PW_DGRAD, > 0: y is an [*, res_h, res_w] image and the residual is the compact
                              // [*, res_h/2, res_w/2] grid of a stride-2 1x1 conv's data grad, added at even (h, w) only
+  const float* out_coef;     // PW_APPLY: [4][N] BN coefficients (scale, shift, ...) applied to the conv output
+  const float* res_coef;     // PW_APPLY: the residual is BN'd first: bf16(residual * res_coef[n] + res_coef[N + n])
+  uint8_t* out_bits;         // PW_APPLY: ReLU bits of y ([M][N/8]), or nullptr
 };
 
 }  // namespace dpe

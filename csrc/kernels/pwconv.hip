@@ -75,6 +75,8 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
   __shared__ __attribute__((aligned(16))) char smem[NS * TILE + 4 * STG];
   __shared__ __attribute__((aligned(16))) float bnin[2 * K];  // in_coef: [scale | shift] of the K input channels
 
+  // PW_DSUM: the data grad's BN-backward partials are the sums of dz only (no pre-BN input)
+  constexpr bool DG = EPI == PW_DGRAD || EPI == PW_DSUM;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int M = (int)a.M, N = (int)a.N, RG = a.rg;
@@ -93,7 +95,7 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       const int n = n0w + 16 * ni + li, k0 = 32 * kc + 8 * g;
-      if constexpr (EPI == PW_FWD) {
+      if constexpr (!DG) {
         wf[ni][kc] = __builtin_bit_cast(bf16x8, *(const u32x4*)(a.w + (int64_t)n * K + k0));
       } else {  // W stored [K][N]: gather the column (once per block)
         s16x8 v;
@@ -104,8 +106,9 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
     }
   // BatchNorm-backward coefficients of the lane's 8 channels
   float bsc[8], bsh[8], bmu[8];
-  const bool bnb = EPI == PW_DGRAD && a.st_x != nullptr;
-  if (bnb) {
+  const bool bnb = EPI == PW_DSUM || (EPI == PW_DGRAD && a.st_x != nullptr);
+  const bool bnx = EPI == PW_DGRAD && a.st_x != nullptr;
+  if (bnx) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       bsc[e] = a.st_coef[nch + e];
@@ -138,6 +141,17 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
   float s[8], ss[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
+  // PW_APPLY: the BN applied to this lane's 8 output channels (+ the residual's own BN)
+  float osc[8], osh[8], rsc[8], rsh[8];
+  if constexpr (EPI == PW_APPLY) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      osc[e] = a.out_coef[nch + e];
+      osh[e] = a.out_coef[N + nch + e];
+      rsc[e] = a.res_coef ? a.res_coef[nch + e] : 1.f;
+      rsh[e] = a.res_coef ? a.res_coef[N + nch + e] : 0.f;
+    }
+  }
   // residual element offset of output row m (chunk nch); -1: no residual term at this row (the odd
   // positions of a stride-2 downsample branch's compact data grad)
   const int rh = a.res_h, rw = a.res_w;
@@ -148,7 +162,7 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
     return ((int64_t)(n * (rh >> 1) + (h >> 1)) * (rw >> 1) + (w >> 1)) * N + nch;
   };
 
-  if (EPI == PW_FWD && a.in_coef) {  // before the ring's first DMA (its counted waits start after this)
+  if (!DG && a.in_coef) {  // before the ring's first DMA (its counted waits start after this)
     for (int i = tid; i < 2 * K; i += 256) bnin[i] = a.in_coef[i];
     __syncthreads();
   }
@@ -176,7 +190,7 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
     // in the epilogue they stalled each half for a full HBM round trip).  They are older than the
     // stage's DMAs, so the compiler's wait for them leaves the ring's counted vmcnt intact.  The
     // wider-WN tiles have no registers for it (they would spill).
-    constexpr bool HOIST = (EPI == PW_DGRAD) && (WN == 32);
+    constexpr bool HOIST = (EPI != PW_FWD) && (WN == 32);
     constexpr int HN = HOIST ? NPS : 1;
     const int m0 = (rg + j * RG) * BM;
     u32x4 hrv[2][HN], hxv[2][HN];
@@ -189,12 +203,14 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
           const int m = min(m0 + 32 * hf + ps * RPP + lane / CPRW, M - 1);
           const int64_t off = (int64_t)m * N + nch;
           if (a.residual) {
-            const int64_t ro = res_off(m);
+            const int64_t ro = EPI == PW_APPLY ? off : res_off(m);
             hrv[hf][ps] = ro >= 0 ? *(const u32x4*)(a.residual + ro) : u32x4{0u, 0u, 0u, 0u};
           }
-          hrmb[hf][ps] = a.res_mask ? (uint32_t)a.res_mask[off >> 3] : 0xffu;
-          if (bnb) hxv[hf][ps] = *(const u32x4*)(a.st_x + off);
-          hsmb[hf][ps] = (bnb && a.st_mask) ? (uint32_t)a.st_mask[off >> 3] : 0xffu;
+          if constexpr (DG) {
+            hrmb[hf][ps] = a.res_mask ? (uint32_t)a.res_mask[off >> 3] : 0xffu;
+            if (bnx) hxv[hf][ps] = *(const u32x4*)(a.st_x + off);
+            hsmb[hf][ps] = (bnb && a.st_mask) ? (uint32_t)a.st_mask[off >> 3] : 0xffu;
+          }
         }
     }
     if (j + NS - 1 < nt) issue(rg + (j + NS - 1) * RG, (j + NS - 1) % NS);
@@ -249,7 +265,7 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
           rmb[ps] = hrmb[hf][ps];
           smb[ps] = hsmb[hf][ps];
         }
-      } else if constexpr (EPI == PW_DGRAD) {
+      } else if constexpr (DG) {
 #pragma unroll
         for (int ps = 0; ps < NPS; ++ps) {
           const int m = min(m0 + 32 * hf + ps * RPP + lane / CPRW, M - 1);
@@ -259,7 +275,7 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
             rv[ps] = ro >= 0 ? *(const u32x4*)(a.residual + ro) : u32x4{0u, 0u, 0u, 0u};
           }
           rmb[ps] = a.res_mask ? (uint32_t)a.res_mask[off >> 3] : 0xffu;
-          if (bnb) xv[ps] = *(const u32x4*)(a.st_x + off);
+          if (bnx) xv[ps] = *(const u32x4*)(a.st_x + off);
           smb[ps] = (bnb && a.st_mask) ? (uint32_t)a.st_mask[off >> 3] : 0xffu;
         }
       }
@@ -282,7 +298,20 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
         const bool valid = m < M;
         float f[8];
         unpack8(v, f);
-        if constexpr (EPI == PW_FWD) {
+        if constexpr (EPI == PW_APPLY) {
+          // y = relu(v * scale + shift + residual) from the rounded conv output v, as bn_apply /
+          // bn_apply2 compute it from the stored pre-BN tensor (a BN'd residual rounded to bf16 first)
+          float r[8];
+          if (a.residual) unpack8(rv[ps], r);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float t = fmaf(f[e], osc[e], osh[e]);
+            if (a.residual) t += a.res_coef ? bf2f(f2bf(fmaf(r[e], rsc[e], rsh[e]))) : r[e];
+            f[e] = fmaxf(t, 0.f);
+          }
+          v = pack8(f);
+          if (valid && a.out_bits) a.out_bits[((int64_t)m * N + nch) >> 3] = relu_mask_byte(v);
+        } else if constexpr (EPI == PW_FWD) {
           // statistics of the stored (rounded) values (rows past M: zeros, or relu(shift) terms
           // with in_coef -- masked)
           const float vm = valid ? 1.f : 0.f;
@@ -303,13 +332,13 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
           }
           if (bnb && valid) {  // (sum dz, sum dz*(x - mean)), dz = v * relu'(BN output)
             float x8[8];
-            unpack8(xv[ps], x8);
+            if (bnx) unpack8(xv[ps], x8);
             if (a.st_mask) {
 #pragma unroll
               for (int e = 0; e < 8; ++e) {
                 f[e] = ((smb[ps] >> e) & 1u) ? f[e] : 0.f;
                 s[e] += f[e];
-                ss[e] = fmaf(f[e], x8[e] - bmu[e], ss[e]);
+                if (bnx) ss[e] = fmaf(f[e], x8[e] - bmu[e], ss[e]);
               }
               v = pack8(f);  // the stored gradient is dz itself
             } else {
@@ -328,7 +357,7 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
   }
   // statistics: reduce over the lanes holding the same channel chunk (lane = row * CPRW + ch),
   // one partial column per row group
-  if (a.stats) {
+  if (EPI != PW_APPLY && a.stats) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
 #pragma unroll
@@ -341,7 +370,7 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         a.stats[(int64_t)(nch + e) * RG + rg] = s[e];
-        a.stats[(int64_t)(N + nch + e) * RG + rg] = ss[e];
+        if (EPI != PW_DSUM) a.stats[(int64_t)(N + nch + e) * RG + rg] = ss[e];
       }
     }
   }
@@ -371,6 +400,8 @@ extern "C" int dpe_cu_reserve();  // comm.cpp
 #define DPE_PW128_FWD_WN 64
 #endif
 static int pw_wn(int K, int epi) {
+  if (epi == PW_APPLY) return 32;  // epilogue operand (the residual) hoisted ahead of the MFMAs, as the data grads
+  if (epi == PW_DSUM) epi = PW_DGRAD;
   if (K == 64) return epi == PW_DGRAD ? DPE_PW64_DGRAD_WN : DPE_PW64_FWD_WN;
   if (K == 128) return epi == PW_FWD ? DPE_PW128_FWD_WN : 32;
   return 32;
@@ -392,21 +423,30 @@ static int pw_slots() {
 }
 template <int EPI>
 static int pw_capacity(int K) {
-  if (K == 64) return EPI == PW_FWD ? pw_slots<64, DPE_PW64_FWD_WN, 4, EPI>() : pw_slots<64, DPE_PW64_DGRAD_WN, 4, EPI>();
-  if (K == 128) return EPI == PW_FWD ? pw_slots<128, DPE_PW128_FWD_WN, 3, EPI>() : pw_slots<128, 32, 3, EPI>();
-  return pw_slots<256, 32, 2, EPI>();
+  if constexpr (EPI == PW_APPLY || EPI == PW_DSUM) {
+    if (K == 64) return pw_slots<64, 32, 4, EPI>();
+    if (K == 128) return pw_slots<128, 32, 3, EPI>();
+    return pw_slots<256, 32, 2, EPI>();
+  } else {
+    if (K == 64) return EPI == PW_FWD ? pw_slots<64, DPE_PW64_FWD_WN, 4, EPI>() : pw_slots<64, DPE_PW64_DGRAD_WN, 4, EPI>();
+    if (K == 128) return EPI == PW_FWD ? pw_slots<128, DPE_PW128_FWD_WN, 3, EPI>() : pw_slots<128, 32, 3, EPI>();
+    return pw_slots<256, 32, 2, EPI>();
+  }
 }
 
 extern "C" int dpe_pw_rowgroups(int64_t M, int64_t N, int64_t K, int epi) {
   if (K != 64 && K != 128 && K != 256) return 0;
-  if (epi != PW_FWD && epi != PW_DGRAD) return 0;
+  if (epi != PW_FWD && epi != PW_DGRAD && epi != PW_APPLY && epi != PW_DSUM) return 0;
   const int bnb = 4 * pw_wn((int)K, epi);
   if (N % bnb || N < 2 * K) return 0;  // write-heavy shapes only (N >= 2K)
   if (M * K * 2 >= (1ll << 31) - 4096 || M * N >= (1ll << 31)) return 0;
   const int64_t tiles = (M + pw::BM - 1) / pw::BM;
   const int64_t nbN = N / bnb;
   // resident capacity minus the slots left to in-flight RCCL channel blocks (comm.cpp CU budget)
-  const int cap = (epi == PW_FWD ? pw_capacity<PW_FWD>((int)K) : pw_capacity<PW_DGRAD>((int)K)) - dpe_cu_reserve();
+  const int cap = (epi == PW_FWD ? pw_capacity<PW_FWD>((int)K)
+                                 : epi == PW_APPLY ? pw_capacity<PW_APPLY>((int)K)
+                                 : epi == PW_DSUM  ? pw_capacity<PW_DSUM>((int)K) : pw_capacity<PW_DGRAD>((int)K)) -
+                  dpe_cu_reserve();
   int64_t rg = cap / nbN;  // one resident wave of blocks over the whole launch
   if (rg < 1) rg = 1;
   if (rg > tiles) rg = tiles;
@@ -418,7 +458,19 @@ extern "C" int dpe_pw_launch(const PwArgs* args, int epi, hipStream_t st) {
   if (a.rg <= 0 || a.rg != dpe_pw_rowgroups(a.M, a.N, a.K, epi)) return -1;
   if (epi == PW_FWD && (a.residual || a.st_x)) return -1;
   if (a.st_x && !a.st_coef) return -1;
-  if (a.res_h > 0 && (epi != PW_DGRAD || a.res_mask || a.res_h % 2 || a.res_w % 2 || a.M % ((int64_t)a.res_h * a.res_w)))
+  if (epi == PW_DSUM && (a.st_x || !a.st_mask || !a.stats)) return -1;
+  if (epi == PW_APPLY && (!a.out_coef || a.st_x || a.stats || a.res_h > 0 || (a.res_coef && !a.residual))) return -1;
+  if (epi == PW_APPLY || epi == PW_DSUM) {
+    const dim3 grid_a((unsigned)(a.rg * (a.N / 128))), blk(256);
+#define PW_L2(E_)                                                                                        \
+    if (a.K == 64) hipLaunchKernelGGL((pw::pw_stream_kernel<64, 32, 4, E_>), grid_a, blk, 0, st, a);       \
+    else if (a.K == 128) hipLaunchKernelGGL((pw::pw_stream_kernel<128, 32, 3, E_>), grid_a, blk, 0, st, a); \
+    else hipLaunchKernelGGL((pw::pw_stream_kernel<256, 32, 2, E_>), grid_a, blk, 0, st, a);
+    if (epi == PW_APPLY) { PW_L2(PW_APPLY) } else { PW_L2(PW_DSUM) }
+#undef PW_L2
+    return 0;
+  }
+  if (a.res_h > 0 && ((epi != PW_DGRAD && epi != PW_DSUM) || a.res_mask || a.res_h % 2 || a.res_w % 2 || a.M % ((int64_t)a.res_h * a.res_w)))
     return -1;
   const int nbN = (int)(a.N / (4 * pw_wn((int)a.K, epi)));
   const dim3 grid((unsigned)(a.rg * nbN)), block(256);

@@ -100,6 +100,13 @@ _AX_BWD_MAXC = int(os.environ.get("DPE_AX_BWD_MAXC", "512"))
 # row tile of the on-load forward at 64 output channels (128: 4 blocks/CU, 256: 2; the
 # downsample-identity form spills at 128)
 _AX_TILE = int(os.environ.get("DPE_AX_TILE", "256"))
+# DPE_BN3_GRAM=1: BN3 by Gram algebra (csrc/kernels/bngram.hip).  h3 = a2 W3^T is linear in a2, so BN3's
+# statistics come from G = a2^T a2 and s = colsum(a2) BEFORE conv3 runs: conv3's epilogue writes the
+# block output relu(BN3(h3) + idn) directly (no h3 tensor, no bn_apply pass), and the backward needs
+# neither h3 nor dh3 (dW3 = diag(a) dz3^T a2 + diag(b) W3 G + c s^T; da2 = [dz3 | a2] x [diag(a) W3 ; Q]),
+# so there is no bn_bwd_apply pass and the next block's data-grad epilogue reads no h3.  For blocks whose
+# conv3 runs on the streaming pointwise kernel and whose successor chains BN3's backward.
+_GRAM = _BN3_CHAIN and os.environ.get("DPE_BN3_GRAM", "1") != "0"
 
 
 def _ax_ok(conv, cin) -> bool:
@@ -124,11 +131,12 @@ class _BN3Link:
     fused-epilogue result (BN3_i partials, identity of the masked dz3_i)
     handed back to block i's backward."""
 
-    __slots__ = ("h3", "coef", "mask", "part", "dz_ptr", "dz_shape", "pending")
+    __slots__ = ("h3", "coef", "mask", "part", "dz_ptr", "dz_shape", "pending", "gram")
 
     def __init__(self):
         self.h3 = self.coef = self.mask = self.part = None
         self.dz_ptr, self.dz_shape = 0, None
+        self.gram = False  # block i ran BN3 by Gram algebra: block i+1's epilogue emits only the sum-dz partials
         # (h3, coef3, idn, idn_coef, out, bits): block i's output, allocated but not yet written --
         # block i+1's conv1 writes it (conv1x1_bnin_fwd)
         self.pending = None
@@ -140,7 +148,7 @@ def _conv_conf(conv):
 
 class BottleneckFn(Function):
     @staticmethod
-    def forward(ctx, x, block, link_in, link_out, defer_out, *params):
+    def forward(ctx, x, block, link_in, link_out, defer_out, gram_next, *params):
         C = ext()
         convs = [block.c1, block.c2, block.c3] + ([block.down] if block.down is not None else [])
         ws = [shadow(cb.conv.weight) for cb in convs]
@@ -207,8 +215,27 @@ class BottleneckFn(Function):
                                     bn2.running_var, bn2.momentum, bn2.eps, True, None, st2)
         # the next block's fused data-grad epilogue reads this output's ReLU mask as bits
         want_bits = True  # 1/16 of out: read by the next block's fused epilogue or by this block's BN3 backward
-        h3, c3 = conv_coef(2, h2, c2) if a2 is None else conv_coef(2, a2)
-        if defer_out and link_out is not None:
+        gram = None
+        if (gram_next and link_out is not None and not defer_out and h1_st is None
+                and C.gram_ok(list(h2.shape), convs[2].conv.out_channels, gram_next)):
+            # BN3 statistics from G = a2^T a2, s = colsum(a2); conv3 writes relu(BN3(h3) + idn) directly
+            src, src_coef = (h2, c2) if a2 is None else (a2, None)
+            G, sv = C.bn_gram(src, src_coef)
+            bn3 = convs[2].bn
+            M3 = h2.numel() // h2.shape[-1]
+            c3, u3 = C.bn_gram_coef(G, sv, ws[2], M3, bn3.weight.detach(), bn3.bias.detach(), bn3.running_mean,
+                                    bn3.running_var, bn3.momentum, bn3.eps)
+            if block.down is not None:
+                out, bits = C.conv1x1_apply(src, ws[2], src_coef, c3, hd, cd)
+            else:
+                out, bits = C.conv1x1_apply(src, ws[2], src_coef, c3, x, None)
+            h3 = None
+            gram = (u3, sv, M3)
+        else:
+            h3, c3 = conv_coef(2, h2, c2) if a2 is None else conv_coef(2, a2)
+        if gram is not None:
+            pass
+        elif defer_out and link_out is not None:
             # written later by the next block's conv1 (conv1x1_bnin_fwd): no bn_apply pass
             out = torch.empty_like(h3)
             bits = torch.empty(*h3.shape[:-1], h3.shape[-1] // 8, dtype=torch.uint8, device=h3.device)
@@ -225,12 +252,17 @@ class BottleneckFn(Function):
         strided_ok = block.down is not None and _DOWN_CHAIN and tuple(block.down.conv.stride) == (2, 2) and \
             tuple(block.down.conv.kernel_size) == (1, 1) and tuple(convs[0].conv.stride) == (1, 1) and \
             C.pw_dgrad_strided_residual_ok(list(x.shape), convs[0].conv.out_channels)
-        ctx.link_in = (link_in if (link_in is not None and (block.down is None or strided_ok) and link_in.h3 is not None
-                                   and link_in.mask is not None) else None)
+        ctx.link_in = (link_in if (link_in is not None and (block.down is None or strided_ok)
+                                   and (link_in.h3 is not None or link_in.gram) and link_in.mask is not None) else None)
+        if link_in is not None and link_in.gram:
+            # the previous block has no h3 and no standalone BN3 backward: this block must chain it
+            assert ctx.link_in is not None, "BN3 Gram path: the next block cannot chain the BN3 backward"
         ctx.link_out = link_out
         ctx.bits = bits  # ReLU mask of out as bits: the standalone BN3 backward reads these, not out
+        ctx.gram = gram
         if link_out is not None:
             link_out.h3, link_out.coef, link_out.mask = h3, c3, bits
+            link_out.gram = gram is not None
         ctx.block = block
         ctx.convs = convs
         ctx.ws = ws
@@ -300,7 +332,37 @@ class BottleneckFn(Function):
             return dh
 
         lk = ctx.link_out
-        if lk is not None and lk.part is not None and lk.dz_ptr == dout.data_ptr() and lk.dz_shape == tuple(dout.shape):
+        chained = (lk is not None and lk.part is not None and lk.dz_ptr == dout.data_ptr()
+                   and lk.dz_shape == tuple(dout.shape))
+        gram = ctx.gram
+        ctx.gram = None
+        if gram is not None:
+            # BN3 by Gram algebra: dz3 = dout came from the next block's epilogue with the sum-dz partials
+            assert chained, "BN3 Gram path: the block output's gradient did not come from the chained epilogue"
+            u3, sv, M3 = gram
+            dz3 = dout
+            src, src_coef = (h2, c2) if a2 is None else (a2, None)
+            w3 = convs[2].conv.weight
+            s3, p3, d3 = _conv_conf(convs[2].conv)
+            P = torch.zeros(w3.shape, dtype=torch.float32, device=w3.device)
+            C.conv_wgrad(dz3, src, P, s3, p3, d3, 1.0, src_coef)  # P = dz3^T a2
+            bn, gb, gd, bb, bd = bn_sinks(2)
+            wbuf, wdirect = grad_sink(w3)
+            bcat, ebias = C.bn_gram_bwd(lk.part, P, ws[2], u3, sv, c3, bn.weight.detach(), M3, gb, bb, wbuf)
+            bn_done(bn, gb, gd, bb, bd)
+            grad_done(w3, wdirect)
+            grads[id(w3)] = None if wdirect else wbuf
+            lk.part = None
+            lk.h3 = lk.coef = lk.mask = None
+            ctx.bits = None
+            # da2 = [dz3 | a2] x [diag(a) W3 ; W3^T diag(b) W3] + c W3, with BN2's backward partials
+            da2, part2 = C.conv1x1_dgrad_cat(dz3, src, src_coef, bcat, ebias, h2, c2)
+            bn, gb, gd, bb, bd = bn_sinks(1)
+            dh2 = C.bn_bwd_partials(da2, h2, bn.weight.detach(), c2, part2, gb, bb)
+            bn_done(bn, gb, gd, bb, bd)
+            return BottleneckFn._backward_tail(ctx, C, dz3, None, dh2, grads, bn_sinks, bn_done, bn_bwd, wgrad, dgrad,
+                                               dgrad_bnb)
+        if chained:
             # the next block's dgrad epilogue already produced dz3 = dout*relu'(out) and BN3's partials
             dz3 = dout
             bn, gb, gd, bb, bd = bn_sinks(2)
@@ -345,6 +407,15 @@ class BottleneckFn(Function):
             else:
                 wgrad(2, dh3, a2)
             dh2 = dgrad_bnb(2, dh3, 1, a2, h2, c2)  # (a2 unused: _EPI_BNB recomputes the mask from h2)
+        return BottleneckFn._backward_tail(ctx, C, dz3, res_mask, dh2, grads, bn_sinks, bn_done, bn_bwd, wgrad, dgrad,
+                                           dgrad_bnb, dhd)
+
+    @staticmethod
+    def _backward_tail(ctx, C, dz3, res_mask, dh2, grads, bn_sinks, bn_done, bn_bwd, wgrad, dgrad, dgrad_bnb, dhd=None):
+        """conv2 / conv1 / downsample gradients and dx, from dh2 (shared by the BN3 paths)."""
+        x, h1, a1, h2, a2, h3, out, hd, c1, c2, c3, cd = ctx.saved_tensors
+        convs, ws = ctx.convs, ctx.ws
+        has_down = len(convs) == 4
         if a1 is None:  # a1 = relu(BN1(h1)) recomputed on load by the row-walking weight grad
             wgrad(1, dh2, h1, c1)
         else:
@@ -361,7 +432,12 @@ class BottleneckFn(Function):
                 n, hh, ww, cin = x.shape
                 dxd = C.conv_dgrad(dhd, ws[3], [n, hh // 2, ww // 2, cin], [1, 1], [0, 0], [1, 1])  # compact
                 s, p, d = _conv_conf(convs[0].conv)
-                dx, part = C.conv_dgrad_bn(dh1, ws[0], list(x.shape), s, p, d, dxd, li.h3, li.coef, li.mask, None, True)
+                if li.gram:  # the previous block's BN3 runs by Gram algebra: only the sum-dz partials
+                    dx, part = C.conv_dgrad_bn(dh1, ws[0], list(x.shape), s, p, d, dxd, None, None, None, None, True,
+                                               li.mask)
+                else:
+                    dx, part = C.conv_dgrad_bn(dh1, ws[0], list(x.shape), s, p, d, dxd, li.h3, li.coef, li.mask, None,
+                                               True)
                 li.part, li.dz_ptr, li.dz_shape = part, dx.data_ptr(), tuple(dx.shape)
             elif has_down:
                 if dhd is None:
@@ -375,7 +451,11 @@ class BottleneckFn(Function):
             elif ctx.link_in is not None:
                 li = ctx.link_in
                 s, p, d = _conv_conf(convs[0].conv)
-                dx, part = C.conv_dgrad_bn(dh1, ws[0], list(x.shape), s, p, d, dz3, li.h3, li.coef, li.mask, res_mask)
+                if li.gram:
+                    dx, part = C.conv_dgrad_bn(dh1, ws[0], list(x.shape), s, p, d, dz3, None, None, None, res_mask, False,
+                                               li.mask)
+                else:
+                    dx, part = C.conv_dgrad_bn(dh1, ws[0], list(x.shape), s, p, d, dz3, li.h3, li.coef, li.mask, res_mask)
                 li.part, li.dz_ptr, li.dz_shape = part, dx.data_ptr(), tuple(dx.shape)
             else:
                 s, p, d = _conv_conf(convs[0].conv)
@@ -385,10 +465,25 @@ class BottleneckFn(Function):
                 dhd, _ = bn_bwd(3, dz3, None, hd, cd, False)
             wgrad(3, dhd, x)
         pgrads = [grads.get(id(p)) for p in ctx.block._fused_params]
-        return (dx, None, None, None, None, *pgrads)
+        return (dx, None, None, None, None, None, *pgrads)
 
 
-def bottleneck_forward(block, x, link_in=None, chain=False, count_batches=True, defer_out=False):
+def gram_successor_width(nxt) -> int:
+    """For the block before ``nxt``: nxt's conv1 width when nxt will chain the BN3 backward in the form
+    the Gram path needs (sum-dz partials from its conv1 data grad), else 0."""
+    if not _GRAM or nxt is None or not nxt.fused:
+        return 0
+    c1 = nxt.c1.conv
+    if tuple(c1.kernel_size) != (1, 1) or tuple(c1.stride) != (1, 1):
+        return 0
+    if nxt.down is not None:
+        d = nxt.down.conv
+        if not (_DOWN_CHAIN and tuple(d.stride) == (2, 2) and tuple(d.kernel_size) == (1, 1)):
+            return 0
+    return c1.out_channels
+
+
+def bottleneck_forward(block, x, link_in=None, chain=False, count_batches=True, defer_out=False, gram_next=0):
     """Fused block forward.  ``chain=True`` (the ResNet's own block loop, where
     this block's output feeds only the next block) returns ``(out, link)`` for
     the next block's ``link_in``.  ``count_batches=False``: the ResNet advanced
@@ -402,5 +497,5 @@ def bottleneck_forward(block, x, link_in=None, chain=False, count_batches=True, 
         torch._foreach_add_(nbt, 1)
     link_out = _BN3Link() if (chain and _BN3_CHAIN) else None
     out = BottleneckFn.apply(x, block, link_in if _BN3_CHAIN else None, link_out, bool(defer_out and link_out is not None),
-                             *params)
+                             int(gram_next) if link_out is not None else 0, *params)
     return (out, link_out) if chain else out

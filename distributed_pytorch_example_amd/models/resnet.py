@@ -59,7 +59,7 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         return self.forward_chained(x, None, chain=False)
 
-    def forward_chained(self, x, link=None, chain=True, count_batches=True, defer_out=False):
+    def forward_chained(self, x, link=None, chain=True, count_batches=True, defer_out=False, gram_next=0):
         """``chain=True``: returns (out, link); the link lets the next block's
         backward fuse this block's BN3 backward (``_resnet_fused``).
         ``count_batches=False``: the caller already advanced the BNs' num_batches_tracked.
@@ -67,7 +67,7 @@ class Bottleneck(nn.Module):
         if x.is_cuda and self.training and self.fused:
             from ._resnet_fused import bottleneck_forward
 
-            return bottleneck_forward(self, x, link, chain, count_batches, defer_out)
+            return bottleneck_forward(self, x, link, chain, count_batches, defer_out, gram_next)
         out = self._forward_per_op(x)
         return (out, None) if chain else out
 
@@ -137,8 +137,15 @@ class ResNet(nn.Module):
 
             defer = [f and i + 1 < len(fused) and fused[i + 1] and can_materialise_input(self.blocks[i + 1])
                      for i, f in enumerate(fused)]
-        for blk, f, d in zip(self.blocks, fused, defer):  # each block's output feeds only the next block
-            h, link = blk.forward_chained(h, link, count_batches=not f, defer_out=d)
+        # BN3 by Gram algebra (no h3 tensor, no BN3 apply passes) where the next block can chain its backward
+        gram = [0] * len(fused)
+        if any(fused):
+            from ._resnet_fused import gram_successor_width
+
+            gram = [gram_successor_width(self.blocks[i + 1]) if (f and i + 1 < len(fused) and fused[i + 1]) else 0
+                    for i, f in enumerate(fused)]
+        for blk, f, d, gn in zip(self.blocks, fused, defer, gram):  # each block's output feeds only the next block
+            h, link = blk.forward_chained(h, link, count_batches=not f, defer_out=d, gram_next=gn)
         h = Fx.global_avg_pool_nhwc(h)
         return self.fc(h)
 

@@ -415,6 +415,8 @@ class DistributedDataParallel(nn.Module):
         if not self._queued:
             self._queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+        if os.environ.get("DPE_WG_DEBUG") == "1":
+            print(f"[ddp] ready {i} {tuple(p.shape)}", flush=True)
         self.reducer.mark_ready(i)
 
     def _finalize(self):

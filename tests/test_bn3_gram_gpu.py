@@ -1,0 +1,186 @@
+"""BatchNorm-after-1x1-conv by Gram algebra (csrc/kernels/bngram.hip; the ResNet bottleneck's BN3).
+
+Each piece against a plain fp32/fp64 PyTorch reference of the same math, on random non-zero data with
+row tails: the Gram pass (G = a2^T a2, s = colsum(a2) of the BN + ReLU'd operand), the analytic BN3
+coefficients, the conv3 forward with the BN3 + residual + ReLU epilogue, the backward coefficient
+kernels (dgamma, dbeta, the dW3 correction, the concatenated-K data grad's B operand), the
+concatenated-K data grad itself, and finally a whole ResNet-50 step with the path on vs off.
+"""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from distributed_pytorch_example_amd.ops._ext import ext  # noqa: E402
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).norm() / (b.double().norm() + 1e-30)).item()
+
+
+def _bn_coef(mean, var, gamma, beta, eps):
+    invstd = 1.0 / torch.sqrt(var + eps)
+    sc = gamma * invstd
+    return torch.stack([sc, beta - mean * sc, mean, invstd]).float()
+
+
+def _operand(x, coef):
+    """a2 as the kernels feed it: relu(x * s + t) rounded to bf16 (or x itself)."""
+    if coef is None:
+        return x.float()
+    return torch.relu(x.float() * coef[0] + coef[1]).bfloat16().float()
+
+
+@pytest.mark.parametrize("C", [64, 128, 256])
+@pytest.mark.parametrize("with_coef", [True, False])
+def test_gram_and_coef(C, with_coef):
+    X = ext()
+    g = torch.Generator(device=DEV).manual_seed(C)
+    M = 32 * 97 + 11  # row tail (not a multiple of the 32-row tile)
+    x = torch.randn(M, C, device=DEV, generator=g).bfloat16()
+    coef = None
+    if with_coef:
+        coef = torch.stack([1 + 0.2 * torch.randn(C, device=DEV, generator=g), 0.5 * torch.randn(C, device=DEV, generator=g),
+                            torch.zeros(C, device=DEV), torch.ones(C, device=DEV)]).float()
+    G, s = X.bn_gram(x, coef)
+    a = _operand(x, coef).double()
+    Gr, sr = a.t() @ a, a.sum(0)
+    assert _rel(G, Gr) < 2e-5 and _rel(s, sr) < 2e-5, (_rel(G, Gr), _rel(s, sr))
+    assert torch.allclose(G, G.t())
+    # BN coefficients of h = a W^T without h: mean = w.s / M, E[h^2] = w^T G w / M
+    Cout = 4 * C
+    w = (torch.randn(Cout, 1, 1, C, device=DEV, generator=g) * C ** -0.5).bfloat16()
+    gamma = 1 + 0.1 * torch.randn(Cout, device=DEV, generator=g)
+    beta = 0.1 * torch.randn(Cout, device=DEV, generator=g)
+    rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+    coef3, u = X.bn_gram_coef(G, s, w, M, gamma, beta, rm, rv, 0.1, 1e-5)
+    h = a @ w.reshape(Cout, C).double().t()
+    mean, var = h.mean(0), h.var(0, unbiased=False)
+    ref = _bn_coef(mean, var, gamma.double(), beta.double(), 1e-5)
+    assert _rel(coef3, ref) < 1e-4, _rel(coef3, ref)
+    assert _rel(u, w.reshape(Cout, C).double() @ Gr) < 2e-5
+    assert _rel(rm, 0.1 * mean) < 1e-4 and _rel(rv, 0.9 + 0.1 * h.var(0, unbiased=True)) < 1e-4
+
+
+@pytest.mark.parametrize("K", [64, 128, 256])
+@pytest.mark.parametrize("down", [False, True])
+def test_conv1x1_apply(K, down):
+    """y = relu(BN3(bf16(a W^T)) + idn) (idn = bf16(BN_d(hd)) for a downsample block) and its ReLU bits."""
+    X = ext()
+    g = torch.Generator(device=DEV).manual_seed(K + down)
+    N, M = 4 * K, 64 * 50
+    x = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    cin = torch.stack([1 + 0.2 * torch.randn(K, device=DEV, generator=g), 0.3 * torch.randn(K, device=DEV, generator=g),
+                       torch.zeros(K, device=DEV), torch.ones(K, device=DEV)]).float()
+    w = (torch.randn(N, 1, 1, K, device=DEV, generator=g) * K ** -0.5).bfloat16()
+    cout = torch.stack([1 + 0.2 * torch.randn(N, device=DEV, generator=g), 0.3 * torch.randn(N, device=DEV, generator=g),
+                        torch.zeros(N, device=DEV), torch.ones(N, device=DEV)]).float()
+    res = torch.randn(M, N, device=DEV, generator=g).bfloat16()
+    rcoef = None
+    if down:
+        rcoef = torch.stack([1 + 0.2 * torch.randn(N, device=DEV, generator=g), 0.3 * torch.randn(N, device=DEV, generator=g),
+                             torch.zeros(N, device=DEV), torch.ones(N, device=DEV)]).float()
+    y, bits = X.conv1x1_apply(x, w, cin, cout, res, rcoef)
+    a = _operand(x, cin)
+    h = (a @ w.reshape(N, K).float().t()).bfloat16().float()
+    r = res.float() if rcoef is None else (res.float() * rcoef[0] + rcoef[1]).bfloat16().float()
+    ref = torch.relu(h * cout[0] + cout[1] + r)
+    assert _rel(y.float(), ref) < 5e-3, _rel(y.float(), ref)
+    pos = (y.float() > 0).reshape(M, N // 8, 8)
+    want = (pos.int() << torch.arange(8, device=DEV)).sum(-1).to(torch.uint8)
+    assert torch.equal(bits.reshape(M, N // 8), want)
+
+
+@pytest.mark.parametrize("C", [64, 128, 256])
+def test_gram_backward_and_cat_dgrad(C):
+    """BN3's backward from (sum dz, P = dz^T a2, G): dgamma, dbeta, dW3 against the fp64 autograd of
+    h = a W^T -> BN -> (. dz); the concatenated-K data grad [dz | a2] x B_cat + e against dh W3, with the
+    BN2-backward partials of its epilogue."""
+    X = ext()
+    g = torch.Generator(device=DEV).manual_seed(3 * C)
+    Cout, M = 4 * C, 128 * 40
+    h2 = torch.randn(M, C, device=DEV, generator=g).bfloat16()
+    c2 = torch.stack([1 + 0.2 * torch.randn(C, device=DEV, generator=g), 0.3 * torch.randn(C, device=DEV, generator=g),
+                      0.1 * torch.randn(C, device=DEV, generator=g), 1 + 0.1 * torch.rand(C, device=DEV, generator=g)]).float()
+    a = _operand(h2, c2).double()
+    w = (torch.randn(Cout, 1, 1, C, device=DEV, generator=g) * C ** -0.5).bfloat16()
+    W = w.reshape(Cout, C).double()
+    gamma = 1 + 0.1 * torch.randn(Cout, device=DEV, generator=g)
+    beta = 0.1 * torch.randn(Cout, device=DEV, generator=g)
+    G, s = X.bn_gram(h2, c2)
+    coef3, u = X.bn_gram_coef(G, s, w, M, gamma, beta, None, None, 0.1, 1e-5)
+    dz = torch.randn(M, Cout, device=DEV, generator=g).bfloat16()
+    # reference: autograd of BN over the exact h
+    Wr = W.clone().requires_grad_(True)
+    gr = gamma.double().clone().requires_grad_(True)
+    br = beta.double().clone().requires_grad_(True)
+    ar = a.clone().requires_grad_(True)
+    h = ar @ Wr.t()
+    mean, var = h.mean(0), h.var(0, unbiased=False)
+    y = (h - mean) / torch.sqrt(var + 1e-5) * gr + br
+    (y * dz.double()).sum().backward()
+    # ours: partials row 0 = column sums of dz (any row split), P = dz^T a2 (fp32)
+    part = torch.zeros(2, Cout, 3, device=DEV)
+    part[0, :, 0] = dz.float()[: M // 2].sum(0)
+    part[0, :, 2] = dz.float()[M // 2:].sum(0)
+    part[1] = float("nan")  # row 1 is never read (the sum-only epilogue leaves it unwritten)
+    P = (dz.double().t() @ a).float()
+    dg, db = torch.zeros(Cout, device=DEV), torch.zeros(Cout, device=DEV)
+    dw = torch.full((Cout, 1, 1, C), 0.25, device=DEV)
+    bcat, e = X.bn_gram_bwd(part, P, w, u, s, coef3, gamma, M, dg, db, dw)
+    assert _rel(dg, gr.grad) < 1e-4 and _rel(db, br.grad) < 1e-4, (_rel(dg, gr.grad), _rel(db, br.grad))
+    assert _rel(dw.reshape(Cout, C) - 0.25, Wr.grad) < 1e-3, _rel(dw.reshape(Cout, C) - 0.25, Wr.grad)
+    # data grad: da2 = dh W (exact) vs [dz | a2] x bcat + e
+    da_ref = ar.grad
+    da, p2 = X.conv1x1_dgrad_cat(dz, h2, c2, bcat, e, h2, c2)
+    assert _rel(da.float(), da_ref) < 2e-2, _rel(da.float(), da_ref)
+    # epilogue partials of BN2 + ReLU backward (mask from h2 * scale + shift > 0), of the stored da
+    dzb = da.float() * ((h2.float() * c2[0] + c2[1]) > 0)
+    s1 = dzb.sum(0)
+    s2 = (dzb * (h2.float() - c2[2])).sum(0)
+    assert _rel(p2[0].sum(-1), s1) < 1e-3 and _rel(p2[1].sum(-1), s2) < 1e-3
+    # materialised a2 (no coefficients on load): same result
+    da_m, _ = X.conv1x1_dgrad_cat(dz, _operand(h2, c2).bfloat16(), None, bcat, e, h2, c2)
+    assert _rel(da_m.float(), da.float()) < 1e-6
+
+
+def test_resnet50_step_gram_on_vs_off():
+    """A whole ResNet-50 training step (batch 8, 224^2) with the Gram path on vs off: every parameter
+    gradient and the loss agree to bf16 noise (the path changes summation orders and skips the
+    rounding of h3, not the math), and the BN running statistics agree."""
+    import distributed_pytorch_example_amd.models._resnet_fused as rf
+    from distributed_pytorch_example_amd.models import get_model
+    from distributed_pytorch_example_amd.ops import functional as Fx
+
+    torch.manual_seed(0)
+    base = get_model("resnet50").to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = torch.randn(8, 3, 224, 224, device=DEV, generator=g)
+    y = torch.randint(0, 1000, (8,), device=DEV, generator=g)
+    old = rf._GRAM
+    out = {}
+    try:
+        for on in (False, True):
+            rf._GRAM = on
+            m = copy.deepcopy(base)
+            loss = Fx.cross_entropy(m(x), y, 1000)
+            loss.backward()
+            torch.cuda.synchronize()
+            out[on] = (loss.item(), {n: p.grad.detach().clone() for n, p in m.named_parameters()},
+                       {n: b.detach().clone() for n, b in m.named_buffers() if b.dtype.is_floating_point})
+    finally:
+        rf._GRAM = old
+    (l0, g0, b0), (l1, g1, b1) = out[False], out[True]
+    assert abs(l0 - l1) / abs(l0) < 2e-3, (l0, l1)
+    errs = sorted(((_rel(g1[n], g0[n]), n) for n in g0), reverse=True)
+    print("\nworst gradient deviations gram on vs off:", [(n, f"{e:.2e}") for e, n in errs[:5]])
+    assert errs[0][0] < 5e-2, errs[:5]
+    berr = max(_rel(b1[n], b0[n]) for n in b0)
+    assert berr < 1e-3, berr
