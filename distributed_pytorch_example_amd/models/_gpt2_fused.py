@@ -58,6 +58,10 @@ _wq: list = []  # (dy, x, dw, db | None, overwrite, weight param, bias param | N
 
 def reset_wgrad_queue() -> None:
     """Drop deferred work of a backward that raised (called at every forward)."""
+    for q in _wq:
+        q[5]._dpe_deferred = False
+        if q[6] is not None:
+            q[6]._dpe_deferred = False
     _wq.clear()
 
 
@@ -72,9 +76,10 @@ def flush_wgrad_queue() -> None:
         chunk = items[i:i + 8]
         C.linear_wgrad_group([q[0] for q in chunk], [q[1] for q in chunk], [q[2] for q in chunk],
                              [q[3] if q[3] is not None else _EMPTY(q[2]) for q in chunk], [q[4] for q in chunk])
-    if os.environ.get("DPE_WG_DEBUG") == "1":
-        torch.cuda.synchronize()
-        print(f"[wg] flushed {len(items)} problems", flush=True)
+    for q in items:
+        q[5]._dpe_deferred = False
+        if q[6] is not None:
+            q[6]._dpe_deferred = False
     for q in items:
         grad_done(q[5], True)
         if q[6] is not None:
@@ -156,9 +161,11 @@ class BlockFn(Function):
             buf, d = sink(lin.weight)
             bb, bd = sink(lin.bias) if lin.bias is not None else (None, True)
             if group and d and bd:
-                if os.environ.get("DPE_WG_DEBUG") == "1":
-                    print(f"[wg] defer {tuple(buf.shape)} fresh={getattr(lin.weight, '_dpe_fresh', None)}", flush=True)
-                # deferred to the grouped launch at the end of this block's (or the next one's) backward
+                # deferred to the grouped launch at the end of this block's (or the next one's) backward;
+                # DDP's post-accumulate hook (which fires after this node returns) must not announce them
+                lin.weight._dpe_deferred = True
+                if lin.bias is not None:
+                    lin.bias._dpe_deferred = True
                 _wq.append((dyb, inp, buf, bb, grad_fresh(lin.weight), lin.weight, lin.bias))
                 return C.linear_dgrad(dyb, shadow(lin.weight), None, None, gelu_in) if want_dx else None
             # bias grad from the same launch (row sums of dy^T); a K-split's slab reduction may run on the

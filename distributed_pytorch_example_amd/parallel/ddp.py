@@ -228,7 +228,8 @@ class DistributedDataParallel(nn.Module):
         # small buckets: at 8 GPUs only the final <= last_bucket_mb piece is exposed
         last_mb = p_last if last_bucket_mb == "auto" else last_bucket_mb
         self.last_bucket_bytes = int(last_mb * 1024 * 1024) if last_mb else None
-        self._register = register_buckets
+        # DPE_REGISTER_BUCKETS=0: no ncclCommRegister of the bucket buffers (A/B, debugging)
+        self._register = register_buckets and os.environ.get("DPE_REGISTER_BUCKETS", "1") != "0"
         self._comm = comm if comm is not None else pdist.comm()
         self._force = force_comm
         self._timing = timing
@@ -255,7 +256,7 @@ class DistributedDataParallel(nn.Module):
         for i, p in enumerate(self._params):
             p._dpe_direct = True
             p._dpe_ready = self._on_ready
-            self._hooks.append(p.register_post_accumulate_grad_hook(self._on_ready))
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._on_accumulated))
             if getattr(p, "_dpe_overwrite_ok", False):
                 self._hooks.append(p.register_hook(self._fresh_guard(i)))
 
@@ -403,6 +404,15 @@ class DistributedDataParallel(nn.Module):
 
         return hook
 
+    def _on_accumulated(self, p):
+        """Post-accumulate-grad hook: readiness of parameters written through autograd.  It also fires
+        after a node that wrote the parameter itself (and returned None for it) -- those announce
+        themselves with grad_done, and a parameter whose weight gradient is still queued for a grouped
+        launch (``_dpe_deferred``, models/_gpt2_fused.py) must not be announced before that launch."""
+        if getattr(p, "_dpe_deferred", False):
+            return
+        self._on_ready(p)
+
     # ---------------------------------------------------------- per-step
     def _on_ready(self, p):
         if not self.require_backward_grad_sync:
@@ -415,8 +425,6 @@ class DistributedDataParallel(nn.Module):
         if not self._queued:
             self._queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
-        if os.environ.get("DPE_WG_DEBUG") == "1":
-            print(f"[ddp] ready {i} {tuple(p.shape)}", flush=True)
         self.reducer.mark_ready(i)
 
     def _finalize(self):

@@ -1,0 +1,39 @@
+#!/bin/bash
+# Several GPU steps in one call; a step that fails normally (exit 1) does not stop the call, a
+# timeout / abort / segfault / kill does (no further GPU work after those).
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R && mkdir -p gpurun_out/combo
+run() {  # run <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > gpurun_out/combo/$name.log 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc"
+  case $rc in 124|137|134|139|-6|-11) echo "STOP after $name (rc $rc)"; tail -20 gpurun_out/combo/$name.log; exit $rc;; esac
+  return $rc
+}
+for step in "$@"; do
+  case $step in
+    dbg) for reg in 0 1; do
+           DPE_REGISTER_BUCKETS=$reg DPE_WG_DEBUG=1 DPE_DEBUG_LOCAL=1 run dbg_reg$reg 200 python -u -m pytest -x -q -s --timeout 150 \
+             --timeout-method thread -p no:cacheprovider tests/test_ddp_rccl_world2_gpu.py::test_native_reducer_world2_rccl_gpt2
+           grep -E "passed|failed" gpurun_out/combo/dbg_reg$reg.log | tail -1
+           grep -E "vs avg|vs local" gpurun_out/combo/dbg_reg$reg.log | head -4 | cut -c1-200
+         done ;;
+    gramblocks) run gram_blocks 200 python -u scripts/debug_gram_blocks.py; grep block gpurun_out/combo/gram_blocks.log; tail -3 gpurun_out/combo/gram_blocks.log ;;
+    gramloss) run gram_loss 200 python -u scripts/debug_gram_loss.py; cat gpurun_out/combo/gram_loss.log | grep -v amdgpu.ids ;;
+    gpt2w2) run gpt2w2 300 python -u -m pytest -x -q --timeout 150 --timeout-method thread -p no:cacheprovider \
+              tests/test_ddp_rccl_world2_gpu.py tests/test_comm_gpu.py -k "gpt2 or world4"
+            tail -3 gpurun_out/combo/gpt2w2.log ;;
+    gram) run gram_tests 400 python -u -m pytest -v -s --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_bn3_gram_gpu.py
+          grep -E "PASSED|FAILED|worst|Error" gpurun_out/combo/gram_tests.log | head -30 | cut -c1-220 ;;
+    grambench) for arm in 0 1 0 1; do
+            DPE_BN3_GRAM=$arm run bench_gram$arm 200 python bench.py --steps 20 --warmup 5 && \
+              echo "gram=$arm $(tail -1 gpurun_out/combo/bench_gram$arm.log | cut -c1-110)"
+          done ;;
+    gpt2bench) for arm in 0 2; do
+            DPE_GPT2_WGRAD_GROUP=$arm run bench_gpt2_$arm 200 python bench.py --model gpt2 --steps 20 --warmup 5 && \
+              echo "group=$arm $(tail -1 gpurun_out/combo/bench_gpt2_$arm.log | cut -c1-110)"
+          done ;;
+  esac
+done
+exit 0

@@ -148,7 +148,7 @@ def test_gram_backward_and_cat_dgrad(C):
     assert _rel(p2[0].sum(-1), s1) < 1e-3 and _rel(p2[1].sum(-1), s2) < 1e-3
     # materialised a2 (no coefficients on load): same result
     da_m, _ = X.conv1x1_dgrad_cat(dz, _operand(h2, c2).bfloat16(), None, bcat, e, h2, c2)
-    assert _rel(da_m.float(), da.float()) < 1e-6
+    assert _rel(da_m.float(), da.float()) < 1e-4  # (fmaf on load vs torch mul + add: last-bit rounding)
 
 
 def test_resnet50_step_gram_on_vs_off():
