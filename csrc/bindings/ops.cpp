@@ -27,7 +27,7 @@ int dpe_gram_coef(const float* G, const float* s, const uint16_t* w, int Cin, in
                   hipStream_t st);
 int dpe_gram_bwd(const float* part, int rg, const float* P, const uint16_t* w, const float* u, const float* s,
                  const float* coef3, const float* gamma, int Cin, int Cout, int64_t M, float* dgamma, float* dbeta,
-                 float* dw, uint16_t* bcat, float* abc, float* ebias, hipStream_t st);
+                 float* dw, uint16_t* bcat, float* abc, float* ebias, float* qws, hipStream_t st);
 int dpe_bn_stats_nblocks(int64_t M, int C);
 
 int dpe_bn_stats(const uint16_t* x, int64_t M, int C, int nb, float* part, hipStream_t st);
@@ -1118,8 +1118,9 @@ std::vector<Tensor> bn_gram_bwd(const Tensor& part, const Tensor& P, const Tenso
               "bn_gram_bwd: shapes");
   auto fo = P.options();
   Tensor bcat = at::empty({Cout + Cin, Cin}, w.options()), abc = at::empty({3, Cout}, fo), e = at::empty({Cin}, fo);
+  Tensor qws = at::empty({Cin, Cin}, fo);
   CHECK_RC(dpe_gram_bwd(fp(part), (int)part.size(2), fp(P), bp(w), fp(u), fp(sv), fp(coef), fpo(gamma), (int)Cin,
-                        (int)Cout, M, fpom(dgamma), fpom(dbeta), fp(dw), bpm(bcat), fp(abc), fp(e), cur_stream()),
+                        (int)Cout, M, fpom(dgamma), fpom(dbeta), fp(dw), bpm(bcat), fp(abc), fp(e), fp(qws), cur_stream()),
            "bn_gram_bwd");
   return {bcat, e};
 }

@@ -31,40 +31,50 @@ constexpr int TS = TR * 2 + 16;  // LDS bytes per channel row of the transposed 
 // over rows [blockIdx.x * rpb, +rpb): gp[block][C][C] (full, symmetric), sp[block][C].  x' is rounded
 // to bf16 exactly as the on-load BN transform of the conv kernels rounds their MFMA operand, so G is
 // the Gram matrix of the operand conv3 actually multiplies.
-template <int C>
-__global__ __launch_bounds__(256) void gram_partial_kernel(const uint16_t* __restrict__ x, const float* __restrict__ coef,
+//
+// A 32-row tile is loaded as 16-B row chunks: load slot (wave w, instruction i) covers rows
+// 16 (slot % 2) + [0, 16) x chunks 4 (slot / 2) + [0, 4) (lane: row l / 4, chunk l % 4), and stored
+// TRANSPOSED in LDS ([channel][32 rows], TS bytes per channel) so that an MFMA operand -- 8 consecutive
+// rows of one channel -- is one ds_read_b128.  Lanes l and l + 4 hold rows r, r + 1 of the same
+// channels: one swaps half its chunk with the other so each writes whole row-pair dwords (4 ds_write_b32
+// instead of 8 ds_write_b16; the 16-row x 4-chunk slot spreads a store over 32 banks, 2-way).
+template <int C, int NT = (C == 256 ? 512 : 256)>
+__global__ __launch_bounds__(NT) void gram_partial_kernel(const uint16_t* __restrict__ x, const float* __restrict__ coef,
                                                            int64_t M, int rpb, float* __restrict__ gp,
                                                            float* __restrict__ sp) {
-  constexpr int NB = C / 16, NF = NB * (NB + 1) / 2, FPW = (NF + 3) / 4;
+  constexpr int NW = NT / 64;  // (C = 256: 8 waves, so each holds 17 accumulator fragments, not 34)
+  constexpr int NB = C / 16, NF = NB * (NB + 1) / 2, FPW = (NF + NW - 1) / NW;
   constexpr int CPR = C / 8;          // 16-B chunks per row
-  constexpr int CPT = TR * CPR / 256; // chunks per thread per tile
-  static_assert(CPT >= 1 && CPT * 256 == TR * CPR, "tile split");
+  constexpr int CPT = TR * CPR / NT;  // load slots per wave per tile
+  static_assert(CPT >= 1 && CPT * NT == TR * CPR && CPR % 4 == 0, "tile split");
   __shared__ __attribute__((aligned(16))) char tile[2][C * TS];
-  __shared__ float red[256 / CPR * 8 + 8];
+  __shared__ __attribute__((aligned(16))) float cf[2 * C];  // [scale | shift] of the on-load BN
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
   const int64_t r1 = min<int64_t>(M, r0 + rpb);
   const int ntile = r0 < r1 ? (int)((r1 - r0 + TR - 1) / TR) : 0;
+  const bool odd = (lane >> 2) & 1;  // row r + 1 of its pair
+  if (coef)
+    for (int i = tid; i < 2 * C; i += NT) cf[i] = coef[i];
 
-  // this thread's chunks: q = tid + 256 i -> row q / CPR, channels 8 (q % CPR) .. +7 (the same
-  // channels on every tile: CPR divides 256)
-  const int cc = tid % CPR;
-  float sc[8], sh[8];
+  int srow[CPT], scc[CPT];
+  float csum[CPT][8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    sc[e] = coef ? coef[8 * cc + e] : 1.f;
-    sh[e] = coef ? coef[C + 8 * cc + e] : 0.f;
+  for (int i = 0; i < CPT; ++i) {
+    const int slot = wid + NW * i;
+    srow[i] = 16 * (slot & 1) + (lane >> 2);
+    scc[i] = 4 * (slot >> 1) + (lane & 3);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[i][e] = 0.f;
   }
-  float csum[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+  __syncthreads();
 
-  // fragments (I <= J) of wave wid: f = wid + 4 i
+  // fragments (I <= J) of wave wid: f = wid + NW i
   int fi[FPW], fj[FPW];
 #pragma unroll
   for (int i = 0; i < FPW; ++i) {
-    int f = wid + 4 * i, I = 0;
+    int f = wid + NW * i, I = 0;
     if (f >= NF) f = NF - 1;  // (padding slot: recomputes a valid fragment, never stored)
     while (f >= NB - I) { f -= NB - I; ++I; }
     fi[i] = I;
@@ -78,9 +88,8 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const uint16_t* __res
   auto load = [&](int t) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int q = tid + 256 * i, row = q / CPR;
-      const int64_t m = r0 + (int64_t)t * TR + row;
-      ld[i] = m < r1 ? *(const u32x4*)(x + m * C + 8 * cc) : u32x4{0u, 0u, 0u, 0u};
+      const int64_t m = r0 + (int64_t)t * TR + srow[i];
+      ld[i] = m < r1 ? *(const u32x4*)(x + m * C + 8 * scc[i]) : u32x4{0u, 0u, 0u, 0u};
     }
   };
   if (ntile > 0) load(0);
@@ -88,22 +97,35 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const uint16_t* __res
     char* T = tile[t & 1];
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int q = tid + 256 * i, row = q / CPR;
-      const bool valid = r0 + (int64_t)t * TR + row < r1;
+      const bool valid = r0 + (int64_t)t * TR + srow[i] < r1;
       float f[8];
       unpack8(ld[i], f);
       if (coef) {
+        const f32x4* cs = (const f32x4*)(cf + 8 * scc[i]);
+        const f32x4* ch = (const f32x4*)(cf + C + 8 * scc[i]);
+        const f32x4 s0 = cs[0], s1 = cs[1], h0 = ch[0], h1 = ch[1];
+        const float sc8[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+        const float sh8[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = valid ? fmaxf(fmaf(f[e], sc[e], sh[e]), 0.f) : 0.f;
+        for (int e = 0; e < 8; ++e) f[e] = valid ? fmaxf(fmaf(f[e], sc8[e], sh8[e]), 0.f) : 0.f;
       }
       const u32x4 pk = pack8(f);
       unpack8(pk, f);  // the rounded operand
 #pragma unroll
-      for (int e = 0; e < 8; ++e) csum[e] += f[e];
+      for (int e = 0; e < 8; ++e) csum[i][e] += f[e];
+      // even lane keeps channels 0-3 of its chunk and takes the odd partner's rows for them; the odd
+      // lane keeps channels 4-7
+      const uint32_t s0 = odd ? pk[0] : pk[2], s1 = odd ? pk[1] : pk[3];
+      const uint32_t q0 = (uint32_t)__shfl_xor((int)s0, 4, 64), q1 = (uint32_t)__shfl_xor((int)s1, 4, 64);
+      const uint32_t o0 = odd ? pk[2] : pk[0], o1 = odd ? pk[3] : pk[1];
+      const int cb = 8 * scc[i] + (odd ? 4 : 0), p = srow[i] >> 1;
+      const uint32_t own[2] = {o0, o1}, oth[2] = {q0, q1};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        *(uint16_t*)(T + (8 * cc + 2 * e) * TS + row * 2) = (uint16_t)(pk[e] & 0xffffu);
-        *(uint16_t*)(T + (8 * cc + 2 * e + 1) * TS + row * 2) = (uint16_t)(pk[e] >> 16);
+      for (int u = 0; u < 2; ++u) {
+        // (row r, row r + 1) halves: even lane = own is row r; odd lane = own is row r + 1
+        const uint32_t rlo = odd ? oth[u] : own[u], rhi = odd ? own[u] : oth[u];
+        *(uint32_t*)(T + (cb + 2 * u) * TS + p * 4) = (rlo & 0xffffu) | (rhi << 16);
+        *(uint32_t*)(T + (cb + 2 * u + 1) * TS + p * 4) = (rlo >> 16) | (rhi & 0xffff0000u);
       }
     }
     if (t + 1 < ntile) load(t + 1);  // in flight across the MFMAs below
@@ -120,128 +142,146 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const uint16_t* __res
   }
   // partial G: lane holds D[4 (lane / 16) + e][lane % 16] of fragment (I, J); mirrored below the diagonal
   float* G = gp + (int64_t)blockIdx.x * C * C;
-  const int g = lane >> 4, li = lane & 15;
+  {
+    const int g = lane >> 4, li = lane & 15;
 #pragma unroll
-  for (int i = 0; i < FPW; ++i) {
-    if (wid + 4 * i >= NF) continue;
-    const int I = fi[i], J = fj[i];
+    for (int i = 0; i < FPW; ++i) {
+      if (wid + NW * i >= NF) continue;
+      const int I = fi[i], J = fj[i];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int r = 16 * I + 4 * g + e, c = 16 * J + li;
-      G[(int64_t)r * C + c] = acc[i][e];
-      if (I != J) G[(int64_t)c * C + r] = acc[i][e];
+      for (int e = 0; e < 4; ++e) {
+        const int r = 16 * I + 4 * g + e, c = 16 * J + li;
+        G[(int64_t)r * C + c] = acc[i][e];
+        if (I != J) G[(int64_t)c * C + r] = acc[i][e];
+      }
     }
   }
-  // column sums: threads tid, tid + CPR, ... hold the same channels (fixed-order LDS reduction)
+  // column sums: slot (wave, i) x lane -> chunk scc; fixed-order LDS reduction over the 32 (slot, lane)
+  // pairs holding each chunk (2 row halves x 16 lanes)
   __syncthreads();
-  float* rs = (float*)tile[0];  // [256][8]
+  float* rs = (float*)tile[0];  // [slot][64 lanes][8]
 #pragma unroll
-  for (int e = 0; e < 8; ++e) rs[tid * 8 + e] = csum[e];
+  for (int i = 0; i < CPT; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) rs[((wid + NW * i) * 64 + lane) * 8 + e] = csum[i][e];
   __syncthreads();
-  if (tid < CPR) {
+  for (int c8 = tid; c8 < CPR; c8 += NT) {  // chunk c8: slots 2 (c8 / 4) + {0, 1}, lanes = c8 % 4 (mod 4)
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = 0.f;
-    for (int k = tid; k < 256; k += CPR)
+    for (int h = 0; h < 2; ++h)
+      for (int l = c8 % 4; l < 64; l += 4)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += rs[k * 8 + e];
+        for (int e = 0; e < 8; ++e) v[e] += rs[((2 * (c8 / 4) + h) * 64 + l) * 8 + e];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) sp[(int64_t)blockIdx.x * C + 8 * tid + e] = v[e];
+    for (int e = 0; e < 8; ++e) sp[(int64_t)blockIdx.x * C + 8 * c8 + e] = v[e];
   }
-  (void)red;
 }
 
-// G[i] = sum_b gp[b][i] (i over C*C, then the C column sums), in block order, in double
+// G[i] = sum_b gp[b][i] (i over C*C, then the C column sums), in a fixed order, in double.  A block
+// covers 32 consecutive outputs with 8 slab groups (thread = output x group: group q sums blocks
+// q, q + 8, ...), then the 8 group sums are added in group order.
 __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ gp, const float* __restrict__ sp, int nb,
                                                           int C, float* __restrict__ G, float* __restrict__ s) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  __shared__ double part[8][32];
+  const int o = threadIdx.x & 31, q = threadIdx.x >> 5;
+  const int64_t i = (int64_t)blockIdx.x * 32 + o;
   const int64_t cc = (int64_t)C * C;
+  double a = 0.0;
   if (i < cc) {
-    double a = 0.0;
-    int b = 0;
-    for (; b + 3 < nb; b += 4) {
-      const float v0 = gp[(int64_t)b * cc + i], v1 = gp[(int64_t)(b + 1) * cc + i];
-      const float v2 = gp[(int64_t)(b + 2) * cc + i], v3 = gp[(int64_t)(b + 3) * cc + i];
-      a += v0; a += v1; a += v2; a += v3;
-    }
-    for (; b < nb; ++b) a += gp[(int64_t)b * cc + i];
-    G[i] = (float)a;
+    for (int b = q; b < nb; b += 8) a += gp[(int64_t)b * cc + i];
   } else if (i < cc + C) {
-    const int c = (int)(i - cc);
-    double a = 0.0;
-    for (int b = 0; b < nb; ++b) a += sp[(int64_t)b * C + c];
-    s[c] = (float)a;
+    for (int b = q; b < nb; b += 8) a += sp[(int64_t)b * C + (i - cc)];
+  }
+  part[q][o] = a;
+  __syncthreads();
+  if (q == 0) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += part[k][o];
+    if (i < cc) G[i] = (float)t;
+    else if (i < cc + C) s[i - cc] = (float)t;
   }
 }
 
-constexpr int KPB = 8;  // output channels per block of the coefficient kernels
+// Small fp32 GEMM on 32x32 output tiles: out[m][n] = sum_k A(m, k) B[k][n].
+//   AT = false: A(m, k) = a[m * lda + k]        (row-major, u = W G: A = W3 [Cout][Cin] bf16)
+//   AT = true:  A(m, k) = a[k * lda + m] scale[k] (Q = W^T diag(b) W: A = W3 read down its columns)
+// K chunks of 64 staged in LDS as fp32; 256 threads, each 1 row x 4 columns of the tile.
+template <bool AT, typename TB>
+__global__ __launch_bounds__(256) void gram_mm_kernel(const uint16_t* __restrict__ a, int64_t lda,
+                                                      const float* __restrict__ scale, const TB* __restrict__ b,
+                                                      int64_t ldb, int K, float* __restrict__ out, int64_t ldo) {
+  __shared__ float As[64][33], Bs[64][32];
+  const int tid = threadIdx.x, m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+  const int tm = tid >> 3, tn = (tid & 7) * 4;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += 64) {
+    for (int e = tid; e < 64 * 32; e += 256) {
+      const int kk = e >> 5, c = e & 31, k = k0 + kk;
+      float av = 0.f, bv = 0.f;
+      if (k < K) {
+        if constexpr (AT) av = bf2f(a[(int64_t)k * lda + m0 + c]) * (scale ? scale[k] : 1.f);
+        else av = bf2f(a[(int64_t)(m0 + c) * lda + k]);
+        if constexpr (sizeof(TB) == 2) bv = bf2f((uint16_t)b[(int64_t)k * ldb + n0 + c]);
+        else bv = (float)b[(int64_t)k * ldb + n0 + c];
+      }
+      As[kk][c] = av;
+      Bs[kk][c] = bv;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int kk = 0; kk < 64; ++kk) {
+      const float av = As[kk][tm];
+      const f32x4 bv = *(const f32x4*)&Bs[kk][tn];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] = fmaf(av, bv[e], acc[e]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) out[(int64_t)(m0 + tm) * ldo + n0 + tn + e] = acc[e];
+}
 
-// Forward: per output channel k of conv3 (weights w [Cout][Cin] bf16), u[k][:] = w_k G and
+// Forward: per output channel k of conv3 (weights w [Cout][Cin] bf16, u = W G from gram_mm_kernel),
 //   mean = (w_k . s) / M,  E[h^2] = (w_k . u[k]) / M  ->  coef [4][Cout] = scale, shift, mean, invstd
-// (the layout of bn_finalize_kernel), running stats updated as there (unbiased variance).
-__global__ __launch_bounds__(256) void gram_coef_kernel(const float* __restrict__ G, const float* __restrict__ s,
+// (the layout of bn_finalize_kernel), running stats updated as there (unbiased variance).  One wave per k.
+__global__ __launch_bounds__(256) void gram_coef_kernel(const float* __restrict__ u, const float* __restrict__ s,
                                                         const uint16_t* __restrict__ w, int Cin, int Cout, int64_t M,
                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
                                                         float* __restrict__ rmean, float* __restrict__ rvar, float momentum,
-                                                        float eps, float* __restrict__ coef, float* __restrict__ u) {
-  extern __shared__ float wl[];  // [KPB][Cin]
-  __shared__ double red[2][KPB][4];
-  const int k0 = blockIdx.x * KPB, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int i = tid; i < KPB * Cin; i += 256) {
-    const int kk = i / Cin, j = i - kk * Cin;
-    wl[i] = k0 + kk < Cout ? bf2f(w[(int64_t)(k0 + kk) * Cin + j]) : 0.f;
+                                                        float eps, float* __restrict__ coef) {
+  const int lane = threadIdx.x & 63, k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= Cout) return;
+  double e2 = 0.0, mu = 0.0;
+  for (int j = lane; j < Cin; j += 64) {
+    const double wv = bf2f(w[(int64_t)k * Cin + j]);
+    e2 += wv * u[(int64_t)k * Cin + j];
+    mu += wv * s[j];
   }
-  __syncthreads();
-  double e2[KPB], mu[KPB];
-#pragma unroll
-  for (int kk = 0; kk < KPB; ++kk) { e2[kk] = 0.0; mu[kk] = 0.0; }
-  for (int j = tid; j < Cin; j += 256) {
-    float acc[KPB];
-#pragma unroll
-    for (int kk = 0; kk < KPB; ++kk) acc[kk] = 0.f;
-    for (int jp = 0; jp < Cin; ++jp) {
-      const float gv = G[(int64_t)jp * Cin + j];
-#pragma unroll
-      for (int kk = 0; kk < KPB; ++kk) acc[kk] = fmaf(wl[kk * Cin + jp], gv, acc[kk]);
-    }
-    const float sj = s[j];
-#pragma unroll
-    for (int kk = 0; kk < KPB; ++kk) {
-      if (k0 + kk < Cout) u[(int64_t)(k0 + kk) * Cin + j] = acc[kk];
-      e2[kk] += (double)acc[kk] * wl[kk * Cin + j];
-      mu[kk] += (double)wl[kk * Cin + j] * sj;
-    }
+  for (int o = 32; o > 0; o >>= 1) {
+    e2 += __shfl_xor(e2, o, 64);
+    mu += __shfl_xor(mu, o, 64);
   }
-#pragma unroll
-  for (int kk = 0; kk < KPB; ++kk) {
-    for (int o = 32; o > 0; o >>= 1) {
-      e2[kk] += __shfl_xor(e2[kk], o, 64);
-      mu[kk] += __shfl_xor(mu[kk], o, 64);
-    }
-    if (lane == 0) { red[0][kk][wid] = e2[kk]; red[1][kk][wid] = mu[kk]; }
-  }
-  __syncthreads();
-  if (tid < KPB && k0 + tid < Cout) {
-    const int k = k0 + tid;
-    double E2 = 0.0, S = 0.0;
-    for (int q = 0; q < 4; ++q) { E2 += red[0][tid][q]; S += red[1][tid][q]; }
-    const double mean = S / (double)M;
-    double var = E2 / (double)M - mean * mean;
-    if (var < 0) var = 0;
-    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-    const float gm = gamma ? gamma[k] : 1.f, bt = beta ? beta[k] : 0.f;
-    const float sc = gm * invstd;
-    coef[k] = sc;
-    coef[Cout + k] = bt - (float)mean * sc;
-    coef[2 * Cout + k] = (float)mean;
-    coef[3 * Cout + k] = invstd;
-    if (rmean) {
-      const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-      rmean[k] = (1.f - momentum) * rmean[k] + momentum * (float)mean;
-      rvar[k] = (1.f - momentum) * rvar[k] + momentum * (float)unbiased;
-    }
+  if (lane != 0) return;
+  const double mean = mu / (double)M;
+  double var = e2 / (double)M - mean * mean;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float gm = gamma ? gamma[k] : 1.f, bt = beta ? beta[k] : 0.f;
+  const float sc = gm * invstd;
+  coef[k] = sc;
+  coef[Cout + k] = bt - (float)mean * sc;
+  coef[2 * Cout + k] = (float)mean;
+  coef[3 * Cout + k] = invstd;
+  if (rmean) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    rmean[k] = (1.f - momentum) * rmean[k] + momentum * (float)mean;
+    rvar[k] = (1.f - momentum) * rvar[k] + momentum * (float)unbiased;
   }
 }
+
+constexpr int KPB = 8;  // output channels per block of the backward coefficient kernel
 
 // Backward, per output channel k.  part [2][Cout][RG]: row 0 = partial sums of dz3 (row 1 unused);
 // P [Cout][Cin] = dz3^T a2; u = W3 G; s = colsum(a2); coef3 = BN3's (scale, shift, mean, invstd).
@@ -315,23 +355,30 @@ __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__
   }
 }
 
-// Backward: the data grad's B rows Cout + j' (Q = W3^T diag(b) W3, bf16) and its bias e = c^T W3 (fp32).
-// One thread per (j', j); the j' == 0 threads also produce e[j].
-__global__ __launch_bounds__(256) void gram_q_kernel(const uint16_t* __restrict__ w, const float* __restrict__ abc, int Cin,
-                                                     int Cout, uint16_t* __restrict__ bcat, float* __restrict__ ebias) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)Cin * Cin) return;
-  const int jp = (int)(i / Cin), j = (int)(i - (int64_t)jp * Cin);
-  const float* b = abc + Cout;
+// Backward: the data grad's bias e[j] = sum_k c_k W3[k][j] (fp32) -- block = 32 columns x 8 k groups,
+// fixed-order combine -- and the bf16 cast of Q (gram_mm_kernel, fp32) into the B rows Cout + j'.
+__global__ __launch_bounds__(256) void gram_e_kernel(const uint16_t* __restrict__ w, const float* __restrict__ abc,
+                                                     int Cin, int Cout, const float* __restrict__ Q,
+                                                     uint16_t* __restrict__ bcat, float* __restrict__ ebias) {
+  __shared__ float part[8][32];
+  const int o = threadIdx.x & 31, q = threadIdx.x >> 5, j = blockIdx.x * 32 + o;
   const float* c = abc + 2 * Cout;
-  float q = 0.f, e = 0.f;
-  for (int k = 0; k < Cout; ++k) {
-    const float wj = bf2f(w[(int64_t)k * Cin + j]);
-    q = fmaf(bf2f(w[(int64_t)k * Cin + jp]) * b[k], wj, q);
-    if (jp == 0) e = fmaf(c[k], wj, e);
+  float e = 0.f;
+  if (j < Cin)
+    for (int k = q; k < Cout; k += 8) e = fmaf(c[k], bf2f(w[(int64_t)k * Cin + j]), e);
+  part[q][o] = e;
+  __syncthreads();
+  if (q == 0 && j < Cin) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += part[k][o];
+    ebias[j] = t;
   }
-  bcat[(int64_t)(Cout + jp) * Cin + j] = f2bf(q);
-  if (jp == 0) ebias[j] = e;
+  // Q rows: this block casts rows [blockIdx.x * 32, +32) of the [Cin][Cin] fp32 Q
+  for (int i = threadIdx.x; i < 32 * Cin; i += 256) {
+    const int r = blockIdx.x * 32 + i / Cin, cc = i % Cin;
+    if (r < Cin) bcat[(int64_t)(Cout + r) * Cin + cc] = f2bf(Q[(int64_t)r * Cin + cc]);
+  }
 }
 
 }  // namespace gram
@@ -357,29 +404,35 @@ extern "C" int dpe_gram(const uint16_t* x, const float* coef, int64_t M, int C, 
   float* sp = ws + (int64_t)nb * C * C;
   if (C == 64) hipLaunchKernelGGL(gram::gram_partial_kernel<64>, dim3(nb), dim3(256), 0, st, x, coef, M, rpb, gp, sp);
   else if (C == 128) hipLaunchKernelGGL(gram::gram_partial_kernel<128>, dim3(nb), dim3(256), 0, st, x, coef, M, rpb, gp, sp);
-  else hipLaunchKernelGGL(gram::gram_partial_kernel<256>, dim3(nb), dim3(256), 0, st, x, coef, M, rpb, gp, sp);
+  else hipLaunchKernelGGL(gram::gram_partial_kernel<256>, dim3(nb), dim3(512), 0, st, x, coef, M, rpb, gp, sp);
   const int64_t n = (int64_t)C * C + C;
-  hipLaunchKernelGGL(gram::gram_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, gp, sp, nb, C, G, s);
+  hipLaunchKernelGGL(gram::gram_reduce_kernel, dim3((unsigned)((n + 31) / 32)), dim3(256), 0, st, gp, sp, nb, C, G, s);
   return 0;
 }
 
 extern "C" int dpe_gram_coef(const float* G, const float* s, const uint16_t* w, int Cin, int Cout, int64_t M,
                              const float* gamma, const float* beta, float* rmean, float* rvar, float momentum, float eps,
                              float* coef, float* u, hipStream_t st) {
-  const unsigned nb = (unsigned)((Cout + gram::KPB - 1) / gram::KPB);
-  hipLaunchKernelGGL(gram::gram_coef_kernel, dim3(nb), dim3(256), gram::KPB * Cin * sizeof(float), st, G, s, w, Cin, Cout,
-                     M, gamma, beta, rmean, rvar, momentum, eps, coef, u);
+  if (Cin % 32 || Cout % 32) return -1;
+  // u = W G  (M = Cout, N = Cin, K = Cin)
+  hipLaunchKernelGGL((gram::gram_mm_kernel<false, float>), dim3(Cin / 32, Cout / 32), dim3(256), 0, st, w, (int64_t)Cin,
+                     (const float*)nullptr, G, (int64_t)Cin, Cin, u, (int64_t)Cin);
+  hipLaunchKernelGGL(gram::gram_coef_kernel, dim3((Cout + 3) / 4), dim3(256), 0, st, u, s, w, Cin, Cout, M, gamma, beta,
+                     rmean, rvar, momentum, eps, coef);
   return 0;
 }
 
+// ws (the caller's scratch) >= Cin * Cin floats: Q in fp32 before its bf16 cast
 extern "C" int dpe_gram_bwd(const float* part, int rg, const float* P, const uint16_t* w, const float* u, const float* s,
                             const float* coef3, const float* gamma, int Cin, int Cout, int64_t M, float* dgamma,
-                            float* dbeta, float* dw, uint16_t* bcat, float* abc, float* ebias, hipStream_t st) {
+                            float* dbeta, float* dw, uint16_t* bcat, float* abc, float* ebias, float* qws, hipStream_t st) {
+  if (Cin % 32 || Cout % 32) return -1;
   const unsigned nb = (unsigned)((Cout + gram::KPB - 1) / gram::KPB);
   hipLaunchKernelGGL(gram::gram_bwd_kernel, dim3(nb), dim3(256), 0, st, part, rg, P, w, u, s, coef3, gamma, Cin, Cout, M,
                      dgamma, dbeta, dw, bcat, abc);
-  const int64_t n = (int64_t)Cin * Cin;
-  hipLaunchKernelGGL(gram::gram_q_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, abc, Cin, Cout, bcat,
-                     ebias);
+  // Q = W^T diag(b) W  (M = N = Cin, K = Cout; A = W read down its columns, scaled by b = abc row 1)
+  hipLaunchKernelGGL((gram::gram_mm_kernel<true, uint16_t>), dim3(Cin / 32, Cin / 32), dim3(256), 0, st, w, (int64_t)Cin,
+                     abc + Cout, w, (int64_t)Cin, Cout, qws, (int64_t)Cin);
+  hipLaunchKernelGGL(gram::gram_e_kernel, dim3((Cin + 31) / 32), dim3(256), 0, st, w, abc, Cin, Cout, qws, bcat, ebias);
   return 0;
 }

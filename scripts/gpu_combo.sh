@@ -5,10 +5,10 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R && mkdir -p gpurun_out/combo
 run() {  # run <name> <timeout> <cmd...>
   local name=$1 t=$2; shift 2
-  timeout -k 10 $t "$@" > gpurun_out/combo/$name.log 2>&1
+  timeout -k 10 $t "$@" > $R/gpurun_out/combo/$name.log 2>&1
   local rc=$?
   echo "[$name] rc=$rc"
-  case $rc in 124|137|134|139|-6|-11) echo "STOP after $name (rc $rc)"; tail -20 gpurun_out/combo/$name.log; exit $rc;; esac
+  case $rc in 124|137|134|139|-6|-11) echo "STOP after $name (rc $rc)"; tail -20 $R/gpurun_out/combo/$name.log; exit $rc;; esac
   return $rc
 }
 for step in "$@"; do
@@ -20,6 +20,16 @@ for step in "$@"; do
            grep -E "vs avg|vs local" gpurun_out/combo/dbg_reg$reg.log | head -4 | cut -c1-200
          done ;;
     gramblocks) run gram_blocks 200 python -u scripts/debug_gram_blocks.py; grep block gpurun_out/combo/gram_blocks.log; tail -3 gpurun_out/combo/gram_blocks.log ;;
+    prof) # steady ResNet-50 kernel trace (env passed through, e.g. DPE_BN3_GRAM)
+          ( cd /tmp && export TMPDIR=/tmp && run prof_${PROF_TAG:-x} 300 rocprofv3 --kernel-trace --output-format csv \
+              -d $R/gpurun_out/combo/prof_${PROF_TAG:-x} -o run -- python3 $R/bench.py --steps 6 --warmup 3 ) || true
+          f=$(find $R/gpurun_out/combo/prof_${PROF_TAG:-x} -name "*kernel_trace.csv" | head -1)
+          python3 $R/scripts/prof_steady.py $f 3 sgd_kernel 60 > $R/gpurun_out/combo/steady_${PROF_TAG:-x}.txt && head -40 $R/gpurun_out/combo/steady_${PROF_TAG:-x}.txt
+          python3 $R/scripts/prof_sequence.py $f 4 sgd_kernel > $R/gpurun_out/combo/sequence_${PROF_TAG:-x}.txt
+          rm -f $f ;;
+    parity0) run parity0 400 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider \
+               tests/test_model_parity_gpu.py -k step0
+             grep -E "PASSED|FAILED|% of bound|step-0|Error" $R/gpurun_out/combo/parity0.log | head -20 | cut -c1-200 ;;
     gramloss) run gram_loss 200 python -u scripts/debug_gram_loss.py; cat gpurun_out/combo/gram_loss.log | grep -v amdgpu.ids ;;
     gpt2w2) run gpt2w2 300 python -u -m pytest -x -q --timeout 150 --timeout-method thread -p no:cacheprovider \
               tests/test_ddp_rccl_world2_gpu.py tests/test_comm_gpu.py -k "gpt2 or world4"
