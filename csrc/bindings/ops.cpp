@@ -1118,7 +1118,7 @@ std::vector<Tensor> bn_gram_bwd(const Tensor& part, const Tensor& P, const Tenso
               "bn_gram_bwd: shapes");
   auto fo = P.options();
   Tensor bcat = at::empty({Cout + Cin, Cin}, w.options()), abc = at::empty({3, Cout}, fo), e = at::empty({Cin}, fo);
-  Tensor qws = at::empty({Cin, Cin}, fo);
+  Tensor qws = at::empty({(Cout + 127) / 128, Cin, Cin}, fo);
   CHECK_RC(dpe_gram_bwd(fp(part), (int)part.size(2), fp(P), bp(w), fp(u), fp(sv), fp(coef), fpo(gamma), (int)Cin,
                         (int)Cout, M, fpom(dgamma), fpom(dbeta), fp(dw), bpm(bcat), fp(abc), fp(e), fp(qws), cur_stream()),
            "bn_gram_bwd");

@@ -84,17 +84,26 @@ __global__ __launch_bounds__(NT) void gram_partial_kernel(const uint16_t* __rest
 #pragma unroll
   for (int i = 0; i < FPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u32x4 ld[CPT];
-  auto load = [&](int t) {
+  // register ring: the loads of the next U tiles are in flight while a tile is transposed and multiplied
+  // (one tile ahead left the pass latency-bound: ~1.5 TB/s at C = 64)
+  constexpr int U = CPT == 1 ? 8 : (NT == 256 ? 4 : 1);  // (C = 256 has no registers for a deeper ring)
+  u32x4 ring[U][CPT];
+  auto load = [&](int t, u32x4 (&ld)[CPT]) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int64_t m = r0 + (int64_t)t * TR + srow[i];
-      ld[i] = m < r1 ? *(const u32x4*)(x + m * C + 8 * scc[i]) : u32x4{0u, 0u, 0u, 0u};
+      ld[i] = (t < ntile && m < r1) ? *(const u32x4*)(x + m * C + 8 * scc[i]) : u32x4{0u, 0u, 0u, 0u};
     }
   };
-  if (ntile > 0) load(0);
-  for (int t = 0; t < ntile; ++t) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) load(u, ring[u]);
+  for (int t0 = 0; t0 < ntile; t0 += U)
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int t = t0 + u;
+    if (t >= ntile) break;
     char* T = tile[t & 1];
+    u32x4 (&ld)[CPT] = ring[u];
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const bool valid = r0 + (int64_t)t * TR + srow[i] < r1;
@@ -128,7 +137,7 @@ __global__ __launch_bounds__(NT) void gram_partial_kernel(const uint16_t* __rest
         *(uint32_t*)(T + (cb + 2 * u + 1) * TS + p * 4) = (rlo >> 16) | (rhi & 0xffff0000u);
       }
     }
-    if (t + 1 < ntile) load(t + 1);  // in flight across the MFMAs below
+    load(t + U, ld);  // refill this ring slot (in flight across the next U - 1 tiles)
     __syncthreads();
     const int g = lane >> 4, li = lane & 15;
 #pragma unroll
@@ -211,16 +220,20 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restric
 template <bool AT, typename TB>
 __global__ __launch_bounds__(256) void gram_mm_kernel(const uint16_t* __restrict__ a, int64_t lda,
                                                       const float* __restrict__ scale, const TB* __restrict__ b,
-                                                      int64_t ldb, int K, float* __restrict__ out, int64_t ldo) {
+                                                      int64_t ldb, int K, int kslice, float* __restrict__ out,
+                                                      int64_t ldo, int64_t slab) {
+  // blockIdx.z: K slice [z * kslice, +kslice) -> out + z * slab (partials summed by the caller, in order)
   __shared__ float As[64][33], Bs[64][32];
   const int tid = threadIdx.x, m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
   const int tm = tid >> 3, tn = (tid & 7) * 4;
+  const int kb = blockIdx.z * kslice, ke = min(K, kb + kslice);
+  out += (int64_t)blockIdx.z * slab;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < K; k0 += 64) {
+  for (int k0 = kb; k0 < ke; k0 += 64) {
     for (int e = tid; e < 64 * 32; e += 256) {
       const int kk = e >> 5, c = e & 31, k = k0 + kk;
       float av = 0.f, bv = 0.f;
-      if (k < K) {
+      if (k < ke) {
         if constexpr (AT) av = bf2f(a[(int64_t)k * lda + m0 + c]) * (scale ? scale[k] : 1.f);
         else av = bf2f(a[(int64_t)(m0 + c) * lda + k]);
         if constexpr (sizeof(TB) == 2) bv = bf2f((uint16_t)b[(int64_t)k * ldb + n0 + c]);
@@ -358,8 +371,25 @@ __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__
 // Backward: the data grad's bias e[j] = sum_k c_k W3[k][j] (fp32) -- block = 32 columns x 8 k groups,
 // fixed-order combine -- and the bf16 cast of Q (gram_mm_kernel, fp32) into the B rows Cout + j'.
 __global__ __launch_bounds__(256) void gram_e_kernel(const uint16_t* __restrict__ w, const float* __restrict__ abc,
-                                                     int Cin, int Cout, const float* __restrict__ Q,
+                                                     int Cin, int Cout, const float* __restrict__ Q, int qslices,
                                                      uint16_t* __restrict__ bcat, float* __restrict__ ebias) {
+  const int ne = (Cin + 31) / 32;
+  if ((int)blockIdx.x >= ne) {
+    // Q cast: blocks [ne, grid) own 1024-element spans of the [Cin][Cin] fp32 Q; the K-slice partials
+    // are summed in slice order (fixed, run-to-run identical)
+    const int64_t n = (int64_t)Cin * Cin, slab = n;
+    const int64_t i = ((int64_t)(blockIdx.x - ne) * 256 + threadIdx.x) * 4;
+    if (i < n) {
+      float4 acc = *(const float4*)(Q + i);
+      for (int z = 1; z < qslices; ++z) {
+        const float4 v = *(const float4*)(Q + z * slab + i);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+      uint16_t* dst = bcat + (int64_t)Cout * Cin + i;
+      *(uint2*)dst = make_uint2(pack_bf2(acc.x, acc.y), pack_bf2(acc.z, acc.w));
+    }
+    return;
+  }
   __shared__ float part[8][32];
   const int o = threadIdx.x & 31, q = threadIdx.x >> 5, j = blockIdx.x * 32 + o;
   const float* c = abc + 2 * Cout;
@@ -373,11 +403,6 @@ __global__ __launch_bounds__(256) void gram_e_kernel(const uint16_t* __restrict_
 #pragma unroll
     for (int k = 0; k < 8; ++k) t += part[k][o];
     ebias[j] = t;
-  }
-  // Q rows: this block casts rows [blockIdx.x * 32, +32) of the [Cin][Cin] fp32 Q
-  for (int i = threadIdx.x; i < 32 * Cin; i += 256) {
-    const int r = blockIdx.x * 32 + i / Cin, cc = i % Cin;
-    if (r < Cin) bcat[(int64_t)(Cout + r) * Cin + cc] = f2bf(Q[(int64_t)r * Cin + cc]);
   }
 }
 
@@ -415,14 +440,14 @@ extern "C" int dpe_gram_coef(const float* G, const float* s, const uint16_t* w, 
                              float* coef, float* u, hipStream_t st) {
   if (Cin % 32 || Cout % 32) return -1;
   // u = W G  (M = Cout, N = Cin, K = Cin)
-  hipLaunchKernelGGL((gram::gram_mm_kernel<false, float>), dim3(Cin / 32, Cout / 32), dim3(256), 0, st, w, (int64_t)Cin,
-                     (const float*)nullptr, G, (int64_t)Cin, Cin, u, (int64_t)Cin);
+  hipLaunchKernelGGL((gram::gram_mm_kernel<false, float>), dim3(Cin / 32, Cout / 32, 1), dim3(256), 0, st, w,
+                     (int64_t)Cin, (const float*)nullptr, G, (int64_t)Cin, Cin, Cin, u, (int64_t)Cin, (int64_t)0);
   hipLaunchKernelGGL(gram::gram_coef_kernel, dim3((Cout + 3) / 4), dim3(256), 0, st, u, s, w, Cin, Cout, M, gamma, beta,
                      rmean, rvar, momentum, eps, coef);
   return 0;
 }
 
-// ws (the caller's scratch) >= Cin * Cin floats: Q in fp32 before its bf16 cast
+// qws (the caller's scratch) >= ceil(Cout / 128) * Cin * Cin floats: Q's K-slice partials before the bf16 cast
 extern "C" int dpe_gram_bwd(const float* part, int rg, const float* P, const uint16_t* w, const float* u, const float* s,
                             const float* coef3, const float* gamma, int Cin, int Cout, int64_t M, float* dgamma,
                             float* dbeta, float* dw, uint16_t* bcat, float* abc, float* ebias, float* qws, hipStream_t st) {
@@ -431,8 +456,12 @@ extern "C" int dpe_gram_bwd(const float* part, int rg, const float* P, const uin
   hipLaunchKernelGGL(gram::gram_bwd_kernel, dim3(nb), dim3(256), 0, st, part, rg, P, w, u, s, coef3, gamma, Cin, Cout, M,
                      dgamma, dbeta, dw, bcat, abc);
   // Q = W^T diag(b) W  (M = N = Cin, K = Cout; A = W read down its columns, scaled by b = abc row 1)
-  hipLaunchKernelGGL((gram::gram_mm_kernel<true, uint16_t>), dim3(Cin / 32, Cin / 32), dim3(256), 0, st, w, (int64_t)Cin,
-                     abc + Cout, w, (int64_t)Cin, Cout, qws, (int64_t)Cin);
-  hipLaunchKernelGGL(gram::gram_e_kernel, dim3((Cin + 31) / 32), dim3(256), 0, st, w, abc, Cin, Cout, qws, bcat, ebias);
+  // (split over K = Cout in 128-deep slices: the 32x32-tile grid alone is 4-64 blocks)
+  const int qs = (Cout + 127) / 128;
+  hipLaunchKernelGGL((gram::gram_mm_kernel<true, uint16_t>), dim3(Cin / 32, Cin / 32, qs), dim3(256), 0, st, w,
+                     (int64_t)Cin, abc + Cout, w, (int64_t)Cin, Cout, 128, qws, (int64_t)Cin, (int64_t)Cin * Cin);
+  const int ncast = (int)(((int64_t)Cin * Cin + 1023) / 1024);
+  hipLaunchKernelGGL(gram::gram_e_kernel, dim3((Cin + 31) / 32 + ncast), dim3(256), 0, st, w, abc, Cin, Cout, qws, qs,
+                     bcat, ebias);
   return 0;
 }

@@ -40,6 +40,9 @@ for step in "$@"; do
             DPE_BN3_GRAM=$arm run bench_gram$arm 200 python bench.py --steps 20 --warmup 5 && \
               echo "gram=$arm $(tail -1 gpurun_out/combo/bench_gram$arm.log | cut -c1-110)"
           done ;;
+    bench) for i in 1 2; do
+            run bench_r$i 200 python bench.py --steps 20 --warmup 5 && echo "run $i $(tail -1 gpurun_out/combo/bench_r$i.log | cut -c1-110)"
+          done ;;
     gpt2bench) for arm in 0 2; do
             DPE_GPT2_WGRAD_GROUP=$arm run bench_gpt2_$arm 200 python bench.py --model gpt2 --steps 20 --warmup 5 && \
               echo "group=$arm $(tail -1 gpurun_out/combo/bench_gpt2_$arm.log | cut -c1-110)"
