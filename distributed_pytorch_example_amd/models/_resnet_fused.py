@@ -263,6 +263,10 @@ class BottleneckFn(Function):
         if link_out is not None:
             link_out.h3, link_out.coef, link_out.mask = h3, c3, bits
             link_out.gram = gram is not None
+            if gram is not None and block.down is not None:
+                # the next block's data-grad epilogue reduces the downsample BN's partials instead
+                # (sum dz, sum dz*(hd - mean_d)): row 0 serves BN3's Gram backward, both rows BN_d's
+                link_out.h3, link_out.coef = hd, cd
         ctx.block = block
         ctx.convs = convs
         ctx.ws = ws
@@ -352,6 +356,11 @@ class BottleneckFn(Function):
             bn_done(bn, gb, gd, bb, bd)
             grad_done(w3, wdirect)
             grads[id(w3)] = None if wdirect else wbuf
+            dhd = None
+            if has_down and lk.h3 is not None:  # BN_d's partials came with dz3 (forward: link_out.h3 = hd)
+                bn, gb, gd, bb, bd = bn_sinks(3)
+                dhd = C.bn_bwd_partials(dz3, hd, bn.weight.detach(), cd, lk.part, gb, bb, relu_mask=False)
+                bn_done(bn, gb, gd, bb, bd)
             lk.part = None
             lk.h3 = lk.coef = lk.mask = None
             ctx.bits = None
@@ -361,7 +370,7 @@ class BottleneckFn(Function):
             dh2 = C.bn_bwd_partials(da2, h2, bn.weight.detach(), c2, part2, gb, bb)
             bn_done(bn, gb, gd, bb, bd)
             return BottleneckFn._backward_tail(ctx, C, dz3, None, dh2, grads, bn_sinks, bn_done, bn_bwd, wgrad, dgrad,
-                                               dgrad_bnb)
+                                               dgrad_bnb, dhd)
         if chained:
             # the next block's dgrad epilogue already produced dz3 = dout*relu'(out) and BN3's partials
             dz3 = dout
@@ -432,7 +441,7 @@ class BottleneckFn(Function):
                 n, hh, ww, cin = x.shape
                 dxd = C.conv_dgrad(dhd, ws[3], [n, hh // 2, ww // 2, cin], [1, 1], [0, 0], [1, 1])  # compact
                 s, p, d = _conv_conf(convs[0].conv)
-                if li.gram:  # the previous block's BN3 runs by Gram algebra: only the sum-dz partials
+                if li.gram and li.h3 is None:  # the previous block's BN3 runs by Gram algebra: only the sum-dz partials
                     dx, part = C.conv_dgrad_bn(dh1, ws[0], list(x.shape), s, p, d, dxd, None, None, None, None, True,
                                                li.mask)
                 else:
@@ -451,7 +460,7 @@ class BottleneckFn(Function):
             elif ctx.link_in is not None:
                 li = ctx.link_in
                 s, p, d = _conv_conf(convs[0].conv)
-                if li.gram:
+                if li.gram and li.h3 is None:  # (li.h3 set: the previous block's downsample BN input, reduced too)
                     dx, part = C.conv_dgrad_bn(dh1, ws[0], list(x.shape), s, p, d, dz3, None, None, None, res_mask, False,
                                                li.mask)
                 else:
