@@ -55,6 +55,7 @@ constexpr double kBw = 4.0e12;    // slab write + finalize read bandwidth
 constexpr double kLaunch = 3.0e-6;
 
 int g_force_cfg = -1, g_force_splits = -1;
+bool g_budget_tail = [] { const char* e = getenv("DPE_HGEMM_BUDGET_TAIL"); return !(e && e[0] == '0'); }();  // A/B
 bool g_dynamic = [] { const char* e = getenv("DPE_HGEMM_DYNAMIC"); return !(e && e[0] == '0'); }();  // A/B
 
 // Dynamic-schedule state of the persistent GEMM (hgemm.hip: 8 per-XCD claim counters + exit
@@ -63,7 +64,7 @@ bool g_dynamic = [] { const char* e = getenv("DPE_HGEMM_DYNAMIC"); return !(e &&
 // Launches on different streams may overlap and get different buffers.  A stream first seen while
 // it is being captured into a graph gets none (its zeroing memset would only run at replay): such a
 // launch uses the static schedule.
-unsigned* sched_buffer(hipStream_t st) {
+unsigned* sched_buffer_impl(hipStream_t st) {
   if (!g_dynamic) return nullptr;
   static std::mutex mu;
   static std::unordered_map<uint64_t, unsigned*> bufs;
@@ -86,6 +87,8 @@ unsigned* sched_buffer(hipStream_t st) {
   return b;
 }
 }  // namespace
+
+unsigned* sched_buffer(hipStream_t st) { return sched_buffer_impl(st); }
 
 int num_cus() {
   static const int n = [] {
@@ -142,6 +145,11 @@ Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int
       const double t_unit = 2.0 * c.bm * c.bn * kt * 64 / rate_blk + kEpi * c.bm * c.bn * (s > 1 ? 4 : out_bytes) *
                                                                           (alone ? 1 : c.bpc);
       double t = rounds * t_unit + kFix;
+      // CU budget in force (collectives in flight): a foreign workgroup fits beside our blocks and slows
+      // the CU it shares, so the launch ends about one unit after its even share (the dynamic claims
+      // balance everything but the last unit): favour more, shorter units.  Unchanged without a budget.
+      // (whole-K plans only: with K splits the shorter units would buy balance with slab traffic)
+      if (reserve > 0 && g_budget_tail && s == 1) t += t_unit;
       if (s > 1) t += ((double)s * M * N * 4 * 2 + (double)M * N * out_bytes) / kBw + kLaunch;
       if (t < best.est_s * 0.995) best = Plan{c.cfg, s, (int)(kt * 64), (int)std::min<int64_t>(units, slots), t};
     }
@@ -206,7 +214,7 @@ void launch_planned(dpe::HgemmArgs a, const Plan& pl, int ak, int bk, int epi, h
   a.splits = pl.splits;
   a.kps = pl.kps;
   if (a.group_m == 0) a.group_m = group_rows(pl);
-  a.sched = sched_buffer(cur_stream());
+  a.sched = sched_buffer_impl(cur_stream());
   Tensor ws;
   if (pl.splits > 1) {
     // one allocation: [splits][M][N] partial slabs (+ [splits][M] bias-gradient partials)
@@ -297,6 +305,18 @@ Plan plan_bnb(int64_t M, int64_t N, int64_t K, int ak, int bk, int* partial_cols
   wr = pl.cfg == dpe::HC_256x128 ? 4 : 2;  // wave rows of the configuration (hgemm.h HCfg)
   *partial_cols = pl.cfg >= 0 ? (int)((M + bm - 1) / bm) * wr : 0;
   return pl;
+}
+
+void run_conv_wgrad(dpe::HgemmArgs& a, hipStream_t fin_stream) {
+  // one launch (no two-launch split: a column cut would shift the implicit im2col's tap / channel origin)
+  const Plan pl = plan(a.M, a.N, a.K, 0, 0, true, 4);
+  TORCH_CHECK(pl.cfg == dpe::HC_256x256, "hgemm conv weight grad: no plan");
+  launch_planned(a, pl, 0, 0, dpe::HE_ACC_F32, fin_stream);
+}
+
+void launch_plain(dpe::HgemmArgs& a, const Plan& pl, int ak, int bk) {
+  TORCH_CHECK(pl.cfg >= 0 && pl.splits == 1, "hgemm: bad single-launch plan");
+  launch_planned(a, pl, ak, bk, dpe::HE_BF16, nullptr);
 }
 
 void run_bnb(dpe::HgemmArgs& a, const Plan& pl, int ak, int bk) {
@@ -405,7 +425,7 @@ Tensor hgemm_raw(const Tensor& A, const Tensor& B, Tensor C, int64_t M, int64_t 
   a.splits = pl.splits;
   a.kps = pl.kps;
   a.group_m = group_m != 0 ? (int)group_m : group_rows(pl);
-  a.sched = sched_buffer(cur_stream());
+  a.sched = sched_buffer_impl(cur_stream());
   Tensor ws;
   if (pl.splits > 1) {
     const int64_t slab = (int64_t)pl.splits * M * N;
@@ -472,7 +492,7 @@ void linear_wgrad_group(const std::vector<Tensor>& dys, const std::vector<Tensor
   a.kps = (int)K;
   a.group_m = 4;
   const int slots = std::max(1, num_cus() - dpe_cu_reserve());
-  a.sched = sched_buffer(cur_stream());
+  a.sched = sched_buffer_impl(cur_stream());
   const int rc = dpe_hgemm_group_launch(&a, std::min(tiles, slots), cur_stream());
   const hipError_t e = hipGetLastError();
   TORCH_CHECK(rc == 0 && e == hipSuccess, "hgemm group launch failed rc=", rc, " ", hipGetErrorString(e));

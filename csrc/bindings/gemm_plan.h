@@ -25,6 +25,11 @@ struct Plan2 {
 };
 
 int num_cus();
+// The per-(device, stream) zeroed claim-counter buffer of the dynamic schedules (HGEMM_SCHED_BYTES; the
+// persistent GEMM's and the streaming pointwise conv's -- launches on one stream are ordered and each
+// leaves it zeroed), or nullptr (dynamic schedules off, or the stream is being captured).
+#include <hip/hip_runtime.h>
+unsigned* sched_buffer(hipStream_t st);
 bool layout_ok(int cfg, int ak, int bk);
 // out_bytes: bytes per output element of the final epilogue (slab traffic estimate)
 Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int out_bytes, int force_cfg = -1,
@@ -39,5 +44,10 @@ int run(dpe::HgemmArgs& a, int ak, int bk, int epi, bool allow_split, int out_by
 // plan and the number of partial columns it writes (tile rows x wave rows); run_bnb launches it.
 Plan plan_bnb(int64_t M, int64_t N, int64_t K, int ak, int bk, int* partial_cols);
 void run_bnb(dpe::HgemmArgs& a, const Plan& pl, int ak, int bk);  // a.act: HACT_BNB (default) or HACT_BNF
+// dW (+)= dy^T im2col(x) (a.conv = 2: the TN layout with an implicit-im2col B), planned and launched in one
+// piece (K-split slabs + finalize when the planner splits; fin_stream as run()).
+void run_conv_wgrad(dpe::HgemmArgs& a, hipStream_t fin_stream);
+// A plan's single launch, bf16 out, no epilogue extras (the implicit-im2col convs without statistics).
+void launch_plain(dpe::HgemmArgs& a, const Plan& pl, int ak, int bk);
 
 }  // namespace dpe_gemm

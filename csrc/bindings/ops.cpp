@@ -69,7 +69,8 @@ int dpe_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
 int dpe_act(const void* a, const void* b, void* out, int64_t n, int op, int bf16, hipStream_t st);
 int dpe_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, uint64_t offset, int bf16, hipStream_t st);
 int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, int vgprs, const unsigned* stop, float* sink,
-               int sleepy, hipStream_t st);
+               int sleepy, float* buf, hipStream_t st);
+int64_t dpe_cu_hog_buf_floats(int nblocks);
 int dpe_hog_stop(unsigned* stop, unsigned v, hipStream_t st);
 int dpe_conv3x3_rows_blocks(int N, int H, int W);
 int dpe_wgrad3x3_rows_blocks(int N, int H, int W);
@@ -150,7 +151,9 @@ Cfg pick_cfg(int64_t M, int64_t N, int64_t K, bool allow_split) {
     // worse, docs/perf_notes.md); the LDS-DMA im2col weight-grad kernel re-derives its split (run_igemm)
     // (at the CU budget -- an overlapped RCCL collective holding `reserve` slots -- a slot fewer per
     // reserved workgroup, so the split still fits one resident wave: SURVEY §5.8 item 7)
-    const int64_t target_blocks = std::max<int64_t>(64, 2 * (int64_t)dpe_gemm::num_cus() - dpe_cu_reserve());
+    // (budget in force: two such rounds, as the LDS-DMA weight grads in run_igemm)
+    const int64_t target_blocks =
+        std::max<int64_t>(64, (dpe_cu_reserve() > 0 ? 2 : 1) * (2 * (int64_t)dpe_gemm::num_cus() - dpe_cu_reserve()));
     const int64_t per = dpe_cu_reserve() > 0 ? target_blocks / t : (target_blocks + t - 1) / t;
     int64_t splits = std::max<int64_t>(1, std::min<int64_t>(per, ksteps / 8));
     const int64_t kps = (ksteps + splits - 1) / splits;
@@ -222,7 +225,8 @@ void dma_tile(const dpe::IgemmArgs& a, int aload, int bload, int& bm, int& bn) {
   else if (mode >= 2 && a.N > 64) { bm = 256; bn = 128; }
 }
 
-void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_split, bool conv = false) {
+void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_split, bool conv = false,
+               bool deterministic = false) {
   Cfg c = pick_cfg(a.M, a.N, a.K, allow_split && epi == dpe::EPI_ATOMIC_F32);
   a.k_split = c.k_split;
   // weight grads over an im2col B (3x3 / strided; split-K fp32 atomics): LDS-DMA kernel, measured 1.3-1.5x
@@ -241,7 +245,13 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
       // comm.cpp): a split that needs more blocks than fit beside the collective's workgroups runs a
       // second, nearly empty wave (x1.56-1.60 per kernel next to 16 RCCL-sized workgroups,
       // profiles/cu_hog_probe_r3.txt).  Rounded down, so tiles x splits <= the target.
-      const int64_t dma_target = std::max<int64_t>(64, 3 * (int64_t)dpe_gemm::num_cus() - dpe_cu_reserve());
+      // With a CU budget in force the split targets TWO rounds of blocks: foreign workgroups do not take
+      // our slots away (they fit beside them) but slow the CUs they share, and with one round the
+      // slowest CU set the kernel's time (x1.27 next to 16 VALU-bound hogs, profiles/cu_hog_probe_r4.txt);
+      // with two, the dispatcher gives those CUs fewer blocks.
+      static const bool two_rounds = [] { const char* e = getenv("DPE_WGRAD_TWO_ROUNDS"); return !(e && e[0] == '0'); }();
+      const int rsv = dpe_cu_reserve();
+      const int64_t dma_target = std::max<int64_t>(64, (rsv > 0 && two_rounds ? 2 : 1) * (3 * (int64_t)dpe_gemm::num_cus() - rsv));
       const int64_t t = (int64_t)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn), ksteps = (a.K + 31) / 32;
       const int64_t rs = dpe_cu_reserve() > 0 ? dma_target / t : (dma_target + t - 1) / t;  // (unchanged at no reserve)
       const int64_t sp = std::max<int64_t>(1, std::min<int64_t>(rs, ksteps / 8));
@@ -260,8 +270,22 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
       a.k_split = (int)(kps * 32);
       splits = (int)((ksteps + kps - 1) / kps);
     }
+    Tensor slab;
+    if (deterministic && splits > 1) {
+      // split partials stored to slabs, summed in split order below (no atomics: bitwise reproducible)
+      slab = at::empty({(int64_t)splits * a.M * a.N}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA));
+      a.slab = fp(slab);
+    }
     const int rc = dpe_igemm_wgrad_dma_launch(&a, bm, bn, bload, splits, cur_stream());
-    TORCH_CHECK(rc == 0 || !a.b_coef, "weight grad with BN on load: outside the LDS-DMA kernel's envelope (rc=", rc, ")");
+    a.slab = nullptr;
+    TORCH_CHECK(rc == 0 || (!a.b_coef && !deterministic),
+                "weight grad with BN on load / deterministic: outside the LDS-DMA kernel's envelope (rc=", rc, ")");
+    if (rc == 0 && slab.defined()) {
+      dpe::HgemmArgs f;
+      memset(&f, 0, sizeof(f));
+      f.C = a.C; f.ws = fp(slab); f.M = a.M; f.N = a.N; f.ldc = a.ldc; f.splits = splits; f.alpha = 1.f;
+      CHECK_RC(dpe_hgemm_finalize(&f, dpe::HE_ACC_F32, cur_stream()), "weight-grad slab finalize");
+    }
     a.k_split = c.k_split;  // (register-staged fallback uses pick_cfg's split)
     if (rc == 0) {
       const hipError_t e = hipGetLastError();
@@ -560,6 +584,45 @@ bool wgrad_hgemm_on() {
 }
 void set_wgrad_hgemm(bool on) { g_wgrad_hgemm = on ? 1 : 0; }
 
+// Forward-form convolutions with taps (3x3, stride 1 or 2, and the stride-1 data grads run as forward
+// convs of dy with the flipped filter) and >= 256 output channels on the persistent GEMM with an
+// implicit-im2col A (hgemm.hip AC): its BK-64 ping-pong schedule ran the dense GEMMs of these shapes at
+// 818-1,102 TF where the implicit-GEMM kernel ran them at 668-829 (profiles/conv_as_gemm_r3.jsonl);
+// with 128 output channels the 256-wide tiles lose (481 vs 680 TF), so those stay.
+// DPE_HGEMM_CONV=0 (or set_hgemm_conv(false)): the implicit-GEMM kernel (A/B, tests).
+int g_hgemm_conv = [] { const char* e = getenv("DPE_HGEMM_CONV"); return (e && e[0] == '0') ? 0 : 1; }();
+void set_hgemm_conv(bool on) { g_hgemm_conv = on ? 1 : 0; }
+bool hconv_ok(const dpe::ConvGeom& f, int64_t nout) {
+  if (!g_hgemm_conv || f.R * f.S <= 1 || f.R * f.S > 32 || f.C < 64 || (f.C & (f.C - 1)) || nout < 256 || nout % 8) return false;
+  const int64_t abytes = (((int64_t)f.N * f.H * f.W * f.C) + ((int64_t)f.ph * f.W + f.pw) * f.C) * 2;
+  return abytes < (1ll << 31) - 4096 && (int64_t)f.N * f.OH * f.OW < (1ll << 31);
+}
+// y [M = N*OH*OW][nout] = im2col(x) . w^T with the BN-forward sums (act HACT_BNF) or the BN-backward
+// partials of dL/d relu(BN(st_x)) (HACT_BNB) or neither (ACT_NONE); stats sized by the plan.  Returns
+// false when no plan fits.
+bool run_hconv(const uint16_t* x, const uint16_t* w, uint16_t* y, const dpe::ConvGeom& f, int64_t nout, int act,
+               const Tensor& like, Tensor* stats, const uint16_t* st_x, const float* st_coef) {
+  const int64_t M = (int64_t)f.N * f.OH * f.OW, K = (int64_t)f.R * f.S * f.C;
+  int pcols = 0;
+  const auto pl = dpe_gemm::plan_bnb(M, nout, K, 1, 1, &pcols);
+  if (pl.cfg < 0 || pl.splits != 1 || pcols <= 0) return false;
+  auto h = hargs();
+  h.A = x; h.B = w; h.C = y;
+  h.M = (int)M; h.N = (int)nout; h.K = (int)K;
+  h.lda = K; h.ldb = K; h.ldc = nout;
+  h.conv = 1; h.conv_g = f; h.conv_smagic = (65536 + f.S - 1) / f.S;
+  h.act = act;
+  if (act != dpe::ACT_NONE) {
+    *stats = at::empty({2, nout, pcols}, like.options().dtype(at::kFloat));
+    h.col_stats = fp(*stats); h.stats_ld = pcols;
+    h.st_x = st_x; h.st_coef = st_coef;
+    dpe_gemm::run_bnb(h, pl, 1, 1);
+  } else {
+    dpe_gemm::launch_plain(h, pl, 1, 1);
+  }
+  return true;
+}
+
 // DPE_HGEMM_DGRAD=0: 1x1 convs (data grads, and forwards with BN statistics) with K >= 1024 stay on the
 // implicit-GEMM kernel (A/B reference)
 bool hgemm_dgrad_on() {
@@ -627,7 +690,7 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
     dpe::PwArgs pa{};
     pa.x = bp(x); pa.w = bp(w); pa.y = bpm(y); pa.stats = want_stats ? fp(stats) : nullptr;
     pa.in_coef = icoef;
-    pa.M = a.M; pa.N = a.N; pa.K = a.K; pa.rg = pw_rg;
+    pa.M = a.M; pa.N = a.N; pa.K = a.K; pa.rg = pw_rg; pa.sched = dpe_gemm::sched_buffer(cur_stream());
     CHECK_RC(dpe_pw_launch(&pa, dpe::PW_FWD, cur_stream()), "pw_stream fwd");
     return {y, stats};
   }
@@ -650,6 +713,9 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
       return {y, stats};
     }
   }
+  if (!is_pointwise(g) && !a.bias && !icoef && hconv_ok(g, a.N) &&
+      run_hconv(bp(x), bp(w), bpm(y), g, a.N, want_stats ? dpe::HACT_BNF : dpe::ACT_NONE, x, &stats, nullptr, nullptr))
+    return {y, stats};
   if (want_stats) {
     // [2][K][tilesM] partial (sum, sumsq) per output channel and M-tile, reduced by bn_fwd_train
     const Cfg c = pick_cfg(a.M, a.N, a.K, false);
@@ -754,7 +820,7 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
     pa.residual = a.residual; pa.res_mask = a.res_mask;
     if (res_stride2) { pa.res_h = g.H; pa.res_w = g.W; }
     pa.st_mask = (const uint8_t*)sum_mask->data_ptr();
-    pa.M = a.M; pa.N = a.N; pa.K = a.K; pa.rg = rg;
+    pa.M = a.M; pa.N = a.N; pa.K = a.K; pa.rg = rg; pa.sched = dpe_gemm::sched_buffer(cur_stream());
     part = at::empty({2, g.C, rg}, dy.options().dtype(at::kFloat));
     pa.stats = fp(part);
     CHECK_RC(dpe_pw_launch(&pa, dpe::PW_DSUM, cur_stream()), "pw_stream dgrad (sum dz)");
@@ -766,7 +832,7 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
     pa.residual = a.residual; pa.res_mask = a.res_mask;
     if (res_stride2) { pa.res_h = g.H; pa.res_w = g.W; }
     pa.st_x = a.st_x; pa.st_coef = a.st_coef; pa.st_mask = a.st_mask;
-    pa.M = a.M; pa.N = a.N; pa.K = a.K; pa.rg = pw_rg;
+    pa.M = a.M; pa.N = a.N; pa.K = a.K; pa.rg = pw_rg; pa.sched = dpe_gemm::sched_buffer(cur_stream());
     if (want_bn) {
       part = at::empty({2, g.C, pw_rg}, dy.options().dtype(at::kFloat));
       pa.stats = fp(part);
@@ -810,6 +876,9 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
                "conv3x3 rows dgrad");
       return {dx, part};
     }
+    if (!acc_into && !a.residual && !a.st_mask && !a.res_mask && hconv_ok(f, g.C) &&
+        run_hconv(bp(dy), bp(wt), bpm(dx), f, g.C, want_bn ? dpe::HACT_BNB : dpe::ACT_NONE, dy, &part, a.st_x, a.st_coef))
+      return {dx, part};
     auto b = a;
     b.g = f;
     b.B = bp(wt);
@@ -907,7 +976,8 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape
 // dw [K,R,S,C] fp32 (+)= alpha * dy^T (x) im2col(x)
 // in_coef: as conv_fwd's (x pre-BN, BN+ReLU applied on load; row-walking 64-channel 3x3 kernel only)
 void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64_t> stride, std::vector<int64_t> pad,
-                std::vector<int64_t> dil, double alpha, const c10::optional<Tensor>& in_coef, int64_t fin_stream) {
+                std::vector<int64_t> dil, double alpha, const c10::optional<Tensor>& in_coef, int64_t fin_stream,
+                bool deterministic) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(x); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
   auto g = geom(x, dw, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], dy.size(1), dy.size(2));
   TORCH_CHECK(dy.size(3) == g.K && dy.size(0) == g.N, "conv_wgrad: dy shape mismatch");
@@ -926,7 +996,7 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64
     // B fragments (b_coef); outside that kernel's envelope there is no such path
     TORCH_CHECK(is_pointwise(g), "conv_wgrad: in_coef needs a 1x1 conv or the row-walking 64-channel 3x3 kernel");
     a.b_coef = icoef;
-    run_igemm(a, dpe::A_DENSE_M, dpe::B_DENSE_N, dpe::EPI_ATOMIC_F32, true, true);
+    run_igemm(a, dpe::A_DENSE_M, dpe::B_DENSE_N, dpe::EPI_ATOMIC_F32, true, true, deterministic);
     return;
   }
   if (row && (row_wgrad_on() || icoef)) {
@@ -959,6 +1029,22 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64
     h.a_dim = (int)((g.K + 7) / 8 * 8);
     h.alpha = (float)alpha;
     dpe_gemm::run(h, 0, 0, dpe::HE_ACC_F32, true, 4, (hipStream_t)(uintptr_t)fin_stream);
+    return;
+  }
+  // 3x3 weight grads with >= 256 output channels (layers 3-4): the persistent GEMM's TN layout with an
+  // implicit-im2col B (hgemm.hip CV = 2); dense TN GEMMs of these shapes ran at 846-960 TF where the
+  // LDS-DMA im2col weight grad ran them at 648-748 (profiles/wgrad_as_gemm_r4.jsonl).  Split-K partials
+  // in slabs summed in a fixed order (no atomics).  Not with BN-on-load inputs (none at these shapes).
+  if (g_hgemm_conv && !is_pointwise(g) && g.K >= 256 && g.K % 8 == 0 && g.C >= 8 && (g.C & (g.C - 1)) == 0 &&
+      a.K % 64 == 0 && a.K < (1 << 24) && g.R * g.S <= 32 &&
+      (((int64_t)g.N * g.H * g.W * g.C) + ((int64_t)g.ph * g.W + g.pw) * g.C) * 2 < (1ll << 31) - 4096) {
+    auto h = hargs();
+    h.A = bp(dy); h.B = bp(x); h.C = dw.data_ptr();
+    h.M = a.M; h.N = a.N; h.K = a.K;
+    h.lda = g.K; h.ldb = a.N; h.ldc = a.N;
+    h.alpha = (float)alpha;
+    h.conv = 2; h.conv_g = g; h.conv_smagic = (65536 + g.S - 1) / g.S;
+    dpe_gemm::run_conv_wgrad(h, (hipStream_t)(uintptr_t)fin_stream);
     return;
   }
   run_igemm(a, dpe::A_DENSE_M, is_pointwise(g) ? dpe::B_DENSE_N : dpe::B_CONV_WGRAD, dpe::EPI_ATOMIC_F32, true, true);
@@ -1099,7 +1185,7 @@ std::vector<Tensor> conv1x1_apply(const Tensor& x, const Tensor& w, const c10::o
   pa.residual = bp(residual);
   pa.res_coef = fpo(res_coef);
   pa.out_bits = (uint8_t*)bits.data_ptr();
-  pa.M = M; pa.N = N; pa.K = K; pa.rg = rg;
+  pa.M = M; pa.N = N; pa.K = K; pa.rg = rg; pa.sched = dpe_gemm::sched_buffer(cur_stream());
   CHECK_RC(dpe_pw_launch(&pa, dpe::PW_APPLY, cur_stream()), "pw_stream apply");
   return {y, bits};
 }
@@ -1739,7 +1825,9 @@ void register_ops(pybind11::module& m) {
         py::arg("dil"), py::arg("residual") = py::none(), py::arg("residual_mask") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), py::arg("alpha") = 1.0, py::arg("in_coef") = py::none(), py::arg("fin_stream") = 0,
-        "dw (+)= alpha dW; fin_stream: a K-split hgemm's slab reduction runs on that stream (caller orders consumers)");
+        py::arg("deterministic") = false,
+        "dw (+)= alpha dW; fin_stream: a K-split hgemm's slab reduction runs on that stream (caller orders consumers); "
+        "deterministic: 1x1 weight grads over a pre-BN input sum their K splits in a fixed order (no atomics)");
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),
         py::arg("momentum"), py::arg("eps"), py::arg("relu"), py::arg("residual") = py::none(), py::arg("stats") = py::none());
   m.def("bn_fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),
@@ -1775,20 +1863,24 @@ void register_ops(pybind11::module& m) {
         py::arg("dw"), py::arg("db") = py::none(), py::arg("dx_out") = py::none());
   m.def("set_pw_stream", &set_pw_stream, "streaming pointwise-conv kernel on/off (pwconv.hip)");
   m.def("cu_hog", [](int64_t nblocks, int64_t threads, int64_t lds_bytes, double us, int64_t vgprs,
-                     const c10::optional<Tensor>& stop, bool sleepy) {
+                     const c10::optional<Tensor>& stop, bool sleepy, int64_t mode) {
           static Tensor sink = at::empty({1024}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA));
+          static Tensor buf;
+          const int md = mode >= 0 ? (int)mode : (sleepy ? 1 : 0);
+          if (md == 2 && (!buf.defined() || buf.numel() < dpe_cu_hog_buf_floats((int)nblocks)))
+            buf = at::zeros({dpe_cu_hog_buf_floats((int)nblocks)}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA));
           const unsigned* sp = nullptr;
           if (stop.has_value() && stop->defined()) {
             TORCH_CHECK(stop->is_cuda() && stop->scalar_type() == at::kInt && stop->numel() >= 1, "cu_hog: stop is an int32 GPU tensor");
             sp = (const unsigned*)stop->data_ptr();
           }
           CHECK_RC(dpe_cu_hog((int)nblocks, (int)threads, (int)lds_bytes, us, (int)vgprs, sp, (float*)sink.data_ptr(),
-                              sleepy ? 1 : 0, cur_stream()),
+                              md, md == 2 ? (float*)buf.data_ptr() : nullptr, cur_stream()),
                    "cu_hog");
         }, py::arg("nblocks"), py::arg("threads") = 256, py::arg("lds_bytes") = 0, py::arg("us") = 1000.0,
-        py::arg("vgprs") = 8, py::arg("stop") = py::none(), py::arg("sleepy") = false,
+        py::arg("vgprs") = 8, py::arg("stop") = py::none(), py::arg("sleepy") = false, py::arg("mode") = -1,
         "occupancy probe: nblocks workgroups holding a CU slot (threads, LDS, ~vgprs per lane) until stop[0] != 0 or `us` "
-        "microseconds pass (current stream)");
+        "microseconds pass (current stream); mode 0 VALU-bound, 1 idle (= sleepy), 2 RCCL-like reduce-copy streaming");
   m.def("hog_stop", [](Tensor& stop, int64_t v) {
           TORCH_CHECK(stop.is_cuda() && stop.scalar_type() == at::kInt, "hog_stop: int32 GPU tensor");
           CHECK_RC(dpe_hog_stop((unsigned*)stop.data_ptr(), (unsigned)v, cur_stream()), "hog_stop");
@@ -1797,6 +1889,8 @@ void register_ops(pybind11::module& m) {
   m.def("set_rowconv", &set_rowconv, "64-channel 3x3 convs on the row-walking kernel (rowconv.hip) on/off");
   m.def("set_stem_kernel", &set_stem_kernel, "s2d stem conv on its row-walking kernel (stem.hip) on/off");
   m.def("set_wgrad_hgemm", &set_wgrad_hgemm, "1x1 conv weight grads on the persistent hgemm kernel on/off");
+  m.def("set_hgemm_conv", &set_hgemm_conv,
+        "3x3 forward-form convs with >= 256 output channels on the persistent GEMM (implicit im2col A) on/off");
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("H"), py::arg("scale"), py::arg("causal") = true);
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"), py::arg("H"),
         py::arg("scale"), py::arg("causal") = true);

@@ -382,15 +382,32 @@ extern "C" int dpe_embedding_bwd(const int64_t* idx, const float* dout, float* d
 // until `stop` becomes non-zero or `ticks` of the 100 MHz wall clock pass -- a stand-in for RCCL's
 // channel workgroups sharing the CUs with backward kernels (scripts/hog_probe.py).  Every wave leaves
 // at the deadline, so a stop flag that is never set cannot hang the device.
+// mode 0: VALU-saturating (worst case); 1: resident but idle; 2: RCCL-like reduce-copy -- each block
+// streams its own window of `buf` (dst = src0 + src1 over HOG_WIN floats, the shape of an all-reduce
+// channel's inner loop), memory-bound with little VALU.
+constexpr int64_t HOG_WIN = 1 << 20;  // floats per block and operand (4 MiB)
 template <int V>
-__global__ __launch_bounds__(256) void cu_hog_kernel(int64_t ticks, const unsigned* stop, float* sink, int sleepy) {
+__global__ __launch_bounds__(256) void cu_hog_kernel(int64_t ticks, const unsigned* stop, float* sink, int sleepy,
+                                                     float* buf) {
   extern __shared__ float lds[];
   const int64_t t0 = wall_clock64();
   float r[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) r[i] = (float)(threadIdx.x + i);
+  int64_t pos = 0;
+  float* const w0 = buf ? buf + (int64_t)blockIdx.x * 3 * HOG_WIN : nullptr;
   while (wall_clock64() - t0 < ticks) {
-    if (sleepy) {  // resident but idle: slot occupancy only (an RCCL block waiting on its peers)
+    if (sleepy == 2 && w0) {
+      // 64 KiB per operand per trip: two reads and one write of f32x4 per thread x 16
+#pragma unroll 4
+      for (int k = 0; k < 16; ++k) {
+        const int64_t i = (pos + (int64_t)k * blockDim.x + threadIdx.x) * 4;
+        const f32x4 a = *(const f32x4*)(w0 + i), b = *(const f32x4*)(w0 + HOG_WIN + i);
+        *(f32x4*)(w0 + 2 * HOG_WIN + i) = a + b;
+      }
+      pos += 16 * blockDim.x;
+      if ((pos + 16 * blockDim.x) * 4 > HOG_WIN) pos = 0;
+    } else if (sleepy) {  // resident but idle: slot occupancy only (an RCCL block waiting on its peers)
       __builtin_amdgcn_s_sleep(127);
     } else {       // VALU-saturating: slot occupancy plus issue-cycle contention (worst case)
 #pragma unroll 1
@@ -409,14 +426,17 @@ __global__ __launch_bounds__(256) void cu_hog_kernel(int64_t ticks, const unsign
 __global__ void hog_stop_kernel(unsigned* stop, unsigned v) {
   __hip_atomic_store(stop, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// buf (mode 2): >= nblocks * 3 * HOG_WIN floats
+extern "C" int64_t dpe_cu_hog_buf_floats(int nblocks) { return (int64_t)nblocks * 3 * HOG_WIN; }
 extern "C" int dpe_cu_hog(int nblocks, int threads, int lds_bytes, double us, int vgprs, const unsigned* stop, float* sink,
-                          int sleepy, hipStream_t st) {
+                          int sleepy, float* buf, hipStream_t st) {
   if (nblocks <= 0 || threads <= 0 || threads > 256 || us <= 0 || us > 1e6) return -1;  // RCCL-sized: 256 threads
+  if (sleepy == 2 && (!buf || threads % 64)) return -1;
   const int64_t t = (int64_t)(us * 100.0);
-  if (vgprs <= 16) hipLaunchKernelGGL(cu_hog_kernel<8>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink, sleepy);
-  else if (vgprs <= 64) hipLaunchKernelGGL(cu_hog_kernel<56>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink, sleepy);
-  else if (vgprs <= 128) hipLaunchKernelGGL(cu_hog_kernel<120>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink, sleepy);
-  else hipLaunchKernelGGL(cu_hog_kernel<136>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink, sleepy);  // RCCL: 140
+  if (vgprs <= 16) hipLaunchKernelGGL(cu_hog_kernel<8>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink, sleepy, buf);
+  else if (vgprs <= 64) hipLaunchKernelGGL(cu_hog_kernel<56>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink, sleepy, buf);
+  else if (vgprs <= 128) hipLaunchKernelGGL(cu_hog_kernel<120>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink, sleepy, buf);
+  else hipLaunchKernelGGL(cu_hog_kernel<136>, dim3(nblocks), dim3(threads), lds_bytes, st, t, stop, sink, sleepy, buf);  // RCCL: 140
   return (int)hipGetLastError();
 }
 extern "C" int dpe_hog_stop(unsigned* stop, unsigned v, hipStream_t st) {

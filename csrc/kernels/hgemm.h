@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "igemm.h"  // ConvGeom
+
 namespace dpe {
 
 // Epilogue of one output tile (or K-split partial of it).
@@ -70,6 +72,12 @@ struct HgemmArgs {
   // HE_GROUP: the problems (A, B, C, M, N, lda, ldb, ldc, a_dim, dbias above are ignored)
   int ngroup;
   HgemmProblem grp[HGEMM_MAX_GROUP];
+  // conv != 0 (K-contiguous A only): A is the implicit im2col of an NHWC tensor (conv_g: input N,H,W,C,
+  // output OH,OW, filter R,S, stride / pad / dilation): row m = (n, oh, ow), column k = (r, s, ci);
+  // C a power of two >= 64 (a 64-deep K-tile lies in one filter tap), conv_smagic = ceil(65536 / S)
+  int conv;
+  ConvGeom conv_g;
+  int conv_smagic;
 };
 
 // Tile configurations (BMxBN, waves WRxWC).

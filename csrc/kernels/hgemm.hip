@@ -97,6 +97,14 @@ DPE_DEVICE void glds(const char* src, char* dst) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory");
 }
 
+// LDS-DMA of one 16-B chunk per lane through a buffer resource (voffset past num_records -> zeros: the
+// implicit-im2col padding), same inline-asm reasoning as glds
+DPE_DEVICE void bdma16(__amdgpu_buffer_rsrc_t r, char* dst, uint32_t voff, uint32_t soff) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)dst);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               ::"s"(m0), "v"(voff), "s"(r), "s"(soff) : "memory");
+}
+
 // K-image fragment read, rows r0 + [0,16), k-step s
 DPE_DEVICE int kread_off(int r0, int s) {
   const int lane = threadIdx.x & 63;
@@ -167,9 +175,16 @@ DPE_DEVICE float gelu_grad(float x) {
 // db[m] += alpha * sum_k A[k][m] -- the units of the first tile column sum the A fragments they
 // already hold in registers (wave wc takes fragment row-block wc, v_dot2 with ones: 8 VALU per half
 // image per K-tile), so dy is not streamed a second time by a column-sum kernel.
-template <int BM, int BN, int WR, int WC, bool AK, bool BK, int EPI, int ACT, bool BG = false>
+// AC: A is the implicit im2col of an NHWC conv input (HgemmArgs::conv; K-contiguous A): the A half images
+// are staged by buffer_load ... lds with per-row tap-validity masks (padding reads as zeros) and the
+// K-tile's filter-tap offset in soffset -- the forward-form 3x3 convolutions on this kernel's schedule.
+// CV = 2 (BC): B is the implicit im2col of an NHWC conv input in the TN weight-grad layout (B[k][n], k = output
+// pixel, n = (r, s, ci); N-contiguous): every lane's 16-B chunk is one (tap, 8 channels) column for the whole
+// unit, and its pixel row is decomposed per K-tile (padding and the pixel tail read as zeros).
+template <int BM, int BN, int WR, int WC, bool AK, bool BK, int EPI, int ACT, bool BG = false, int CV = 0>
 // (4-wave tiles run 2 blocks per CU: 2 waves per SIMD, so at most 256 VGPRs + AGPRs per wave)
 __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kernel(HgemmArgs p) {
+  constexpr bool AC = CV == 1, BC = CV == 2;
   using G = Geo<BM, BN, WR, WC>;
   constexpr int NW = G::NW, RH = G::RH, CH = G::CH, FMH = G::FMH, FNH = G::FNH, GA = G::GA, GB = G::GB;
   constexpr int AHB = G::AHB, BHB = G::BHB;
@@ -305,6 +320,18 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
       rb[j][s] = G::B_REGION + (BK ? kread_off(wc * CH + j * 16, s) : mnread_off(wc * CH + j * 16) + s * 8192);
 
   uint32_t ga[2][GA], gb[2][GB];
+  uint32_t gam[2][AC ? GA : 1];  // AC: per-row tap-validity masks of the A pieces
+  uint32_t gbt[2][BC ? GB : 1];  // BC: per-column tap displacement (r dh - ph, s dw - pw) as two int16
+  static_assert(!AC || AK, "implicit-im2col A is K-contiguous");
+  static_assert(!BC || (!AK && !BK && !GRP), "implicit-im2col B: the TN weight-grad layout");
+  const ConvGeom& cg = p.conv_g;
+  // (the conv resource is built for every instantiation -- unused without CV -- as it has no null value)
+  const int64_t apre = CV ? ((int64_t)cg.ph * cg.W + cg.pw) * cg.C : 0;  // every in-range tap offset >= 0
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>((const void*)((const uint16_t*)(BC ? p.B : p.A) - apre)), (short)0,
+      CV ? (int)((((int64_t)cg.N * cg.H * cg.W * cg.C) + apre) * 2) : 0, 0x00020000);
+  const int cshift = CV ? 31 - __builtin_clz(cg.C) : 0;
+  const float inv_ow = BC ? 1.f / (float)cg.OW : 0.f, inv_hw = BC ? 1.f / (float)(cg.OH * cg.OW) : 0.f;
   int m0, n0, kb, nt, split;
   // Grouped tile order: consecutive unit ids (which run together on one XCD -- xcd_remap) walk
   // GROUP_M tile rows before moving one tile column, so an XCD's concurrent tiles form a
@@ -339,27 +366,103 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
     n0 = (in / grows) * BN;
     kb = split * p.kps;
     nt = (min(p.K, kb + p.kps) - kb) / TK;
-    stage_setup<BM, WR, RH, GA, AK>(qlda, qadim > 0 ? qadim : qM, m0, AK ? kb : 0, ga);
-    stage_setup<BN, WC, CH, GB, BK>(qldb, p.b_dim > 0 ? p.b_dim : qN, n0, BK ? kb : 0, gb);
+    if constexpr (AC) {
+      // per A piece row: the input pixel of output row m (byte offset from the resource base) and the
+      // filter taps that stay inside the image
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < GA; ++i) {
+          const int r = 8 * (wid * GA + i) + (lane >> 3);
+          const int m = m0 + hmap<BM, WR, RH>(h, r);
+          const int ch = (lane & 7) ^ kswz(r);
+          uint32_t off = 0u, mask = 0u;
+          if (m < qM) {
+            const int ow = m % cg.OW, t = m / cg.OW, oh = t % cg.OH, n = t / cg.OH;
+            const int ih0 = oh * cg.sh - cg.ph, iw0 = ow * cg.sw - cg.pw;
+            off = (uint32_t)((((int64_t)n * cg.H + oh * cg.sh) * cg.W + ow * cg.sw) * cg.C * 2) + ch * 16u;
+            for (int rr = 0; rr < cg.R; ++rr) {
+              const bool vr = (unsigned)(ih0 + rr * cg.dh) < (unsigned)cg.H;
+              for (int ss = 0; ss < cg.S; ++ss)
+                if (vr && (unsigned)(iw0 + ss * cg.dw) < (unsigned)cg.W) mask |= 1u << (rr * cg.S + ss);
+            }
+          }
+          ga[h][i] = off;
+          gam[h][i] = mask;
+        }
+    } else {
+      stage_setup<BM, WR, RH, GA, AK>(qlda, qadim > 0 ? qadim : qM, m0, AK ? kb : 0, ga);
+    }
+    if constexpr (BC) {
+      // per B piece column chunk: its filter tap's byte offset + channel, and the tap's displacement
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < GB; ++i) {
+          const int k = 4 * (wid * GB + i) + (lane >> 4);
+          const int c = (lane & 15) ^ mnswz(k);
+          const int gc = n0 + hmap<BN, WC, CH>(h, c * 8);
+          uint32_t off = 0u, disp = 0x80008000u;  // invalid column: displacement never in range
+          if (gc < qN) {
+            const int tap = gc >> cshift, ci = gc & (cg.C - 1);
+            const int r = (tap * p.conv_smagic) >> 16, s = tap - r * cg.S;
+            off = (uint32_t)(((r * cg.dh * cg.W + s * cg.dw) << cshift) + ci) * 2u;
+            disp = ((uint32_t)(r * cg.dh - cg.ph) << 16) | ((uint32_t)(s * cg.dw - cg.pw) & 0xffffu);
+          }
+          gb[h][i] = off;
+          gbt[h][i] = disp;
+        }
+    } else {
+      stage_setup<BN, WC, CH, GB, BK>(qldb, p.b_dim > 0 ? p.b_dim : qN, n0, BK ? kb : 0, gb);
+    }
     if constexpr (GRP) {
       astep = AK ? (int64_t)TK * 2 : (int64_t)TK * qlda * 2;
       bstep = BK ? (int64_t)TK * 2 : (int64_t)TK * qldb * 2;
     }
     if constexpr (!AK) { for (int h = 0; h < 2; ++h) for (int i = 0; i < GA; ++i) ga[h][i] += (uint32_t)((int64_t)kb * qlda * 2); }
-    if constexpr (!BK) { for (int h = 0; h < 2; ++h) for (int i = 0; i < GB; ++i) gb[h][i] += (uint32_t)((int64_t)kb * qldb * 2); }
+    if constexpr (!BK && !BC) { for (int h = 0; h < 2; ++h) for (int i = 0; i < GB; ++i) gb[h][i] += (uint32_t)((int64_t)kb * qldb * 2); }
   };
 
 #define STAGE_A(h, buf, t)                                                                   \
   do {                                                                                       \
-    const char* b_ = Ab + (int64_t)(t) * astep;                                              \
-    _Pragma("unroll") for (int i_ = 0; i_ < GA; ++i_)                                        \
-      glds(b_ + ga[h][i_], wdA + ((buf) * 2 + (h)) * AHB + i_ * 1024);                       \
+    if constexpr (AC) {                                                                      \
+      const int k0_ = kb + (t) * TK, tap_ = k0_ >> cshift;                                   \
+      const int r_ = (tap_ * p.conv_smagic) >> 16, s_ = tap_ - r_ * cg.S;                    \
+      const uint32_t so_ = (uint32_t)(((r_ * cg.dh * cg.W + s_ * cg.dw) << cshift) + (k0_ & (cg.C - 1))) * 2u; \
+      _Pragma("unroll") for (int i_ = 0; i_ < GA; ++i_)                                      \
+        bdma16(arsrc, wdA + ((buf) * 2 + (h)) * AHB + i_ * 1024,                             \
+               ((gam[h][i_] >> tap_) & 1u) ? ga[h][i_] : 0x80000000u, so_);                  \
+    } else {                                                                                 \
+      const char* b_ = Ab + (int64_t)(t) * astep;                                            \
+      _Pragma("unroll") for (int i_ = 0; i_ < GA; ++i_)                                      \
+        glds(b_ + ga[h][i_], wdA + ((buf) * 2 + (h)) * AHB + i_ * 1024);                     \
+    }                                                                                        \
   } while (0)
 #define STAGE_B(h, buf, t)                                                                   \
   do {                                                                                       \
-    const char* b_ = Bb + (int64_t)(t) * bstep;                                              \
-    _Pragma("unroll") for (int i_ = 0; i_ < GB; ++i_)                                        \
-      glds(b_ + gb[h][i_], wdB + ((buf) * 2 + (h)) * BHB + i_ * 1024);                       \
+    if constexpr (BC) {                                                                      \
+      _Pragma("unroll") for (int i_ = 0; i_ < GB; ++i_) {                                    \
+        /* this lane's pixel row of the K-tile: (image, oh, ow) by float reciprocals, corrected */ \
+        const int px_ = kb + (t) * TK + 4 * (wid * GB + i_) + (lane >> 4);                   \
+        int img_ = (int)((float)px_ * inv_hw);                                               \
+        img_ -= img_ * cg.OH * cg.OW > px_;                                                  \
+        img_ += (img_ + 1) * cg.OH * cg.OW <= px_;                                           \
+        const int rem_ = px_ - img_ * cg.OH * cg.OW;                                         \
+        int oh_ = (int)((float)rem_ * inv_ow);                                               \
+        oh_ -= oh_ * cg.OW > rem_;                                                           \
+        oh_ += (oh_ + 1) * cg.OW <= rem_;                                                    \
+        const int ow_ = rem_ - oh_ * cg.OW;                                                  \
+        const int ih_ = oh_ * cg.sh + ((int)gbt[h][i_] >> 16);                               \
+        const int iw_ = ow_ * cg.sw + (int)(int16_t)(gbt[h][i_] & 0xffffu);                  \
+        const bool v_ = px_ < p.K && (unsigned)ih_ < (unsigned)cg.H && (unsigned)iw_ < (unsigned)cg.W; \
+        const uint32_t po_ = (uint32_t)((((int64_t)img_ * cg.H + oh_ * cg.sh) * cg.W + ow_ * cg.sw) << cshift) * 2u; \
+        bdma16(arsrc, wdB + ((buf) * 2 + (h)) * BHB + i_ * 1024, v_ ? po_ + gb[h][i_] : 0x80000000u, 0u); \
+      }                                                                                      \
+    } else {                                                                                 \
+      const char* b_ = Bb + (int64_t)(t) * bstep;                                            \
+      _Pragma("unroll") for (int i_ = 0; i_ < GB; ++i_)                                      \
+        glds(b_ + gb[h][i_], wdB + ((buf) * 2 + (h)) * BHB + i_ * 1024);                     \
+    }                                                                                        \
   } while (0)
 #if HG_SCHED == 1
   // tile 0 -> buf 0 (all halves), tile 1 -> buf 1 (A0, B1, A1; B0(1) is staged in tile 0's phase 1)
@@ -876,8 +979,38 @@ int launch_epi(const HgemmArgs& p, int epi, int grid, hipStream_t st) {
   return 0;
 }
 
+// implicit-im2col A (NT layout, bf16 out, no K split): plain, BN-forward or BN-backward partials epilogue
+template <int BM, int BN, int WR, int WC>
+int launch_conv(const HgemmArgs& p, int epi, int grid, hipStream_t st) {
+  if (epi != HE_BF16 || p.splits != 1 || p.dbias || p.bias) return -3;
+  const dim3 g((unsigned)grid), b(WR * WC * 64);
+#define HC(A) hipLaunchKernelGGL((hg::hgemm_kernel<BM, BN, WR, WC, true, true, HE_BF16, A, false, 1>), g, b, 0, st, p)
+  if (p.act == ACT_NONE) HC(ACT_NONE);
+  else if (p.act == HACT_BNF && p.col_stats) HC(HACT_BNF);
+  else if (p.act == HACT_BNB && p.col_stats && p.st_x && p.st_coef) HC(HACT_BNB);
+  else return -3;
+#undef HC
+  return 0;
+}
+
+// implicit-im2col B (TN weight grads, 256x256 only): K-split slabs or fp32 accumulate
+int launch_conv_wgrad(const HgemmArgs& p, int epi, int grid, hipStream_t st) {
+  if (p.act != ACT_NONE || p.dbias || p.bias) return -3;
+  const dim3 g((unsigned)grid), b(512);
+  if (epi == HE_SLAB) hipLaunchKernelGGL((hg::hgemm_kernel<256, 256, 2, 4, false, false, HE_SLAB, ACT_NONE, false, 2>), g, b, 0, st, p);
+  else if (epi == HE_ACC_F32 && p.splits == 1)
+    hipLaunchKernelGGL((hg::hgemm_kernel<256, 256, 2, 4, false, false, HE_ACC_F32, ACT_NONE, false, 2>), g, b, 0, st, p);
+  else return -3;
+  return 0;
+}
+
 template <int BM, int BN, int WR, int WC>
 int launch_layout(const HgemmArgs& p, int a_k, int b_k, int epi, int grid, hipStream_t st) {
+  if (p.conv == 2) {
+    if constexpr (BM == 256 && BN == 256) return (!a_k && !b_k) ? launch_conv_wgrad(p, epi, grid, st) : -2;
+    return -2;
+  }
+  if (p.conv) return (a_k && b_k) ? launch_conv<BM, BN, WR, WC>(p, epi, grid, st) : -2;
   if (a_k && b_k) return launch_epi<BM, BN, WR, WC, true, true>(p, epi, grid, st);
   if constexpr (BN == 256) {
     if (a_k && !b_k) return launch_epi<BM, BN, WR, WC, true, false>(p, epi, grid, st);
@@ -901,7 +1034,24 @@ extern "C" int dpe_hgemm_launch(const HgemmArgs* a, int cfg, int a_k, int b_k, i
   if (!b_k && (bdim % 8 || p.ldb < bdim)) return -1;
   if (p.lda % 8 || p.ldb % 8) return -1;
   // per-lane LDS-DMA source offsets are 32-bit
-  if ((a_k ? (int64_t)adim * p.lda : (int64_t)p.K * p.lda) * 2 >= (1ll << 32)) return -4;
+  if (p.conv == 1) {
+    const ConvGeom& g = p.conv_g;
+    if (!a_k || g.C < 64 || (g.C & (g.C - 1)) || g.R * g.S > 32 || g.R * g.S * g.C != p.K || p.kps != p.K ||
+        (int64_t)g.N * g.OH * g.OW != p.M || p.conv_smagic != (65536 + g.S - 1) / g.S)
+      return -1;
+    if ((((int64_t)g.N * g.H * g.W * g.C) + ((int64_t)g.ph * g.W + g.pw) * g.C) * 2 >= (1ll << 31) - 4096) return -4;
+  } else if (p.conv == 2) {
+    // pixel decomposition by float reciprocals: exact for pixel indices < 2^24 with the +-1 correction
+    const ConvGeom& g = p.conv_g;
+    if (a_k || b_k || g.C < 8 || (g.C & (g.C - 1)) || g.R * g.S > 32 || g.R * g.S * g.C != p.N ||
+        (int64_t)g.N * g.OH * g.OW != p.K || p.K >= (1 << 24) || p.conv_smagic != (65536 + g.S - 1) / g.S ||
+        g.ph > 32767 || g.pw > 32767)
+      return -1;
+    if ((((int64_t)g.N * g.H * g.W * g.C) + ((int64_t)g.ph * g.W + g.pw) * g.C) * 2 >= (1ll << 31) - 4096) return -4;
+    if ((int64_t)p.K * p.lda * 2 >= (1ll << 32)) return -4;
+  } else if ((a_k ? (int64_t)adim * p.lda : (int64_t)p.K * p.lda) * 2 >= (1ll << 32)) {
+    return -4;
+  }
   if ((b_k ? (int64_t)bdim * p.ldb : (int64_t)p.K * p.ldb) * 2 >= (1ll << 32)) return -4;
   switch (cfg) {
     case HC_256x256: return launch_layout<256, 256, 2, 4>(p, a_k, b_k, epi, grid, st);

@@ -93,6 +93,8 @@ struct IgemmArgs {
   uint8_t* a_bits;          // [M][lda/8] ReLU-mask bits of a_out (AX_BN_RES / _RES2), or nullptr
   int k1;                   // AX_CAT: K of the first segment (multiple of 32)
   int64_t lda2;             // AX_CAT: row stride of a2
+  float* slab;              // LDS-DMA weight grad only: EPI_ATOMIC_F32 partials STORED to slab[split][M][N]
+                            //   (summed in split order by a finalize pass: deterministic) instead of atomics
 };
 
 }  // namespace dpe

@@ -510,13 +510,15 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* sm
 // "Global float atomics"); a 16-rows x 4-dwords shape runs ~17x slower.
 template <int BM, int BN, int LDS, int WGM = 2, int WGN = 2>
 DPE_DEVICE void epilogue_atomic_f32(const IgemmArgs& p, f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16], char* smem, int m0,
-                                    int n0, int wn) {
+                                    int n0, int wn, int split = 0) {
   constexpr int RM = BM / WGM / 16, RN = BN / WGN / 16, NW = WGM * WGN;
   constexpr int HR = BM / WGM;        // rows per pass (one wave-row at a time)
   constexpr int FROW = BN + 4;        // fp32 row stride (pad: conflict-free b128 writes)
   static_assert(HR * FROW * 4 <= LDS, "atomic staging must fit the kernel's LDS");
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lm = lane & 15, ln4 = (lane >> 4) * 4;
+  // p.slab: this split's partial tile is stored (plain, same row-segment shape) into its own slab
+  float* const slab = p.slab ? p.slab + (int64_t)split * p.M * p.N : nullptr;
   float* C = (float*)p.C;
   float* st = (float*)smem;
 #pragma unroll
@@ -538,7 +540,10 @@ DPE_DEVICE void epilogue_atomic_f32(const IgemmArgs& p, f32x4 (&acc)[BM / WGM / 
     for (int s = wid; s < HR * SEGS_PER_ROW; s += NW) {
       const int r = s / SEGS_PER_ROW, c = (s % SEGS_PER_ROW) * SEG + lane;
       const int m = m0 + half * HR + r, n = n0 + c;
-      if (m < p.M && n < p.N) atomicAdd(C + (int64_t)m * p.ldc + n, st[r * FROW + c]);
+      if (m < p.M && n < p.N) {
+        if (slab) slab[(int64_t)m * p.N + n] = st[r * FROW + c];
+        else atomicAdd(C + (int64_t)m * p.ldc + n, st[r * FROW + c]);
+      }
     }
     __syncthreads();
   }
@@ -1214,7 +1219,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (BN / WGN > 64) ? 2 : 1) void igemm
   }
   __syncthreads();
   if (p.alpha_ptr) p.alpha *= *p.alpha_ptr;
-  epilogue_atomic_f32<BM, BN, LDS, WGM, WGN>(p, acc, smem, m0, n0, wn);
+  epilogue_atomic_f32<BM, BN, LDS, WGM, WGN>(p, acc, smem, m0, n0, wn, split);
 }
 
 template <int BM, int BN, int AL, int BL, int EPI>
@@ -1242,6 +1247,7 @@ extern "C" int dpe_igemm_launch(const IgemmArgs* args, int bm, int bn, int aload
                                 hipStream_t st) {
   const IgemmArgs& a = *args;
   if (a.M <= 0 || a.N <= 0) return 0;
+  if (a.slab) return -1;  // slab partials: LDS-DMA weight grad only
   if (splits < 1) splits = 1;
 #define DPE_CASE(AL, BL, EP) \
   if (aload == AL && bload == BL && epi == EP) return launch_tiles<AL, BL, EP>(a, bm, bn, splits, st);

@@ -266,6 +266,8 @@ extern "C" int dpe_layernorm_fwd(const void* x, int x_bf16, const float* w, cons
 // Partial-sum blocks of the LN backward: ~2 rows per wave (4 waves per block) up to
 // 1024 blocks -- 16 waves per CU on the GPT-2 shape (8192 rows); with 8 rows per
 // wave (256 blocks) the row-serial wave ran latency-bound at ~2.7 TB/s.
+// (Under the CU budget two rounds of half-size blocks were tried: x1.29 -> x1.24 next to 16 VALU-bound
+// RCCL-sized workgroups, but twice the partials cost the finalize more than that, profiles/cu_hog_probe_r4.txt.)
 extern "C" int dpe_layernorm_bwd_nblocks(int64_t rows) {
   const int64_t nb = (rows + 7) / 8;
   return (int)(nb < 1 ? 1 : (nb > 1024 ? 1024 : nb));

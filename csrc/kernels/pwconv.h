@@ -31,11 +31,15 @@ struct PwArgs {
   const float* out_coef;     // PW_APPLY: [4][N] BN coefficients (scale, shift, ...) applied to the conv output
   const float* res_coef;     // PW_APPLY: the residual is BN'd first: bf16(residual * res_coef[n] + res_coef[N + n])
   uint8_t* out_bits;         // PW_APPLY: ReLU bits of y ([M][N/8]), or nullptr
+  unsigned* sched;           // claim counters (HGEMM_SCHED_BYTES, zeroed, left zeroed) for the dynamic schedule,
+                             // or nullptr: static (see dpe_pw_rowgroups)
 };
 
 }  // namespace dpe
 
 // Row groups of the launch for (M, N, K, epi), or 0 outside the kernel's envelope
-// (K in {64, 128, 256}, N a multiple of the block's column slice, N >= 2K).
+// (K in {64, 128, 256}, N a multiple of the block's column slice, N >= 2K).  With a CU budget in force
+// (dpe_cu_reserve() > 0: collectives in flight) there are twice as many row groups as resident block
+// rows and the second half is claimed at run time (PwArgs::sched); otherwise one per resident block row.
 extern "C" int dpe_pw_rowgroups(int64_t M, int64_t N, int64_t K, int epi);
 extern "C" int dpe_pw_launch(const dpe::PwArgs* args, int epi, hipStream_t stream);

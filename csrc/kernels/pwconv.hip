@@ -25,6 +25,7 @@
 //     at the end: one partial column per row group ([2][N][row groups]) instead of one per
 //     128-row tile, and no per-tile LDS reduction or barrier.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "igemm.h"
@@ -56,7 +57,8 @@ DPE_DEVICE void wait_vm() {  // s_waitcnt vmcnt(N): loads, LDS-DMA and stores co
 }
 
 // K: reduction depth; WN: output columns per wave (4 waves -> 4*WN per block); NS: ring depth
-template <int K, int WN, int NS, int EPI>
+// DYN: the dynamic row-group schedule (a compile-time variant: the static kernels keep their registers)
+template <int K, int WN, int NS, int EPI, bool DYN = false>
 __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_stream_kernel(PwArgs a) {
   constexpr int KC = K / 32;                  // 32-deep K chunks
   constexpr int TILE = BM * K * 2;            // bytes of one x tile in LDS ([KC][64 rows][64 B])
@@ -82,7 +84,14 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
   const int M = (int)a.M, N = (int)a.N, RG = a.rg;
   const int nbN = N / (4 * WN);
   const int bid = xcd_remap(blockIdx.x, gridDim.x);  // the nbN column slices of a row group share an XCD
-  const int rg = bid / nbN, nb = bid % nbN;
+  const int nb = bid % nbN;
+  int rg = bid / nbN;
+  // Dynamic schedule (a.sched, RG > resident row groups SRG): row groups [0, SRG) start statically, the
+  // rest are claimed per column slice from counter nb, so a block whose CU is shared with foreign work
+  // (RCCL channel blocks) takes fewer of them.  A row group's tiles, their summation order and its
+  // partial column do not depend on which block runs it: results are schedule-independent, bitwise.
+  const int SRG = (int)gridDim.x / nbN;  // row groups started statically (DYN: the rest are claimed)
+  __shared__ int claim_slot;
   const int n0w = nb * 4 * WN + wid * WN;  // the wave's first output channel
   const int tiles = (M + BM - 1) / BM;
   const int ch = lane % CPRW;              // the lane's 16-B chunk of each staged row
@@ -167,24 +176,9 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
     __syncthreads();
   }
 
-  // this row group's tiles: rg, rg + RG, ...
-  const int nt = rg < tiles ? (tiles - 1 - rg) / RG + 1 : 0;
-#pragma unroll
-  for (int j = 0; j < NS - 1; ++j)
-    if (j < nt) issue(rg + j * RG, j);
-  for (int j = 0; j < nt; ++j) {
-    // Tile j landed.  In steady state NS-2 later tiles' DMAs and NS-1 tiles' stores were issued
-    // after it (VM); a prologue tile j < NS-1 has only the NS-2 prologue DMAs and j tiles'
-    // stores behind it, so it waits for fewer (a larger count would let the wave read a tile
-    // still in flight); near the end fewer DMAs follow -> vmcnt(0).
-    if (j + NS - 2 >= nt) wait_vm<0>();
-    else if (j == 0) wait_vm<(NS - 2) * P>();
-    else if (NS >= 3 && j == 1) wait_vm<S + (NS - 2) * P>();
-    else if (NS >= 4 && j == 2) wait_vm<2 * S + (NS - 2) * P>();
-    else wait_vm<VM>();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's pieces of tile j are in; slot (j-1)%NS is free
-    asm volatile("" ::: "memory");
+  // one tile: its epilogue operands, the DMA of the ring stage NS-1 ahead (nxt_tile < 0: none), the MFMAs
+  // over the landed tile in ring slot cur_slot, the staged stores and the statistics
+  auto tile_body = [&](const int m0, const int cur_slot, const int nxt_tile, const int nxt_slot) {
     // K = 256 data grads: this tile's epilogue operands (residual, pre-BN input, masks) are issued
     // before the next ring stage's DMAs and the MFMAs, so their latency overlaps the K loop (issued
     // in the epilogue they stalled each half for a full HBM round trip).  They are older than the
@@ -192,7 +186,6 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
     // wider-WN tiles have no registers for it (they would spill).
     constexpr bool HOIST = (EPI != PW_FWD) && (WN == 32);
     constexpr int HN = HOIST ? NPS : 1;
-    const int m0 = (rg + j * RG) * BM;
     u32x4 hrv[2][HN], hxv[2][HN];
     uint32_t hrmb[2][HN], hsmb[2][HN];
     if constexpr (HOIST) {
@@ -213,8 +206,8 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
           }
         }
     }
-    if (j + NS - 1 < nt) issue(rg + (j + NS - 1) * RG, (j + NS - 1) % NS);
-    const char* img = smem + (j % NS) * TILE;
+    if (nxt_tile >= 0) issue(nxt_tile, nxt_slot);
+    const char* img = smem + cur_slot * TILE;
     f32x4 acc[MI][NI];
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
@@ -354,23 +347,116 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
         if (valid) *(u32x4*)(a.y + (int64_t)m * N + nch) = v;
       }
     }
-  }
+  };
   // statistics: reduce over the lanes holding the same channel chunk (lane = row * CPRW + ch),
   // one partial column per row group
-  if (EPI != PW_APPLY && a.stats) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-#pragma unroll
-      for (int o = CPRW; o < 64; o <<= 1) {
-        s[e] += __shfl_xor(s[e], o, 64);
-        ss[e] += __shfl_xor(ss[e], o, 64);
-      }
-    }
-    if (lane < CPRW) {
+  auto flush_stats = [&](int col) {
+    if (EPI != PW_APPLY && a.stats) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        a.stats[(int64_t)(nch + e) * RG + rg] = s[e];
-        if (EPI != PW_DSUM) a.stats[(int64_t)(N + nch + e) * RG + rg] = ss[e];
+#pragma unroll
+        for (int o = CPRW; o < 64; o <<= 1) {
+          s[e] += __shfl_xor(s[e], o, 64);
+          ss[e] += __shfl_xor(ss[e], o, 64);
+        }
+      }
+      if (lane < CPRW) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          a.stats[(int64_t)(nch + e) * RG + col] = s[e];
+          if (EPI != PW_DSUM) a.stats[(int64_t)(N + nch + e) * RG + col] = ss[e];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
+    }
+  };
+  // Tile p of the block's stream landed.  In steady state NS-2 later tiles' DMAs and NS-1 tiles' stores
+  // were issued after it (VM); a prologue tile p < NS-1 has only the NS-2 prologue DMAs and p tiles'
+  // stores behind it, so it waits for fewer (a larger count would let the wave read a tile still in
+  // flight); near the end fewer DMAs follow -> vmcnt(0).  (Any extra younger memory op -- a claim, a
+  // statistics store -- only makes a count stricter.)
+  auto ring_wait = [&](int p, bool ending) {
+    if (ending) wait_vm<0>();
+    else if (p == 0) wait_vm<(NS - 2) * P>();
+    else if (NS >= 3 && p == 1) wait_vm<S + (NS - 2) * P>();
+    else if (NS >= 4 && p == 2) wait_vm<2 * S + (NS - 2) * P>();
+    else wait_vm<VM>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of tile p are in; slot (p-1)%NS is free
+    asm volatile("" ::: "memory");
+  };
+
+  if constexpr (!DYN) {
+    // static: this row group's tiles rg, rg + RG, ...
+    const int nt = rg < tiles ? (tiles - 1 - rg) / RG + 1 : 0;
+#pragma unroll
+    for (int j = 0; j < NS - 1; ++j)
+      if (j < nt) issue(rg + j * RG, j);
+    for (int j = 0; j < nt; ++j) {
+      ring_wait(j, j + NS - 2 >= nt);
+      tile_body((rg + j * RG) * BM, j % NS, j + NS - 1 < nt ? rg + (j + NS - 1) * RG : -1, (j + NS - 1) % NS);
+    }
+    flush_stats(rg);
+  } else {
+    // Dynamic: one continuous tile stream over the row groups this block runs -- the static one, then
+    // row groups claimed per column slice from counter nb, each claimed near the end of the previous one
+    // but early enough that the ring never drains at a row-group boundary (every row group has >= NS + 3
+    // tiles: pw_plan).  A row group's tiles, their summation order and its partial column do not depend
+    // on which block runs it: results are schedule-independent, bitwise.
+    auto ntiles = [&](int u) { return (tiles - 1 - u) / RG + 1; };
+    int cu = rg, ntc = ntiles(cu), jc = 0;  // consumption: row group, its tile count, index
+    int nu = -2;                            // the next row group (-2: not yet known, -1: none)
+    int iu = cu, ij = 0;                    // issue cursor: row group, index
+    int p = 0;                              // stream position being consumed
+    int claimv = 0;                         // tid 0: the in-flight claim
+    auto next_issue = [&]() -> int {        // tile at the issue cursor (advancing it), or -1
+      if (iu < 0) return -1;
+      if (ij == ntiles(iu)) {
+        iu = iu == cu ? nu : -1;  // (the cursor never runs more than one row group ahead)
+        ij = 0;
+        if (iu < 0) return -1;
+      }
+      return iu + (ij++) * RG;
+    };
+    int issued = 0;
+#pragma unroll
+    for (int j = 0; j < NS - 1; ++j) {
+      const int t = next_issue();
+      if (t >= 0) { issue(t, j); ++issued; }
+    }
+    while (true) {
+      ring_wait(p, issued < p + NS - 1);
+      // the claim for the next row group is issued NS + 2 tiles before this one ends (late: a block that
+      // claimed at the start of a row group would hold its next one while still slow), published one
+      // tile later and read after the next barrier -- one tile before the issue cursor crosses over
+      const int jcl = ntc - (NS + 2);
+      if (jc == jcl && tid == 0)
+        claimv = SRG + (int)__hip_atomic_fetch_add(a.sched + nb * 256, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (jc == jcl + 1 && tid == 0) claim_slot = claimv;  // published by the next barrier
+      if (jc == jcl + 2) {
+        const int c = __builtin_amdgcn_readfirstlane(claim_slot);
+        nu = c < RG ? c : -1;
+      }
+      const int t = next_issue();
+      if (t >= 0) ++issued;
+      tile_body((cu + jc * RG) * BM, p % NS, t, (p + NS - 1) % NS);
+      ++p;
+      if (++jc == ntc) {
+        flush_stats(cu);
+        if (nu < 0) break;
+        cu = nu;
+        ntc = ntiles(cu);
+        jc = 0;
+        nu = -2;
+      }
+    }
+    if (tid == 0) {
+      // the last block out re-zeroes the counters for the next launch on this stream (every block's final,
+      // failed claim precedes its exit count, so no claim follows the reset)
+      if (__hip_atomic_fetch_add(a.sched + 16 * 256, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u) {
+        for (int k = 0; k < nbN; ++k) __hip_atomic_store(a.sched + k * 256, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.sched + 16 * 256, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -410,48 +496,70 @@ static int pw_wn(int K, int epi) {
 // Every block carries the same number of tiles, so the grid must be exactly the resident
 // capacity (blocks per CU from the occupancy API x CUs): a grid that lets the dispatcher put
 // 3 blocks on some CUs and 1 on others finishes at the pace of the fullest CU.
-template <int K, int WN, int NS, int EPI>
+template <int K, int WN, int NS, int EPI, bool DYN>
 static int pw_slots() {
   static int slots = [] {
     int dev = 0, cus = 0, per = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pw::pw_stream_kernel<K, WN, NS, EPI>, 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pw::pw_stream_kernel<K, WN, NS, EPI, DYN>, 256, 0);
     return std::max(1, per) * std::max(1, cus);
   }();
   return slots;
 }
-template <int EPI>
+// resident blocks of the static (DYN = false) or the dynamic-schedule variant
+template <int EPI, bool DYN = false>
 static int pw_capacity(int K) {
   if constexpr (EPI == PW_APPLY || EPI == PW_DSUM) {
-    if (K == 64) return pw_slots<64, 32, 4, EPI>();
-    if (K == 128) return pw_slots<128, 32, 3, EPI>();
-    return pw_slots<256, 32, 2, EPI>();
+    if (K == 64) return pw_slots<64, 32, 4, EPI, DYN>();
+    if (K == 128) return pw_slots<128, 32, 3, EPI, DYN>();
+    return pw_slots<256, 32, 2, EPI, DYN>();
   } else {
-    if (K == 64) return EPI == PW_FWD ? pw_slots<64, DPE_PW64_FWD_WN, 4, EPI>() : pw_slots<64, DPE_PW64_DGRAD_WN, 4, EPI>();
-    if (K == 128) return EPI == PW_FWD ? pw_slots<128, DPE_PW128_FWD_WN, 3, EPI>() : pw_slots<128, 32, 3, EPI>();
-    return pw_slots<256, 32, 2, EPI>();
+    if (K == 64) return EPI == PW_FWD ? pw_slots<64, DPE_PW64_FWD_WN, 4, EPI, DYN>() : pw_slots<64, DPE_PW64_DGRAD_WN, 4, EPI, DYN>();
+    if (K == 128) return EPI == PW_FWD ? pw_slots<128, DPE_PW128_FWD_WN, 3, EPI, DYN>() : pw_slots<128, 32, 3, EPI, DYN>();
+    return pw_slots<256, 32, 2, EPI, DYN>();
   }
 }
 
-extern "C" int dpe_pw_rowgroups(int64_t M, int64_t N, int64_t K, int epi) {
-  if (K != 64 && K != 128 && K != 256) return 0;
-  if (epi != PW_FWD && epi != PW_DGRAD && epi != PW_APPLY && epi != PW_DSUM) return 0;
+// DPE_PW_DYNAMIC=0: the static schedule under a CU budget too (A/B)
+static bool pw_dynamic() {
+  static const bool on = [] { const char* e = getenv("DPE_PW_DYNAMIC"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
+template <bool DYN>
+static int pw_cap(int64_t K, int epi) {
+  return epi == PW_FWD ? pw_capacity<PW_FWD, DYN>((int)K)
+                       : epi == PW_APPLY ? pw_capacity<PW_APPLY, DYN>((int)K)
+                       : epi == PW_DSUM  ? pw_capacity<PW_DSUM, DYN>((int)K) : pw_capacity<PW_DGRAD, DYN>((int)K);
+}
+
+// Row groups of a launch: rg (= partial columns) and srg, the row groups started statically (the grid is
+// srg x nbN blocks).  srg == rg: static schedule, one resident wave of blocks over the whole launch,
+// sized to the resident capacity minus the slots left to in-flight RCCL channel blocks (comm.cpp CU
+// budget).  srg < rg (CU budget in force): the dynamic variant, rg = 2 srg row groups of >= 7 tiles each
+// (>= NS + 3: the stream claims the next row group NS + 2 tiles before the current one ends).
+struct PwPlan { int rg, srg; };
+static PwPlan pw_plan(int64_t M, int64_t N, int64_t K, int epi) {
+  if (K != 64 && K != 128 && K != 256) return {0, 0};
+  if (epi != PW_FWD && epi != PW_DGRAD && epi != PW_APPLY && epi != PW_DSUM) return {0, 0};
   const int bnb = 4 * pw_wn((int)K, epi);
-  if (N % bnb || N < 2 * K) return 0;  // write-heavy shapes only (N >= 2K)
-  if (M * K * 2 >= (1ll << 31) - 4096 || M * N >= (1ll << 31)) return 0;
+  if (N % bnb || N < 2 * K) return {0, 0};  // write-heavy shapes only (N >= 2K)
+  if (M * K * 2 >= (1ll << 31) - 4096 || M * N >= (1ll << 31)) return {0, 0};
   const int64_t tiles = (M + pw::BM - 1) / pw::BM;
   const int64_t nbN = N / bnb;
-  // resident capacity minus the slots left to in-flight RCCL channel blocks (comm.cpp CU budget)
-  const int cap = (epi == PW_FWD ? pw_capacity<PW_FWD>((int)K)
-                                 : epi == PW_APPLY ? pw_capacity<PW_APPLY>((int)K)
-                                 : epi == PW_DSUM  ? pw_capacity<PW_DSUM>((int)K) : pw_capacity<PW_DGRAD>((int)K)) -
-                  dpe_cu_reserve();
-  int64_t rg = cap / nbN;  // one resident wave of blocks over the whole launch
-  if (rg < 1) rg = 1;
-  if (rg > tiles) rg = tiles;
-  return (int)rg;
+  const int reserve = dpe_cu_reserve();
+  if (reserve > 0 && pw_dynamic()) {
+    const int64_t srg = std::max<int64_t>(1, (pw_cap<true>(K, epi) - reserve) / nbN);
+    const int64_t rg = std::min<int64_t>(2 * srg, tiles / 7);
+    if (rg > srg) return {(int)rg, (int)srg};
+  }
+  int64_t rg = (pw_cap<false>(K, epi) - reserve) / nbN;
+  rg = std::max<int64_t>(1, std::min<int64_t>(rg, tiles));
+  return {(int)rg, (int)rg};
 }
+
+extern "C" int dpe_pw_rowgroups(int64_t M, int64_t N, int64_t K, int epi) { return pw_plan(M, N, K, epi).rg; }
 
 extern "C" int dpe_pw_launch(const PwArgs* args, int epi, hipStream_t st) {
   const PwArgs& a = *args;
@@ -460,43 +568,25 @@ extern "C" int dpe_pw_launch(const PwArgs* args, int epi, hipStream_t st) {
   if (a.st_x && !a.st_coef) return -1;
   if (epi == PW_DSUM && (a.st_x || !a.st_mask || !a.stats)) return -1;
   if (epi == PW_APPLY && (!a.out_coef || a.st_x || a.stats || a.res_h > 0 || (a.res_coef && !a.residual))) return -1;
-  if (epi == PW_APPLY || epi == PW_DSUM) {
-    const dim3 grid_a((unsigned)(a.rg * (a.N / 128))), blk(256);
-#define PW_L2(E_)                                                                                        \
-    if (a.K == 64) hipLaunchKernelGGL((pw::pw_stream_kernel<64, 32, 4, E_>), grid_a, blk, 0, st, a);       \
-    else if (a.K == 128) hipLaunchKernelGGL((pw::pw_stream_kernel<128, 32, 3, E_>), grid_a, blk, 0, st, a); \
-    else hipLaunchKernelGGL((pw::pw_stream_kernel<256, 32, 2, E_>), grid_a, blk, 0, st, a);
-    if (epi == PW_APPLY) { PW_L2(PW_APPLY) } else { PW_L2(PW_DSUM) }
-#undef PW_L2
-    return 0;
-  }
   if (a.res_h > 0 && ((epi != PW_DGRAD && epi != PW_DSUM) || a.res_mask || a.res_h % 2 || a.res_w % 2 || a.M % ((int64_t)a.res_h * a.res_w)))
     return -1;
-  const int nbN = (int)(a.N / (4 * pw_wn((int)a.K, epi)));
-  const dim3 grid((unsigned)(a.rg * nbN)), block(256);
-#define PW_L(K_, WN_, NS_)                                                                              \
-  if (a.K == K_) {                                                                                      \
-    if (epi == PW_FWD) hipLaunchKernelGGL((pw::pw_stream_kernel<K_, WN_, NS_, PW_FWD>), grid, block, 0, st, a); \
-    else hipLaunchKernelGGL((pw::pw_stream_kernel<K_, WN_, NS_, PW_DGRAD>), grid, block, 0, st, a);    \
-    return 0;                                                                                           \
+  // resident row groups: all of them, or (CU budget in force) the first half, the rest claimed
+  // (no claim counters -- a stream being captured: the static variant over all rg row groups)
+  const int srg = a.sched ? pw_plan(a.M, a.N, a.K, epi).srg : a.rg;
+  const bool dyn = srg < a.rg;
+  const int wn = pw_wn((int)a.K, epi);
+  const dim3 grid((unsigned)(srg * (a.N / (4 * wn)))), block(256);
+#define PW_GO(K_, WN_, NS_, E_)                                                                            \
+  if (a.K == K_ && wn == WN_ && epi == E_) {                                                             \
+    if (dyn) hipLaunchKernelGGL((pw::pw_stream_kernel<K_, WN_, NS_, E_, true>), grid, block, 0, st, a);    \
+    else hipLaunchKernelGGL((pw::pw_stream_kernel<K_, WN_, NS_, E_, false>), grid, block, 0, st, a);       \
+    return 0;                                                                                            \
   }
-  if (a.K == 64 && epi == PW_DGRAD) {
-    hipLaunchKernelGGL((pw::pw_stream_kernel<64, DPE_PW64_DGRAD_WN, 4, PW_DGRAD>), grid, block, 0, st, a);
-    return 0;
-  }
-  if (a.K == 64) {
-    hipLaunchKernelGGL((pw::pw_stream_kernel<64, DPE_PW64_FWD_WN, 4, PW_FWD>), grid, block, 0, st, a);
-    return 0;
-  }
-  if (a.K == 128 && epi == PW_DGRAD) {
-    hipLaunchKernelGGL((pw::pw_stream_kernel<128, 32, 3, PW_DGRAD>), grid, block, 0, st, a);
-    return 0;
-  }
-  if (a.K == 128) {
-    hipLaunchKernelGGL((pw::pw_stream_kernel<128, DPE_PW128_FWD_WN, 3, PW_FWD>), grid, block, 0, st, a);
-    return 0;
-  }
-  PW_L(256, 32, 2)
-#undef PW_L
+  PW_GO(64, 32, 4, PW_APPLY) PW_GO(128, 32, 3, PW_APPLY) PW_GO(256, 32, 2, PW_APPLY)
+  PW_GO(64, 32, 4, PW_DSUM) PW_GO(128, 32, 3, PW_DSUM) PW_GO(256, 32, 2, PW_DSUM)
+  PW_GO(64, DPE_PW64_DGRAD_WN, 4, PW_DGRAD) PW_GO(64, DPE_PW64_FWD_WN, 4, PW_FWD)
+  PW_GO(128, 32, 3, PW_DGRAD) PW_GO(128, DPE_PW128_FWD_WN, 3, PW_FWD)
+  PW_GO(256, 32, 2, PW_DGRAD) PW_GO(256, 32, 2, PW_FWD)
+#undef PW_GO
   return -1;
 }

@@ -481,9 +481,15 @@ int rows_slots() {  // resident blocks of the row-walking kernels (2 per CU), mi
   return max(2, 2 * ncu - dpe_cu_reserve());
 }
 // One block per resident slot, each owning a contiguous range of the N*H output rows (>= 16 rows):
-// a single wave of blocks whatever the CU budget -- a fixed N*2 grid went from exactly 2 waves to
-// 2 + a sliver when RCCL channel blocks held 16 slots (x1.4-1.6, profiles/cu_hog_probe_r3.txt).
-int rows_grid(int N, int H) { return (int)std::max<int64_t>(1, std::min<int64_t>(rows_slots(), (int64_t)N * H / 16)); }
+// a single wave of blocks -- a fixed N*2 grid went from exactly 2 waves to 2 + a sliver when RCCL
+// channel blocks held 16 slots (x1.4-1.6, profiles/cu_hog_probe_r3.txt).  While the budget is in force,
+// two rounds of half-size blocks instead: a foreign workgroup that fits beside a block still slows its
+// CU, and with one round the slowest CU's block set the launch's time (x1.7-1.8 next to 16 VALU-bound
+// RCCL-sized workgroups, profiles/cu_hog_probe_r4.txt); with two, the dispatcher hands it fewer.
+int rows_grid(int N, int H) {
+  const int slots = rows_slots() * (dpe_cu_reserve() > 0 ? 2 : 1);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(slots, (int64_t)N * H / 16));
+}
 }  // namespace
 
 // Blocks of the launch for an [N, H, W, 64] input (0: outside the kernel's envelope).  Depends on the

@@ -17,6 +17,8 @@
 //     and are reduced once: one partial column per block ([2][64][blocks]).
 // One barrier per output row.  Same K order as the implicit GEMM (two taps per K-step), so the
 // output is bitwise identical to it.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dpe {
@@ -218,13 +220,16 @@ DPE_DEVICE bf16x8 xfrag(const char* img, int row0) {
 
 __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const uint16_t* __restrict__ x,
                                                             const uint16_t* __restrict__ dy,
-                                                            float* __restrict__ part, int H, int W) {
+                                                            float* __restrict__ part, int H, int W, int halves) {
   __shared__ __attribute__((aligned(16))) char smem[LDS];
   char* const ring = smem;                     // input row ih in slot (ih + 2) % 5
   char* const dbuf = smem + NSLOT * XSLOT;     // dY row oh in slot oh & 1
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // filter row dy = w
-  const int n = blockIdx.x;
+  // halves = 2: block b covers output rows [oh0, oh1) = half b & 1 of image b >> 1 (more, shorter blocks:
+  // the dispatcher balances them around foreign workgroups -- the CU budget, comm.cpp)
+  const int n = (int)blockIdx.x / halves, hb = (int)blockIdx.x % halves;
+  const int oh0 = hb * ((H + halves - 1) / halves), oh1 = min(H, oh0 + (H + halves - 1) / halves);
   const int64_t ximg = (int64_t)n * H * W * 16, dimg = (int64_t)n * H * W * 64;
   const int xch = W * 2, dch = W * 8;          // 16-B chunks per row
 
@@ -255,15 +260,15 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const uint16_t* __re
   __syncthreads();
   {
 #pragma unroll
-    for (int d = -2; d < 2; ++d) putx(d, loadx(d));
+    for (int d = -2; d < 2; ++d) putx(oh0 + d, loadx(oh0 + d));
     u32x4 t[4];
-    loadd(0, t);
-    putd(0, t);
+    loadd(oh0, t);
+    putd(oh0, t);
   }
-  u32x4 px0 = loadx(2), px1 = loadx(3);  // input rows oh + 2, oh + 3
-  u32x4 pd0[4], pd1[4];                  // dY rows oh + 1, oh + 2
-  loadd(1, pd0);
-  loadd(2, pd1);
+  u32x4 px0 = loadx(oh0 + 2), px1 = loadx(oh0 + 3);  // input rows oh + 2, oh + 3
+  u32x4 pd0[4], pd1[4];                              // dY rows oh + 1, oh + 2
+  loadd(oh0 + 1, pd0);
+  loadd(oh0 + 2, pd1);
   __syncthreads();
 
   f32x4 acc[4][4];
@@ -299,12 +304,12 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const uint16_t* __re
     loadd(oh + 3, pdA);
     __syncthreads();
   };
-  for (int oh = 0; oh < H; oh += 2) {
+  for (int oh = oh0; oh < oh1; oh += 2) {
     step(oh, px0, pd0);
-    if (oh + 1 < H) step(oh + 1, px1, pd1);
+    if (oh + 1 < oh1) step(oh + 1, px1, pd1);
   }
   // acc[m][t][e]: o = 16 m + (lane & 15), c = 4 (lane >> 4) + e, tap (dy = w, dx = t)
-  float* pb = part + (int64_t)n * PART;
+  float* pb = part + (int64_t)blockIdx.x * PART;
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -349,10 +354,19 @@ extern "C" int dpe_stem_launch(const uint16_t* x, const uint16_t* w, uint16_t* y
   return (int)hipGetLastError();
 }
 
-// Scratch floats of the stem weight-grad launch (per-image partials), 0: outside the envelope.
+extern "C" int dpe_cu_reserve();  // comm.cpp
+
+// Blocks per image of the stem weight grad: 2 (half-image blocks) while a CU budget is in force
+// (collectives in flight: two dispatch rounds balance around their workgroups), else 1.
+static int stem_wgrad_halves(int H) {
+  static const bool on = [] { const char* e = getenv("DPE_STEM_HALVES"); return !(e && e[0] == '0'); }();
+  return (on && dpe_cu_reserve() > 0 && H >= 8) ? 2 : 1;
+}
+
+// Scratch floats of the stem weight-grad launch (per-block partials), 0: outside the envelope.
 extern "C" int64_t dpe_stem_wgrad_scratch(int N, int H, int W) {
   if (N <= 0 || H < 2 || W < 1 || W > 112) return 0;
-  return (int64_t)N * dpe::stem::wg::PART;
+  return (int64_t)N * stem_wgrad_halves(H) * dpe::stem::wg::PART;
 }
 
 // dw [64][4][4][16] (+)= alpha * filter gradient of the s2d stem conv, given dY [N, H, W, 64].
@@ -360,9 +374,11 @@ extern "C" int dpe_stem_wgrad_launch(const uint16_t* x, const uint16_t* dy, floa
                                      float alpha, hipStream_t st) {
   if (dpe_stem_wgrad_scratch(N, H, W) <= 0 || !scratch) return -1;
   using namespace dpe::stem::wg;
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(N), dim3(256), 0, st, x, dy, scratch, H, W);
-  const int groups = N >= 64 ? 16 : 1;
-  const int per = (N + groups - 1) / groups;
-  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(PART / 1024, groups), dim3(256), 0, st, scratch, dw, N, per, alpha);
+  const int halves = stem_wgrad_halves(H), nparts = N * halves;
+  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(nparts), dim3(256), 0, st, x, dy, scratch, H, W, halves);
+  const int groups = nparts >= 64 ? 16 : 1;
+  const int per = (nparts + groups - 1) / groups;
+  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(PART / 1024, groups), dim3(256), 0, st, scratch, dw, nparts, per,
+                     alpha);
   return (int)hipGetLastError();
 }

@@ -349,7 +349,8 @@ class BottleneckFn(Function):
             w3 = convs[2].conv.weight
             s3, p3, d3 = _conv_conf(convs[2].conv)
             P = torch.zeros(w3.shape, dtype=torch.float32, device=w3.device)
-            C.conv_wgrad(dz3, src, P, s3, p3, d3, 1.0, src_coef)  # P = dz3^T a2
+            # P = dz3^T a2 with its K splits summed in a fixed order: BN3's dgamma comes from it
+            C.conv_wgrad(dz3, src, P, s3, p3, d3, 1.0, src_coef, deterministic=True)
             bn, gb, gd, bb, bd = bn_sinks(2)
             wbuf, wdirect = grad_sink(w3)
             bcat, ebias = C.bn_gram_bwd(lk.part, P, ws[2], u3, sv, c3, bn.weight.detach(), M3, gb, bb, wbuf)

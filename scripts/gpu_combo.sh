@@ -13,24 +13,18 @@ run() {  # run <name> <timeout> <cmd...>
 }
 for step in "$@"; do
   case $step in
-    dbg) for reg in 0 1; do
-           DPE_REGISTER_BUCKETS=$reg DPE_WG_DEBUG=1 DPE_DEBUG_LOCAL=1 run dbg_reg$reg 200 python -u -m pytest -x -q -s --timeout 150 \
-             --timeout-method thread -p no:cacheprovider tests/test_ddp_rccl_world2_gpu.py::test_native_reducer_world2_rccl_gpt2
-           grep -E "passed|failed" gpurun_out/combo/dbg_reg$reg.log | tail -1
-           grep -E "vs avg|vs local" gpurun_out/combo/dbg_reg$reg.log | head -4 | cut -c1-200
-         done ;;
-    gramblocks) run gram_blocks 200 python -u scripts/debug_gram_blocks.py; grep block gpurun_out/combo/gram_blocks.log; tail -3 gpurun_out/combo/gram_blocks.log ;;
     prof) # steady ResNet-50 kernel trace (env passed through, e.g. DPE_BN3_GRAM)
           ( cd /tmp && export TMPDIR=/tmp && run prof_${PROF_TAG:-x} 300 rocprofv3 --kernel-trace --output-format csv \
-              -d $R/gpurun_out/combo/prof_${PROF_TAG:-x} -o run -- python3 $R/bench.py --steps 6 --warmup 3 ) || true
+              -d $R/gpurun_out/combo/prof_${PROF_TAG:-x} -o run -- python3 $R/bench.py --model ${PROF_MODEL:-resnet50} --steps 6 --warmup 3 ) || true
           f=$(find $R/gpurun_out/combo/prof_${PROF_TAG:-x} -name "*kernel_trace.csv" | head -1)
-          python3 $R/scripts/prof_steady.py $f 3 sgd_kernel 60 > $R/gpurun_out/combo/steady_${PROF_TAG:-x}.txt && head -40 $R/gpurun_out/combo/steady_${PROF_TAG:-x}.txt
-          python3 $R/scripts/prof_sequence.py $f 4 sgd_kernel > $R/gpurun_out/combo/sequence_${PROF_TAG:-x}.txt
+          python3 $R/scripts/prof_steady.py $f 3 ${PROF_MARK:-sgd_kernel} 60 > $R/gpurun_out/combo/steady_${PROF_TAG:-x}.txt && head -40 $R/gpurun_out/combo/steady_${PROF_TAG:-x}.txt
+          python3 $R/scripts/prof_sequence.py $f 4 ${PROF_MARK:-sgd_kernel} > $R/gpurun_out/combo/sequence_${PROF_TAG:-x}.txt
           rm -f $f ;;
+    convs) run convs 300 python -u scripts/bench_convs.py --batch 512 --miopen 0 --reps 10 --json gpurun_out/combo/convs_${PROF_TAG:-x}.jsonl
+           tail -30 gpurun_out/combo/convs.log ;;
     parity0) run parity0 400 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider \
                tests/test_model_parity_gpu.py -k step0
              grep -E "PASSED|FAILED|% of bound|step-0|Error" $R/gpurun_out/combo/parity0.log | head -20 | cut -c1-200 ;;
-    gramloss) run gram_loss 200 python -u scripts/debug_gram_loss.py; cat gpurun_out/combo/gram_loss.log | grep -v amdgpu.ids ;;
     gpt2w2) run gpt2w2 300 python -u -m pytest -x -q --timeout 150 --timeout-method thread -p no:cacheprovider \
               tests/test_ddp_rccl_world2_gpu.py tests/test_comm_gpu.py -k "gpt2 or world4"
             tail -3 gpurun_out/combo/gpt2w2.log ;;
@@ -39,6 +33,10 @@ for step in "$@"; do
     grambench) for arm in 0 1 0 1; do
             DPE_BN3_GRAM=$arm run bench_gram$arm 200 python bench.py --steps 20 --warmup 5 && \
               echo "gram=$arm $(tail -1 gpurun_out/combo/bench_gram$arm.log | cut -c1-110)"
+          done ;;
+    hconvab) for arm in 0 1 0 1; do
+            DPE_HGEMM_CONV=$arm run bench_hconv$arm 200 python bench.py --steps 20 --warmup 5 && \
+              echo "hconv=$arm $(tail -1 gpurun_out/combo/bench_hconv$arm.log | cut -c100-220)"
           done ;;
     bench) for i in 1 2; do
             run bench_r$i 200 python bench.py --steps 20 --warmup 5 && echo "run $i $(tail -1 gpurun_out/combo/bench_r$i.log | cut -c1-110)"

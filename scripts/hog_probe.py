@@ -31,7 +31,9 @@ ap.add_argument("--threads", type=int, default=256)
 ap.add_argument("--lds", type=int, default=20480)
 ap.add_argument("--vgprs", type=int, default=64)
 ap.add_argument("--steps", type=int, default=6, help="timed steps per mode per round")
-ap.add_argument("--sleepy", type=int, default=0, help="1: hogs resident but idle (s_sleep), 0: VALU-saturating")
+ap.add_argument("--sleepy", type=int, default=0,
+                help="0: VALU-saturating hogs (worst case), 1: resident but idle (s_sleep), "
+                     "2: RCCL-like reduce-copy streaming (two reads + one write per element, little VALU)")
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--modes", nargs="+", default=["0:0", "16:0", "16:16", "0:16"])
 args = ap.parse_args()
@@ -69,7 +71,7 @@ def step(hogs, reserve):
         C.hog_stop(stop, 0)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            C.cu_hog(hogs, args.threads, args.lds, 200000.0, args.vgprs, stop, bool(args.sleepy))  # bounded: 200 ms
+            C.cu_hog(hogs, args.threads, args.lds, 200000.0, args.vgprs, stop, mode=args.sleepy)  # bounded: 200 ms
     C.set_cu_reserve(reserve)
     C.set_comm_active(reserve > 0)
     loss.backward()

@@ -164,10 +164,6 @@ def main_gpt2():
         torch.cuda.synchronize()
         assert ddp.reducer.launch_order() == list(range(ddp.num_buckets()))
         errs = {n: rel(p.grad, w) for (n, p), w in zip(m.named_parameters(), want)}
-        if os.environ.get("DPE_DEBUG_LOCAL") == "1":
-            loc = {n: rel(p.grad, r.grad) for (n, p), r in zip(m.named_parameters(), ref.parameters())}
-            print(f"rank {rank} step {step}: vs avg {sorted(errs.items(), key=lambda kv: -kv[1])[:6]}\n"
-                  f"   vs local {sorted(loc.items(), key=lambda kv: kv[1])[:6]}", flush=True)
         checks.append(max(errs.values()))
         assert checks[-1] < 1e-4, (step, sorted(errs.items(), key=lambda kv: -kv[1])[:4])
     assert ddp.bucket_rebuilds == 1

@@ -991,6 +991,21 @@ def test_row_wgrad_matches_reference(C, N, H, W):
         outs[on] = dw - dw0
     assert rel_err(outs[True], 0.5 * ref.permute(0, 2, 3, 1)) < 1e-4
     assert rel_err(outs[True], outs[False]) < 1e-4
+    # under a CU budget (H >= 8): half-image blocks (their partials reach dw through the same grouped
+    # reduce: fp32 atomics across groups when there are >= 64 partials, so equal to fp32 rounding)
+    C.set_cu_reserve(16)
+    C.set_comm_active(True)
+    try:
+        dws = []
+        for _ in range(2):
+            dw = dw0.clone()
+            C.conv_wgrad(dy, xs, dw, [1, 1], [2, 2], [1, 1], 0.5)
+            dws.append(dw - dw0)
+    finally:
+        C.set_comm_active(False)
+        C.set_cu_reserve(0)
+    assert rel_err(dws[0], dws[1]) < 1e-6
+    assert rel_err(dws[0], outs[True]) < 1e-5
 
 
 @pytest.mark.parametrize("reserve", [16, 300])
@@ -1079,6 +1094,21 @@ def test_stem_wgrad_matches_reference(C, N, H, W):
         outs[on] = dw - dw0
     assert rel_err(outs[True], 0.5 * ref.permute(0, 2, 3, 1)) < 1e-4
     assert rel_err(outs[True], outs[False]) < 1e-4
+    # under a CU budget (H >= 8): half-image blocks (their partials reach dw through the same grouped
+    # reduce: fp32 atomics across groups when there are >= 64 partials, so equal to fp32 rounding)
+    C.set_cu_reserve(16)
+    C.set_comm_active(True)
+    try:
+        dws = []
+        for _ in range(2):
+            dw = dw0.clone()
+            C.conv_wgrad(dy, xs, dw, [1, 1], [2, 2], [1, 1], 0.5)
+            dws.append(dw - dw0)
+    finally:
+        C.set_comm_active(False)
+        C.set_cu_reserve(0)
+    assert rel_err(dws[0], dws[1]) < 1e-6
+    assert rel_err(dws[0], outs[True]) < 1e-5
 
 
 @pytest.mark.parametrize("N,H,W,Ci,Co", [(8, 56, 56, 64, 256), (3, 7, 30, 64, 128), (8, 28, 28, 128, 512)])
@@ -1104,3 +1134,112 @@ def test_pointwise_bn_on_load(C, N, H, W, Ci, Co):
     C.conv_wgrad(dy, h, dw1, *z, 1.0, coef)
     C.conv_wgrad(dy, a, dw2, *z, 1.0)
     assert rel_err(dw1, dw2) < 1e-5
+
+
+@pytest.mark.parametrize("K,N", [(64, 256), (128, 512), (256, 1024)])
+def test_pw_stream_dynamic_schedule_under_cu_budget(C, K, N):
+    """The streaming pointwise conv under a CU budget runs twice the row groups and claims the second
+    half at run time (pwconv.hip, DYN): the forward output and the data grad are bitwise the unbudgeted
+    ones, the BN partials (a different, equally fixed layout) sum to the same totals, two budgeted runs
+    are bitwise identical (schedule-independent row groups), and the claim counters are left zeroed
+    (the unbudgeted run after them is bitwise the first one)."""
+    torch.manual_seed(53)
+    n, h = 224, 56  # M = 702,464 rows: enough tiles for every row group to keep >= 7 of them
+    x = bf(torch.randn(n, h, h, K, device=dev))
+    w = bf(torch.randn(N, 1, 1, K, device=dev) / K ** 0.5)  # forward K -> N
+    w2 = bf(torch.randn(K, 1, 1, N, device=dev) / K ** 0.5)  # a conv N -> K: its data grad is K -> N
+    dy = bf(torch.randn(n, h, h, K, device=dev))
+    hx = bf(torch.randn(n, h, h, N, device=dev))
+    coef = _bn_coef(C, N)
+    z = [1, 1], [0, 0], [1, 1]
+
+    def run():
+        y, st = C.conv_fwd(x, w, *z, True, None)
+        dx, part = C.conv_dgrad_bn(dy, w2, [n, h, h, N], *z, None, hx, coef)
+        torch.cuda.synchronize()
+        return y, st, dx, part
+
+    y0, st0, dx0, p0 = run()
+    C.set_cu_reserve(16)
+    C.set_comm_active(True)
+    try:
+        runs = [run(), run()]
+    finally:
+        C.set_comm_active(False)
+        C.set_cu_reserve(0)
+    y3, st3, dx3, p3 = run()
+    (y1, st1, dx1, p1), (y2, st2, dx2, p2) = runs
+    assert st1.shape[-1] > st0.shape[-1] and p1.shape[-1] > p0.shape[-1]  # the dynamic layout
+    assert torch.equal(y0, y1) and torch.equal(dx0, dx1)
+    assert rel_err(st1.sum(-1), st0.sum(-1)) < 1e-5 and rel_err(p1.sum(-1), p0.sum(-1)) < 1e-5
+    assert torch.equal(st1, st2) and torch.equal(p1, p2) and torch.equal(y1, y2) and torch.equal(dx1, dx2)
+    assert torch.equal(st3, st0) and torch.equal(p3, p0) and torch.equal(y3, y0)
+
+
+@pytest.mark.parametrize("N,H,Ci,Co,s", [(16, 14, 256, 256, 1), (16, 28, 256, 256, 2), (3, 7, 512, 512, 1),
+                                         (64, 14, 512, 512, 2), (2, 9, 128, 256, 1)])
+def test_hgemm_implicit_conv(C, N, H, Ci, Co, s):
+    """3x3 convs with >= 256 output channels on the persistent GEMM with an implicit-im2col A (hgemm.hip
+    AC: per-row tap masks, filter-tap offset per 64-deep K-tile, padding from out-of-range buffer loads)
+    vs the implicit-GEMM kernel and fp32 torch: forward with and without the BN-forward sums, and the
+    stride-1 data grad (a forward conv of dy with the flipped filter) with the BN-backward partials.
+    M tails (not a multiple of the tile) included."""
+    torch.manual_seed(61)
+    x = bf(torch.randn(N, H, H, Ci, device=dev))
+    w = bf(torch.randn(Co, 3, 3, Ci, device=dev) / (9 * Ci) ** 0.5)
+    z = [s, s], [1, 1], [1, 1]
+    ref = F.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), None, s, 1).permute(0, 2, 3, 1)
+    outs = {}
+    for on in (True, False):
+        C.set_hgemm_conv(on)
+        try:
+            y, st = C.conv_fwd(x, w, *z, True, None)
+            y2, _ = C.conv_fwd(x, w, *z, False, None)
+        finally:
+            C.set_hgemm_conv(True)
+        outs[on] = (y, st, y2)
+    (y1, s1, y1b), (y0, s0, _) = outs[True], outs[False]
+    assert rel_err(y1.float(), ref) < 1e-2
+    assert torch.equal(y1, y1b)
+    assert rel_err(y1.float(), y0.float()) < 1e-2
+    # weight grad: the TN layout with an implicit-im2col B (K-split slabs summed in a fixed order)
+    OH = (H - 1) // s + 1
+    dyw = bf(torch.randn(N, OH, OH, Co, device=dev))
+    wref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).float(), (Co, Ci, 3, 3), dyw.permute(0, 3, 1, 2).float(),
+                                       s, 1).permute(0, 2, 3, 1)
+    dws = {}
+    for on in (True, False):
+        C.set_hgemm_conv(on)
+        try:
+            dw = torch.full((Co, 3, 3, Ci), 0.25, device=dev)
+            C.conv_wgrad(dyw, x, dw, *z, 0.5)
+            dw2 = torch.full((Co, 3, 3, Ci), 0.25, device=dev)
+            C.conv_wgrad(dyw, x, dw2, *z, 0.5)
+        finally:
+            C.set_hgemm_conv(True)
+        dws[on] = (dw - 0.25, dw2 - 0.25)
+    assert rel_err(dws[True][0], 0.5 * wref) < 1e-4 and rel_err(dws[True][0], dws[False][0]) < 1e-4
+    if (N * OH * OH) % 64 == 0:  # (the hgemm route: no atomics, bitwise repeatable)
+        assert torch.equal(dws[True][0], dws[True][1])
+    # BN-forward sums of the stored (rounded) values
+    yf = y1.float().reshape(-1, Co)
+    assert rel_err(s1.sum(-1)[0], yf.sum(0)) < 1e-4 and rel_err(s1.sum(-1)[1], (yf * yf).sum(0)) < 1e-4
+    if s == 1:
+        # data grad: dx = conv_transpose(dy, w) with the BN-backward partials of relu(BN(h))
+        dy = bf(torch.randn(N, H, H, Co, device=dev))
+        h = bf(torch.randn(N, H, H, Ci, device=dev))
+        coef = _bn_coef(C, Ci)
+        res = {}
+        for on in (True, False):
+            C.set_hgemm_conv(on)
+            try:
+                res[on] = C.conv_dgrad_bn(dy, w, [N, H, H, Ci], *z, None, h, coef)
+            finally:
+                C.set_hgemm_conv(True)
+        (dx1, p1), (dx0, p0) = res[True], res[False]
+        dref = torch.nn.grad.conv2d_input((N, Ci, H, H), w.permute(0, 3, 1, 2).float(), dy.permute(0, 3, 1, 2).float(),
+                                          1, 1).permute(0, 2, 3, 1)
+        assert rel_err(dx1.float(), dref) < 1e-2 and rel_err(dx1.float(), dx0.float()) < 1e-2
+        dz = dx1.float() * ((h.float() * coef[0] + coef[1]) > 0)
+        assert rel_err(p1.sum(-1)[0], dz.reshape(-1, Ci).sum(0)) < 1e-3
+        assert rel_err(p1.sum(-1)[1], (dz * (h.float() - coef[2])).reshape(-1, Ci).sum(0)) < 1e-3
