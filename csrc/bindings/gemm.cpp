@@ -55,7 +55,9 @@ constexpr double kBw = 4.0e12;    // slab write + finalize read bandwidth
 constexpr double kLaunch = 3.0e-6;
 
 int g_force_cfg = -1, g_force_splits = -1;
-bool g_budget_tail = [] { const char* e = getenv("DPE_HGEMM_BUDGET_TAIL"); return !(e && e[0] == '0'); }();  // A/B
+// (off by default: with it the budgeted planner traded whole-K plans for K splits whose slab traffic
+// cost more than the balance bought -- GPT-2 data grads x1.7 -> x3.0, profiles/cu_hog_probe_r4.txt)
+bool g_budget_tail = [] { const char* e = getenv("DPE_HGEMM_BUDGET_TAIL"); return e && e[0] == '1'; }();  // A/B
 bool g_dynamic = [] { const char* e = getenv("DPE_HGEMM_DYNAMIC"); return !(e && e[0] == '0'); }();  // A/B
 
 // Dynamic-schedule state of the persistent GEMM (hgemm.hip: 8 per-XCD claim counters + exit

@@ -39,7 +39,7 @@ struct PwArgs {
 
 // Row groups of the launch for (M, N, K, epi), or 0 outside the kernel's envelope
 // (K in {64, 128, 256}, N a multiple of the block's column slice, N >= 2K).  With a CU budget in force
-// (dpe_cu_reserve() > 0: collectives in flight) there are twice as many row groups as resident block
-// rows and the second half is claimed at run time (PwArgs::sched); otherwise one per resident block row.
+// (dpe_cu_reserve() > 0: collectives in flight) there are three times as many row groups as resident block
+// rows and the last two thirds are claimed at run time (PwArgs::sched); otherwise one per resident block row.
 extern "C" int dpe_pw_rowgroups(int64_t M, int64_t N, int64_t K, int epi);
 extern "C" int dpe_pw_launch(const dpe::PwArgs* args, int epi, hipStream_t stream);
