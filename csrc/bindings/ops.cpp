@@ -591,6 +591,8 @@ void set_wgrad_hgemm(bool on) { g_wgrad_hgemm = on ? 1 : 0; }
 // with 128 output channels the 256-wide tiles lose (481 vs 680 TF), so those stay.
 // DPE_HGEMM_CONV=0 (or set_hgemm_conv(false)): the implicit-GEMM kernel (A/B, tests).
 int g_hgemm_conv = [] { const char* e = getenv("DPE_HGEMM_CONV"); return (e && e[0] == '0') ? 0 : 1; }();
+// the weight-grad half (implicit-im2col B) separately: DPE_HGEMM_CONV_WGRAD=0/1 (A/B)
+int g_hgemm_conv_wgrad = [] { const char* e = getenv("DPE_HGEMM_CONV_WGRAD"); return (e && e[0] == '0') ? 0 : 1; }();
 void set_hgemm_conv(bool on) { g_hgemm_conv = on ? 1 : 0; }
 bool hconv_ok(const dpe::ConvGeom& f, int64_t nout) {
   if (!g_hgemm_conv || f.R * f.S <= 1 || f.R * f.S > 32 || f.C < 64 || (f.C & (f.C - 1)) || nout < 256 || nout % 8) return false;
@@ -1035,7 +1037,7 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64
   // implicit-im2col B (hgemm.hip CV = 2); dense TN GEMMs of these shapes ran at 846-960 TF where the
   // LDS-DMA im2col weight grad ran them at 648-748 (profiles/wgrad_as_gemm_r4.jsonl).  Split-K partials
   // in slabs summed in a fixed order (no atomics).  Not with BN-on-load inputs (none at these shapes).
-  if (g_hgemm_conv && !is_pointwise(g) && g.K >= 256 && g.K % 8 == 0 && g.C >= 8 && (g.C & (g.C - 1)) == 0 &&
+  if (g_hgemm_conv && g_hgemm_conv_wgrad && !is_pointwise(g) && g.K >= 256 && g.K % 8 == 0 && g.C >= 8 && (g.C & (g.C - 1)) == 0 &&
       a.K % 64 == 0 && a.K < (1 << 24) && g.R * g.S <= 32 &&
       (((int64_t)g.N * g.H * g.W * g.C) + ((int64_t)g.ph * g.W + g.pw) * g.C) * 2 < (1ll << 31) - 4096) {
     auto h = hargs();

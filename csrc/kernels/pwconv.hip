@@ -427,14 +427,16 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
     }
     while (true) {
       ring_wait(p, issued < p + NS - 1);
-      // the claim for the next row group is issued NS + 2 tiles before this one ends (late: a block that
-      // claimed at the start of a row group would hold its next one while still slow), published one
-      // tile later and read after the next barrier -- one tile before the issue cursor crosses over
-      const int jcl = ntc - (NS + 2);
+      // the claim for the next row group is issued 8 + NS tiles before this one ends (late: a block that
+      // claimed at the start of a row group would hold its next one while still slow; early enough that
+      // the agent-scope atomic -- microseconds -- has returned when wave 0 publishes it), published
+      // NS + 1 tiles before the end and read after the next barrier, one tile before the issue cursor
+      // crosses over
+      const int jpub = ntc - (NS + 1), jcl = max(0, jpub - 7);
       if (jc == jcl && tid == 0)
         claimv = SRG + (int)__hip_atomic_fetch_add(a.sched + nb * 256, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (jc == jcl + 1 && tid == 0) claim_slot = claimv;  // published by the next barrier
-      if (jc == jcl + 2) {
+      if (jc == jpub && tid == 0) claim_slot = claimv;  // published by the next barrier
+      if (jc == jpub + 1) {
         const int c = __builtin_amdgcn_readfirstlane(claim_slot);
         nu = c < RG ? c : -1;
       }

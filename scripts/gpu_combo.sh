@@ -38,6 +38,10 @@ for step in "$@"; do
             DPE_HGEMM_CONV=$arm run bench_hconv$arm 200 python bench.py --steps 20 --warmup 5 && \
               echo "hconv=$arm $(tail -1 gpurun_out/combo/bench_hconv$arm.log | cut -c100-220)"
           done ;;
+    hwgab) for arm in 0 1 0 1; do
+            DPE_HGEMM_CONV_WGRAD=$arm run bench_hwg$arm 200 python bench.py --steps 20 --warmup 5 && \
+              echo "hconv_wgrad=$arm $(tail -1 gpurun_out/combo/bench_hwg$arm.log | cut -c100-220)"
+          done ;;
     bench) for i in 1 2; do
             run bench_r$i 200 python bench.py --steps 20 --warmup 5 && echo "run $i $(tail -1 gpurun_out/combo/bench_r$i.log | cut -c1-110)"
           done ;;
