@@ -1225,6 +1225,25 @@ std::vector<Tensor> conv1x1_dgrad_cat(const Tensor& dz, const Tensor& a2src, con
                   bn_x.sizes() == a2src.sizes() && bn_coef.numel() == 4 * C && K1 % 32 == 0 && C % 32 == 0,
               "conv1x1_dgrad_cat: shapes");
   Tensor dx = at::empty_like(bn_x);
+  // a2 materialised and >= 256 channels (layer 3): the persistent GEMM's NN layout with the two A segments
+  // (hgemm.hip CV = 3) and its BN-backward-partials epilogue; 156-167 us per call on the LDS-DMA kernel
+  // here (416 TF, profiles/resnet50_bs512_sequence_r4.txt)
+  if (g_hgemm_conv && !(a2_coef.has_value() && a2_coef->defined()) && C >= 256 && C % 64 == 0 && K1 % 64 == 0) {
+    int pcols = 0;
+    const auto pl = dpe_gemm::plan_bnb(M, C, K1 + C, 1, 0, &pcols);
+    if (pl.cfg >= 0 && pl.splits == 1 && pcols > 0) {
+      Tensor part = at::empty({2, C, pcols}, dz.options().dtype(at::kFloat));
+      auto h = hargs();
+      h.A = bp(dz); h.B = bp(bcat); h.C = dx.data_ptr();
+      h.M = (int)M; h.N = (int)C; h.K = (int)(K1 + C);
+      h.lda = K1; h.ldb = C; h.ldc = C;
+      h.bias = fp(e);
+      h.conv = 3; h.A2 = bp(a2src); h.lda2 = C; h.k1 = (int)K1;
+      h.col_stats = fp(part); h.stats_ld = pcols; h.st_x = bp(bn_x); h.st_coef = fp(bn_coef);
+      dpe_gemm::run_bnb(h, pl, 1, 0);
+      return {dx, part};
+    }
+  }
   auto a = base_args();
   a.A = bp(dz); a.B = bp(bcat); a.C = dx.data_ptr();
   a.M = (int)M; a.N = (int)C; a.K = (int)(K1 + C);

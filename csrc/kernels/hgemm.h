@@ -78,6 +78,11 @@ struct HgemmArgs {
   int conv;
   ConvGeom conv_g;
   int conv_smagic;
+  // conv == 3 (K-contiguous A only): A is the concatenation [A (k1 columns, lda) | A2 (K - k1 columns,
+  // lda2)] along K -- the Gram-algebra BN3 data grad [dz3 | a2] (bngram.hip); k1 % 64 == 0, no K split
+  const uint16_t* A2;
+  int64_t lda2;
+  int k1;
 };
 
 // Tile configurations (BMxBN, waves WRxWC).

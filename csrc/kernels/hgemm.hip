@@ -184,7 +184,7 @@ DPE_DEVICE float gelu_grad(float x) {
 template <int BM, int BN, int WR, int WC, bool AK, bool BK, int EPI, int ACT, bool BG = false, int CV = 0>
 // (4-wave tiles run 2 blocks per CU: 2 waves per SIMD, so at most 256 VGPRs + AGPRs per wave)
 __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kernel(HgemmArgs p) {
-  constexpr bool AC = CV == 1, BC = CV == 2;
+  constexpr bool AC = CV == 1, BC = CV == 2, ACAT = CV == 3;
   using G = Geo<BM, BN, WR, WC>;
   constexpr int NW = G::NW, RH = G::RH, CH = G::CH, FMH = G::FMH, FNH = G::FNH, GA = G::GA, GB = G::GB;
   constexpr int AHB = G::AHB, BHB = G::BHB;
@@ -321,6 +321,7 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
 
   uint32_t ga[2][GA], gb[2][GB];
   uint32_t gam[2][AC ? GA : 1];  // AC: per-row tap-validity masks of the A pieces
+  uint32_t ga2[2][ACAT ? GA : 1];  // ACAT: the A pieces' offsets in the second segment (lda2)
   uint32_t gbt[2][BC ? GB : 1];  // BC: per-column tap displacement (r dh - ph, s dw - pw) as two int16
   static_assert(!AC || AK, "implicit-im2col A is K-contiguous");
   static_assert(!BC || (!AK && !BK && !GRP), "implicit-im2col B: the TN weight-grad layout");
@@ -392,6 +393,7 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
         }
     } else {
       stage_setup<BM, WR, RH, GA, AK>(qlda, qadim > 0 ? qadim : qM, m0, AK ? kb : 0, ga);
+      if constexpr (ACAT) stage_setup<BM, WR, RH, GA, true>(p.lda2, qM, m0, 0, ga2);
     }
     if constexpr (BC) {
       // per B piece column chunk: its filter tap's byte offset + channel, and the tap's displacement
@@ -432,6 +434,17 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
       _Pragma("unroll") for (int i_ = 0; i_ < GA; ++i_)                                      \
         bdma16(arsrc, wdA + ((buf) * 2 + (h)) * AHB + i_ * 1024,                             \
                ((gam[h][i_] >> tap_) & 1u) ? ga[h][i_] : 0x80000000u, so_);                  \
+    } else if constexpr (ACAT) {                                                             \
+      const int k0_ = (t) * TK;                                                              \
+      if (k0_ < p.k1) {                                                                      \
+        const char* b_ = Ab + (int64_t)k0_ * 2;                                              \
+        _Pragma("unroll") for (int i_ = 0; i_ < GA; ++i_)                                    \
+          glds(b_ + ga[h][i_], wdA + ((buf) * 2 + (h)) * AHB + i_ * 1024);                   \
+      } else {                                                                               \
+        const char* b_ = (const char*)p.A2 + (int64_t)(k0_ - p.k1) * 2;                      \
+        _Pragma("unroll") for (int i_ = 0; i_ < GA; ++i_)                                    \
+          glds(b_ + ga2[h][i_], wdA + ((buf) * 2 + (h)) * AHB + i_ * 1024);                  \
+      }                                                                                      \
     } else {                                                                                 \
       const char* b_ = Ab + (int64_t)(t) * astep;                                            \
       _Pragma("unroll") for (int i_ = 0; i_ < GA; ++i_)                                      \
@@ -1004,8 +1017,25 @@ int launch_conv_wgrad(const HgemmArgs& p, int epi, int grid, hipStream_t st) {
   return 0;
 }
 
+// concatenated-K A (NN layout, bf16 out with bias, BN-backward partials or none; no K split)
+template <int BM, int BN, int WR, int WC>
+int launch_cat(const HgemmArgs& p, int epi, int grid, hipStream_t st) {
+  if (epi != HE_BF16 || p.splits != 1 || p.dbias) return -3;
+  const dim3 g((unsigned)grid), b(WR * WC * 64);
+  if (p.act == HACT_BNB && p.col_stats && p.st_x && p.st_coef)
+    hipLaunchKernelGGL((hg::hgemm_kernel<BM, BN, WR, WC, true, false, HE_BF16, HACT_BNB, false, 3>), g, b, 0, st, p);
+  else if (p.act == ACT_NONE)
+    hipLaunchKernelGGL((hg::hgemm_kernel<BM, BN, WR, WC, true, false, HE_BF16, ACT_NONE, false, 3>), g, b, 0, st, p);
+  else return -3;
+  return 0;
+}
+
 template <int BM, int BN, int WR, int WC>
 int launch_layout(const HgemmArgs& p, int a_k, int b_k, int epi, int grid, hipStream_t st) {
+  if (p.conv == 3) {
+    if constexpr (BN == 256) return (a_k && !b_k) ? launch_cat<BM, BN, WR, WC>(p, epi, grid, st) : -2;
+    return -2;
+  }
   if (p.conv == 2) {
     if constexpr (BM == 256 && BN == 256) return (!a_k && !b_k) ? launch_conv_wgrad(p, epi, grid, st) : -2;
     return -2;
@@ -1040,6 +1070,11 @@ extern "C" int dpe_hgemm_launch(const HgemmArgs* a, int cfg, int a_k, int b_k, i
         (int64_t)g.N * g.OH * g.OW != p.M || p.conv_smagic != (65536 + g.S - 1) / g.S)
       return -1;
     if ((((int64_t)g.N * g.H * g.W * g.C) + ((int64_t)g.ph * g.W + g.pw) * g.C) * 2 >= (1ll << 31) - 4096) return -4;
+  } else if (p.conv == 3) {
+    if (!a_k || !p.A2 || p.k1 <= 0 || p.k1 % 64 || p.k1 >= p.K || p.kps != p.K || p.lda < p.k1 ||
+        p.lda2 < p.K - p.k1 || p.lda2 % 8)
+      return -1;
+    if ((int64_t)p.M * p.lda * 2 >= (1ll << 32) || (int64_t)p.M * p.lda2 * 2 >= (1ll << 32)) return -4;
   } else if (p.conv == 2) {
     // pixel decomposition by float reciprocals: exact for pixel indices < 2^24 with the +-1 correction
     const ConvGeom& g = p.conv_g;

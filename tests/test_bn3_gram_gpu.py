@@ -147,8 +147,17 @@ def test_gram_backward_and_cat_dgrad(C):
     s2 = (dzb * (h2.float() - c2[2])).sum(0)
     assert _rel(p2[0].sum(-1), s1) < 1e-3 and _rel(p2[1].sum(-1), s2) < 1e-3
     # materialised a2 (no coefficients on load): same result
-    da_m, _ = X.conv1x1_dgrad_cat(dz, _operand(h2, c2).bfloat16(), None, bcat, e, h2, c2)
+    da_m, pm = X.conv1x1_dgrad_cat(dz, _operand(h2, c2).bfloat16(), None, bcat, e, h2, c2)
     assert _rel(da_m.float(), da.float()) < 1e-4  # (fmaf on load vs torch mul + add: last-bit rounding)
+    assert _rel(pm[0].sum(-1), s1) < 1e-3 and _rel(pm[1].sum(-1), s2) < 1e-3
+    # (C >= 256: the persistent GEMM's concatenated-K A; the LDS-DMA kernel as the reference)
+    X.set_hgemm_conv(False)
+    try:
+        da_i, pi = X.conv1x1_dgrad_cat(dz, _operand(h2, c2).bfloat16(), None, bcat, e, h2, c2)
+    finally:
+        X.set_hgemm_conv(True)
+    assert _rel(da_m.float(), da_i.float()) < 1e-4
+    assert _rel(pm.sum(-1), pi.sum(-1)) < 1e-4
 
 
 def test_resnet50_step_gram_on_vs_off():
