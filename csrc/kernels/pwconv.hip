@@ -207,6 +207,31 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
         }
     }
     if (nxt_tile >= 0) issue(nxt_tile, nxt_slot);
+    if (!DG && a.in_coef) {
+      // BN + ReLU of the producer applied to the landed tile ONCE, cooperatively in LDS (every wave reads
+      // the whole tile as its MFMA operand: transformed in each wave's registers it was done four times
+      // -- the layer-1/2 kernels were VALU-bound).  Chunk c: K slab c / 256, row (c % 256) / 4, physical
+      // 16-B chunk c % 4 = logical chunk ^ swizzle(row) (an involution).  Rows past M: relu(shift)
+      // values that are never stored and kept out of the statistics.
+      char* timg = smem + cur_slot * TILE;
+#pragma unroll
+      for (int q = 0; q < TILE / 16 / 256; ++q) {
+        const int c = q * 256 + tid, kc = c / (BM * 4), rem = c % (BM * 4), row = rem >> 2, pc = rem & 3;
+        const int lc = pc ^ ((0x78 >> (((row >> 2) & 3) << 1)) & 3);
+        u32x4* pch = (u32x4*)(timg + kc * (BM * 64) + row * 64 + pc * 16);
+        const f32x4* cs = (const f32x4*)(bnin + 32 * kc + 8 * lc);
+        const f32x4* chh = (const f32x4*)(bnin + K + 32 * kc + 8 * lc);
+        const f32x4 s0 = cs[0], s1 = cs[1], h0 = chh[0], h1 = chh[1];
+        const float sc8[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+        const float sh8[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        float f[8];
+        unpack8(*pch, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], sc8[e], sh8[e]), 0.f);
+        *pch = pack8(f);
+      }
+      __syncthreads();
+    }
     const char* img = smem + cur_slot * TILE;
     f32x4 acc[MI][NI];
 #pragma unroll
@@ -218,23 +243,6 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
       bf16x8 xf[MI];
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) xf[mi] = kfrag(img + kc * (BM * 64), 16 * mi);
-      if (a.in_coef) {
-        // BN + ReLU of the producer applied to the operand (channels 32 kc + 8 g .. +7 of this lane;
-        // rows past M are never stored and are kept out of the statistics)
-        const f32x4* cs = (const f32x4*)(bnin + 32 * kc + 8 * g);
-        const f32x4* ch = (const f32x4*)(bnin + K + 32 * kc + 8 * g);
-        const f32x4 s0 = cs[0], s1 = cs[1], h0 = ch[0], h1 = ch[1];
-        const float sc8[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-        const float sh8[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi) {
-          float f[8];
-          unpack8(__builtin_bit_cast(u32x4, xf[mi]), f);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], sc8[e], sh8[e]), 0.f);
-          xf[mi] = __builtin_bit_cast(bf16x8, pack8(f));
-        }
-      }
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
