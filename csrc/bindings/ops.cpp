@@ -594,8 +594,14 @@ int g_hgemm_conv = [] { const char* e = getenv("DPE_HGEMM_CONV"); return (e && e
 // the weight-grad half (implicit-im2col B) separately: DPE_HGEMM_CONV_WGRAD=0/1 (A/B)
 int g_hgemm_conv_wgrad = [] { const char* e = getenv("DPE_HGEMM_CONV_WGRAD"); return (e && e[0] == '0') ? 0 : 1; }();
 void set_hgemm_conv(bool on) { g_hgemm_conv = on ? 1 : 0; }
+// DPE_HGEMM_CONV_1X1S=0: the strided 1x1 convs (bottleneck downsamples) stay on the implicit-GEMM kernel (A/B)
+bool g_hgemm_conv_1x1s = [] { const char* e = getenv("DPE_HGEMM_CONV_1X1S"); return !(e && e[0] == '0'); }();
 bool hconv_ok(const dpe::ConvGeom& f, int64_t nout) {
-  if (!g_hgemm_conv || f.R * f.S <= 1 || f.R * f.S > 32 || f.C < 64 || (f.C & (f.C - 1)) || nout < 256 || nout % 8) return false;
+  // 1x1 only when strided (a stride-1 1x1 conv is a dense GEMM, routed elsewhere) and at >= 512 input
+  // channels: the layer-3/4 downsamples 185 -> 169 and 145 -> 139 us, the layer-2 one (K = 256) slower
+  // there, 287 vs 272 us (scripts/bench_down_fwd.py, profiles/down_fwd_r4.jsonl)
+  const bool one = f.R * f.S == 1 && (f.sh > 1 || f.sw > 1) && f.ph == 0 && f.pw == 0 && f.C >= 512 && g_hgemm_conv_1x1s;
+  if (!g_hgemm_conv || (f.R * f.S <= 1 && !one) || f.R * f.S > 32 || f.C < 64 || (f.C & (f.C - 1)) || nout < 256 || nout % 8) return false;
   const int64_t abytes = (((int64_t)f.N * f.H * f.W * f.C) + ((int64_t)f.ph * f.W + f.pw) * f.C) * 2;
   return abytes < (1ll << 31) - 4096 && (int64_t)f.N * f.OH * f.OW < (1ll << 31);
 }

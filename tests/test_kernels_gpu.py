@@ -1175,6 +1175,30 @@ def test_pw_stream_dynamic_schedule_under_cu_budget(C, K, N):
     assert torch.equal(st3, st0) and torch.equal(p3, p0) and torch.equal(y3, y0)
 
 
+@pytest.mark.parametrize("N,H,Ci,Co", [(8, 28, 512, 1024), (4, 14, 1024, 2048), (3, 9, 512, 256), (2, 14, 256, 512)])
+def test_hgemm_strided_pointwise_conv(C, N, H, Ci, Co):
+    """Strided 1x1 convs (the bottleneck downsamples, >= 512 input channels) on the persistent GEMM's
+    implicit-im2col A (one filter tap; the row's input pixel at (s*oh, s*ow)) vs the implicit-GEMM kernel
+    and fp32 torch, with the BN-forward sums; odd spatial size included (M tail); 256 input channels
+    stay on the implicit-GEMM kernel (both arms equal)."""
+    torch.manual_seed(67)
+    x = bf(torch.randn(N, H, H, Ci, device=dev))
+    w = bf(torch.randn(Co, 1, 1, Ci, device=dev) / Ci ** 0.5)
+    z = [2, 2], [0, 0], [1, 1]
+    ref = F.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), None, 2, 0).permute(0, 2, 3, 1)
+    outs = {}
+    for on in (True, False):
+        C.set_hgemm_conv(on)
+        try:
+            outs[on] = C.conv_fwd(x, w, *z, True, None)
+        finally:
+            C.set_hgemm_conv(True)
+    (y1, s1), (y0, s0) = outs[True], outs[False]
+    assert rel_err(y1.float(), ref) < 1e-2 and rel_err(y1.float(), y0.float()) < 1e-2
+    yf = y1.float().reshape(-1, Co)
+    assert rel_err(s1.sum(-1)[0], yf.sum(0)) < 1e-4 and rel_err(s1.sum(-1)[1], (yf * yf).sum(0)) < 1e-4
+
+
 @pytest.mark.parametrize("N,H,Ci,Co,s", [(16, 14, 256, 256, 1), (16, 28, 256, 256, 2), (3, 7, 512, 512, 1),
                                          (64, 14, 512, 512, 2), (2, 9, 128, 256, 1)])
 def test_hgemm_implicit_conv(C, N, H, Ci, Co, s):
