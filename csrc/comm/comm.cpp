@@ -10,8 +10,14 @@
 #include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPGuard.h>
 
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <mutex>
+#include <thread>
 #include <stdexcept>
 
 #include <pybind11/functional.h>
@@ -71,6 +77,49 @@ std::string Communicator::unique_id() {
   return std::string(id.internal, sizeof(id.internal));
 }
 
+// ---------------------------------------------------------------- native watchdog backstop
+// The Python watchdog (parallel/dist.py Watchdog) is a thread that needs the GIL and HIP's runtime
+// locks to check progress.  A rank whose main thread is stuck inside a GIL-holding native call (a kernel
+// launch blocked on a full launch queue behind a collective that can never complete, a stream sync)
+// starves it, and the rank would hang forever.  This thread needs neither: the Python watchdog pets it
+// on every check; when no pet has come for the armed limit, it reports, aborts the communicator
+// (bounded) and exits the process non-zero.
+namespace {
+std::atomic<int64_t> g_wd_pet_ns{0};
+std::atomic<int64_t> g_wd_limit_ns{0};  // 0: disarmed
+std::atomic<Communicator*> g_wd_comm{nullptr};
+std::once_flag g_wd_once;
+int64_t wd_now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+void wd_loop() {
+  while (true) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(500));
+    const int64_t lim = g_wd_limit_ns.load(std::memory_order_relaxed);
+    if (lim <= 0) continue;
+    const int64_t idle = wd_now_ns() - g_wd_pet_ns.load(std::memory_order_relaxed);
+    if (idle <= lim) continue;
+    std::fprintf(stderr,
+                 "[dpe native watchdog] watchdog: no check by the Python watchdog for %.0fs (starved or blocked); "
+                 "aborting communicator\n",
+                 (double)idle * 1e-9);
+    std::fflush(stderr);
+    if (Communicator* c = g_wd_comm.load()) {
+      std::thread([c] { c->abort(); }).detach();
+      std::this_thread::sleep_for(std::chrono::seconds(5));  // bounded: exit whether or not the abort returned
+    }
+    _exit(1);
+  }
+}
+}  // namespace
+
+void watchdog_backstop(double limit_s) {
+  g_wd_pet_ns.store(wd_now_ns(), std::memory_order_relaxed);
+  g_wd_limit_ns.store(limit_s > 0 ? (int64_t)(limit_s * 1e9) : 0, std::memory_order_relaxed);
+  if (limit_s > 0) std::call_once(g_wd_once, [] { std::thread(wd_loop).detach(); });
+}
+void watchdog_pet() { g_wd_pet_ns.store(wd_now_ns(), std::memory_order_relaxed); }
+
 Communicator::Communicator(const std::string& uid, int rank, int world, int device)
     : rank_(rank), world_(world), device_(device), stream_(c10::hip::getStreamFromPool(true, device)) {
   if (uid.size() != sizeof(ncclUniqueId::internal)) throw std::runtime_error("bad RCCL unique id size");
@@ -81,9 +130,12 @@ Communicator::Communicator(const std::string& uid, int rank, int world, int devi
   HIP_CHECK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
   barrier_buf_ = at::zeros({1}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device));
+  g_wd_comm.store(this);
 }
 
 Communicator::~Communicator() {
+  Communicator* self = this;
+  g_wd_comm.compare_exchange_strong(self, nullptr);
   if (comm_ && !aborted_) ncclCommDestroy(comm_);
   if (ev_in_) (void)hipEventDestroy(ev_in_);
   if (ev_out_) (void)hipEventDestroy(ev_out_);
@@ -104,6 +156,7 @@ void Communicator::post(const at::Tensor&) {
 }
 
 void Communicator::all_reduce(at::Tensor& t, const std::string& op) {
+  TORCH_CHECK(!aborted_, "RCCL communicator was aborted");
   pre(t);
   NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), to_nccl_op(op), comm_,
                            stream_.stream()));
@@ -111,16 +164,19 @@ void Communicator::all_reduce(at::Tensor& t, const std::string& op) {
 }
 
 void Communicator::all_reduce_raw(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
+  TORCH_CHECK(!aborted_, "RCCL communicator was aborted");
   NCCL_CHECK(ncclAllReduce(buf, buf, count, dt, op, comm_, s));
 }
 
 void Communicator::broadcast(at::Tensor& t, int root) {
+  TORCH_CHECK(!aborted_, "RCCL communicator was aborted");
   pre(t);
   NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root, comm_, stream_.stream()));
   post(t);
 }
 
 void Communicator::all_gather(const at::Tensor& in, at::Tensor& out) {
+  TORCH_CHECK(!aborted_, "RCCL communicator was aborted");
   TORCH_CHECK(out.numel() == in.numel() * world_, "all_gather: out must hold world*in elements");
   pre(in);
   c10::hip::HIPCachingAllocator::recordStream(out.storage().data_ptr(), stream_);
@@ -129,6 +185,7 @@ void Communicator::all_gather(const at::Tensor& in, at::Tensor& out) {
 }
 
 void Communicator::reduce_scatter(const at::Tensor& in, at::Tensor& out, const std::string& op) {
+  TORCH_CHECK(!aborted_, "RCCL communicator was aborted");
   TORCH_CHECK(in.numel() == out.numel() * world_, "reduce_scatter: in must hold world*out elements");
   pre(in);
   c10::hip::HIPCachingAllocator::recordStream(out.storage().data_ptr(), stream_);
@@ -138,6 +195,7 @@ void Communicator::reduce_scatter(const at::Tensor& in, at::Tensor& out, const s
 }
 
 void Communicator::all_to_all(const at::Tensor& in, at::Tensor& out) {
+  TORCH_CHECK(!aborted_, "RCCL communicator was aborted");
   TORCH_CHECK(in.numel() == out.numel() && in.numel() % world_ == 0, "all_to_all: equal sizes divisible by world");
   pre(in);
   c10::hip::HIPCachingAllocator::recordStream(out.storage().data_ptr(), stream_);
@@ -178,10 +236,9 @@ std::string Communicator::async_error() {
 }
 
 void Communicator::abort() {
-  if (comm_ && !aborted_) {
-    ncclCommAbort(comm_);
-    aborted_ = true;
-  }
+  // the flag first: an enqueue racing with the abort (a reducer launch) refuses instead of touching a
+  // communicator being torn down
+  if (comm_ && !aborted_.exchange(true)) ncclCommAbort(comm_);
   set_comm_active(false);  // no collective of this communicator is in flight any more
 }
 
@@ -392,6 +449,10 @@ std::vector<std::tuple<int64_t, double, double>> Reducer::last_timings() {
 void register_comm(pybind11::module& m) {
   namespace py = pybind11;
   m.def("rccl_unique_id", []() { return py::bytes(Communicator::unique_id()); });
+  m.def("watchdog_backstop", &watchdog_backstop, py::arg("limit_s"),
+        "arm (limit_s > 0) / disarm the native watchdog backstop: no watchdog_pet() for limit_s seconds -> "
+        "report, abort the communicator (bounded), exit(1)");
+  m.def("watchdog_pet", &watchdog_pet, "the Python watchdog made a check");
   m.def("set_aux_stream", [](int device, uint64_t stream) {
     TORCH_CHECK(device >= 0 && device < 64, "set_aux_stream: bad device");
     g_aux_streams[device] = (hipStream_t)(uintptr_t)stream;
@@ -414,13 +475,14 @@ void register_comm(pybind11::module& m) {
            py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"))
       .def_property_readonly("rank", &Communicator::rank)
       .def_property_readonly("world", &Communicator::world)
-      .def("all_reduce", &Communicator::all_reduce, py::arg("tensor"), py::arg("op") = "sum")
-      .def("broadcast", &Communicator::broadcast, py::arg("tensor"), py::arg("root") = 0)
+      .def("all_reduce", &Communicator::all_reduce, py::arg("tensor"), py::arg("op") = "sum", py::call_guard<py::gil_scoped_release>())
+      .def("broadcast", &Communicator::broadcast, py::arg("tensor"), py::arg("root") = 0, py::call_guard<py::gil_scoped_release>())
       .def("all_gather", &Communicator::all_gather)
       .def("reduce_scatter", &Communicator::reduce_scatter, py::arg("input"), py::arg("output"), py::arg("op") = "sum")
       .def("all_to_all", &Communicator::all_to_all)
-      .def("barrier", &Communicator::barrier)
+      .def("barrier", &Communicator::barrier, py::call_guard<py::gil_scoped_release>())
       .def("async_error", &Communicator::async_error)
+      // (abort keeps the GIL: Python-side collectives cannot be enqueued on the communicator meanwhile)
       .def("abort", &Communicator::abort)
       .def("comm_stream_ptr", [](Communicator& c) { return (uint64_t)(uintptr_t)c.comm_stream().stream(); })
       .def("register_buffer", [](Communicator& c, const at::Tensor& t) {

@@ -9,6 +9,7 @@
 
 #include <functional>
 #include <memory>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -61,7 +62,7 @@ class Communicator {
   c10::hip::HIPStream stream_;
   hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
   at::Tensor barrier_buf_;
-  bool aborted_ = false;
+  std::atomic<bool> aborted_{false};  // (set by the watchdog thread, read by every enqueue)
 };
 
 ncclDataType_t to_nccl(at::ScalarType t);

@@ -224,6 +224,12 @@ class Watchdog:
         self._on_fail = on_fail
         self.failure: Optional[str] = None
         self._thread = threading.Thread(target=self._run, name="dpe-watchdog", daemon=True)
+        # native backstop (csrc/comm/comm.cpp): this thread needs the GIL and HIP's locks to check anything;
+        # if it is starved or blocked for timeout_s + 15 s (at least 3 check intervals + 15 s), a native thread
+        # aborts the communicator and exits
+        self._native = _native_watchdog()
+        if self._native is not None:
+            self._native.watchdog_backstop(max(float(timeout_s), 3.0 * float(interval_s)) + 15.0)
         self._thread.start()
 
     def beat(self) -> None:
@@ -292,11 +298,15 @@ class Watchdog:
     def stop(self) -> None:
         self._stop.set()
         self._thread.join(timeout=5)
+        if self._native is not None:
+            self._native.watchdog_backstop(0.0)
 
     def _run(self):
         import threading
 
         while not self._stop.wait(self.interval_s):
+            if self._native is not None:
+                self._native.watchdog_pet()
             err = check_health()
             self._device_progress()
             stalled = 0.0 if self._paused else self._time.monotonic() - self._last
@@ -311,6 +321,8 @@ class Watchdog:
                     t.start()
                     t.join(timeout=10.0)
                 if self._on_fail is not None:
+                    if self._native is not None:
+                        self._native.watchdog_backstop(0.0)  # the caller handles the failure
                     self._on_fail(self.failure)
                     return
                 for h in log.handlers + __import__("logging").getLogger().handlers:
@@ -319,6 +331,17 @@ class Watchdog:
                     except Exception:  # noqa: BLE001
                         pass
                 os._exit(1)
+
+
+def _native_watchdog():
+    """The extension module for the native watchdog backstop (None where it is not built)."""
+    try:
+        from ..ops._ext import ext
+
+        C = ext()
+        return C if hasattr(C, "watchdog_backstop") else None
+    except Exception:  # noqa: BLE001
+        return None
 
 
 def _try_abort(c) -> None:

@@ -155,6 +155,28 @@ def test_default_collective_timeout_on_rccl_world_gt_1():
     assert default_watchdog_timeout(15.0, "rccl", 8) == 15.0
 
 
+def test_native_watchdog_backstop_exits_a_starved_rank():
+    """A rank whose Python watchdog thread cannot run (its main thread stuck in a GIL-holding native call
+    behind a dead peer's collective) must still exit: the native backstop (csrc/comm/comm.cpp) fires when
+    the Python watchdog's pets stop, and stays quiet while they come."""
+    import subprocess
+    import sys
+    import time
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    starved = ("from distributed_pytorch_example_amd.ops._ext import ext; import time; C = ext(); "
+               "C.watchdog_backstop(1.0); time.sleep(30)")
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-c", starved], cwd=root, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "aborting communicator" in r.stderr, (r.returncode, r.stderr[-500:])
+    assert time.time() - t0 < 30
+    petted = ("from distributed_pytorch_example_amd.ops._ext import ext; import time; C = ext(); "
+              "C.watchdog_backstop(1.0)\nfor _ in range(15):\n    C.watchdog_pet(); time.sleep(0.2)\n"
+              "C.watchdog_backstop(0.0); time.sleep(2.0); print('alive')")
+    r = subprocess.run([sys.executable, "-c", petted], cwd=root, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "alive" in r.stdout, (r.returncode, r.stderr[-500:])
+
+
 def test_watchdog_keeps_newest_beat_when_full():
     """a full pending list must not drop the newest beat (a false 'no progress' abort)."""
     from distributed_pytorch_example_amd.parallel.dist import Watchdog

@@ -43,14 +43,22 @@ def _run_world(n, args, extra_env=None, timeout=100):
         env.update(extra_env or {})
         procs.append(subprocess.Popen([sys.executable, "-u", *args], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))
-    outs = []
+    import time
+
+    outs = [None] * n
+    deadline = time.time() + timeout
     try:
-        for p in procs:
-            outs.append(p.communicate(timeout=timeout)[0])
+        for i, p in enumerate(procs):
+            try:
+                outs[i] = p.communicate(timeout=max(1.0, deadline - time.time()))[0]
+            except subprocess.TimeoutExpired:
+                break  # (every process still running is killed below; its output is kept for the report)
     finally:
-        for p in procs:
+        for i, p in enumerate(procs):
             if p.poll() is None:
                 p.kill()
+            if outs[i] is None:
+                outs[i] = (p.communicate()[0] or "") + f"\n[killed by the test after {timeout}s]"
     return [p.returncode for p in procs], outs
 
 
@@ -129,7 +137,7 @@ def test_rank_death_world4_aborts_every_survivor(tmp_path):
     codes, outs = _run_world(4, [os.path.join(ROOT, "train.py"), "--backend", "rccl", "--model", "resnet_tiny",
                                  "--image-size", "32", "--batch-size", "8", "--num-samples", "2048", "--epochs", "2",
                                  "--checkpoint-dir", str(tmp_path), "--watchdog-timeout", "15"],
-                             extra_env={"DPE_FAULT_INJECT": "2:0:3:kill"}, timeout=150)
+                             extra_env={"DPE_FAULT_INJECT": "2:0:3:kill"}, timeout=130)
     dt = time.time() - t0
     assert codes[2] == -9, outs[2][-2000:]
     for r in (0, 1, 3):
