@@ -635,6 +635,178 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const uint16_t* __restric
   }
 }
 
+// dK / dV with the query tile's four images (Q and dO, each K-contiguous and permuted-row) staged
+// global -> LDS by LDS-DMA one tile ahead (no staging registers, no ds_write_b128 per image: 8 of
+// them per thread and tile in attn_bwd_kernel); lse / -delta still go through registers (128 floats).
+// Each lane fetches the chunk the swizzled image places at its slot (the swizzles are involutions).
+__global__ __launch_bounds__(256) void attn_bwd_dma_kernel(const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dout,
+                                                       const float* __restrict__ lse2, const float* __restrict__ delta,
+                                                       uint16_t* __restrict__ dqkv, int B, int T, int H, float sl2,
+                                                       float scale) {
+  // per buffer: Qk Qm dOk dOm (8 KB each) + lse, delta (512 B)
+  constexpr int BUF = 4 * 8192 + 512;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int nqt = T / AQ, BH = B * H;
+  const int kt = (int)(blockIdx.x / BH);  // heaviest key tiles (most query tiles) first
+  const int bh = blockIdx.x % BH, b = bh / H, h = bh % H;
+  const int64_t RS = 3LL * H * AD;
+  const uint16_t* qb = qkv + (int64_t)b * T * RS + (int64_t)h * AD;
+  const uint16_t* kb = qb + H * AD;
+  const uint16_t* vb = qb + 2 * H * AD;
+  const int64_t ORS = (int64_t)H * AD;  // dO / O row stride
+  const uint16_t* ob = dout + (int64_t)b * T * ORS + (int64_t)h * AD;
+  const int k0w = kt * BKW + 32 * w;  // the wave's first key
+  const bool live = k0w < T;
+  const int qtw = k0w / AQ;           // first query tile that reaches the wave's keys
+
+  // wave's own 32 keys as B operands (key on lane)
+  bf16x8 kf[2][2], vf[2][2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int64_t off = (int64_t)(k0w + 16 * r + li) * RS + 32 * kk + 8 * g;
+      kf[r][kk] = live ? __builtin_bit_cast(bf16x8, *(const u32x4*)(kb + off)) : bf16x8{};
+      vf[r][kk] = live ? __builtin_bit_cast(bf16x8, *(const u32x4*)(vb + off)) : bf16x8{};
+    }
+  // Q / dO of a query tile: LDS-DMA into [Qk | Qm | Ok | Om] (8 KiB each); lse / -delta via registers
+  float lv = 0.f;
+  const float* pl = (tid < 64 ? lse2 + tid : delta + (tid - 64)) + (int64_t)bh * T;
+  const __amdgpu_buffer_rsrc_t rq =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(qb), (short)0, (int)(T * RS * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rdo =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(ob), (short)0, (int)(T * ORS * 2), 0x00020000);
+  uint32_t voff[8];  // piece w + 4 i of the 32 KiB image set: i < 4 Q, else dO; (i & 2) permuted-row image
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int oo = ((w + 4 * i) * 1024 + lane * 16) & 8191;  // byte slot inside its 8 KiB image
+    int row, dc;
+    if ((i & 2) == 0) {  // K-contiguous halves: (dc >> 2) * 4096 + kimg(row, dc & 3)
+      const int o2 = oo & 4095;
+      row = o2 >> 6;
+      dc = 4 * (oo >> 12) + (((o2 >> 4) & 3) ^ ((0x78 >> (((row >> 2) & 3) << 1)) & 3));
+    } else {             // permuted-row image: pimg(row, dc)
+      row = oo >> 7;
+      dc = ((oo >> 4) & 7) ^ (((row >> 1) & 3) << 1);
+    }
+    voff[i] = (uint32_t)(((int64_t)row * (i < 4 ? RS : ORS) + dc * 8) * 2);
+  }
+  auto dma_tile = [&](int qt, int buf) {
+    char* base = smem + buf * BUF;
+    const uint32_t sq = (uint32_t)((int64_t)qt * AQ * RS * 2), so = (uint32_t)((int64_t)qt * AQ * ORS * 2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) attn_dma16(i < 4 ? rq : rdo, base + (w + 4 * i) * 1024, voff[i], i < 4 ? sq : so);
+    if (tid < 128) lv = pl[qt * AQ];
+  };
+  auto stash = [&](int buf) {  // after the tile's DMA has landed (attn_vm_drain)
+    if (tid < 128) ((float*)(smem + buf * BUF + 4 * 8192))[tid] = tid < 64 ? lv : -lv;  // [0,64) lse, [64,128) -delta
+  };
+  const int qs = (kt * BKW) / AQ;
+  dma_tile(qs, 0);
+  attn_vm_drain();
+  stash(0);
+  f32x4 dk[2][4], dv[2][4];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) { dk[r][d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[r][d] = dk[r][d]; }
+  __syncthreads();
+
+  // the tile loop unrolled by two: the LDS buffer of each step is a compile-time constant, so every
+  // fragment address is a hoisted per-lane offset plus an immediate
+  auto step = [&](int qt, auto bufc) {
+    constexpr int cur = decltype(bufc)::value;
+    const bool more = qt + 1 < nqt;
+    if (more) dma_tile(qt + 1, cur ^ 1);  // in flight during this tile's MFMAs (cur ^ 1 last read before the previous barrier)
+    auto compute = [&](const char* base, auto maskc) {
+      constexpr bool MASK = decltype(maskc)::value;
+      const char* Qk = base;
+      const char* Qm = base + 8192;
+      const char* Ok = base + 2 * 8192;
+      const char* Om = base + 3 * 8192;
+      const float* sl = (const float*)(base + 4 * 8192);
+      const float* snd = sl + 64;
+      // S[q][key], dP[q][key] - delta[q]: lane = key, rows q = 16mt + 4g + e (the dP chain starts
+      // from -delta, so dS = P * dP' needs no subtraction)
+      f32x4 ps[2][4], dp[2][4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const bf16x8 q0 = kfrag64(Qk, 16 * mt), q1 = kfrag64(Qk + 4096, 16 * mt);
+        const bf16x8 o0 = kfrag64(Ok, 16 * mt), o1 = kfrag64(Ok + 4096, 16 * mt);
+        const f32x4 nd4 = *(const f32x4*)(snd + 16 * mt + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          ps[r][mt] = MFMA(q1, kf[r][1], MFMA(q0, kf[r][0], (f32x4{0.f, 0.f, 0.f, 0.f})));
+          dp[r][mt] = MFMA(o1, vf[r][1], MFMA(o0, vf[r][0], nd4));
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const f32x4 l4 = *(const f32x4*)(sl + 16 * mt + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float p = __builtin_amdgcn_exp2f(fmaf(ps[r][mt][e], sl2, -l4[e]));
+            if constexpr (MASK)
+              if (k0w + 16 * r + li > qt * AQ + 16 * mt + 4 * g + e) p = 0.f;
+            ps[r][mt][e] = p;                        // P
+            dp[r][mt][e] = p * dp[r][mt][e];  // dS (unscaled)
+          }
+      }
+      // dV^T += dO^T . P ; dK^T += Q^T . dS   (k = q, permuted order matches the accumulators)
+      bf16x8 pp[2][2], ss[2][2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        pp[r][0] = pack_frag(ps[r][0], ps[r][1]); pp[r][1] = pack_frag(ps[r][2], ps[r][3]);
+        ss[r][0] = pack_frag(dp[r][0], dp[r][1]); ss[r][1] = pack_frag(dp[r][2], dp[r][3]);
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const bf16x8 a0 = trfrag(Om, 0, 16 * d), a1 = trfrag(Om, 32, 16 * d);
+        const bf16x8 c0 = trfrag(Qm, 0, 16 * d), c1 = trfrag(Qm, 32, 16 * d);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          dv[r][d] = MFMA(a1, pp[r][1], MFMA(a0, pp[r][0], dv[r][d]));
+          dk[r][d] = MFMA(c1, ss[r][1], MFMA(c0, ss[r][0], dk[r][d]));
+        }
+      }
+    };
+    // query tiles whose first query is past the wave's last key need no causal mask
+    if (live && qt >= qtw) {
+      if (qt * AQ >= k0w + 31) compute(smem + cur * BUF, std::false_type{});
+      else compute(smem + cur * BUF, std::true_type{});
+    }
+    if (more) {
+      attn_vm_drain();
+      stash(cur ^ 1);
+    }
+    __syncthreads();
+  };
+  for (int qt = qs; qt < nqt; qt += 2) {
+    step(qt, std::integral_constant<int, 0>{});
+    if (qt + 1 < nqt) step(qt + 1, std::integral_constant<int, 1>{});
+  }
+  if (!live) return;
+  // dK, dV (bf16) -> dqkv[b, key, 1|2, h, :]
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    uint16_t* dkb = dqkv + (int64_t)b * T * RS + (int64_t)(k0w + 16 * r + li) * RS + H * AD + (int64_t)h * AD;
+    uint16_t* dvb = dkb + H * AD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      u32x2 a, c;
+      a[0] = pack_bf2(dk[r][d][0] * scale, dk[r][d][1] * scale);
+      a[1] = pack_bf2(dk[r][d][2] * scale, dk[r][d][3] * scale);
+      c[0] = pack_bf2(dv[r][d][0], dv[r][d][1]);
+      c[1] = pack_bf2(dv[r][d][2], dv[r][d][3]);
+      *(u32x2*)(dkb + 16 * d + 4 * g) = a;
+      *(u32x2*)(dvb + 16 * d + 4 * g) = c;
+    }
+  }
+}
+
 // dQ: the forward's structure with the query on the lane (one workgroup = 128 queries,
 // 4 waves x 32 queries, looping over key tiles <= the query tile).  S^T = K.Q^T and
 // dP^T = V.dO^T are recomputed (A = K / V images, B = the wave's Q / dO in registers);
@@ -777,6 +949,159 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
   }
 }
 
+// The same with the key tile's three images (K, V K-contiguous; K permuted-row) staged global -> LDS by
+// LDS-DMA one tile ahead instead of through registers and ds_write_b128 (as attn_bwd_dma_kernel).
+// (ATTN_DQ_WAVES=3 caps it at 168 VGPRs: 26 spilled registers, 88.5 vs 74.0 us for the backward pair)
+#ifndef ATTN_DQ_WAVES
+#define ATTN_DQ_WAVES 2
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATTN_DQ_WAVES))) void attn_bwd_dq_dma_kernel(const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ o,
+                                                          const uint16_t* __restrict__ dout,
+                                                          const float* __restrict__ lse2, float* __restrict__ delta,
+                                                          uint16_t* __restrict__ dqkv, int B, int T, int H, float sl2,
+                                                          float scale) {
+  // per buffer: K (two d-halves, K-contig) 8K | V (same) 8K | K permuted-row image 8K
+  constexpr int KI = 0, VI = 2 * AKV * 64, KP = 4 * AKV * 64, STG = KP + AKV * 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int nq = (T + FQ - 1) / FQ, BH = B * H;
+  const int qt = nq - 1 - (int)(blockIdx.x / BH);  // heaviest query tiles first
+  const int bh = blockIdx.x % BH, b = bh / H, h = bh % H;
+  const int64_t RS = 3LL * H * AD;
+  const int64_t ORS = (int64_t)H * AD;
+  const uint16_t* qb = qkv + (int64_t)b * T * RS + (int64_t)h * AD;
+  const uint16_t* kb = qb + H * AD;
+  const uint16_t* vb = qb + 2 * H * AD;
+  const int q0w = qt * FQ + 32 * w;
+  const bool live = q0w < T;
+  const int ktw = live ? (q0w + 31) / AKV : -1;
+  const int kd = (q0w + 1) / AKV;  // key tiles below kd need no causal mask
+  const int nkt = min((qt * FQ + FQ - 1) / AKV, T / AKV - 1) + 1;
+
+  // the wave's Q / dO rows as B operands; delta = rowsum(dO * O) from the same lanes (the
+  // lane's 16 d-values, then the 4-group permlane reduce), published for the dK/dV kernel
+  bf16x8 qf[2][2], of[2][2];
+  float lq[2], ndl[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int myq = live ? q0w + 16 * r + li : 0;
+    float dot = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int64_t oo = ((int64_t)b * T + myq) * ORS + (int64_t)h * AD + 32 * kk + 8 * g;
+      const u32x4 dov = *(const u32x4*)(dout + oo);
+      qf[r][kk] = __builtin_bit_cast(bf16x8, *(const u32x4*)(qb + (int64_t)myq * RS + 32 * kk + 8 * g));
+      of[r][kk] = __builtin_bit_cast(bf16x8, dov);
+      float fa[8], fb[8];
+      unpack8(dov, fa);
+      unpack8(*(const u32x4*)(o + oo), fb);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dot = fmaf(fa[e], fb[e], dot);
+    }
+    dot = rowsum4(dot);
+    if (live && g == 0) delta[(int64_t)bh * T + myq] = dot;
+    lq[r] = lse2[(int64_t)bh * T + myq];
+    ndl[r] = -dot;
+  }
+
+  // the sequence's qkv rows from K of head h on: one buffer resource, tile advance in soffset
+  const __amdgpu_buffer_rsrc_t rkv =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(kb), (short)0, (int)(T * RS * 2), 0x00020000);
+  uint32_t voff[6];  // piece w + 4 i of the 24 KiB image set: [K halves | V halves | K permuted-row]
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int oo = ((w + 4 * i) * 1024 + lane * 16) & 8191;
+    int row, dc;
+    if (i < 4) {  // (dc >> 2) * 4096 + kimg(row, dc & 3)
+      const int o2 = oo & 4095;
+      row = o2 >> 6;
+      dc = 4 * (oo >> 12) + (((o2 >> 4) & 3) ^ ((0x78 >> (((row >> 2) & 3) << 1)) & 3));
+    } else {      // pimg(row, dc)
+      row = oo >> 7;
+      dc = ((oo >> 4) & 7) ^ (((row >> 1) & 3) << 1);
+    }
+    voff[i] = (uint32_t)(((int64_t)row * RS + ((i & 6) == 2 ? H * AD : 0) + dc * 8) * 2);
+  }
+  auto dma_tile = [&](int kt, int buf) {
+    char* base = smem + buf * STG;
+    const uint32_t so = (uint32_t)((int64_t)kt * AKV * RS * 2);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) attn_dma16(rkv, base + (w + 4 * i) * 1024, voff[i], so);
+  };
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc[r][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  dma_tile(0, 0);
+  attn_vm_drain();
+  __syncthreads();
+  // the tile loop unrolled by two: the LDS buffer of each step is a compile-time constant, so every
+  // fragment address is a hoisted per-lane offset plus an immediate
+  auto step = [&](int kt, auto bufc) {
+    constexpr int cur = decltype(bufc)::value;
+    const bool more = kt + 1 < nkt;
+    if (more) dma_tile(kt + 1, cur ^ 1);  // cur ^ 1 last read before the previous barrier
+    auto compute = [&](const char* s, auto maskc) {
+      constexpr bool MASK = decltype(maskc)::value;
+      f32x4 sc[2][4], dp[2][4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const bf16x8 k0 = kfrag64(s + KI, 16 * nt), k1 = kfrag64(s + KI + AKV * 64, 16 * nt);
+        const bf16x8 v0 = kfrag64(s + VI, 16 * nt), v1 = kfrag64(s + VI + AKV * 64, 16 * nt);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          sc[r][nt] = MFMA(k1, qf[r][1], MFMA(k0, qf[r][0], (f32x4{0.f, 0.f, 0.f, 0.f})));
+          dp[r][nt] = MFMA(v1, of[r][1], MFMA(v0, of[r][0], (f32x4{ndl[r], ndl[r], ndl[r], ndl[r]})));
+        }
+      }
+      bf16x8 dd[2][2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int myq = q0w + 16 * r + li;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float p = __builtin_amdgcn_exp2f(fmaf(sc[r][nt][e], sl2, -lq[r]));
+            if constexpr (MASK)
+              if (kt * AKV + 16 * nt + 4 * g + e > myq) p = 0.f;
+            dp[r][nt][e] = p * dp[r][nt][e];  // dS^T (unscaled); dP^T started from -delta
+          }
+        dd[r][0] = pack_frag(dp[r][0], dp[r][1]);
+        dd[r][1] = pack_frag(dp[r][2], dp[r][3]);
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const bf16x8 a0 = trfrag(s + KP, 0, 16 * d), a1 = trfrag(s + KP, 32, 16 * d);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) acc[r][d] = MFMA(a1, dd[r][1], MFMA(a0, dd[r][0], acc[r][d]));
+      }
+    };
+    if (kt < kd) compute(smem + cur * STG, std::false_type{});
+    else if (kt <= ktw) compute(smem + cur * STG, std::true_type{});
+    if (more) attn_vm_drain();
+    __syncthreads();
+  };
+  for (int kt = 0; kt < nkt; kt += 2) {
+    step(kt, std::integral_constant<int, 0>{});
+    if (kt + 1 < nkt) step(kt + 1, std::integral_constant<int, 1>{});
+  }
+  if (!live) return;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    uint16_t* o = dqkv + ((int64_t)b * T + q0w + 16 * r + li) * RS + (int64_t)h * AD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      u32x2 pk;
+      pk[0] = pack_bf2(acc[r][d][0] * scale, acc[r][d][1] * scale);
+      pk[1] = pack_bf2(acc[r][d][2] * scale, acc[r][d][3] * scale);
+      *(u32x2*)(o + 16 * d + 4 * g) = pk;
+    }
+  }
+}
+
 }  // namespace dpe
 
 using namespace dpe;
@@ -805,9 +1130,28 @@ extern "C" int dpe_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint
   if (D != AD || T % AKV != 0 || !causal) return -1;
   const float sl2 = scale * 1.4426950408889634f;
   // dQ first: it also writes delta = rowsum(dO * O), which the dK/dV kernel reads
+#ifdef DPE_ATTN_BWD_STAGED
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(B * H * ((T + FQ - 1) / FQ)), dim3(256), 0, st, qkv, out, dout, lse, delta,
                      dqkv, B, T, H, sl2, scale);
+#else
+  if ((int64_t)T * 3 * H * AD * 2 < (1LL << 31))
+    hipLaunchKernelGGL(attn_bwd_dq_dma_kernel, dim3(B * H * ((T + FQ - 1) / FQ)), dim3(256), 0, st, qkv, out, dout, lse,
+                       delta, dqkv, B, T, H, sl2, scale);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(B * H * ((T + FQ - 1) / FQ)), dim3(256), 0, st, qkv, out, dout, lse, delta,
+                       dqkv, B, T, H, sl2, scale);
+#endif
+#ifdef DPE_ATTN_BWD_STAGED
   hipLaunchKernelGGL(attn_bwd_kernel, dim3(B * H * ((T + BKW - 1) / BKW)), dim3(256), 0, st, qkv, dout, lse, delta, dqkv, B,
                      T, H, sl2, scale);
+#else
+  // one sequence's qkv / dO rows must fit the DMA kernel's 32-bit buffer ranges
+  if ((int64_t)T * 3 * H * AD * 2 < (1LL << 31))
+    hipLaunchKernelGGL(attn_bwd_dma_kernel, dim3(B * H * ((T + BKW - 1) / BKW)), dim3(256), 0, st, qkv, dout, lse, delta,
+                       dqkv, B, T, H, sl2, scale);
+  else
+    hipLaunchKernelGGL(attn_bwd_kernel, dim3(B * H * ((T + BKW - 1) / BKW)), dim3(256), 0, st, qkv, dout, lse, delta, dqkv,
+                       B, T, H, sl2, scale);
+#endif
   return 0;
 }
