@@ -105,6 +105,8 @@ int64_t dpe_layernorm_bwd_scratch(int64_t rows, int D);
 int dpe_layernorm_bwd(const uint16_t* dy, const void* x, int x_bf16, const float* w, const float* mean, const float* rstd,
                       void* dx, int dx_accumulate_f32, const float* res_in, uint16_t* dx_bf16, float* dw, float* db,
                       float* part, int64_t rows, int D, hipStream_t st);
+int dpe_layernorm_bwd_finalize_group(const float* const* parts, const int64_t* rows, const int* Ds, float* const* dws,
+                                     float* const* dbs, int n, hipStream_t st);
 int dpe_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int T, int H, int D, float scale, int causal,
                  hipStream_t st);
 int dpe_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse, float* delta,
@@ -1703,9 +1705,11 @@ Tensor layernorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const T
 // Residual-stream form (pre-LN transformer block): dx = res_in + dLN(dy) in fp32 (a new tensor,
 // res_in untouched) plus its bf16 copy for the next data/weight-grad GEMMs -- one pass instead of
 // LN-bwd + add + cast.
+// defer: dw / db are not touched; the third output is the [nblocks][2][D] partial scratch, finalized into
+// dw / db later by layernorm_bwd_finalize_group (several LayerNorms per launch).
 std::vector<Tensor> layernorm_bwd_residual(const Tensor& dy, const Tensor& x, const Tensor& w, const Tensor& mean,
                                            const Tensor& rstd, Tensor& dw, const c10::optional<Tensor>& db,
-                                           const Tensor& res_in) {
+                                           const Tensor& res_in, bool defer) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw);
   CHECK_F32(res_in); CHECK_CONTIG(res_in);
   const bool xb = x.scalar_type() == at::kBFloat16;
@@ -1715,8 +1719,35 @@ std::vector<Tensor> layernorm_bwd_residual(const Tensor& dy, const Tensor& x, co
   Tensor dxb = at::empty(x.sizes(), x.options().dtype(at::kBFloat16));
   Tensor part = at::empty({dpe_layernorm_bwd_scratch(rows, (int)D)}, x.options().dtype(at::kFloat));
   CHECK_RC(dpe_layernorm_bwd(bp(dy), x.data_ptr(), xb, fp(w), fp(mean), fp(rstd), dx.data_ptr(), 1, fp(res_in), bpm(dxb),
-                             fp(dw), fpom(db), fp(part), rows, (int)D, cur_stream()), "layernorm_bwd_residual");
+                             defer ? nullptr : fp(dw), defer ? nullptr : fpom(db), fp(part), rows, (int)D, cur_stream()),
+           "layernorm_bwd_residual");
+  if (defer) return {dx, dxb, part};
   return {dx, dxb};
+}
+
+// The deferred LayerNorm-backward finalizes: dw_i (+)= sum of part_i's dw partials (db_i likewise, when
+// given), rows_i = the LayerNorm's row count; at most 8 per call.
+void layernorm_bwd_finalize_group(const std::vector<Tensor>& parts, const std::vector<int64_t>& rows,
+                                  const std::vector<Tensor>& dws, const std::vector<c10::optional<Tensor>>& dbs) {
+  const size_t n = parts.size();
+  TORCH_CHECK(n >= 1 && n <= 8 && rows.size() == n && dws.size() == n && dbs.size() == n,
+              "layernorm_bwd_finalize_group: 1..8 problems, equal list lengths");
+  std::vector<const float*> pp(n);
+  std::vector<float*> pw(n), pb(n);
+  std::vector<int> Ds(n);
+  for (size_t i = 0; i < n; ++i) {
+    CHECK_GPU(parts[i]); CHECK_F32(parts[i]); CHECK_F32(dws[i]); CHECK_CONTIG(dws[i]);
+    const int64_t D = dws[i].numel();
+    TORCH_CHECK(D > 0 && D % 8 == 0 && parts[i].numel() >= (int64_t)dpe_layernorm_bwd_nblocks(rows[i]) * 2 * D,
+                "layernorm_bwd_finalize_group: partial scratch too small for rows / D");
+    pp[i] = fp(parts[i]);
+    pw[i] = fp(dws[i]);
+    pb[i] = fpom(dbs[i]);
+    if (pb[i]) TORCH_CHECK(dbs[i]->numel() == D, "layernorm_bwd_finalize_group: db size");
+    Ds[i] = (int)D;
+  }
+  CHECK_RC(dpe_layernorm_bwd_finalize_group(pp.data(), rows.data(), Ds.data(), pw.data(), pb.data(), (int)n, cur_stream()),
+           "layernorm_bwd_finalize_group");
 }
 
 // ---------------------------------------------------------------- attention
@@ -1884,7 +1915,9 @@ void register_ops(pybind11::module& m) {
   m.def("optim_chunk_size", []() { return dpe_optim_chunk_size(); });
   m.def("optim_desc_bytes", []() { return dpe_optim_desc_bytes(); });
   m.def("layernorm_bwd_residual", &layernorm_bwd_residual, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"),
-        py::arg("rstd"), py::arg("dw"), py::arg("db"), py::arg("res_in"));
+        py::arg("rstd"), py::arg("dw"), py::arg("db"), py::arg("res_in"), py::arg("defer") = false);
+  m.def("layernorm_bwd_finalize_group", &layernorm_bwd_finalize_group, py::arg("parts"), py::arg("rows"), py::arg("dws"),
+        py::arg("dbs"));
   m.def("layernorm_fwd", &layernorm_fwd, py::arg("x"), py::arg("w"), py::arg("b") = py::none(), py::arg("eps") = 1e-5);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
         py::arg("dw"), py::arg("db") = py::none(), py::arg("dx_out") = py::none());

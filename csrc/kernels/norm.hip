@@ -5,6 +5,7 @@
 //      dx is either written (x dtype) or ACCUMULATED into an f32 residual-stream grad.
 #include "common.h"
 
+#define DPE_LN_FIN_GROUP_MAX 8
 namespace dpe {
 
 template <bool XBF>
@@ -209,13 +210,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
 // lane, fixed-order tree over the stripes; blockIdx.y picks dw (0) or db (1).  96 blocks at D = 768
 // (64 columns per block gave 24 blocks on 24 CUs: ~8 us, latency-bound, 25 calls per GPT-2 step).
 constexpr int LNF_W = 16, LNF_C = 16, LNF_S = LNF_W * (64 / LNF_C);
-__global__ __launch_bounds__(64 * LNF_W) void ln_bwd_finalize_kernel(const float* __restrict__ part, int nb, int D,
-                                                                     float* __restrict__ dw, float* __restrict__ db) {
+DPE_DEVICE void ln_fin_body(const float* __restrict__ part, int nb, int D, float* __restrict__ dw, float* __restrict__ db,
+                            int which, int bx) {
   __shared__ float red[LNF_S][LNF_C];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int cl = lane % LNF_C, stripe = wid * (64 / LNF_C) + lane / LNF_C;
-  const int which = blockIdx.y;
-  const int col = blockIdx.x * LNF_C + cl;
+  const int col = bx * LNF_C + cl;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (col < D) {
     const float* src = part + (int64_t)which * D + col;
@@ -237,6 +237,23 @@ __global__ __launch_bounds__(64 * LNF_W) void ln_bwd_finalize_kernel(const float
     if (which == 0) dw[col] += t;
     else if (db) db[col] += t;
   }
+}
+__global__ __launch_bounds__(64 * LNF_W) void ln_bwd_finalize_kernel(const float* __restrict__ part, int nb, int D,
+                                                                     float* __restrict__ dw, float* __restrict__ db) {
+  ln_fin_body(part, nb, D, dw, db, blockIdx.y, blockIdx.x);
+}
+// Several LayerNorms' deferred finalizes in one launch (blockIdx.z = problem): GPT-2 runs two per block,
+// each a ~5 us latency-bound launch alone.
+struct LnFinGroup {
+  const float* part[DPE_LN_FIN_GROUP_MAX];
+  float* dw[DPE_LN_FIN_GROUP_MAX];
+  float* db[DPE_LN_FIN_GROUP_MAX];
+  int nb[DPE_LN_FIN_GROUP_MAX], D[DPE_LN_FIN_GROUP_MAX];
+};
+__global__ __launch_bounds__(64 * LNF_W) void ln_bwd_finalize_group_kernel(LnFinGroup g) {
+  const int z = blockIdx.z;
+  if ((int)blockIdx.x * LNF_C >= g.D[z] || (blockIdx.y == 1 && !g.db[z])) return;  // (block-uniform)
+  ln_fin_body(g.part[z], g.nb[z], g.D[z], g.dw[z], g.db[z], blockIdx.y, blockIdx.x);
 }
 
 }  // namespace dpe
@@ -306,7 +323,27 @@ extern "C" int dpe_layernorm_bwd(const uint16_t* dy, const void* x, int x_bf16, 
   if (x_bf16) { DPE_LNB_J(true); } else { DPE_LNB_J(false); }
 #undef DPE_LNB_J
 #undef DPE_LNB
+  if (!dw && !db) return 0;  // deferred: the caller finalizes `part` later (dpe_layernorm_bwd_finalize_group)
   hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + LNF_C - 1) / LNF_C, db ? 2 : 1), dim3(64 * LNF_W), 0, st, part, nbc, D,
                      dw, db);
+  return 0;
+}
+
+// The deferred finalizes of n <= DPE_LN_FIN_GROUP_MAX LayerNorm backwards (each: its `part` scratch, its row
+// count, dw [D] and optional db [D], accumulated into) in one launch.
+extern "C" int dpe_layernorm_bwd_finalize_group(const float* const* parts, const int64_t* rows, const int* Ds, float* const* dws,
+                                                float* const* dbs, int n, hipStream_t st) {
+  if (n < 1 || n > DPE_LN_FIN_GROUP_MAX) return -1;
+  LnFinGroup g{};
+  int dmax = 0, anyb = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!parts[i] || !dws[i] || Ds[i] <= 0) return -1;
+    g.part[i] = parts[i]; g.dw[i] = dws[i]; g.db[i] = dbs[i];
+    g.nb[i] = dpe_layernorm_bwd_nblocks(rows[i]);
+    g.D[i] = Ds[i];
+    dmax = Ds[i] > dmax ? Ds[i] : dmax;
+    anyb |= dbs[i] != nullptr;
+  }
+  hipLaunchKernelGGL(ln_bwd_finalize_group_kernel, dim3((dmax + LNF_C - 1) / LNF_C, anyb ? 2 : 1, n), dim3(64 * LNF_W), 0, st, g);
   return 0;
 }

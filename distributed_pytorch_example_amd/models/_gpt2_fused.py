@@ -54,6 +54,11 @@ _carry: list = [None]
 # gradient autograd would receive from this node must be complete when backward returns).  0 = off.
 _WG_GROUP = int(os.environ.get("DPE_GPT2_WGRAD_GROUP", "2"))
 _wq: list = []  # (dy, x, dw, db | None, overwrite, weight param, bias param | None)
+# The LayerNorm weight / bias gradients of the same layers: their [blocks][2][D] partial sums are kept and
+# reduced by one grouped launch at the same flush (a standalone finalize is a ~5 us latency-bound launch,
+# two per block).  DPE_GPT2_LN_GROUP=0: finalized per LayerNorm.
+_LN_GROUP = os.environ.get("DPE_GPT2_LN_GROUP", "1") == "1"
+_lnq: list = []  # (part, rows, dw, db | None, weight param, bias param | None)
 
 
 def reset_wgrad_queue() -> None:
@@ -63,10 +68,37 @@ def reset_wgrad_queue() -> None:
         if q[6] is not None:
             q[6]._dpe_deferred = False
     _wq.clear()
+    for q in _lnq:
+        q[4]._dpe_deferred = False
+        if q[5] is not None:
+            q[5]._dpe_deferred = False
+    _lnq.clear()
+
+
+def flush_ln_queue() -> None:
+    """Reduce the queued LayerNorm weight / bias partials (groups of at most 8) and announce them."""
+    if not _lnq:
+        return
+    C = ext()
+    items = list(_lnq)
+    _lnq.clear()
+    for i in range(0, len(items), 8):
+        chunk = items[i:i + 8]
+        C.layernorm_bwd_finalize_group([q[0] for q in chunk], [q[1] for q in chunk], [q[2] for q in chunk],
+                                       [q[3] for q in chunk])
+    for q in items:
+        q[4]._dpe_deferred = False
+        if q[5] is not None:
+            q[5]._dpe_deferred = False
+    for q in items:
+        grad_done(q[4], True)
+        if q[5] is not None:
+            grad_done(q[5], True)
 
 
 def flush_wgrad_queue() -> None:
     """Launch the queued weight gradients (groups of at most 8 problems) and announce them."""
+    flush_ln_queue()
     if not _wq:
         return
     C = ext()
@@ -180,6 +212,17 @@ class BlockFn(Function):
         def ln_bwd(ln, dy, xin, mean, rstd, res):
             wb, wd = sink(ln.weight)
             bb, bd = sink(ln.bias) if ln.bias is not None else (None, False)
+            if group and _LN_GROUP and wd and (ln.bias is None or bd):
+                # partials kept; reduced into the bucket views by the grouped launch at the next flush
+                ln.weight._dpe_deferred = True
+                if ln.bias is not None:
+                    ln.bias._dpe_deferred = True
+                dx, dxb, part = C.layernorm_bwd_residual(dy, xin, ln.weight.detach(), mean, rstd, wb, bb, res, True)
+                _lnq.append((part, xin.numel() // xin.shape[-1], wb, bb, ln.weight, ln.bias))
+                grads[id(ln.weight)] = None
+                if ln.bias is not None:
+                    grads[id(ln.bias)] = None
+                return dx, dxb
             dx, dxb = C.layernorm_bwd_residual(dy, xin, ln.weight.detach(), mean, rstd, wb, bb, res)
             done(ln.weight, wb, wd)
             if ln.bias is not None:
@@ -195,7 +238,7 @@ class BlockFn(Function):
         dqkv = dqkv.view(a.shape[0], a.shape[1], -1)
         dh1 = linear_bwd(blk.c_attn, dqkv, h1)
         g1, g1b = ln_bwd(blk.ln_1, dh1, x, m1, r1, g2)
-        if _wq and (len(_wq) >= 4 * _WG_GROUP or getattr(blk, "_dpe_layer", 0) == 0 or not group):
+        if (_wq or _lnq) and (len(_wq) >= 4 * _WG_GROUP or getattr(blk, "_dpe_layer", 0) == 0 or not group):
             flush_wgrad_queue()  # every _WG_GROUP layers, and always at the first block (end of backward)
         _carry[0] = (g1, g1b, g1._version)
         pgrads = [grads.get(id(p)) for p in block_params(blk)]

@@ -407,6 +407,37 @@ def test_layernorm(C, D):
     assert rel_err(acc - 1, gx) < 1e-2
 
 
+def test_layernorm_bwd_deferred_grouped_finalize(C):
+    """The residual-stream LayerNorm backward with its dw / db reduction deferred (partials returned) and
+    several LayerNorms' partials reduced by one grouped launch (GPT-2 two per block, norm.hip
+    ln_bwd_finalize_group_kernel): bitwise the per-LayerNorm finalize, dx untouched by the deferral;
+    mixed widths, one problem without a bias, accumulation into non-zero gradients."""
+    torch.manual_seed(17)
+    probs = []
+    for rows, D, with_b in ((333, 768, True), (256, 64, False), (97, 1024, True), (512, 768, True)):
+        x = torch.randn(rows, D, device=dev) * 2 + 1
+        w, b = torch.rand(D, device=dev) + 0.5, torch.randn(D, device=dev)
+        _, mean, rstd = C.layernorm_fwd(x, w, b, 1e-5)
+        dy = bf(torch.randn(rows, D, device=dev))
+        res = torch.randn(rows, D, device=dev)
+        probs.append((x, w, mean, rstd, dy, res, with_b))
+    ref, parts, outs = [], [], []
+    for x, w, mean, rstd, dy, res, with_b in probs:
+        D = x.shape[-1]
+        dw, db = torch.full((D,), 0.5, device=dev), (torch.full((D,), -0.25, device=dev) if with_b else None)
+        dx, dxb = C.layernorm_bwd_residual(dy, x, w, mean, rstd, dw, db, res)
+        ref.append((dx, dxb, dw, db))
+        dw2, db2 = torch.full((D,), 0.5, device=dev), (torch.full((D,), -0.25, device=dev) if with_b else None)
+        dx2, dxb2, part = C.layernorm_bwd_residual(dy, x, w, mean, rstd, dw2, db2, res, True)
+        assert torch.equal(dw2, torch.full((D,), 0.5, device=dev))  # untouched until the finalize
+        parts.append(part)
+        outs.append((dx2, dxb2, dw2, db2))
+    C.layernorm_bwd_finalize_group(parts, [p[0].shape[0] for p in probs], [o[2] for o in outs], [o[3] for o in outs])
+    for (dx, dxb, dw, db), (dx2, dxb2, dw2, db2) in zip(ref, outs):
+        assert torch.equal(dx, dx2) and torch.equal(dxb, dxb2) and torch.equal(dw, dw2)
+        assert (db is None and db2 is None) or torch.equal(db, db2)
+
+
 def test_embedding(C):
     idx = torch.randint(0, 1000, (4, 64), device=dev)
     wte, wpe = bf(torch.randn(1000, 128, device=dev)), bf(torch.randn(64, 128, device=dev))
