@@ -8,8 +8,8 @@ samples/sec for the whole node, one process per GPU over RCCL.
 Per step (all inside the timed region): forward, fused cross-entropy,
 backward with bucketed RCCL all-reduce overlapped on a side stream, fused SGD
 (momentum 0.9, wd 5e-5) update of fp32 masters + bf16 shadows.  Synthetic,
-device-resident ImageNet-shaped batches (3x224x224, generated directly in the
-model's NHWC-bf16 input format, several distinct batches cycled), random-init
+device-resident ImageNet-shaped batches (NCHW fp32 3x224x224, several distinct
+batches cycled; the model packs them into its stem layout inside the step), random-init
 weights.  Weak scaling: --batch-size images per GPU (default 512, the per-GPU
 batch BASELINE.json names for ResNet-50 (config 5); measured on one MI355X:
 256 -> 9.2k, 512 -> 10.0k, 1024 -> 10.7k img/s; stock PyTorch-ROCm 6.3k / 6.7k
@@ -95,13 +95,9 @@ def main():
         wd = 5e-5
         g = torch.Generator(device=dev)
         g.manual_seed(99 + rank)
-        if dev.type == "cuda":
-            # device-resident batches in the stem's packed input layout (space-to-depth bf16)
-            from distributed_pytorch_example_amd.ops import functional as Fx
-
-            xs = [Fx.to_s2d_input(torch.randn(bs, 3, 224, 224, device=dev, generator=g)) for _ in range(args.nbatches)]
-        else:
-            xs = [torch.randn(bs, 3, 224, 224, generator=g, device=dev) for _ in range(args.nbatches)]
+        # device-resident NCHW fp32 batches (a normalising loader's output): the model's packing into the
+        # stem's space-to-depth bf16 layout runs inside every timed step, as a real input would
+        xs = [torch.randn(bs, 3, 224, 224, generator=g, device=dev) for _ in range(args.nbatches)]
         ys = [torch.randint(0, 1000, (bs,), device=dev, generator=g) for _ in range(args.nbatches)]
         samples_per_step = bs * args.grad_accum
         unit_mult = 1

@@ -21,7 +21,8 @@ extern "C" {
 int dpe_cu_reserve();  // comm.cpp: slots to leave to in-flight collectives
 int dpe_gram_blocks(int64_t M, int C);
 int64_t dpe_gram_ws_floats(int64_t M, int C);
-int dpe_gram(const uint16_t* x, const float* coef, int64_t M, int C, float* ws, float* G, float* s, hipStream_t st);
+int dpe_gram(const uint16_t* x, const float* coef, const float* scoef, int64_t M, int C, float* ws, float* G, float* s,
+             hipStream_t st);
 int dpe_gram_coef(const float* G, const float* s, const uint16_t* w, int Cin, int Cout, int64_t M, const float* gamma,
                   const float* beta, float* rmean, float* rvar, float momentum, float eps, float* coef, float* u,
                   hipStream_t st);
@@ -1139,19 +1140,28 @@ std::vector<Tensor> bn_bwd(const Tensor& dy, const c10::optional<Tensor>& y, con
 }
 
 // ------------------------------------------------------------ BN3 by Gram algebra (bngram.hip)
-// G = a2^T a2 [C][C] and s = colsum(a2) [C] of a2 = relu(x * coef[0] + coef[1]) (coef: the BN's [4][C]) or x.
-std::vector<Tensor> bn_gram(const Tensor& x, const c10::optional<Tensor>& coef) {
+// G = a'^T a' [C][C] and s = [colsum(a'), mu] [2][C] of a' = a2 - mu, a2 = relu(x * coef[0] + coef[1]) (coef: the
+// BN's [4][C]) or x, centred on the pilot shift mu (bngram.hip relu_gauss_mean) of the BN coefficients
+// shift_coef (default: coef; neither: mu = 0).
+std::vector<Tensor> bn_gram(const Tensor& x, const c10::optional<Tensor>& coef, const c10::optional<Tensor>& shift_coef) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x);
   const int64_t C = x.size(-1), M = x.numel() / C;
   TORCH_CHECK(C == 64 || C == 128 || C == 256, "bn_gram: C must be 64, 128 or 256");
   if (coef.has_value() && coef->defined()) {
-    CHECK_F32((*coef));
+    CHECK_F32((*coef)); CHECK_CONTIG((*coef));
     TORCH_CHECK(coef->numel() >= 2 * C, "bn_gram: coef must be the BN's [4][C] coefficients");
+  }
+  const float* scoef = fpo(coef);
+  if (scoef) TORCH_CHECK(coef->numel() == 4 * C, "bn_gram: the shift needs coef's full [4][C] (scale, shift, mean, invstd)");
+  if (shift_coef.has_value() && shift_coef->defined()) {
+    CHECK_F32((*shift_coef)); CHECK_CONTIG((*shift_coef));
+    TORCH_CHECK(shift_coef->numel() == 4 * C, "bn_gram: shift_coef must be the BN's [4][C] coefficients");
+    scoef = fp(*shift_coef);
   }
   auto fo = x.options().dtype(at::kFloat);
   Tensor ws = at::empty({dpe_gram_ws_floats(M, (int)C)}, fo);
-  Tensor G = at::empty({C, C}, fo), sv = at::empty({C}, fo);
-  CHECK_RC(dpe_gram(bp(x), fpo(coef), M, (int)C, fp(ws), fp(G), fp(sv), cur_stream()), "bn_gram");
+  Tensor G = at::empty({C, C}, fo), sv = at::empty({2, C}, fo);
+  CHECK_RC(dpe_gram(bp(x), fpo(coef), scoef, M, (int)C, fp(ws), fp(G), fp(sv), cur_stream()), "bn_gram");
   return {G, sv};
 }
 
@@ -1163,7 +1173,8 @@ std::vector<Tensor> bn_gram_coef(const Tensor& G, const Tensor& sv, const Tensor
                                  double eps) {
   CHECK_GPU(G); CHECK_F32(G); CHECK_F32(sv); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(G);
   const int64_t Cin = G.size(0), Cout = w.size(0);
-  TORCH_CHECK(w.numel() == Cout * Cin && sv.numel() == Cin, "bn_gram_coef: shapes");
+  TORCH_CHECK(w.numel() == Cout * Cin && sv.numel() == 2 * Cin, "bn_gram_coef: shapes (s is bn_gram's [2][C])");
+  CHECK_CONTIG(sv);
   Tensor coef = at::empty({4, Cout}, G.options()), u = at::empty({Cout, Cin}, G.options());
   CHECK_RC(dpe_gram_coef(fp(G), fp(sv), bp(w), (int)Cin, (int)Cout, M, fpo(gamma), fpo(beta), fpom(rmean), fpom(rvar),
                          (float)momentum, (float)eps, fp(coef), fp(u), cur_stream()), "bn_gram_coef");
@@ -1210,7 +1221,7 @@ std::vector<Tensor> bn_gram_bwd(const Tensor& part, const Tensor& P, const Tenso
   CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(P); CHECK_CONTIG(dw); CHECK_CONTIG(part);
   const int64_t Cout = w.size(0), Cin = w.numel() / Cout;
   TORCH_CHECK(part.dim() == 3 && part.size(1) == Cout && P.numel() == Cout * Cin && u.numel() == Cout * Cin &&
-                  dw.numel() == Cout * Cin && sv.numel() == Cin && coef.numel() == 4 * Cout,
+                  dw.numel() == Cout * Cin && sv.numel() == 2 * Cin && coef.numel() == 4 * Cout && sv.is_contiguous(),
               "bn_gram_bwd: shapes");
   auto fo = P.options();
   Tensor bcat = at::empty({Cout + Cin, Cin}, w.options()), abc = at::empty({3, Cout}, fo), e = at::empty({Cin}, fo);
@@ -1847,8 +1858,9 @@ void register_ops(pybind11::module& m) {
         py::arg("residual_stride2") = false, py::arg("sum_mask") = py::none(),
         "data grad; with bn_x/bn_coef also the BN-backward partials of the BN+ReLU that produced the conv input; "
         "with bn_mask (BN + residual + ReLU) the mask is bn_mask > 0 and dx is stored masked");
-  m.def("bn_gram", &bn_gram, py::arg("x"), py::arg("coef") = py::none(),
-        "(G = a2^T a2, s = colsum(a2)) of a2 = relu(x * coef[0] + coef[1]) (or x), fp32, deterministic");
+  m.def("bn_gram", &bn_gram, py::arg("x"), py::arg("coef") = py::none(), py::arg("shift_coef") = py::none(),
+        "(G = a'^T a', s = [colsum(a'), mu]) of a' = a2 - mu, a2 = relu(x * coef[0] + coef[1]) (or x), centred on the "
+        "pilot shift of shift_coef (default coef); fp32, deterministic");
   m.def("bn_gram_coef", &bn_gram_coef, py::arg("G"), py::arg("s"), py::arg("w"), py::arg("M"), py::arg("gamma"),
         py::arg("beta"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
         "BN coefficients [4][Cout] of the never-computed h = a2 W^T from (G, s), and u = W G");

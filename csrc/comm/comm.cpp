@@ -88,6 +88,9 @@ namespace {
 std::atomic<int64_t> g_wd_pet_ns{0};
 std::atomic<int64_t> g_wd_limit_ns{0};  // 0: disarmed
 std::atomic<Communicator*> g_wd_comm{nullptr};
+// held by the abort thread for the whole abort and by ~Communicator while it unregisters: the
+// communicator cannot be destroyed under a running abort (the process _exits 5 s after it starts)
+std::mutex g_wd_mu;
 std::once_flag g_wd_once;
 int64_t wd_now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -104,8 +107,11 @@ void wd_loop() {
                  "aborting communicator\n",
                  (double)idle * 1e-9);
     std::fflush(stderr);
-    if (Communicator* c = g_wd_comm.load()) {
-      std::thread([c] { c->abort(); }).detach();
+    if (g_wd_comm.load()) {
+      std::thread([] {
+        std::lock_guard<std::mutex> lk(g_wd_mu);
+        if (Communicator* c = g_wd_comm.load()) c->abort();
+      }).detach();
       std::this_thread::sleep_for(std::chrono::seconds(5));  // bounded: exit whether or not the abort returned
     }
     _exit(1);
@@ -134,8 +140,11 @@ Communicator::Communicator(const std::string& uid, int rank, int world, int devi
 }
 
 Communicator::~Communicator() {
-  Communicator* self = this;
-  g_wd_comm.compare_exchange_strong(self, nullptr);
+  {
+    std::lock_guard<std::mutex> lk(g_wd_mu);  // waits out a running backstop abort (then _exit follows)
+    Communicator* self = this;
+    g_wd_comm.compare_exchange_strong(self, nullptr);
+  }
   if (comm_ && !aborted_) ncclCommDestroy(comm_);
   if (ev_in_) (void)hipEventDestroy(ev_in_);
   if (ev_out_) (void)hipEventDestroy(ev_out_);

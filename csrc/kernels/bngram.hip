@@ -27,10 +27,35 @@ namespace gram {
 constexpr int TR = 32;           // rows per tile (= the MFMA's K)
 constexpr int TS = TR * 2 + 16;  // LDS bytes per channel row of the transposed tile (16 B pad: conflict-free b128 reads)
 
+// Pilot shift of a = relu(z), z = x * scale + shift the BN output ([4][C] coefficients: scale, shift, mean,
+// invstd of x): z ~ N(beta, sigma^2) with beta = shift + mean * scale, sigma = |scale| / invstd, so
+// E[a] ~ beta Phi(beta / sigma) + sigma phi(beta / sigma).  Only an estimate is needed: any mu within
+// O(std) of the true mean removes the cancellation.  mu is rounded to 5 significant bits: then for every
+// bf16 a in [mu / 2, 8 mu] (and a = 0, the ReLU's zeros) bf16(a - mu) is EXACT -- mu's lowest bit is no
+// finer than a's ulp -- so the once-more-rounded MFMA operand carries no error where the data sit, and no
+// bias from mu's own low bits anywhere (what remains, a in (0, mu / 2), rounds a's varying low bits).
+__device__ inline float relu_gauss_mean(const float* sc, int C, int c) {
+  const float scale = sc[c], sh = sc[C + c], mean = sc[2 * C + c], invstd = sc[3 * C + c];
+  const float beta = fmaf(mean, scale, sh);
+  const float sigma = invstd > 0.f ? fabsf(scale) / invstd : 0.f;
+  float mu = fmaxf(beta, 0.f);
+  if (sigma > 0.f && isfinite(sigma)) {
+    const float t = beta / sigma;
+    mu = beta * 0.5f * (1.f + erff(t * 0.70710678f)) + sigma * 0.39894228f * expf(-0.5f * t * t);
+  }
+  if (!isfinite(mu)) return 0.f;
+  const uint32_t b = (__float_as_uint(mu) + (1u << 18)) & ~((1u << 19) - 1u);  // 4 explicit mantissa bits
+  return __uint_as_float(b);
+}
+
 // Partial Gram matrix and column sums of x' = relu(x * coef[c] + coef[C + c]) (coef != nullptr) or x,
-// over rows [blockIdx.x * rpb, +rpb): gp[block][C][C] (full, symmetric), sp[block][C].  x' is rounded
-// to bf16 exactly as the on-load BN transform of the conv kernels rounds their MFMA operand, so G is
-// the Gram matrix of the operand conv3 actually multiplies.
+// CENTRED on the pilot shift mu (relu_gauss_mean of scoef; 0 without scoef), over rows
+// [blockIdx.x * rpb, +rpb): gp[block][C][C] (full, symmetric), sp[block][C] of x' - mu; block 0 also
+// writes mu.  x' is rounded to bf16 exactly as the on-load BN transform of the conv kernels rounds their
+// MFMA operand, so G + (mu terms) is the Gram matrix of the operand conv3 actually multiplies; x' - mu is
+// exact in fp32 and rounded to bf16 once more for the MFMA (exact whenever it cancels, i.e. whenever
+// precision matters).  Without the shift, E[h^2] - mean^2 cancels catastrophically once a channel's
+// |mean| / std reaches ~30 (post-ReLU operands are non-negative): tests/test_bn3_gram_robust_gpu.py.
 //
 // A 32-row tile is loaded as 16-B row chunks: load slot (wave w, instruction i) covers rows
 // 16 (slot % 2) + [0, 16) x chunks 4 (slot / 2) + [0, 4) (lane: row l / 4, chunk l % 4), and stored
@@ -40,8 +65,9 @@ constexpr int TS = TR * 2 + 16;  // LDS bytes per channel row of the transposed 
 // instead of 8 ds_write_b16; the 16-row x 4-chunk slot spreads a store over 32 banks, 2-way).
 template <int C, int NT = (C == 256 ? 512 : 256)>
 __global__ __launch_bounds__(NT) void gram_partial_kernel(const uint16_t* __restrict__ x, const float* __restrict__ coef,
-                                                           int64_t M, int rpb, float* __restrict__ gp,
-                                                           float* __restrict__ sp) {
+                                                           const float* __restrict__ scoef, int64_t M, int rpb,
+                                                           float* __restrict__ gp, float* __restrict__ sp,
+                                                           float* __restrict__ mu_out) {
   constexpr int NW = NT / 64;  // (C = 256: 8 waves, so each holds 17 accumulator fragments, not 34)
   constexpr int NB = C / 16, NF = NB * (NB + 1) / 2, FPW = (NF + NW - 1) / NW;
   constexpr int CPR = C / 8;          // 16-B chunks per row
@@ -49,6 +75,7 @@ __global__ __launch_bounds__(NT) void gram_partial_kernel(const uint16_t* __rest
   static_assert(CPT >= 1 && CPT * NT == TR * CPR && CPR % 4 == 0, "tile split");
   __shared__ __attribute__((aligned(16))) char tile[2][C * TS];
   __shared__ __attribute__((aligned(16))) float cf[2 * C];  // [scale | shift] of the on-load BN
+  __shared__ __attribute__((aligned(16))) float mus[C];     // pilot shift
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
@@ -57,6 +84,11 @@ __global__ __launch_bounds__(NT) void gram_partial_kernel(const uint16_t* __rest
   const bool odd = (lane >> 2) & 1;  // row r + 1 of its pair
   if (coef)
     for (int i = tid; i < 2 * C; i += NT) cf[i] = coef[i];
+  for (int c = tid; c < C; c += NT) {
+    const float m = scoef ? relu_gauss_mean(scoef, C, c) : 0.f;
+    mus[c] = m;
+    if (blockIdx.x == 0) mu_out[c] = m;
+  }
 
   int srow[CPT], scc[CPT];
   float csum[CPT][8];
@@ -117,9 +149,18 @@ __global__ __launch_bounds__(NT) void gram_partial_kernel(const uint16_t* __rest
         const float sh8[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] = valid ? fmaxf(fmaf(f[e], sc8[e], sh8[e]), 0.f) : 0.f;
+        const u32x4 pr = pack8(f);
+        unpack8(pr, f);  // the rounded operand
+      }
+      {
+        const f32x4* cm = (const f32x4*)(mus + 8 * scc[i]);
+        const f32x4 m0 = cm[0], m1 = cm[1];
+        const float mu8[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = valid ? f[e] - mu8[e] : 0.f;  // (pad rows stay 0, not -mu)
       }
       const u32x4 pk = pack8(f);
-      unpack8(pk, f);  // the rounded operand
+      unpack8(pk, f);  // the centred MFMA operand
 #pragma unroll
       for (int e = 0; e < 8; ++e) csum[i][e] += f[e];
       // even lane keeps channels 0-3 of its chunk and takes the odd partner's rows for them; the odd
@@ -256,9 +297,11 @@ __global__ __launch_bounds__(256) void gram_mm_kernel(const uint16_t* __restrict
   for (int e = 0; e < 4; ++e) out[(int64_t)(m0 + tm) * ldo + n0 + tn + e] = acc[e];
 }
 
-// Forward: per output channel k of conv3 (weights w [Cout][Cin] bf16, u = W G from gram_mm_kernel),
-//   mean = (w_k . s) / M,  E[h^2] = (w_k . u[k]) / M  ->  coef [4][Cout] = scale, shift, mean, invstd
-// (the layout of bn_finalize_kernel), running stats updated as there (unbiased variance).  One wave per k.
+// Forward: per output channel k of conv3 (weights w [Cout][Cin] bf16, u = W G from gram_mm_kernel, G and
+// s = s[0 .. Cin) centred on mu = s[Cin .. 2 Cin)):
+//   ms = (w_k . s) / M,  mean = w_k . mu + ms,  var = (w_k . u[k]) / M - ms^2   (no cancellation: ms ~ 0)
+//   -> coef [4][Cout] = scale, shift, mean, invstd (the layout of bn_finalize_kernel), running stats
+// updated as there (unbiased variance).  One wave per k.
 __global__ __launch_bounds__(256) void gram_coef_kernel(const float* __restrict__ u, const float* __restrict__ s,
                                                         const uint16_t* __restrict__ w, int Cin, int Cout, int64_t M,
                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -266,19 +309,22 @@ __global__ __launch_bounds__(256) void gram_coef_kernel(const float* __restrict_
                                                         float eps, float* __restrict__ coef) {
   const int lane = threadIdx.x & 63, k = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (k >= Cout) return;
-  double e2 = 0.0, mu = 0.0;
+  double e2 = 0.0, ws = 0.0, wm = 0.0;
   for (int j = lane; j < Cin; j += 64) {
     const double wv = bf2f(w[(int64_t)k * Cin + j]);
     e2 += wv * u[(int64_t)k * Cin + j];
-    mu += wv * s[j];
+    ws += wv * s[j];
+    wm += wv * s[Cin + j];
   }
   for (int o = 32; o > 0; o >>= 1) {
     e2 += __shfl_xor(e2, o, 64);
-    mu += __shfl_xor(mu, o, 64);
+    ws += __shfl_xor(ws, o, 64);
+    wm += __shfl_xor(wm, o, 64);
   }
   if (lane != 0) return;
-  const double mean = mu / (double)M;
-  double var = e2 / (double)M - mean * mean;
+  const double ms = ws / (double)M;
+  const double mean = wm + ms;
+  double var = e2 / (double)M - ms * ms;
   if (var < 0) var = 0;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   const float gm = gamma ? gamma[k] : 1.f, bt = beta ? beta[k] : 0.f;
@@ -297,12 +343,15 @@ __global__ __launch_bounds__(256) void gram_coef_kernel(const float* __restrict_
 constexpr int KPB = 8;  // output channels per block of the backward coefficient kernel
 
 // Backward, per output channel k.  part [2][Cout][RG]: row 0 = partial sums of dz3 (row 1 unused);
-// P [Cout][Cin] = dz3^T a2; u = W3 G; s = colsum(a2); coef3 = BN3's (scale, shift, mean, invstd).
-//   Sdz = sum dz,  Sdzh = w_k . P[k],  Sdzx = invstd (Sdzh - mean Sdz)
+// P [Cout][Cin] = dz3^T a2 (uncentred: the weight-grad GEMM); G, u = W3 G and s centred on mu (gram_partial);
+// coef3 = BN3's (scale, shift, mean, invstd).  With a' = a2 - mu, h = h' + w_k . mu (h' = w_k . a'):
+//   Sdz = sum dz,  P'[k] = P[k] - Sdz mu = dz^T a',  ms = w_k . s / M  (the centred mean, ~0)
+//   Sdzx = invstd sum dz (h - mean) = invstd (w_k . P'[k] - Sdz ms)
 //   dgamma += Sdzx, dbeta += Sdz;  a = gamma invstd, b = -a invstd Sdzx / M, c = -a Sdz / M - b mean
-//   dW3[k] += a P[k] + b u[k] + c s                       (fp32, the gradient buffer)
+//   dW3[k] += sum dh a2 = sum dh a' (sum dh = 0) = a P'[k] + b u[k] + (-a Sdz / M - b ms) s
 //   bcat[k][:] = bf16(a w_k)                              (the data grad's B rows 0 .. Cout-1)
 //   abc [3][Cout] = (a, b, c) for gram_q_kernel
+// Every term is formed from centred quantities in double: no E[h^2] - mean^2 style cancellation.
 __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__ part, int rg, const float* __restrict__ P,
                                                        const uint16_t* __restrict__ w, const float* __restrict__ u,
                                                        const float* __restrict__ s, const float* __restrict__ coef3,
@@ -310,60 +359,91 @@ __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__
                                                        float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                        float* __restrict__ dw, uint16_t* __restrict__ bcat,
                                                        float* __restrict__ abc) {
-  __shared__ double red[2][KPB][4];
-  __shared__ float kc[KPB][3];
+  __shared__ double red[3][KPB][4];
+  __shared__ double sdz_s[KPB];
+  __shared__ double kc[KPB][4];  // A, B, the s coefficient, Sdz
   const int k0 = blockIdx.x * KPB, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  double sdz[KPB], sdzh[KPB];
-#pragma unroll
-  for (int kk = 0; kk < KPB; ++kk) { sdz[kk] = 0.0; sdzh[kk] = 0.0; }
+  const float* mu = s + Cin;
+  // pass 1: Sdz
+  double sdz[KPB];
 #pragma unroll
   for (int kk = 0; kk < KPB; ++kk) {
+    sdz[kk] = 0.0;
+    const int k = k0 + kk;
+    if (k < Cout)
+      for (int q = tid; q < rg; q += 256) sdz[kk] += part[(int64_t)k * rg + q];
+  }
+#pragma unroll
+  for (int kk = 0; kk < KPB; ++kk) {
+    for (int o = 32; o > 0; o >>= 1) sdz[kk] += __shfl_xor(sdz[kk], o, 64);
+    if (lane == 0) red[0][kk][wid] = sdz[kk];
+  }
+  __syncthreads();
+  if (tid < KPB) {
+    double t = 0.0;
+    for (int q = 0; q < 4; ++q) t += red[0][tid][q];
+    sdz_s[tid] = t;
+  }
+  __syncthreads();
+  // pass 2: w_k . P'[k] and w_k . s (centred)
+  double sdzh[KPB], wsv[KPB];
+#pragma unroll
+  for (int kk = 0; kk < KPB; ++kk) {
+    sdzh[kk] = 0.0;
+    wsv[kk] = 0.0;
     const int k = k0 + kk;
     if (k >= Cout) continue;
-    for (int j = tid; j < Cin; j += 256) sdzh[kk] += (double)bf2f(w[(int64_t)k * Cin + j]) * P[(int64_t)k * Cin + j];
-    for (int q = tid; q < rg; q += 256) sdz[kk] += part[(int64_t)k * rg + q];
+    const double Sdz = sdz_s[kk];
+    for (int j = tid; j < Cin; j += 256) {
+      const double wv = bf2f(w[(int64_t)k * Cin + j]);
+      sdzh[kk] += wv * ((double)P[(int64_t)k * Cin + j] - Sdz * (double)mu[j]);
+      wsv[kk] += wv * (double)s[j];
+    }
   }
 #pragma unroll
   for (int kk = 0; kk < KPB; ++kk) {
     for (int o = 32; o > 0; o >>= 1) {
-      sdz[kk] += __shfl_xor(sdz[kk], o, 64);
       sdzh[kk] += __shfl_xor(sdzh[kk], o, 64);
+      wsv[kk] += __shfl_xor(wsv[kk], o, 64);
     }
-    if (lane == 0) { red[0][kk][wid] = sdz[kk]; red[1][kk][wid] = sdzh[kk]; }
+    if (lane == 0) { red[1][kk][wid] = sdzh[kk]; red[2][kk][wid] = wsv[kk]; }
   }
   __syncthreads();
   if (tid < KPB) {
     const int k = k0 + tid;
-    float a = 0.f, b = 0.f, c = 0.f;
+    double A = 0.0, B = 0.0, Cs = 0.0;
     if (k < Cout) {
-      double Sdz = 0.0, Sdzh = 0.0;
-      for (int q = 0; q < 4; ++q) { Sdz += red[0][tid][q]; Sdzh += red[1][tid][q]; }
+      const double Sdz = sdz_s[tid];
+      double Sdzh = 0.0, Ws = 0.0;
+      for (int q = 0; q < 4; ++q) { Sdzh += red[1][tid][q]; Ws += red[2][tid][q]; }
+      const double ms = Ws / (double)M;
       const double mean = coef3[2 * Cout + k], invstd = coef3[3 * Cout + k];
-      const double Sdzx = invstd * (Sdzh - mean * Sdz);
+      const double Sdzx = invstd * (Sdzh - Sdz * ms);
       const double gm = gamma ? gamma[k] : 1.0;
       if (dgamma) dgamma[k] += (float)Sdzx;
       if (dbeta) dbeta[k] += (float)Sdz;
-      const double A = gm * invstd;
-      const double B = -A * invstd * Sdzx / (double)M;
+      A = gm * invstd;
+      B = -A * invstd * Sdzx / (double)M;
       const double Cc = -A * Sdz / (double)M - B * mean;
-      a = (float)A; b = (float)B; c = (float)Cc;
-      abc[k] = a;
-      abc[Cout + k] = b;
-      abc[2 * Cout + k] = c;
+      Cs = -A * Sdz / (double)M - B * ms;
+      abc[k] = (float)A;
+      abc[Cout + k] = (float)B;
+      abc[2 * Cout + k] = (float)Cc;
     }
-    kc[tid][0] = a; kc[tid][1] = b; kc[tid][2] = c;
+    kc[tid][0] = A; kc[tid][1] = B; kc[tid][2] = Cs; kc[tid][3] = k < Cout ? sdz_s[tid] : 0.0;
   }
   __syncthreads();
 #pragma unroll
   for (int kk = 0; kk < KPB; ++kk) {
     const int k = k0 + kk;
     if (k >= Cout) continue;
-    const float a = kc[kk][0], b = kc[kk][1], c = kc[kk][2];
+    const double A = kc[kk][0], B = kc[kk][1], Cs = kc[kk][2], Sdz = kc[kk][3];
     for (int j = tid; j < Cin; j += 256) {
       const int64_t o = (int64_t)k * Cin + j;
       const float wv = bf2f(w[o]);
-      dw[o] += fmaf(a, P[o], fmaf(b, u[o], c * s[j]));
-      bcat[o] = f2bf(a * wv);
+      const double pc = (double)P[o] - Sdz * (double)mu[j];  // P' = dz^T (a2 - mu)
+      dw[o] += (float)(A * pc + B * (double)u[o] + Cs * (double)s[j]);
+      bcat[o] = f2bf((float)A * wv);
     }
   }
 }
@@ -412,24 +492,29 @@ __global__ __launch_bounds__(256) void gram_e_kernel(const uint16_t* __restrict_
 using namespace dpe;
 
 // Gram pass: x [M][C] bf16 (C in {64, 128, 256}), coef = BN [scale | shift] applied with ReLU on load (or
-// nullptr); ws >= dpe_gram_ws_floats(M, C) floats.  Writes G [C][C], s [C].
+// nullptr), scoef = the [4][C] BN coefficients the pilot shift comes from (nullptr: no shift);
+// ws >= dpe_gram_ws_floats(M, C) floats.  Writes G [C][C] and s [2][C] = (colsum, mu), centred on mu.
 extern "C" int dpe_gram_blocks(int64_t M, int C) {
   const int nb = C <= 128 ? 256 : 128;
   return (int)std::min<int64_t>(nb, std::max<int64_t>(1, (M + gram::TR - 1) / gram::TR));
 }
 extern "C" int64_t dpe_gram_ws_floats(int64_t M, int C) { return (int64_t)dpe_gram_blocks(M, C) * ((int64_t)C * C + C); }
 
-extern "C" int dpe_gram(const uint16_t* x, const float* coef, int64_t M, int C, float* ws, float* G, float* s,
-                        hipStream_t st) {
+extern "C" int dpe_gram(const uint16_t* x, const float* coef, const float* scoef, int64_t M, int C, float* ws, float* G,
+                        float* s, hipStream_t st) {
   if (C != 64 && C != 128 && C != 256) return -1;
   const int nb = dpe_gram_blocks(M, C);
   const int64_t tiles = (M + gram::TR - 1) / gram::TR;
   const int rpb = (int)(((tiles + nb - 1) / nb) * gram::TR);
   float* gp = ws;
   float* sp = ws + (int64_t)nb * C * C;
-  if (C == 64) hipLaunchKernelGGL(gram::gram_partial_kernel<64>, dim3(nb), dim3(256), 0, st, x, coef, M, rpb, gp, sp);
-  else if (C == 128) hipLaunchKernelGGL(gram::gram_partial_kernel<128>, dim3(nb), dim3(256), 0, st, x, coef, M, rpb, gp, sp);
-  else hipLaunchKernelGGL(gram::gram_partial_kernel<256>, dim3(nb), dim3(512), 0, st, x, coef, M, rpb, gp, sp);
+  float* mu = s + C;
+  if (C == 64)
+    hipLaunchKernelGGL(gram::gram_partial_kernel<64>, dim3(nb), dim3(256), 0, st, x, coef, scoef, M, rpb, gp, sp, mu);
+  else if (C == 128)
+    hipLaunchKernelGGL(gram::gram_partial_kernel<128>, dim3(nb), dim3(256), 0, st, x, coef, scoef, M, rpb, gp, sp, mu);
+  else
+    hipLaunchKernelGGL(gram::gram_partial_kernel<256>, dim3(nb), dim3(512), 0, st, x, coef, scoef, M, rpb, gp, sp, mu);
   const int64_t n = (int64_t)C * C + C;
   hipLaunchKernelGGL(gram::gram_reduce_kernel, dim3((unsigned)((n + 31) / 32)), dim3(256), 0, st, gp, sp, nb, C, G, s);
   return 0;

@@ -229,6 +229,10 @@ class BlockFn(Function):
                 done(ln.bias, bb, bd)
             return dx, dxb
 
+        # one grouped launch needs one token count: a backward over two graphs of different B*T (two
+        # micro-batches' losses summed) flushes what the other graph queued before queueing its own
+        if (_wq and _wq[0][0].numel() // _wq[0][0].shape[-1] != T) or (_lnq and _lnq[0][1] != T):
+            flush_wgrad_queue()
         dv = linear_bwd(blk.mlp_proj, gb, u, gelu_in=v)  # GELU backward in the data-grad epilogue
         dh2 = linear_bwd(blk.c_fc, dv, h2)
         g2, g2b = ln_bwd(blk.ln_2, dh2, x2, m2, r2, g)

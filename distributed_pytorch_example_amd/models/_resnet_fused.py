@@ -216,11 +216,15 @@ class BottleneckFn(Function):
         # the next block's fused data-grad epilogue reads this output's ReLU mask as bits
         want_bits = True  # 1/16 of out: read by the next block's fused epilogue or by this block's BN3 backward
         gram = None
+        # gram_next < 0: the successor is a downsample block, which chains this block's BN3 backward only
+        # when its strided conv1 data grad can take the residual (the successor's own strided_ok test)
+        out_shape = [*h2.shape[:3], convs[2].conv.out_channels]
         if (gram_next and link_out is not None and not defer_out and h1_st is None
-                and C.gram_ok(list(h2.shape), convs[2].conv.out_channels, gram_next)):
+                and (gram_next > 0 or C.pw_dgrad_strided_residual_ok(out_shape, -gram_next))
+                and C.gram_ok(list(h2.shape), convs[2].conv.out_channels, abs(gram_next))):
             # BN3 statistics from G = a2^T a2, s = colsum(a2); conv3 writes relu(BN3(h3) + idn) directly
             src, src_coef = (h2, c2) if a2 is None else (a2, None)
-            G, sv = C.bn_gram(src, src_coef)
+            G, sv = C.bn_gram(src, src_coef, c2)  # centred on a pilot shift from BN2's coefficients
             bn3 = convs[2].bn
             M3 = h2.numel() // h2.shape[-1]
             c3, u3 = C.bn_gram_coef(G, sv, ws[2], M3, bn3.weight.detach(), bn3.bias.detach(), bn3.running_mean,
@@ -254,9 +258,11 @@ class BottleneckFn(Function):
             C.pw_dgrad_strided_residual_ok(list(x.shape), convs[0].conv.out_channels)
         ctx.link_in = (link_in if (link_in is not None and (block.down is None or strided_ok)
                                    and (link_in.h3 is not None or link_in.gram) and link_in.mask is not None) else None)
-        if link_in is not None and link_in.gram:
+        if link_in is not None and link_in.gram and ctx.link_in is None:
             # the previous block has no h3 and no standalone BN3 backward: this block must chain it
-            assert ctx.link_in is not None, "BN3 Gram path: the next block cannot chain the BN3 backward"
+            # (gram_successor_width + the strided test above make this unreachable; fail loudly if not)
+            raise RuntimeError("BN3 Gram path: the next block cannot chain the BN3 backward "
+                               f"(input {tuple(x.shape)}, downsample={block.down is not None})")
         ctx.link_out = link_out
         ctx.bits = bits  # ReLU mask of out as bits: the standalone BN3 backward reads these, not out
         ctx.gram = gram
@@ -342,7 +348,8 @@ class BottleneckFn(Function):
         ctx.gram = None
         if gram is not None:
             # BN3 by Gram algebra: dz3 = dout came from the next block's epilogue with the sum-dz partials
-            assert chained, "BN3 Gram path: the block output's gradient did not come from the chained epilogue"
+            if not chained:
+                raise RuntimeError("BN3 Gram path: the block output's gradient did not come from the chained epilogue")
             u3, sv, M3 = gram
             dz3 = dout
             src, src_coef = (h2, c2) if a2 is None else (a2, None)
@@ -480,7 +487,9 @@ class BottleneckFn(Function):
 
 def gram_successor_width(nxt) -> int:
     """For the block before ``nxt``: nxt's conv1 width when nxt will chain the BN3 backward in the form
-    the Gram path needs (sum-dz partials from its conv1 data grad), else 0."""
+    the Gram path needs (sum-dz partials from its conv1 data grad), else 0.  NEGATIVE for a downsample
+    successor: the forward then also runs the successor's shape test (even H/W, strided-residual data
+    grad on the streaming kernel) on the actual output shape before taking the Gram path."""
     if not _GRAM or nxt is None or not nxt.fused:
         return 0
     c1 = nxt.c1.conv
@@ -490,6 +499,7 @@ def gram_successor_width(nxt) -> int:
         d = nxt.down.conv
         if not (_DOWN_CHAIN and tuple(d.stride) == (2, 2) and tuple(d.kernel_size) == (1, 1)):
             return 0
+        return -c1.out_channels
     return c1.out_channels
 
 

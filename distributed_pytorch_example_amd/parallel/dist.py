@@ -228,9 +228,19 @@ class Watchdog:
         # if it is starved or blocked for timeout_s + 15 s (at least 3 check intervals + 15 s), a native thread
         # aborts the communicator and exits
         self._native = _native_watchdog()
-        if self._native is not None:
-            self._native.watchdog_backstop(max(float(timeout_s), 3.0 * float(interval_s)) + 15.0)
+        self._arm_native()
         self._thread.start()
+
+    def _arm_native(self) -> None:
+        """(Re-)arm the native backstop for the CURRENT deadline: timeout (+ the grace in force) + 15 s;
+        disarmed while suspended -- the Python check is off there too, so a legitimately long checkpoint
+        write or the barrier behind it never meets a shorter native limit than the Python one."""
+        if self._native is None:
+            return
+        if self._paused:
+            self._native.watchdog_backstop(0.0)
+        else:
+            self._native.watchdog_backstop(max(float(self.timeout_s), 3.0 * float(self.interval_s)) + self._grace + 15.0)
 
     def beat(self) -> None:
         """A step finished on the host.  On a GPU job progress is what the DEVICE completes: the beat
@@ -269,11 +279,13 @@ class Watchdog:
         @contextlib.contextmanager
         def _ctx():
             self._paused += 1
+            self._arm_native()
             try:
                 yield self
             finally:
                 self._paused -= 1
                 self.beat()
+                self._arm_native()
 
         return _ctx()
 
@@ -287,11 +299,13 @@ class Watchdog:
             old = self._grace
             self._grace = max(old, float(extra_s))
             self.beat()
+            self._arm_native()  # the native limit follows the raised deadline
             try:
                 yield self
             finally:
                 self._grace = old
                 self.beat()
+                self._arm_native()
 
         return _ctx()
 

@@ -98,8 +98,11 @@ def _datasets(args, device):
     return tr, va, vocab
 
 
-def train_epoch(model, loader, optimizer, criterion, device, epoch, rank, grad_accum=1, max_steps=None, watchdog=None):
-    """Reference `train_epoch` (`train.py:119-151`); loss accumulated on device."""
+def train_epoch(model, loader, optimizer, criterion, device, epoch, rank, grad_accum=1, max_steps=None, watchdog=None,
+                fused_loss=False):
+    """Reference `train_epoch` (`train.py:119-151`); loss accumulated on device.  ``fused_loss``: the
+    model takes the targets and returns the loss itself (GPT-2's fused LM head + CE, reference
+    `train.py:136-137` as one op: the [B, T, V] logits never materialise)."""
     model.train()
     total_loss = torch.zeros((), dtype=torch.float64, device=device)
     num_batches = 0
@@ -116,8 +119,11 @@ def train_epoch(model, loader, optimizer, criterion, device, epoch, rank, grad_a
         ctx = model.no_sync() if (not sync and hasattr(model, "no_sync")) else _null()
         with ctx:
             with tracing.range("forward"):
-                output = model(data)
-                loss = criterion(output, target)
+                if fused_loss:
+                    loss = model(data, target)
+                else:
+                    output = model(data)
+                    loss = criterion(output, target)
             with tracing.range("backward"):
                 (loss / grad_accum if grad_accum > 1 else loss).backward()
         if sync:
@@ -219,7 +225,7 @@ def main(argv=None):
         epoch_start = time.time()
         train_sampler.set_epoch(epoch)
         train_loss = train_epoch(model, train_loader, optimizer, criterion, device, epoch, rank, args.grad_accum,
-                                 args.max_steps, watchdog)
+                                 args.max_steps, watchdog, fused_loss=args.model.startswith("gpt2"))
         val_loss, val_accuracy = validate(model, val_loader, criterion, device, num_classes, args.max_steps, watchdog)
 
         metrics = torch.tensor([train_loss, val_loss, val_accuracy], device=device)

@@ -52,8 +52,23 @@ def test_gram_and_coef(C, with_coef):
     G, s = X.bn_gram(x, coef)
     a = _operand(x, coef).double()
     Gr, sr = a.t() @ a, a.sum(0)
-    assert _rel(G, Gr) < 2e-5 and _rel(s, sr) < 2e-5, (_rel(G, Gr), _rel(s, sr))
+    # centred on the pilot shift mu = s[1] (bf16 values; 0 without coefficients): G, s[0] are exactly the
+    # Gram matrix / column sums of the bf16 MFMA operand bf16(a - mu)
+    mu = s[1].double()
+    if coef is None:
+        assert torch.equal(s[1], torch.zeros_like(s[1]))
+    else:  # E[relu(z)], z ~ N(shift, scale^2): a per-channel estimate of a's mean (bf16-rounded)
+        mb = s[1].view(torch.int32)
+        assert torch.equal(mb & ((1 << 19) - 1), torch.zeros_like(mb))  # 5 significant bits
+        assert ((mu - a.mean(0)).abs() <= 0.1 * a.std(0) + 0.05).all(), (mu - a.mean(0)).abs().max()
+    ac = (a - mu).float().bfloat16().double()
+    Gc, sc = ac.t() @ ac, ac.sum(0)
+    assert _rel(G, Gc) < 2e-5 and _rel(s[0], sc) < 2e-5, (_rel(G, Gc), _rel(s[0], sc))
     assert torch.allclose(G, G.t())
+    # the uncentred Gram matrix it stands for: G + mu s^T + s mu^T + M mu mu^T (bf16(a - mu) is exact where
+    # it cancels, rounded where it does not)
+    Gfull = G.double() + torch.outer(mu, s[0].double()) + torch.outer(s[0].double(), mu) + M * torch.outer(mu, mu)
+    assert _rel(Gfull, Gr) < 1e-3 and _rel(s[0].double() + M * mu, sr) < 1e-3
     # BN coefficients of h = a W^T without h: mean = w.s / M, E[h^2] = w^T G w / M
     Cout = 4 * C
     w = (torch.randn(Cout, 1, 1, C, device=DEV, generator=g) * C ** -0.5).bfloat16()
@@ -65,7 +80,7 @@ def test_gram_and_coef(C, with_coef):
     mean, var = h.mean(0), h.var(0, unbiased=False)
     ref = _bn_coef(mean, var, gamma.double(), beta.double(), 1e-5)
     assert _rel(coef3, ref) < 1e-4, _rel(coef3, ref)
-    assert _rel(u, w.reshape(Cout, C).double() @ Gr) < 2e-5
+    assert _rel(u, w.reshape(Cout, C).double() @ Gc) < 2e-5  # (u = W G of the centred G)
     assert _rel(rm, 0.1 * mean) < 1e-4 and _rel(rv, 0.9 + 0.1 * h.var(0, unbiased=True)) < 1e-4
 
 
@@ -161,9 +176,11 @@ def test_gram_backward_and_cat_dgrad(C):
 
 
 def test_resnet50_step_gram_on_vs_off():
-    """A whole ResNet-50 training step (batch 8, 224^2) with the Gram path on vs off: every parameter
-    gradient and the loss agree to bf16 noise (the path changes summation orders and skips the
-    rounding of h3, not the math), and the BN running statistics agree."""
+    """A whole ResNet-50 training step (batch 8, 224^2) with the Gram path on vs off: the loss agrees to
+    bf16 noise and the BN running statistics agree; the parameter gradients are only checked finite here
+    (at step 0 BN parameter gradients differ by O(1) between any two bf16 implementations).  The
+    discriminating gradient checks are test_chained_blocks_gram_matches_per_op (block level, per tensor)
+    and test_model_parity_gpu.py's fp32-oracle bound."""
     import distributed_pytorch_example_amd.models._resnet_fused as rf
     from distributed_pytorch_example_amd.models import get_model
     from distributed_pytorch_example_amd.ops import functional as Fx
@@ -199,3 +216,53 @@ def test_resnet50_step_gram_on_vs_off():
     berrs = sorted(((_rel(b1[n], b0[n]), n) for n in b0), reverse=True)
     print("worst running-stat deviations:", [(n, f"{e:.2e}") for e, n in berrs[:3]])
     assert berrs[0][0] < 5e-2, berrs[:3]
+
+
+def test_chained_blocks_gram_gradient_parity():
+    """Bottlenecks chained as ResNet.forward chains them, with BN3 by Gram algebra on every block whose
+    successor chains its backward (identity blocks, the block before a downsample, the downsample block):
+    every parameter gradient -- W3 and BN3's included -- per tensor against an fp32 torch twin of the
+    same blocks, bounded by twice torch's own bf16-autocast error on that tensor (+ 2e-3).  (Against our
+    per-op path this cannot be a tight check: the Gram path's forward does not round h3, and step-0 BN
+    gradients amplify any forward difference.)"""
+    import torch.nn as nn
+    from test_model_parity_gpu import _TBottleneck, _grad_check, _no_tf32
+
+    from distributed_pytorch_example_amd.models import _resnet_fused as RF
+    from distributed_pytorch_example_amd.models.resnet import Bottleneck
+
+    if not RF._GRAM:
+        pytest.skip("DPE_BN3_GRAM=0")
+    _no_tf32()
+    torch.manual_seed(3)
+    cfg = [(256, 64, 1, False)] * 3 + [(256, 128, 2, True), (512, 128, 1, False)]
+    ours = nn.ModuleList([Bottleneck(*c) for c in cfg]).to(DEV)
+    twin = nn.Sequential(*[_TBottleneck(b) for b in ours]).to(DEV)
+    twin_bf = copy.deepcopy(twin)
+    x = torch.randn(32, 28, 28, 256, device=DEV).bfloat16()
+    h, link, used = x, None, []
+    for i, b in enumerate(ours):
+        gn = RF.gram_successor_width(ours[i + 1]) if i + 1 < len(ours) else 0
+        h, link = b.forward_chained(h, link, gram_next=gn)
+        used.append(gn != 0 and link.gram)
+    assert used == [True, True, True, True, False]
+    gy = torch.randn_like(h)
+    h.backward(gy)
+    xt = x.float().permute(0, 3, 1, 2).contiguous()
+    gt = gy.float().permute(0, 3, 1, 2)
+    twin(xt).backward(gt)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        yb = twin_bf(xt)
+    yb.float().backward(gt)
+    names, go, gf, gb = [], [], [], []
+    for i, (b, t, tb) in enumerate(zip(ours, twin, twin_bf)):
+        for k in ("c1", "c2", "c3", "down"):
+            cb = getattr(b, k)
+            if cb is None:
+                continue
+            ct, cbf = getattr(t, k), getattr(tb, k)
+            go += [cb.conv.weight.grad.float().permute(0, 3, 1, 2), cb.bn.weight.grad.float(), cb.bn.bias.grad.float()]
+            gf += [ct.conv.weight.grad, ct.bn.weight.grad, ct.bn.bias.grad]
+            gb += [cbf.conv.weight.grad.float(), cbf.bn.weight.grad.float(), cbf.bn.bias.grad.float()]
+            names += [f"b{i}.{k}.conv.weight", f"b{i}.{k}.bn.weight", f"b{i}.{k}.bn.bias"]
+    _grad_check("Gram-chained bottlenecks bs32 28^2", names, go, gf, gb)

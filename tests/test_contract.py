@@ -88,6 +88,48 @@ def test_grad_accum_syncs_at_max_steps_cutoff():
     assert opt.steps == [2, 3]  # after micro-batch 2 (accum boundary) and after the cut-off batch 3
 
 
+def test_gpt2_train_epoch_uses_fused_loss_path():
+    """``train.py --model gpt2`` calls model(x, y) (the fused LM head + CE op the
+    bench times) and its loss equals the generic criterion over the materialised logits."""
+    import torch
+
+    from distributed_pytorch_example_amd.models import get_model
+    from distributed_pytorch_example_amd.ops import functional as Fx
+    from distributed_pytorch_example_amd.train import train_epoch
+
+    torch.manual_seed(0)
+    m = get_model("gpt2_tiny")
+    x = torch.randint(0, 512, (2, 16))
+    y = torch.randint(0, 512, (2, 16))
+    with torch.no_grad():
+        ref = Fx.cross_entropy(m(x), y, 512)
+        fused = m(x, y)
+    assert torch.allclose(fused, ref, rtol=1e-5, atol=1e-6)
+    calls = []
+
+    class Spy(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.m = m
+
+        def forward(self, *a):
+            calls.append(len(a))
+            return self.m(*a)
+
+    class Opt:
+        def step(self):
+            pass
+
+        def zero_grad(self):
+            pass
+
+    def crit(out, tgt):
+        raise AssertionError("the generic criterion must not run on the GPT-2 path")
+
+    loss = train_epoch(Spy(), [(x, y)], Opt(), crit, torch.device("cpu"), 0, 1, fused_loss=True)
+    assert calls == [2] and abs(loss - ref.item()) < 1e-4
+
+
 def test_watchdog_suspended_during_checkpoint_write():
     import time
 
@@ -122,6 +164,36 @@ def test_watchdog_grace_is_bounded():
             assert fails and "no progress" in fails[0]
     finally:
         wd.stop()
+
+
+def test_watchdog_native_backstop_follows_grace_and_suspension(monkeypatch):
+    """the native backstop's limit is re-armed to timeout + grace + 15 s inside grace()
+    (and disarmed inside suspended()), then restored -- it never kills a rank the Python watchdog
+    would still wait for."""
+    from distributed_pytorch_example_amd.parallel import dist as pdist
+
+    armed = []
+
+    class FakeNative:
+        def watchdog_backstop(self, s):
+            armed.append(s)
+
+        def watchdog_pet(self):
+            pass
+
+    monkeypatch.setattr(pdist, "_native_watchdog", lambda: FakeNative())
+    wd = pdist.Watchdog(timeout_s=100.0, interval_s=1.0)
+    try:
+        assert armed == [115.0]
+        with wd.grace(600.0):
+            assert armed[-1] == 715.0
+            with wd.suspended():
+                assert armed[-1] == 0.0
+            assert armed[-1] == 715.0
+        assert armed[-1] == 115.0
+    finally:
+        wd.stop()
+    assert armed[-1] == 0.0
 
 
 def test_watchdog_suspension_ends_on_exception():

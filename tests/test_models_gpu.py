@@ -81,6 +81,22 @@ def test_chained_blocks_bn3_fusion_matches_per_op(C):
         assert rel(p1.grad, p2.grad) < 5e-2, n
 
 
+def test_resnet50_step_with_odd_layer4_input(C):
+    """at 112x112 the layer-4 downsample block's input is [N, 7, 7, 1024] (odd H/W), so
+    that block cannot chain the previous block's BN3 backward; the previous block must then NOT take the
+    Gram path (it has no standalone BN3 backward).  A whole step runs and its gradients are finite."""
+    torch.manual_seed(2)
+    m = get_model("resnet50").to(dev)
+    x = torch.randn(32, 3, 112, 112, device=dev)
+    y = torch.randint(0, 1000, (32,), device=dev)
+    loss = Fx.cross_entropy(m(x), y, 1000)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).item()
+    for n, p in m.named_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all().item(), n
+
+
 def test_resnet_gpu_vs_cpu_reference(C):
     torch.manual_seed(1)
     cpu = get_model("resnet_tiny", num_classes=10)
