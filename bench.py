@@ -67,6 +67,9 @@ def parse():
                          "after the warm-up and replay it; each step copies its batch into the graph's input "
                          "buffers (world 1, grad-accum 1; dropout masks, seeded from a host counter, are "
                          "frozen at capture -- SimpleNet's)")
+    ap.add_argument("--overlap-optimizer", type=int, default=0,
+                    help="1: the fused optimizer steps each gradient bucket during backward on its own stream "
+                         "(DDP.overlap_optimizer) instead of after it")
     ap.add_argument("--dtype", default=None, choices=[None, "fp32", "bf16"],
                     help="simplenet compute dtype (default fp32, the reference's); resnet50/gpt2 are bf16")
     return ap.parse_args()
@@ -147,6 +150,9 @@ def main():
         cfg["rccl_max_channels"] = pdist.comm_max_channels()
         cfg["cu_reserve_slots"] = _ext().cu_reserve_config() if dev.type == "cuda" else 0
     opt = build_optimizer(opt_name, model.parameters(), lr=lr, weight_decay=wd)
+    if args.overlap_optimizer and dev.type == "cuda" and not args.graph:
+        ddp.overlap_optimizer(opt)
+        cfg["optimizer_in_backward"] = True
 
     def step(i):
         for a in range(args.grad_accum):

@@ -302,6 +302,7 @@ Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_
   HIP_CHECK(hipEventCreateWithFlags(&ev_bwd_end_, flags));
   HIP_CHECK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&ev_step_begin_, flags));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_wait_, hipEventDisableTiming));
   // Register the buffers RCCL actually moves (fp32 buckets, or their bf16 staging copies) once per
   // (re)build; they live exactly as long as this reducer and are deregistered before release.
   if (register_buckets && comm_ && (comm_->world() > 1 || force_)) {
@@ -357,6 +358,14 @@ Reducer::~Reducer() {
   (void)hipEventDestroy(ev_bwd_end_);
   (void)hipEventDestroy(ev_done_);
   (void)hipEventDestroy(ev_step_begin_);
+  (void)hipEventDestroy(ev_wait_);
+}
+
+void Reducer::stream_wait_comm(uint64_t stream) {
+  if (host_launch_ || !comm_ || (comm_->world() == 1 && !force_)) return;
+  // (one event re-recorded each time: a wait captures the event's state when it is issued)
+  HIP_CHECK(hipEventRecord(ev_wait_, comm_->comm_stream().stream()));
+  HIP_CHECK(hipStreamWaitEvent((hipStream_t)(uintptr_t)stream, ev_wait_, 0));
 }
 
 void Reducer::prepare() {
@@ -522,7 +531,9 @@ void register_comm(pybind11::module& m) {
       .def("finalize", &Reducer::finalize)
       .def("last_timings", &Reducer::last_timings)
       .def_property_readonly("num_buckets", &Reducer::num_buckets)
-      .def_property_readonly("buckets_launched", &Reducer::buckets_launched);
+      .def_property_readonly("buckets_launched", &Reducer::buckets_launched)
+      .def("stream_wait_comm", &Reducer::stream_wait_comm, py::arg("stream"),
+           "the given HIP stream waits for every collective issued so far (no-op without collectives)");
 }
 
 }  // namespace dpe

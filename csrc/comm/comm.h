@@ -102,6 +102,9 @@ class Reducer {
   int world() const { return host_launch_ ? host_world_ : (comm_ ? comm_->world() : 1); }
   bool host_mode() const { return (bool)host_launch_; }
   int64_t buckets_launched() const { return next_; }
+  // make `stream` wait for every collective issued so far on the comm stream (no-op when none are issued:
+  // world 1 without force, host transport) -- the overlapped optimizer's per-bucket ordering
+  void stream_wait_comm(uint64_t stream);
   std::vector<int64_t> launch_order() const { return launch_order_; }
 
  private:
@@ -119,7 +122,7 @@ class Reducer {
   std::vector<at::Tensor> staging_;  // bf16 copies of the buckets (comm_bf16)
   std::vector<int64_t> launch_order_;
   std::vector<hipEvent_t> ev_ready_, ev_aux_, ev_start_, ev_end_;
-  hipEvent_t ev_bwd_end_ = nullptr, ev_done_ = nullptr, ev_step_begin_ = nullptr;
+  hipEvent_t ev_bwd_end_ = nullptr, ev_done_ = nullptr, ev_step_begin_ = nullptr, ev_wait_ = nullptr;
   bool step_open_ = false;
   std::vector<uint64_t> reg_handles_;  // ncclCommRegister handles of the buckets / bf16 staging buffers
   std::function<void(int64_t)> host_launch_;

@@ -393,11 +393,12 @@ __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__
     wsv[kk] = 0.0;
     const int k = k0 + kk;
     if (k >= Cout) continue;
-    const double Sdz = sdz_s[kk];
+    const float Sdzf = (float)sdz_s[kk];
     for (int j = tid; j < Cin; j += 256) {
-      const double wv = bf2f(w[(int64_t)k * Cin + j]);
-      sdzh[kk] += wv * ((double)P[(int64_t)k * Cin + j] - Sdz * (double)mu[j]);
-      wsv[kk] += wv * (double)s[j];
+      const float wv = bf2f(w[(int64_t)k * Cin + j]);
+      // P' = P - Sdz mu in one fp32 fma: exact product, one rounding -- an error of P's own size
+      sdzh[kk] += (double)(wv * fmaf(-Sdzf, mu[j], P[(int64_t)k * Cin + j]));
+      wsv[kk] += (double)(wv * s[j]);
     }
   }
 #pragma unroll
@@ -437,13 +438,13 @@ __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__
   for (int kk = 0; kk < KPB; ++kk) {
     const int k = k0 + kk;
     if (k >= Cout) continue;
-    const double A = kc[kk][0], B = kc[kk][1], Cs = kc[kk][2], Sdz = kc[kk][3];
+    const float A = (float)kc[kk][0], B = (float)kc[kk][1], Cs = (float)kc[kk][2], Sdz = (float)kc[kk][3];
     for (int j = tid; j < Cin; j += 256) {
       const int64_t o = (int64_t)k * Cin + j;
       const float wv = bf2f(w[o]);
-      const double pc = (double)P[o] - Sdz * (double)mu[j];  // P' = dz^T (a2 - mu)
-      dw[o] += (float)(A * pc + B * (double)u[o] + Cs * (double)s[j]);
-      bcat[o] = f2bf((float)A * wv);
+      const float pc = fmaf(-Sdz, mu[j], P[o]);  // P' = dz^T (a2 - mu)
+      dw[o] += fmaf(A, pc, fmaf(B, u[o], Cs * s[j]));
+      bcat[o] = f2bf(A * wv);
     }
   }
 }

@@ -38,6 +38,10 @@ class _FusedMixin:
         self._hp = None
         self._steps = None
         self.graph_safe = False  # when True: skip per-step host checks (caller guarantees static pointers)
+        self._ov_stream = None  # DDP.overlap_optimizer: per-bucket steps during backward on this stream
+        self._ov_open = False
+        self._ov_done = set()
+        self._ov_cache = {}
 
     def _all_params(self):
         return [p for g in self.param_groups for p in g["params"]]
@@ -87,6 +91,7 @@ class _FusedMixin:
         params = self._all_params()
         desc = bytearray()
         chunks = []
+        self._ti = {}
         gi_of = {}
         for gi, g in enumerate(self.param_groups):
             for p in g["params"]:
@@ -102,6 +107,7 @@ class _FusedMixin:
             sh = getattr(p, "_dpe_shadow", None)
             if sh is not None and getattr(p, "_dpe_shadow_ver", -1) != p._version:
                 sh = None  # stale shadow: let the layer re-cast it
+            self._ti[id(p)] = ti
             desc += struct.pack("<QQQQQqii", p.data_ptr(), p.grad.data_ptr(), s1.data_ptr() if s1 is not None else 0,
                                 s2.data_ptr() if s2 is not None else 0, sh.data_ptr() if sh is not None else 0,
                                 p.numel(), gi_of[id(p)], ti)
@@ -112,6 +118,8 @@ class _FusedMixin:
         d = torch.frombuffer(desc, dtype=torch.uint8).to(dev)
         ck = torch.tensor(chunks, dtype=torch.int32).reshape(-1, 2).to(dev)
         self._tab = (d, ck)
+        self._chunks_host = chunks
+        self._ov_cache = {}
 
     def _key(self):
         ks = []
@@ -149,8 +157,58 @@ class _FusedMixin:
                 self._hp.copy_(t, non_blocking=False)
             self._hp_key = key
 
+    # -------------------------------------------- optimizer in backward (DDP.overlap_optimizer)
+    def _ov_attach(self, stream):
+        self._ov_stream, self._ov_open, self._ov_done = stream, False, set()
+
+    def _ov_detach(self):
+        if self._ov_open:
+            torch.cuda.current_stream().wait_stream(self._ov_stream)
+        self._ov_stream, self._ov_open = None, False
+
+    def _ov_launch(self, tis, stream):
+        """The fused kernel over the chunks of tensors ``tis`` only (chunk lists cached per bucket)."""
+        key = tuple(tis)
+        ck = self._ov_cache.get(key)
+        if ck is None:
+            want = set(key)
+            ck = torch.tensor([c for c in self._chunks_host if c[0] in want], dtype=torch.int32).reshape(-1, 2).to(
+                self._tab[0].device)
+            self._ov_cache[key] = ck
+        with torch.cuda.stream(stream):
+            ext().optim_step(self._kind, self._tab[0], ck, self._hp, self._steps)
+        self._ov_done.update(key)
+
+    @torch.no_grad()
+    def _ov_bucket_step(self, params, stream):
+        """Step ``params`` (one DDP bucket whose gradients are final and whose readers have returned) on
+        ``stream``, which the caller has already ordered after them.  The first bucket of an iteration
+        refreshes the device table / hyper-parameters and advances every step counter once."""
+        if not self._ov_open:
+            with torch.cuda.stream(stream):
+                self._ensure_state()
+                key = self._key()
+                if key != self._tab_key:
+                    self._build_table()
+                    self._tab_key = key
+                self._write_hp()
+                self._steps.add_(1.0)
+            self._ov_open, self._ov_done = True, set()
+        tis = sorted({self._ti[id(p)] for p in params if id(p) in self._ti} - self._ov_done)
+        if tis:
+            self._ov_launch(tis, stream)
+
     @torch.no_grad()
     def _fused_step(self):
+        if self._ov_open:
+            # the buckets were stepped during backward: step anything left, then join the stream
+            rest = [ti for ti in range(len(self._all_params())) if ti not in self._ov_done]
+            if rest:
+                self._ov_launch(rest, self._ov_stream)
+            torch.cuda.current_stream().wait_stream(self._ov_stream)
+            self._ov_open = False
+            _state.after_optimizer_step()
+            return
         if not self.graph_safe or self._tab is None:
             self._ensure_state()
             key = self._key()

@@ -44,6 +44,12 @@ Design (MI355X-first, not a port of c10d::Reducer):
   broadcast is a single RCCL call with no concatenate / scatter-back copies
   (c10d coalesces into a temporary and copies back: ~2 tiny kernels per
   buffer per step).
+* **Optimizer in backward** (``overlap_optimizer(opt)``, opt-in): the fused optimizer's step runs per
+  gradient bucket on its own stream DURING backward -- bucket b is stepped once its gradients are final
+  (and, at world > 1, all-reduced) and every autograd node that read its parameters has returned (their
+  post-accumulate hooks fired), so no backward kernel can read a weight the step rewrites.  The
+  memory-bound update overlaps the compute-bound tail of backward instead of following it; ``opt.step()``
+  then only joins the stream (and steps anything left).  Same math, same order per parameter.
 """
 from __future__ import annotations
 
@@ -58,6 +64,7 @@ import torch.nn as nn
 
 from . import dist as pdist
 from . import hooks as _hooks
+from ..ops import _state
 from .buckets import assign_buckets, xgmi_bucket_policy
 from ..utils.logging import get_logger
 from ..ops._state import aux_wait as _aux_wait
@@ -250,6 +257,7 @@ class DistributedDataParallel(nn.Module):
         self._flat_views = []
         if broadcast_buffers and self.world_size > 1:
             self._flatten_buffers()
+        self._ov_opt = None  # overlap_optimizer()
         self._build_buckets(None)
         self._queued = False
         self._hooks = []
@@ -305,6 +313,10 @@ class DistributedDataParallel(nn.Module):
             p.grad = self._views[i]
             if old is not None and old[i] is not None:
                 self._views[i].copy_(old[i])
+        self._pbucket = [0] * n
+        for b, bidx in enumerate(self.bucket_indices):
+            for i in bidx:
+                self._pbucket[i] = b
         self._make_reducer()
         if self._debug:
             self._check_layout()
@@ -408,10 +420,80 @@ class DistributedDataParallel(nn.Module):
         """Post-accumulate-grad hook: readiness of parameters written through autograd.  It also fires
         after a node that wrote the parameter itself (and returned None for it) -- those announce
         themselves with grad_done, and a parameter whose weight gradient is still queued for a grouped
-        launch (``_dpe_deferred``, models/_gpt2_fused.py) must not be announced before that launch."""
+        launch (``_dpe_deferred``, models/_gpt2_fused.py) must not be announced before that launch.
+        Either way every node that read the parameter has returned: for the overlapped optimizer the
+        parameter may now be rewritten."""
+        if self._ov_opt is not None and self.require_backward_grad_sync:
+            self._ov_mark(p, 2)
         if getattr(p, "_dpe_deferred", False):
             return
         self._on_ready(p)
+
+    # ------------------------------------------------- optimizer in backward
+    def overlap_optimizer(self, optimizer, enable: bool = True) -> None:
+        """Step the fused ``optimizer`` (optim.Adam / AdamW / SGD) per gradient bucket during backward,
+        on a dedicated HIP stream; the training loop keeps calling ``optimizer.step()`` after backward
+        (it joins the stream and steps whatever is left).  GPU only; with custom comm hooks or a host
+        (gloo) transport at world > 1 the gradients are final only at the end of backward, so the
+        overlap is refused there.  Gradient clipping / unscaling between backward and step cannot be
+        combined with it (the update has already run)."""
+        if not enable:
+            if self._ov_opt is not None:
+                self._ov_opt._ov_detach()
+            self._ov_opt = None
+            return
+        if not hasattr(optimizer, "_ov_bucket_step"):
+            raise TypeError("overlap_optimizer needs one of the fused optimizers (distributed_pytorch_example_amd.optim)")
+        if not (self._params and self._params[0].is_cuda):
+            raise RuntimeError("overlap_optimizer: GPU parameters only")
+        if self.world_size > 1 and not self._native:
+            raise RuntimeError("overlap_optimizer: needs the native RCCL reducer at world size > 1")
+        ids = {id(p) for g in optimizer.param_groups for p in g["params"]}
+        if any(id(p) not in ids for p in self._params):
+            raise ValueError("overlap_optimizer: the optimizer must own every parameter DDP reduces")
+        self._ov_opt = optimizer
+        self._ov_stream = torch.cuda.Stream(device=self._params[0].device)
+        optimizer._ov_attach(self._ov_stream)
+        self._ov_reset()
+
+    def _ov_reset(self):
+        nb = len(self.bucket_indices)
+        self._ov_flags = bytearray(len(self._params))  # bit 1: gradient final, bit 2: every reader returned
+        self._ov_count = [0] * nb
+        self._ov_next = 0
+
+    def _ov_mark(self, p, bit: int):
+        i = self._index.get(id(p))
+        if i is None:
+            return
+        f = self._ov_flags[i]
+        if f & bit:
+            return
+        f |= bit
+        self._ov_flags[i] = f
+        if f == 3:
+            self._ov_count[self._pbucket[i]] += 1
+            self._ov_drain(False)
+
+    def _ov_drain(self, final: bool):
+        """Step the buckets that are complete, in index order (the order the reducer issues them)."""
+        launched = self.reducer.buckets_launched if hasattr(self.reducer, "buckets_launched") else len(self.buckets)
+        while self._ov_next < len(self.bucket_indices):
+            b = self._ov_next
+            if not final and (self._ov_count[b] < len(self.bucket_indices[b]) or b >= launched):
+                break
+            s = self._ov_stream
+            ev = torch.cuda.Event()
+            ev.record()  # everything enqueued so far on the compute stream: the gradients and their readers
+            s.wait_event(ev)
+            dev = self._params[0].device
+            aux = _state._aux_streams.get(dev.index if dev.index is not None else torch.cuda.current_device())
+            if aux is not None:
+                s.wait_stream(aux)
+            if hasattr(self.reducer, "stream_wait_comm"):
+                self.reducer.stream_wait_comm(s.cuda_stream)  # this bucket's all-reduce
+            self._ov_opt._ov_bucket_step([self._params[i] for i in self.bucket_indices[b]], s)
+            self._ov_next += 1
 
     # ---------------------------------------------------------- per-step
     def _on_ready(self, p):
@@ -426,6 +508,8 @@ class DistributedDataParallel(nn.Module):
             self._queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
         self.reducer.mark_ready(i)
+        if self._ov_opt is not None:
+            self._ov_mark(p, 1)
 
     def _finalize(self):
         self._queued = False
@@ -434,6 +518,8 @@ class DistributedDataParallel(nn.Module):
                 p._dpe_fresh = False
                 self._views[i].zero_()
         self.reducer.finalize()
+        if self._ov_opt is not None:
+            self._ov_drain(True)  # backward is over: every remaining bucket (unused parameters too)
         if self._record_order:
             self._record_order = False
             self._rebuild_pending = self._rebuild_enabled
@@ -470,6 +556,8 @@ class DistributedDataParallel(nn.Module):
                 p._dpe_uses = 0
             if self.require_backward_grad_sync:
                 self.reducer.prepare()
+                if self._ov_opt is not None:
+                    self._ov_reset()
         if self.broadcast_buffers and self.world_size > 1:
             self._sync_buffers()
         return self.module(*args, **kwargs)

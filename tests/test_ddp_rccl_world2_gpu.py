@@ -1,4 +1,4 @@
-"""The native C++ Reducer at world 2 and 4 over real RCCL collectives, on a 1-GPU box.
+"""The native C++ Reducer at world 2, 4 and 8 over real RCCL collectives, on a 1-GPU box.
 
 N processes share GPU 0.  Each gets its own NCCL_HOSTID, so RCCL sees N hosts
 (no duplicate-GPU refusal) and connects them with its socket transport over
@@ -145,3 +145,44 @@ def test_rank_death_world4_aborts_every_survivor(tmp_path):
         assert "watchdog:" in outs[r] and "aborting communicator" in outs[r], (r, outs[r][-2000:])
     assert dt < 140, dt
     print(f"survivors rc={[codes[r] for r in (0, 1, 3)]} after {dt:.1f}s")
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_native_reducer_world8_rccl():
+    """the deployment's world size (NPROC_PER_NODE=8) -- an 8-rank RCCL
+    ring (socket transport, 8 processes on GPU 0), rank 0's bucket order broadcast to seven peers, one
+    rebuild, no_sync, registration and the bf16 hook, against rank-averaged grads (< 1e-4)."""
+    codes, outs = _run_world(8, [os.path.join(ROOT, "tests", "_rccl_world2_worker.py")], timeout=280)
+    assert codes == [0] * 8, "\n".join(o[-1500:] for o in outs)
+    for o in outs:
+        print([ln for ln in o.splitlines() if "ok: world-8" in ln][0])
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_native_reducer_world8_rccl_gpt2():
+    codes, outs = _run_world(8, [os.path.join(ROOT, "tests", "_rccl_world2_worker.py"), "gpt2"], timeout=280)
+    assert codes == [0] * 8, "\n".join(o[-1500:] for o in outs)
+    for o in outs:
+        print([ln for ln in o.splitlines() if "ok: world-8" in ln][0])
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_rank_death_world8_aborts_every_survivor(tmp_path):
+    """Rank 5 SIGKILLs itself at batch 3 of epoch 0; the seven survivors are blocked in bucket
+    all-reduces of an 8-rank ring that can never complete.  Every survivor's watchdog must abort its
+    communicator and exit non-zero within the timeout."""
+    import time
+
+    t0 = time.time()
+    codes, outs = _run_world(8, [os.path.join(ROOT, "train.py"), "--backend", "rccl", "--model", "resnet_tiny",
+                                 "--image-size", "32", "--batch-size", "8", "--num-samples", "2048", "--epochs", "2",
+                                 "--checkpoint-dir", str(tmp_path), "--watchdog-timeout", "15"],
+                             extra_env={"DPE_FAULT_INJECT": "5:0:3:kill"}, timeout=200)
+    dt = time.time() - t0
+    assert codes[5] == -9, outs[5][-2000:]
+    survivors = [r for r in range(8) if r != 5]
+    for r in survivors:
+        assert codes[r] not in (0, None) and codes[r] != -9, (r, codes, outs[r][-2000:])
+        assert "watchdog:" in outs[r] and "aborting communicator" in outs[r], (r, outs[r][-2000:])
+    assert dt < 200, dt
+    print(f"7 survivors rc={[codes[r] for r in survivors]} after {dt:.1f}s")
