@@ -54,6 +54,9 @@ int dpe_bn_apply_m(const uint16_t* x, const uint16_t* res, uint16_t* y, int64_t 
                    uint8_t* mbits, hipStream_t st);
 int dpe_bnrelu_maxpool_fwd(const uint16_t* h, const float* coef, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH,
                            int OW, int k, int s, int p, hipStream_t st);
+int dpe_stem_wgrad_launch2(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H, int W,
+                           float alpha, const uint16_t* dyp, const uint8_t* idx, const uint16_t* h, const float* coef,
+                           const float* bcoef, hipStream_t st);
 int dpe_maxpool_bn_bwd_reduce(const uint16_t* dy, const uint8_t* idx, const uint16_t* x, const float* coef, int N, int H, int W,
                               int C, int OH, int OW, int k, int s, int p, int nb, float* part, hipStream_t st);
 int dpe_maxpool_bn_bwd_apply(const uint16_t* dy, const uint8_t* idx, const uint16_t* x, const float* coef, const float* bcoef,
@@ -88,6 +91,9 @@ int dpe_stem_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* st
 int dpe_add(const void* a, const void* b, void* out, int64_t n, float alpha, int bf16, hipStream_t st);
 int dpe_colsum(const void* dy, int64_t M, int N, int64_t ld, float* db, int accumulate, int bf16, hipStream_t st);
 int dpe_nchw_to_s2d(const float* x, uint16_t* y, int N, int C, int H, int W, hipStream_t st);
+int dpe_flip_desc_bytes();
+int dpe_flip_blocks(int K, int C, int Rp, int Sp);
+int dpe_conv_w_flipT_multi(const void* desc, const int* start, int n, int total_blocks, hipStream_t st);
 int dpe_conv_w_flipT(const uint16_t* w, uint16_t* wt, int K, int R, int S, int C, int r0, int rs, int Rp, int s0, int ss,
                      int Sp, hipStream_t st);
 int dpe_nchw_to_nhwc(const float* x, uint16_t* y, int N, int C, int HW, int Cp, hipStream_t st);
@@ -228,8 +234,84 @@ void dma_tile(const dpe::IgemmArgs& a, int aload, int bload, int& bm, int& bn) {
   else if (mode >= 2 && a.N > 64) { bm = 256; bn = 128; }
 }
 
+// ---------------------------------------------------------- flipped filters
+// The stride-1 / per-parity data grads run as forward convs of dy with flipped, transposed filters
+// (conv_w_flipT).  A filter only changes when the optimizer (or a torch-side edit) rewrites the bf16 shadow,
+// which bumps the weight epoch (set_weight_epoch, ops/_state.py).  The flipped copies are cached per (filter,
+// tap subset) and, at the first request of a new epoch, ALL cached copies are refreshed in one launch (one
+// instead of ~26 per ResNet-50 backward); a copy first requested in this epoch is flipped on its own.
+struct FlipDescHost {
+  const uint16_t* w;
+  uint16_t* wt;
+  int K, R, S, C, r0, rs, Rp, s0, ss, Sp;
+};
+struct FlipEntry {
+  Tensor w, wt;
+  FlipDescHost d;
+  int64_t epoch;
+};
+std::vector<FlipEntry> g_flips;
+int64_t g_weight_epoch = 0;
+Tensor g_flip_desc, g_flip_start;  // device copies of the descriptor table (rebuilt when the set changes)
+bool g_flip_table_dirty = true;
+int g_flip_total = 0;
+
+Tensor flipped(const Tensor& w, int K, int R, int S, int C, int r0, int rs, int Rp, int s0, int ss, int Sp) {
+  static const bool cache_on = [] { const char* e = getenv("DPE_FLIP_CACHE"); return !(e && e[0] == '0'); }();
+  if (!cache_on) {
+    Tensor wt = at::empty({C, Rp, Sp, K}, w.options());
+    CHECK_RC(dpe_conv_w_flipT(bp(w), bpm(wt), K, R, S, C, r0, rs, Rp, s0, ss, Sp, cur_stream()), "conv_w_flipT");
+    return wt;
+  }
+  FlipEntry* hit = nullptr;
+  for (auto& e : g_flips)
+    if (e.d.w == bp(w) && e.w.is_same(w) && e.d.K == K && e.d.R == R && e.d.S == S && e.d.C == C && e.d.r0 == r0 &&
+        e.d.rs == rs && e.d.Rp == Rp && e.d.s0 == s0 && e.d.ss == ss && e.d.Sp == Sp) {
+      hit = &e;
+      break;
+    }
+  if (hit && hit->epoch == g_weight_epoch) return hit->wt;
+  if (hit) {
+    // a new epoch: refresh every cached copy at once (their filters are all current now: no optimizer step
+    // runs inside a backward pass before the node that needs them -- DDP.overlap_optimizer included)
+    if (g_flip_table_dirty) {
+      std::vector<int> start(g_flips.size() + 1, 0);
+      std::vector<FlipDescHost> desc(g_flips.size());
+      for (size_t i = 0; i < g_flips.size(); ++i) {
+        desc[i] = g_flips[i].d;
+        start[i + 1] = start[i] + dpe_flip_blocks(desc[i].K, desc[i].C, desc[i].Rp, desc[i].Sp);
+      }
+      TORCH_CHECK((int)sizeof(FlipDescHost) == dpe_flip_desc_bytes(), "FlipDesc ABI mismatch");
+      auto u8 = at::TensorOptions().dtype(at::kByte);
+      Tensor hd = at::empty({(int64_t)(desc.size() * sizeof(FlipDescHost))}, u8);
+      memcpy(hd.data_ptr(), desc.data(), desc.size() * sizeof(FlipDescHost));
+      Tensor hs = at::empty({(int64_t)start.size()}, at::TensorOptions().dtype(at::kInt));
+      memcpy(hs.data_ptr(), start.data(), start.size() * sizeof(int));
+      g_flip_desc = hd.to(w.device());
+      g_flip_start = hs.to(w.device());
+      g_flip_total = start.back();
+      g_flip_table_dirty = false;
+    }
+    CHECK_RC(dpe_conv_w_flipT_multi(g_flip_desc.data_ptr(), (const int*)g_flip_start.data_ptr(), (int)g_flips.size(),
+                                    g_flip_total, cur_stream()),
+             "conv_w_flipT_multi");
+    for (auto& e : g_flips) e.epoch = g_weight_epoch;
+    return hit->wt;
+  }
+  if (g_flips.size() >= 256) {  // (models come and go in tests: bounded, nothing stale is kept alive)
+    g_flips.clear();
+    g_flip_desc = Tensor();
+    g_flip_start = Tensor();
+  }
+  Tensor wt = at::empty({C, Rp, Sp, K}, w.options());
+  CHECK_RC(dpe_conv_w_flipT(bp(w), bpm(wt), K, R, S, C, r0, rs, Rp, s0, ss, Sp, cur_stream()), "conv_w_flipT");
+  g_flips.push_back(FlipEntry{w, wt, FlipDescHost{bp(w), bpm(wt), K, R, S, C, r0, rs, Rp, s0, ss, Sp}, g_weight_epoch});
+  g_flip_table_dirty = true;
+  return wt;
+}
+
 void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_split, bool conv = false,
-               bool deterministic = false) {
+               bool deterministic = false, bool overwrite = false) {
   Cfg c = pick_cfg(a.M, a.N, a.K, allow_split && epi == dpe::EPI_ATOMIC_F32);
   a.k_split = c.k_split;
   // weight grads over an im2col B (3x3 / strided; split-K fp32 atomics): LDS-DMA kernel, measured 1.3-1.5x
@@ -279,6 +361,8 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
       slab = at::empty({(int64_t)splits * a.M * a.N}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA));
       a.slab = fp(slab);
     }
+    if (overwrite && !slab.defined())  // atomics accumulate: start from zeros
+      TORCH_CHECK(hipMemsetAsync(a.C, 0, (size_t)a.M * a.ldc * sizeof(float), cur_stream()) == hipSuccess, "memset");
     const int rc = dpe_igemm_wgrad_dma_launch(&a, bm, bn, bload, splits, cur_stream());
     a.slab = nullptr;
     TORCH_CHECK(rc == 0 || (!a.b_coef && !deterministic),
@@ -287,7 +371,8 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
       dpe::HgemmArgs f;
       memset(&f, 0, sizeof(f));
       f.C = a.C; f.ws = fp(slab); f.M = a.M; f.N = a.N; f.ldc = a.ldc; f.splits = splits; f.alpha = 1.f;
-      CHECK_RC(dpe_hgemm_finalize(&f, dpe::HE_ACC_F32, cur_stream()), "weight-grad slab finalize");
+      // overwrite: the split sum IS the result (the caller's buffer needs no zero fill)
+      CHECK_RC(dpe_hgemm_finalize(&f, overwrite ? dpe::HE_F32 : dpe::HE_ACC_F32, cur_stream()), "weight-grad slab finalize");
     }
     a.k_split = c.k_split;  // (register-staged fallback uses pick_cfg's split)
     if (rc == 0) {
@@ -874,8 +959,7 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
   if (!is_pointwise(g) && g.sh == 1 && g.sw == 1 && g.dh == 1 && g.dw == 1 && dgrad_as_fwd()) {
     // Stride-1 data grad as a forward conv: dx = conv(dy, flipT(w), pad R-1-p) on the
     // forward loaders (K-contiguous filter, im2col gather of dy).
-    Tensor wt = at::empty({g.C, g.R, g.S, g.K}, w.options());
-    CHECK_RC(dpe_conv_w_flipT(bp(w), bpm(wt), g.K, g.R, g.S, g.C, 0, 1, g.R, 0, 1, g.S, cur_stream()), "conv_w_flipT");
+    Tensor wt = flipped(w, g.K, g.R, g.S, g.C, 0, 1, g.R, 0, 1, g.S);
     auto f = geom(dy, wt, 1, 1, g.R - 1 - g.ph, g.S - 1 - g.pw, 1, 1, g.H, g.W);
     if (rowconv_geom(f) && !acc_into && !a.residual && !a.st_mask) {
       // 64-channel 3x3 data grad (layer 1): the row-walking forward kernel over dy with the flipped
@@ -945,9 +1029,7 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
         if (Rp > 0 && Sp > 0 && dgrad_as_fwd()) {
           // this parity as a forward conv of dy with its own flipped tap subset:
           // oh = hh + ph' - t = hh - (Rp-1-ph') + (Rp-1-t)
-          Tensor wt = at::empty({g.C, Rp, Sp, g.K}, w.options());
-          CHECK_RC(dpe_conv_w_flipT(bp(w), bpm(wt), g.K, g.R, g.S, g.C, r0, g.sh, Rp, s0, g.sw, Sp, cur_stream()),
-                   "conv_w_flipT");
+          Tensor wt = flipped(w, g.K, g.R, g.S, g.C, r0, g.sh, Rp, s0, g.sw, Sp);
           phase_w.push_back(wt);
           auto f = geom(dy, wt, 1, 1, Rp - 1 - v.ph, Sp - 1 - v.pw, 1, 1, Hp, Wp);
           f.remap = 2; f.Hr = g.H; f.Wr = g.W; f.oa = pa; f.ob = pb; f.psh = g.sh; f.psw = g.sw;
@@ -988,7 +1070,7 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xshape
 // in_coef: as conv_fwd's (x pre-BN, BN+ReLU applied on load; row-walking 64-channel 3x3 kernel only)
 void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64_t> stride, std::vector<int64_t> pad,
                 std::vector<int64_t> dil, double alpha, const c10::optional<Tensor>& in_coef, int64_t fin_stream,
-                bool deterministic) {
+                bool deterministic, bool overwrite) {
   CHECK_GPU(dy); CHECK_BF16(dy); CHECK_BF16(x); CHECK_CONTIG(dy); CHECK_CONTIG(x); CHECK_F32(dw); CHECK_CONTIG(dw);
   auto g = geom(x, dw, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], dy.size(1), dy.size(2));
   TORCH_CHECK(dy.size(3) == g.K && dy.size(0) == g.N, "conv_wgrad: dy shape mismatch");
@@ -1007,9 +1089,13 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64
     // B fragments (b_coef); outside that kernel's envelope there is no such path
     TORCH_CHECK(is_pointwise(g), "conv_wgrad: in_coef needs a 1x1 conv or the row-walking 64-channel 3x3 kernel");
     a.b_coef = icoef;
-    run_igemm(a, dpe::A_DENSE_M, dpe::B_DENSE_N, dpe::EPI_ATOMIC_F32, true, true, deterministic);
+    run_igemm(a, dpe::A_DENSE_M, dpe::B_DENSE_N, dpe::EPI_ATOMIC_F32, true, true, deterministic, overwrite);
     return;
   }
+  const bool hgemm_1x1 = wgrad_hgemm_on() && is_pointwise(g) && a.K % 64 == 0 && g.K >= 256 && g.C >= 256 &&
+                         g.K % 8 == 0 && g.C % 8 == 0;
+  if (overwrite && !hgemm_1x1)  // the accumulating kernels below: start from zeros
+    TORCH_CHECK(hipMemsetAsync(dw.data_ptr(), 0, dw.numel() * sizeof(float), cur_stream()) == hipSuccess, "memset");
   if (row && (row_wgrad_on() || icoef)) {
     auto scratch = at::empty({dpe_wgrad3x3_rows_scratch(row_nb)}, dw.options());
     CHECK_RC(dpe_wgrad3x3_rows_launch(bp(x), bp(dy), fp(dw), fp(scratch), g.N, g.H, g.W, row_nb, (float)alpha, icoef,
@@ -1031,15 +1117,14 @@ void conv_wgrad(const Tensor& dy, const Tensor& x, Tensor& dw, std::vector<int64
   // persistent hgemm kernel with the planner's K split and a deterministic slab finalize, as
   // linear_wgrad.  With 128 channels the TN layout's only tile (256x256) wastes half its MFMAs and
   // the implicit GEMM is faster (profiles/wgrad_hgemm_ab_r2.txt).
-  if (wgrad_hgemm_on() && is_pointwise(g) && a.K % 64 == 0 && g.K >= 256 && g.C >= 256 && g.K % 8 == 0 &&
-      g.C % 8 == 0) {
+  if (hgemm_1x1) {
     auto h = hargs();
     h.A = bp(dy); h.B = bp(x); h.C = dw.data_ptr();
     h.M = a.M; h.N = a.N; h.K = a.K;
     h.lda = g.K; h.ldb = g.C; h.ldc = g.C;
     h.a_dim = (int)((g.K + 7) / 8 * 8);
     h.alpha = (float)alpha;
-    dpe_gemm::run(h, 0, 0, dpe::HE_ACC_F32, true, 4, (hipStream_t)(uintptr_t)fin_stream);
+    dpe_gemm::run(h, 0, 0, overwrite ? dpe::HE_F32 : dpe::HE_ACC_F32, true, 4, (hipStream_t)(uintptr_t)fin_stream);
     return;
   }
   // 3x3 weight grads with >= 256 output channels (layers 3-4): the persistent GEMM's TN layout with an
@@ -1536,6 +1621,37 @@ Tensor maxpool_bn_bwd(const Tensor& dy, const Tensor& idx, const Tensor& h, cons
   return dh;
 }
 
+// The stem's backward without dY: BN-backward coefficients of the pooled gradient (reduce + finalize; dgamma /
+// dbeta accumulate), then the stem weight grad computing dY = a dz + b h + c on the fly (stem.hip FUSED).
+// dw [64, 4, 4, 16] (s2d filter layout) += dW.  No dY tensor, no apply pass.
+void stem_bwd_fused(const Tensor& dy, const Tensor& idx, const Tensor& h, const Tensor& xs,
+                    const c10::optional<Tensor>& gamma, const Tensor& coef, const c10::optional<Tensor>& dgamma,
+                    const c10::optional<Tensor>& dbeta, Tensor& dw) {
+  CHECK_GPU(dy); CHECK_BF16(dy); CHECK_CONTIG(dy); CHECK_BF16(h); CHECK_CONTIG(h); CHECK_F32(coef); CHECK_BF16(xs);
+  CHECK_CONTIG(xs); CHECK_F32(dw); CHECK_CONTIG(dw);
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.sizes() == dy.sizes(), "stem_bwd_fused: idx must be uint8 of dy's shape");
+  const int64_t N = h.size(0), H = h.size(1), W = h.size(2), C = h.size(3);
+  TORCH_CHECK(C == 64 && dy.size(0) == N && dy.size(1) == H / 2 && dy.size(2) == W / 2 && dy.size(3) == C && H % 2 == 0 &&
+                  W % 2 == 0 && xs.size(0) == N && xs.size(1) == H && xs.size(2) == W && xs.size(3) == 16 &&
+                  dw.numel() == 64 * 256,
+              "stem_bwd_fused: shapes (h [N,H,W,64], dy/idx [N,H/2,W/2,64], xs [N,H,W,16], dw [64,4,4,16])");
+  const int64_t M = N * H * W;
+  hipStream_t st = cur_stream();
+  auto fo = h.options().dtype(at::kFloat);
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(8192, M / 512));
+  Tensor part = at::empty({2, C, nb}, fo);
+  CHECK_RC(dpe_maxpool_bn_bwd_reduce(bp(dy), (const uint8_t*)idx.data_ptr(), bp(h), fp(coef), (int)N, (int)H, (int)W, (int)C,
+                                     (int)dy.size(1), (int)dy.size(2), 3, 2, 1, nb, fp(part), st),
+           "maxpool_bn_bwd_reduce");
+  Tensor bcoef = at::empty({3, C}, fo);
+  CHECK_RC(dpe_bn_bwd_finalize(fp(part), nb, (int)C, M, fpo(gamma), fp(coef), fpom(dgamma), fpom(dbeta), fp(bcoef), st),
+           "bn_bwd_finalize");
+  auto scratch = at::empty({dpe_stem_wgrad_scratch(N, H, W)}, fo);
+  CHECK_RC(dpe_stem_wgrad_launch2(bp(xs), nullptr, fp(dw), fp(scratch), (int)N, (int)H, (int)W, 1.f, bp(dy),
+                                  (const uint8_t*)idx.data_ptr(), bp(h), fp(coef), fp(bcoef), st),
+           "stem wgrad (fused BN / max-pool backward)");
+}
+
 Tensor gavgpool_fwd(const Tensor& x) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_CONTIG(x);
   const int64_t N = x.size(0), C = x.size(-1), HW = x.numel() / (N * C);
@@ -1887,17 +2003,24 @@ void register_ops(pybind11::module& m) {
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("coef"), py::arg("residual") = py::none(),
         py::arg("residual_coef") = py::none(), py::arg("relu") = true, py::arg("want_mask") = false);
   m.def("bnrelu_maxpool_fwd", &bnrelu_maxpool_fwd, py::arg("h"), py::arg("coef"), py::arg("k"), py::arg("s"), py::arg("p"));
+  m.def("stem_bwd_fused", &stem_bwd_fused, py::arg("dy"), py::arg("idx"), py::arg("h"), py::arg("xs"), py::arg("gamma"),
+        py::arg("coef"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dw"),
+        "stem backward without dY: BN-backward coefficients of the pooled gradient, then the stem weight grad "
+        "(s2d filter layout) computing dY on the fly");
   m.def("maxpool_bn_bwd", &maxpool_bn_bwd, py::arg("dy"), py::arg("idx"), py::arg("h"), py::arg("gamma"), py::arg("coef"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("k"), py::arg("s"), py::arg("p"));
   m.def("bn_bwd_partials", &bn_bwd_partials, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("coef"),
         py::arg("partials"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none(), py::arg("relu_mask") = true);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("xshape"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), py::arg("residual") = py::none(), py::arg("residual_mask") = py::none());
+  m.def("set_weight_epoch", [](int64_t e) { g_weight_epoch = e; }, py::arg("epoch"),
+        "bf16 weight shadows changed (optimizer step / re-cast): cached flipped filters are refreshed at next use");
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
         py::arg("dil"), py::arg("alpha") = 1.0, py::arg("in_coef") = py::none(), py::arg("fin_stream") = 0,
-        py::arg("deterministic") = false,
+        py::arg("deterministic") = false, py::arg("overwrite") = false,
         "dw (+)= alpha dW; fin_stream: a K-split hgemm's slab reduction runs on that stream (caller orders consumers); "
-        "deterministic: 1x1 weight grads over a pre-BN input sum their K splits in a fixed order (no atomics)");
+        "deterministic: 1x1 weight grads over a pre-BN input sum their K splits in a fixed order (no atomics); "
+        "overwrite: dw = alpha dW (dw's old contents, e.g. torch.empty, are never read)");
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),
         py::arg("momentum"), py::arg("eps"), py::arg("relu"), py::arg("residual") = py::none(), py::arg("stats") = py::none());
   m.def("bn_fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"),

@@ -247,6 +247,40 @@ __global__ __launch_bounds__(256) void conv_w_flipT_kernel(const uint16_t* __res
   }
 }
 
+// Several flips in ONE launch (the data grads of a backward pass refresh all their flipped filters at
+// once, ops.cpp flipped()): block b belongs to entry e with start[e] <= b < start[e + 1], and runs
+// conv_w_flipT_kernel's block (b - start[e]) of that entry.
+struct FlipDesc {
+  const uint16_t* w;
+  uint16_t* wt;
+  int K, R, S, C, r0, rs, Rp, s0, ss, Sp;
+};
+__global__ __launch_bounds__(256) void conv_w_flipT_multi_kernel(const FlipDesc* __restrict__ fd, const int* __restrict__ start,
+                                                                int n) {
+  __shared__ uint16_t tile[32][33];
+  int e = 0;
+  while (e + 1 < n && (int)blockIdx.x >= start[e + 1]) ++e;
+  const FlipDesc d = fd[e];
+  const int lb = (int)blockIdx.x - start[e];
+  const int gx = (d.C + 31) / 32, gy = (d.K + 31) / 32;
+  const int bx = lb % gx, by = (lb / gx) % gy, bz = lb / (gx * gy);
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c0 = bx * 32, k0 = by * 32;
+  const int r = bz / d.Sp, s = bz % d.Sp;
+  const int rr = d.r0 + d.rs * (d.Rp - 1 - r), sc = d.s0 + d.ss * (d.Sp - 1 - s);
+#pragma unroll
+  for (int q = 0; q < 32; q += 8) {
+    const int k = k0 + q + ty, c = c0 + tx;
+    if (k < d.K && c < d.C) tile[q + ty][tx] = d.w[(((int64_t)k * d.R + rr) * d.S + sc) * d.C + c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 32; q += 8) {
+    const int c = c0 + q + ty, k = k0 + tx;
+    if (k < d.K && c < d.C) d.wt[(((int64_t)c * d.Rp + r) * d.Sp + s) * d.K + k] = tile[tx][q + ty];
+  }
+}
+
 // ----------------------------------------------------------- embedding
 // out[r][:] = wte[idx[r]][:] (+ wpe[r % T][:]) ; D % 8 == 0, weights bf16, out f32
 __global__ __launch_bounds__(ET) void embedding_fwd_kernel(const int64_t* __restrict__ idx, const uint16_t* __restrict__ wte,
@@ -359,6 +393,15 @@ extern "C" int dpe_conv_w_flipT(const uint16_t* w, uint16_t* wt, int K, int R, i
   if (Rp <= 0 || Sp <= 0 || r0 + rs * (Rp - 1) >= R || s0 + ss * (Sp - 1) >= S) return -1;
   hipLaunchKernelGGL(conv_w_flipT_kernel, dim3((C + 31) / 32, (K + 31) / 32, Rp * Sp), dim3(256), 0, st, w, wt, K, R, S, C, r0,
                      rs, Rp, s0, ss, Sp);
+  return (int)hipGetLastError();
+}
+
+extern "C" int dpe_flip_desc_bytes() { return (int)sizeof(FlipDesc); }
+extern "C" int dpe_flip_blocks(int K, int C, int Rp, int Sp) { return ((C + 31) / 32) * ((K + 31) / 32) * Rp * Sp; }
+// desc: n FlipDesc on the device; start: n + 1 block offsets on the device (start[n] = total blocks)
+extern "C" int dpe_conv_w_flipT_multi(const void* desc, const int* start, int n, int total_blocks, hipStream_t st) {
+  if (n <= 0 || total_blocks <= 0) return 0;
+  hipLaunchKernelGGL(conv_w_flipT_multi_kernel, dim3(total_blocks), dim3(256), 0, st, (const FlipDesc*)desc, start, n);
   return (int)hipGetLastError();
 }
 

@@ -351,7 +351,8 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_apply_quad_kernel(const ui
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float dz = fmaf(xv[e], coef[c8 + e], coef[C + c8 + e]) > 0.f ? d[u][e] : 0.f;
-        o[e] = bcoef[c8 + e] * dz + bcoef[C + c8 + e] * xv[e] + bcoef[2 * C + c8 + e];
+        // (explicit fmaf chain: stem.hip's fused weight grad computes the same dx bit for bit)
+        o[e] = fmaf(bcoef[c8 + e], dz, fmaf(bcoef[C + c8 + e], xv[e], bcoef[2 * C + c8 + e]));
       }
       *(u32x4*)(dx + off) = pack8(o);
     }

@@ -218,12 +218,38 @@ DPE_DEVICE bf16x8 xfrag(const char* img, int row0) {
   return tr2(img + x_off(k1) + pp * 8, img + x_off(k1 + 4) + pp * 8);
 }
 
+// FUSED: dY is never materialised.  The stem's forward was h = conv(xs) -> relu(BN(h)) -> 3x3/s2/p1
+// max-pool (never stored either, pool.hip); its backward needs dY = dL/dh = a dz + b h + c with
+// dz = [h scale + shift > 0] * (pooled gradient gathered through the argmax bytes) and (a, b, c) from the
+// BN-backward reduce.  The standalone apply pass (maxpool_bn_bwd_apply_quad: read dy_p, idx, h, write dY
+// = 1.95 GB at batch 512) is replaced by computing each dY row here, where it is staged into LDS anyway:
+// h rows take the dY rows' register prefetch, and the pooled rows (dy_p, idx) a window needs sit in a
+// 2-slot LDS ring (pooled row i covers h rows 2i-1 .. 2i+1: an even row reads one pooled row, an odd row
+// two), each loaded from HBM once per block, one pooled row ahead in registers.  The dY values are
+// computed exactly as the apply kernel computes them (same window order, same fmaf chain): bitwise the
+// same operand.
+struct StemBwd {
+  const uint16_t* dyp;  // pooled gradient [N][H/2][W/2][64]
+  const uint8_t* idx;   // argmax tap per pooled element (same shape)
+  const uint16_t* h;    // pre-BN stem output [N][H][W][64]
+  const float* coef;    // BN forward [4][64]: scale, shift, mean, invstd
+  const float* bcoef;   // BN backward [3][64]: a, b, c
+};
+constexpr int PW = 56;                          // pooled row pixels (W / 2 <= 56)
+constexpr int PDY = PW * 128, PIDX = PW * 64;   // bytes of one pooled dy row / idx row
+constexpr int PSLOT = PDY + PIDX;
+constexpr int LDS_F = LDS + 2 * PSLOT + 5 * 64 * 4;  // + the 5 x 64 BN coefficients
+static_assert(LDS_F <= 163840 / 2, "two blocks per CU (fused)");
+
+template <bool FUSED>
 __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const uint16_t* __restrict__ x,
                                                             const uint16_t* __restrict__ dy,
-                                                            float* __restrict__ part, int H, int W, int halves) {
-  __shared__ __attribute__((aligned(16))) char smem[LDS];
+                                                            float* __restrict__ part, int H, int W, int halves,
+                                                            StemBwd fb) {
+  __shared__ __attribute__((aligned(16))) char smem[FUSED ? LDS_F : LDS];
   char* const ring = smem;                     // input row ih in slot (ih + 2) % 5
   char* const dbuf = smem + NSLOT * XSLOT;     // dY row oh in slot oh & 1
+  char* const pring = smem + LDS;              // FUSED: pooled row i in slot i & 1 (dy, then idx)
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // filter row dy = w
   // halves = 2: block b covers output rows [oh0, oh1) = half b & 1 of image b >> 1 (more, shorter blocks:
@@ -242,22 +268,122 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const uint16_t* __re
   auto putx = [&](int ih, const u32x4& v) {  // chunk t -> pixel t / 2 (slot row + 2), half t & 1
     if (tid < xch) *(u32x4*)(ring + ((ih + 2 + 5 * 4) % NSLOT) * XSLOT + x_off((tid >> 1) + 2) + (tid & 1) * 16) = v;
   };
+  // FUSED: v holds the h row (the dY row's pre-BN input), not dY
+  const uint16_t* const dsrc = FUSED ? fb.h : dy;
   auto loadd = [&](int oh, u32x4 (&v)[4]) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int c = tid + 256 * u;
-      v[u] = (c < dch && oh < H) ? *(const u32x4*)(dy + dimg + (int64_t)oh * W * 64 + c * 8) : zero16();
+      v[u] = (c < dch && oh < H) ? *(const u32x4*)(dsrc + dimg + (int64_t)oh * W * 64 + c * 8) : zero16();
     }
   };
+  // FUSED: pooled row i (dy and argmax bytes) -> registers -> LDS slot i & 1
+  const int OH = H >> 1, OW = W >> 1;
+  const int64_t pimg = (int64_t)n * OH * OW * 64;
+  const int pdch = OW * 8, pich = OW * 4;  // 16-B chunks of a pooled dy / idx row
+  auto loadp = [&](int i, u32x4 (&v)[3]) {
+    if constexpr (FUSED) {
+      const bool ok = i < OH;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = tid + 256 * u;
+        v[u] = (ok && c < pdch) ? *(const u32x4*)(fb.dyp + pimg + (int64_t)i * OW * 64 + c * 8) : zero16();
+      }
+      // an out-of-range pooled row: argmax 0xff never matches a tap
+      v[2] = (ok && tid < pich) ? *(const u32x4*)(fb.idx + pimg + (int64_t)i * OW * 64 + tid * 16)
+                                : u32x4{~0u, ~0u, ~0u, ~0u};
+    }
+  };
+  auto putp = [&](int i, const u32x4 (&v)[3]) {
+    if constexpr (FUSED) {
+      char* sl = pring + (i & 1) * PSLOT;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = tid + 256 * u;
+        if (c < pdch) *(u32x4*)(sl + c * 16) = v[u];
+      }
+      if (tid < pich) *(u32x4*)(sl + PDY + tid * 16) = v[2];
+    }
+  };
+  // FUSED: [scale | shift | a | b | c] x 64 channels in LDS (read per chunk: no 40 registers held all along)
+  float* const pcoef = (float*)(smem + LDS + 2 * PSLOT);
+  if constexpr (FUSED) {
+    if (tid < 128) pcoef[tid] = fb.coef[tid];
+    else pcoef[tid] = fb.bcoef[tid - 128];  // (a, b rows: tid 128 .. 255)
+    if (tid < 64) pcoef[256 + tid] = fb.bcoef[128 + tid];
+  }
   auto putd = [&](int oh, const u32x4 (&v)[4]) {
     char* sl = dbuf + (oh & 1) * DSLOT;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int c = tid + 256 * u;
-      if (c < dch) *(u32x4*)(sl + d_off(c >> 3, c & 7)) = v[u];
+      if (c >= dch) continue;
+      if constexpr (FUSED) {
+        // dY chunk (pixel ow = c / 8, channels 8 (c % 8) ..): the windows (i, j) covering (oh, ow), in the
+        // apply kernel's order (row-major), tap 3 (oh - 2i + 1) + (ow - 2j + 1)
+        const int ow = c >> 3, cg = c & 7;
+        const int i0 = oh >> 1, i1 = (oh + 1) >> 1, j0 = ow >> 1, j1 = (ow + 1) >> 1;
+        float dz[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dz[e] = 0.f;
+#pragma unroll
+        for (int wi = 0; wi < 2; ++wi) {
+          const int i = wi ? i1 : i0;
+          if (wi && i1 == i0) break;
+#pragma unroll
+          for (int wj = 0; wj < 2; ++wj) {
+            const int j = wj ? j1 : j0;
+            if (wj && j1 == j0) break;
+            if (j >= OW) continue;
+            const char* sl2 = pring + (i & 1) * PSLOT;
+            float g[8];
+            unpack8(*(const u32x4*)(sl2 + (j * 8 + cg) * 16), g);
+            const u32x2 b = *(const u32x2*)(sl2 + PDY + (j * 64 + cg * 8));
+            const uint32_t tap = (uint32_t)(3 * (oh - 2 * i + 1) + (ow - 2 * j + 1));
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t t = (b[e >> 2] >> ((e & 3) * 8)) & 0xffu;
+              dz[e] += t == tap ? g[e] : 0.f;
+            }
+          }
+        }
+        float hv[8], o[8];
+        unpack8(v[u], hv);
+        const float* pc = pcoef + cg * 8;
+#pragma unroll
+        for (int h4 = 0; h4 < 2; ++h4) {  // 4 channels at a time: 20 coefficient registers, not 40
+          const f32x4 k0 = *(const f32x4*)(pc + 4 * h4), k1 = *(const f32x4*)(pc + 64 + 4 * h4);
+          const f32x4 k2 = *(const f32x4*)(pc + 128 + 4 * h4), k3 = *(const f32x4*)(pc + 192 + 4 * h4);
+          const f32x4 k4 = *(const f32x4*)(pc + 256 + 4 * h4);
+#pragma unroll
+          for (int e4 = 0; e4 < 4; ++e4) {
+            const int e = 4 * h4 + e4;
+            const float d = fmaf(hv[e], k0[e4], k1[e4]) > 0.f ? dz[e] : 0.f;
+            o[e] = fmaf(k2[e4], d, fmaf(k3[e4], hv[e], k4[e4]));
+          }
+        }
+        *(u32x4*)(sl + d_off(c >> 3, c & 7)) = pack8(o);
+        __builtin_amdgcn_sched_barrier(0);  // one chunk's temporaries at a time (register pressure)
+      } else {
+        *(u32x4*)(sl + d_off(c >> 3, c & 7)) = v[u];
+      }
     }
   };
   __syncthreads();
+  // FUSED pooled-row schedule: dY row oh needs pooled rows oh >> 1 .. (oh + 1) >> 1.  Before the loop the
+  // ring holds rows p0 = oh0 >> 1 and p0 + 1; row q + 2 (q = the slot it replaces) is written during the
+  // step of the odd dY row 2q + 1... see step() below.
+  u32x4 pp[3];
+  const int p0 = oh0 >> 1;
+  if constexpr (FUSED) {
+    u32x4 t[3];
+    loadp(p0, t);
+    putp(p0, t);
+    loadp(p0 + 1, t);
+    putp(p0 + 1, t);
+    loadp(p0 + 2, pp);
+    __syncthreads();
+  }
   {
 #pragma unroll
     for (int d = -2; d < 2; ++d) putx(oh0 + d, loadx(oh0 + d));
@@ -300,6 +426,19 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const uint16_t* __re
     // input row oh + 2 into the slot of row oh - 3, dY row oh + 1 into the slot of row oh - 1
     putx(oh + 2, pxA);
     putd(oh + 1, pdA);
+    if constexpr (FUSED) {
+      // dY row oh + 1 read pooled rows (oh + 1) >> 1 .. (oh + 2) >> 1.  When oh + 1 is even (= 2q), row q - 1
+      // was last read by dY row 2q - 1 (previous step, behind its barrier) and no dY row computed later needs
+      // it: pooled row q + 1 (prefetched in pp) goes into its slot now, read first by dY row 2q + 1 (next
+      // step, behind this step's barrier).
+      if (((oh + 1) & 1) == 0) {
+        const int q = (oh + 1) >> 1;
+        if (q + 1 > p0 + 1) {  // (rows p0, p0 + 1 were placed before the loop)
+          putp(q + 1, pp);
+          loadp(q + 2, pp);
+        }
+      }
+    }
     pxA = loadx(oh + 4);
     loadd(oh + 3, pdA);
     __syncthreads();
@@ -369,16 +508,33 @@ extern "C" int64_t dpe_stem_wgrad_scratch(int N, int H, int W) {
   return (int64_t)N * stem_wgrad_halves(H) * dpe::stem::wg::PART;
 }
 
-// dw [64][4][4][16] (+)= alpha * filter gradient of the s2d stem conv, given dY [N, H, W, 64].
-extern "C" int dpe_stem_wgrad_launch(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H, int W,
-                                     float alpha, hipStream_t st) {
+// dw [64][4][4][16] (+)= alpha * filter gradient of the s2d stem conv, given dY [N, H, W, 64] -- or, with
+// dyp != nullptr, given the stem's pooled gradient: dY = BN-backward(maxpool-backward(dyp)) computed on the
+// fly (stem_wgrad_kernel<true>; 3x3 / s2 / p1 pool, even H and W).
+extern "C" int dpe_stem_wgrad_launch2(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H, int W,
+                                      float alpha, const uint16_t* dyp, const uint8_t* idx, const uint16_t* h,
+                                      const float* coef, const float* bcoef, hipStream_t st) {
   if (dpe_stem_wgrad_scratch(N, H, W) <= 0 || !scratch) return -1;
   using namespace dpe::stem::wg;
   const int halves = stem_wgrad_halves(H), nparts = N * halves;
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(nparts), dim3(256), 0, st, x, dy, scratch, H, W, halves);
+  if (dyp) {
+    if ((H & 1) || (W & 1) || W / 2 > PW || !idx || !h || !coef || !bcoef) return -1;
+    // the pooled-row schedule assumes the block's first row is even (halves of an even H with an even half)
+    if (halves > 1 && (((H + halves - 1) / halves) & 1)) return -1;
+    hipLaunchKernelGGL(stem_wgrad_kernel<true>, dim3(nparts), dim3(256), 0, st, x, dy, scratch, H, W, halves,
+                       StemBwd{dyp, idx, h, coef, bcoef});
+  } else {
+    hipLaunchKernelGGL(stem_wgrad_kernel<false>, dim3(nparts), dim3(256), 0, st, x, dy, scratch, H, W, halves,
+                       StemBwd{nullptr, nullptr, nullptr, nullptr, nullptr});
+  }
   const int groups = nparts >= 64 ? 16 : 1;
   const int per = (nparts + groups - 1) / groups;
   hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(PART / 1024, groups), dim3(256), 0, st, scratch, dw, nparts, per,
                      alpha);
   return (int)hipGetLastError();
+}
+
+extern "C" int dpe_stem_wgrad_launch(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H, int W,
+                                     float alpha, hipStream_t st) {
+  return dpe_stem_wgrad_launch2(x, dy, dw, scratch, N, H, W, alpha, nullptr, nullptr, nullptr, nullptr, nullptr, st);
 }

@@ -355,9 +355,10 @@ class BottleneckFn(Function):
             src, src_coef = (h2, c2) if a2 is None else (a2, None)
             w3 = convs[2].conv.weight
             s3, p3, d3 = _conv_conf(convs[2].conv)
-            P = torch.zeros(w3.shape, dtype=torch.float32, device=w3.device)
-            # P = dz3^T a2 with its K splits summed in a fixed order: BN3's dgamma comes from it
-            C.conv_wgrad(dz3, src, P, s3, p3, d3, 1.0, src_coef, deterministic=True)
+            P = torch.empty(w3.shape, dtype=torch.float32, device=w3.device)
+            # P = dz3^T a2 with its K splits summed in a fixed order: BN3's dgamma comes from it (overwrite:
+            # no zero fill of P)
+            C.conv_wgrad(dz3, src, P, s3, p3, d3, 1.0, src_coef, deterministic=True, overwrite=True)
             bn, gb, gd, bb, bd = bn_sinks(2)
             wbuf, wdirect = grad_sink(w3)
             bcat, ebias = C.bn_gram_bwd(lk.part, P, ws[2], u3, sv, c3, bn.weight.detach(), M3, gb, bb, wbuf)

@@ -86,6 +86,9 @@ class ResNet(nn.Module):
         self.s2d_stem = in_chans <= 4 and os.environ.get("DPE_S2D_STEM", "1") != "0"
         # GPU training: stem BN + ReLU fused into the max-pool (DPE_FUSED_STEM=0: separate passes)
         self.fused_stem = os.environ.get("DPE_FUSED_STEM", "1") != "0"
+        # GPU training: the whole stem as one node whose backward never writes dL/dh (DPE_STEM_BWD_FUSED=0: the
+        # BN / max-pool backward as its own apply pass, A/B)
+        self.stem_bwd_fused = self.fused_stem and os.environ.get("DPE_STEM_BWD_FUSED", "1") != "0"
         self.stem = ConvBN(in_chans, 64, 7, 2, 3)
         blocks = []
         inplanes = 64
@@ -108,7 +111,9 @@ class ResNet(nn.Module):
                 x = x[..., :4].reshape(n, hh // 2, 2, ww // 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(
                     n, hh // 2, ww // 2, 16)
             bn = self.stem.bn
-            if bn.training and self.fused_stem:
+            if bn.training and self.stem_bwd_fused and Fx.stem_fused_ok(x):
+                h = Fx.stem_fused(x, self.stem.conv.weight, bn)
+            elif bn.training and self.fused_stem:
                 # BN statistics from the conv epilogue; BN + ReLU applied inside the max-pool
                 y, st = Fx.stem_conv_s2d(x, self.stem.conv.weight, want_stats=True)
                 h = Fx.stem_bn_relu_maxpool(y, bn, st, 3, 2, 1)

@@ -36,6 +36,7 @@ def shadow(p: torch.Tensor, pad_rows: int = 0) -> torch.Tensor:
 
         ext().cast_bf16(p.detach().reshape(-1), sh.view(-1)[: p.numel()])
         p._dpe_shadow_ver = p._version
+        bump_weight_epoch()
     # one shadow per parameter: a padded (larger) shadow also serves unpadded users
     return sh if sh.shape[0] == rows else sh[:rows]
 
@@ -60,11 +61,26 @@ def derived_shadow(p: torch.Tensor, key: str, fn) -> torch.Tensor:
 
 
 _step_counter = [0]
+_weight_epoch = [0]
+
+
+def bump_weight_epoch() -> None:
+    """The bf16 shadows changed: the native cached flipped filters (ops.cpp flipped()) refresh at next use."""
+    _weight_epoch[0] += 1
+    try:
+        from ._ext import ext
+
+        C = ext()
+        if hasattr(C, "set_weight_epoch"):
+            C.set_weight_epoch(_weight_epoch[0])
+    except Exception:  # noqa: BLE001  (CPU-only use: no extension, nothing cached)
+        pass
 
 
 def after_optimizer_step(params=None) -> None:
     """Refresh derived shadows in place (called by the fused optimizers; capturable)."""
     _step_counter[0] += 1
+    bump_weight_epoch()
     for p, attr, fn in _derived:
         if params is not None and p not in params:
             continue

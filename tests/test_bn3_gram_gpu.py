@@ -266,3 +266,25 @@ def test_chained_blocks_gram_gradient_parity():
             gb += [cbf.conv.weight.grad.float(), cbf.bn.weight.grad.float(), cbf.bn.bias.grad.float()]
             names += [f"b{i}.{k}.conv.weight", f"b{i}.{k}.bn.weight", f"b{i}.{k}.bn.bias"]
     _grad_check("Gram-chained bottlenecks bs32 28^2", names, go, gf, gb)
+
+
+@pytest.mark.parametrize("cin,cout,k,coef", [(64, 256, 1, True), (256, 1024, 1, False), (64, 64, 3, False),
+                                             (128, 512, 1, True)])
+def test_conv_wgrad_overwrite(cin, cout, k, coef):
+    """conv_wgrad(overwrite=True) into a NaN-filled buffer == the accumulating form into zeros (the Gram
+    path's P = dz3^T a2 needs no zero fill): the slab finalize overwrites, the atomic paths zero first."""
+    X = ext()
+    g = torch.Generator(device=DEV).manual_seed(cin + k)
+    x = torch.randn(8, 14, 14, cin, device=DEV, generator=g).bfloat16()
+    dy = torch.randn(8, 14, 14, cout, device=DEV, generator=g).bfloat16()
+    c = None
+    if coef:
+        c = torch.stack([1 + 0.2 * torch.randn(cin, device=DEV, generator=g), 0.3 * torch.randn(cin, device=DEV, generator=g),
+                         torch.zeros(cin, device=DEV), torch.ones(cin, device=DEV)]).float()
+    pad = (k - 1) // 2
+    ref = torch.zeros(cout, k, k, cin, device=DEV)
+    X.conv_wgrad(dy, x, ref, [1, 1], [pad, pad], [1, 1], 1.0, c, deterministic=True)
+    out = torch.full((cout, k, k, cin), float("nan"), device=DEV)
+    X.conv_wgrad(dy, x, out, [1, 1], [pad, pad], [1, 1], 1.0, c, deterministic=True, overwrite=True)
+    assert torch.isfinite(out).all()
+    assert _rel(out, ref) < 1e-6, _rel(out, ref)

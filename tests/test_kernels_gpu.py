@@ -1297,3 +1297,57 @@ def test_hgemm_implicit_conv(C, N, H, Ci, Co, s):
         dz = dx1.float() * ((h.float() * coef[0] + coef[1]) > 0)
         assert rel_err(p1.sum(-1)[0], dz.reshape(-1, Ci).sum(0)) < 1e-3
         assert rel_err(p1.sum(-1)[1], (dz * (h.float() - coef[2])).reshape(-1, Ci).sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("cin,cout,stride,hw", [(128, 128, 1, 28), (256, 256, 1, 14), (128, 128, 2, 28), (64, 64, 1, 56)])
+def test_flipped_filter_cache_refresh(C, cin, cout, stride, hw):
+    """The data grads' flipped filters are cached per weight and refreshed (all at once) when the weight
+    epoch moves: after an in-place change of the filter + set_weight_epoch, the data grad equals the one
+    computed from a fresh tensor holding the new filter; both match an fp32 torch reference."""
+    import torch.nn.functional as F
+
+    g = torch.Generator(device=dev).manual_seed(cin + stride)
+    w = (torch.randn(cout, 3, 3, cin, device=dev, generator=g) * (9 * cin) ** -0.5).bfloat16()
+    oh = hw // stride
+    dy = torch.randn(4, oh, oh, cout, device=dev, generator=g).bfloat16()
+    xs = [4, hw, hw, cin]
+    d1 = C.conv_dgrad(dy, w, xs, [stride, stride], [1, 1], [1, 1])  # registers the cached flip(s)
+    w2 = (torch.randn(cout, 3, 3, cin, device=dev, generator=g) * (9 * cin) ** -0.5).bfloat16()
+    w.copy_(w2)
+    C.set_weight_epoch(10**9 + cin + stride)  # (the optimizer / shadow re-cast does this)
+    d2 = C.conv_dgrad(dy, w, xs, [stride, stride], [1, 1], [1, 1])
+    d_fresh = C.conv_dgrad(dy, w2.clone(), xs, [stride, stride], [1, 1], [1, 1])
+    assert torch.equal(d2, d_fresh)
+    ref = torch.nn.grad.conv2d_input([4, cin, hw, hw], w2.float().permute(0, 3, 1, 2), dy.float().permute(0, 3, 1, 2),
+                                     stride=stride, padding=1).permute(0, 2, 3, 1)
+    assert rel_err(d2, ref) < 2e-2, rel_err(d2, ref)
+    assert rel_err(d1, ref) > 0.5  # (the first call used the old filter)
+
+
+@pytest.mark.parametrize("N", [2, 5])
+def test_stem_bwd_fused_matches_apply_path(C, N):
+    """The stem backward without dL/dh (stem_bwd_fused: dY computed inside the weight grad from the pooled
+    gradient, the argmax bytes and h) equals the apply-pass path bit for bit (same windows, same fmaf
+    chain, same weight-grad accumulation order): dW, dgamma, dbeta."""
+    g = torch.Generator(device=dev).manual_seed(N)
+    H = W = 112
+    xs = torch.randn(N, H, W, 16, device=dev, generator=g).bfloat16()
+    h = torch.randn(N, H, W, 64, device=dev, generator=g).bfloat16()
+    coef = torch.stack([1 + 0.2 * torch.randn(64, device=dev, generator=g), 0.3 * torch.randn(64, device=dev, generator=g),
+                        0.1 * torch.randn(64, device=dev, generator=g), 1 + 0.1 * torch.rand(64, device=dev, generator=g)]).float()
+    y, idx = C.bnrelu_maxpool_fwd(h, coef, 3, 2, 1)
+    dy = torch.randn(y.shape, device=dev, generator=g).bfloat16()
+    gamma = 1 + 0.1 * torch.randn(64, device=dev, generator=g)
+    dg1, db1 = torch.zeros(64, device=dev), torch.zeros(64, device=dev)
+    dh = C.maxpool_bn_bwd(dy, idx, h, gamma, coef, dg1, db1, 3, 2, 1)
+    dw1 = torch.zeros(64, 4, 4, 16, device=dev)
+    C.conv_wgrad(dh, xs, dw1, [1, 1], [2, 2], [1, 1], 1.0)
+    dg2, db2 = torch.zeros(64, device=dev), torch.zeros(64, device=dev)
+    dw2 = torch.zeros(64, 4, 4, 16, device=dev)
+    C.stem_bwd_fused(dy, idx, h, xs, gamma, coef, dg2, db2, dw2)
+    assert torch.equal(dg1, dg2) and torch.equal(db1, db2)
+    assert rel_err(dw2, dw1) < 1e-6, rel_err(dw2, dw1)  # (fp32 atomics of the partial reduce: order may differ)
+    # and against fp32 torch: dW of conv(xs, W) for dL/dh = dh
+    ref = torch.nn.grad.conv2d_weight(torch.nn.functional.pad(xs.float().permute(0, 3, 1, 2), (2, 1, 2, 1)), [64, 16, 4, 4],
+                                      dh.float().permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    assert rel_err(dw2, ref) < 1e-3, rel_err(dw2, ref)
