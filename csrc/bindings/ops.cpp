@@ -1348,6 +1348,20 @@ std::vector<Tensor> conv1x1_dgrad_cat(const Tensor& dz, const Tensor& a2src, con
       return {dx, part};
     }
   }
+  // a2 = relu(BN2(h2)) on load with h2 also the BN-backward input (layers 1-2): the streaming kernel
+  // (pwconv.hip pw_cat_kernel) -- mask and h2 - mean from the h2 tile it holds, no second read of h2
+  if (a2_coef.has_value() && a2_coef->defined() && a2src.data_ptr() == bn_x.data_ptr() && a2_coef->numel() == 4 * C &&
+      bn_coef.data_ptr() == a2_coef->data_ptr()) {
+    const int rg = dpe_pw_cat_blocks(M, K1, C);
+    if (rg > 0) {
+      Tensor part = at::empty({2, C, rg}, dz.options().dtype(at::kFloat));
+      dpe::PwCatArgs pa{};
+      pa.dz = bp(dz); pa.h2 = bp(a2src); pa.coef = fp(bn_coef); pa.bcat = bp(bcat); pa.ebias = fp(e);
+      pa.y = bpm(dx); pa.stats = fp(part); pa.M = M; pa.rg = rg;
+      CHECK_RC(dpe_pw_cat_launch(&pa, K1, C, cur_stream()), "pw_cat data grad");
+      return {dx, part};
+    }
+  }
   auto a = base_args();
   a.A = bp(dz); a.B = bp(bcat); a.C = dx.data_ptr();
   a.M = (int)M; a.N = (int)C; a.K = (int)(K1 + C);

@@ -35,7 +35,27 @@ struct PwArgs {
                              // or nullptr: static (see dpe_pw_rowgroups)
 };
 
+// The concatenated-K data grad of the Gram-path BN3 backward (bngram.hip) on a streaming kernel:
+//   y[M][N] = [dz | relu(h2 * s + t)] . Bcat + e,  N = K2 (the bottleneck width: 64 or 128), K1 = 4 N,
+// with the BN2-backward partials (sum dz, sum dz*(h2 - mean)) of the stored y; mask and h2 from the raw h2
+// tile the kernel already holds in LDS (the LDS-DMA implicit GEMM re-read h2 for its epilogue).
+struct PwCatArgs {
+  const uint16_t* dz;     // [M][K1] bf16
+  const uint16_t* h2;     // [M][K2] bf16, pre-BN2
+  const float* coef;      // BN2 [4][K2]: scale, shift, mean, invstd
+  const uint16_t* bcat;   // [K1 + K2][N] bf16
+  const float* ebias;     // [N]
+  uint16_t* y;            // [M][N] bf16
+  float* stats;           // [2][N][rg]
+  int64_t M;
+  int rg;                 // blocks (= partial columns)
+};
+
 }  // namespace dpe
+
+// Blocks (= partial columns) of the concatenated-K data grad for (M, K1, K2), 0: outside the kernel's envelope.
+extern "C" int dpe_pw_cat_blocks(int64_t M, int64_t K1, int64_t K2);
+extern "C" int dpe_pw_cat_launch(const dpe::PwCatArgs* args, int64_t K1, int64_t K2, hipStream_t stream);
 
 // Row groups of the launch for (M, N, K, epi), or 0 outside the kernel's envelope
 // (K in {64, 128, 256}, N a multiple of the block's column slice, N >= 2K).  With a CU budget in force

@@ -472,10 +472,212 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Concatenated-K data grad (PwCatArgs, pwconv.h): y = [dz | relu(BN2(h2))] . Bcat + e, + BN2-backward
+// partials.  NW = K2 / 16 waves, wave w owning output channels 16 w .. +15 for the whole launch (their
+// Bcat columns gathered once into VGPRs as MFMA A operands: KC = (K1 + K2) / 32 fragments).  Row tiles of
+// CBM = 32 rows stream through an NS-deep LDS ring by LDS-DMA: K1 / 32 dz images then K2 / 32 raw h2
+// images, each [32 rows][64 B] with the kimg swizzle.  Per tile the raw h2 images are transformed ONCE,
+// cooperatively, into a separate a2 image (relu(h2 s + t), rounded to bf16 as every on-load BN here); the
+// MFMAs read dz / a2 fragments; the epilogue adds e, rounds, and takes the BN2 mask and h2 - mean from the
+// RAW h2 images still in the ring slot -- no second HBM read of h2.  One partial column per block.
+constexpr int CBM = 32;
+template <int K1, int K2, int NS>
+__global__ __launch_bounds__(64 * (K2 / 16), K2 == 64 ? 2 : 1) void pw_cat_kernel(PwCatArgs a) {
+  constexpr int NW = K2 / 16, NT = 64 * NW, N = K2;
+  constexpr int KC1 = K1 / 32, KC2 = K2 / 32, KC = KC1 + KC2;
+  constexpr int IMG = CBM * 64;               // one 32-K image of a tile
+  constexpr int TILE = KC * IMG;
+  constexpr int P = KC * 2 / NW;              // 1-KiB DMA pieces per wave per tile
+  static_assert(P * NW == KC * 2, "piece split");
+  constexpr int ROWB = 16 * 2 + 16;           // staged output row: 16 channels + pad
+  constexpr int STG = CBM * ROWB;             // per wave
+  constexpr int S = 1;                        // stores per lane per tile (32 rows x 2 chunks / 64 lanes)
+  constexpr int VM = (NS - 1) * S + (NS - 2) * P;
+  static_assert(VM < 64, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) char smem[NS * TILE + KC2 * IMG + NW * STG];
+  __shared__ __attribute__((aligned(16))) float bnin[2 * K2];
+  char* const a2img = smem + NS * TILE;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int M = (int)a.M, RG = a.rg;
+  const int tiles = (M + CBM - 1) / CBM;
+  const int n0w = wid * 16;
+  char* const stg = smem + NS * TILE + KC2 * IMG + wid * STG;
+  auto swz = [](int row) { return (0x78 >> (((row >> 2) & 3) << 1)) & 3; };
+
+  // Bcat columns of the wave's 16 channels: wf[kc] = A rows n0w + li, K = 32 kc + 8 g .. +7
+  bf16x8 wf[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    s16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (short)a.bcat[(int64_t)(32 * kc + 8 * g + e) * N + n0w + li];
+    wf[kc] = __builtin_bit_cast(bf16x8, v);
+  }
+  // epilogue lane map: pixel row lane >> 1 of the 32, 8 channels nch = n0w + 8 (lane & 1)
+  const int erow = lane >> 1, nch = n0w + 8 * (lane & 1);
+  float eb[4], bsc[8], bsh[8], bmu[8];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) eb[e] = a.ebias[n0w + 4 * g + e];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    bsc[e] = a.coef[nch + e];
+    bsh[e] = a.coef[K2 + nch + e];
+    bmu[e] = a.coef[2 * K2 + nch + e];
+  }
+  for (int i = tid; i < 2 * K2; i += NT) bnin[i] = a.coef[i];
+
+  // DMA: piece q (of 2 KC per tile) = image q >> 1, rows 16 (q & 1) .. +15; lane -> (row, 16-B chunk)
+  const __amdgpu_buffer_rsrc_t r1 = rsrc(a.dz, (uint32_t)((int64_t)M * K1 * 2));
+  const __amdgpu_buffer_rsrc_t r2 = rsrc(a.h2, (uint32_t)((int64_t)M * K2 * 2));
+  uint32_t voff[P];
+  int prow[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const int q = wid * P + i, kc = q >> 1, row = (q & 1) * 16 + (lane >> 2);
+    const int lc = (lane & 3) ^ swz(row);
+    prow[i] = row;
+    voff[i] = kc < KC1 ? (uint32_t)(row * K1 * 2 + kc * 64 + lc * 16) : (uint32_t)(row * K2 * 2 + (kc - KC1) * 64 + lc * 16);
+  }
+  auto issue = [&](int t, int slot) {
+    char* dst = smem + slot * TILE;
+    const int valid_rows = M - t * CBM;
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const int q = wid * P + i, kc = q >> 1;
+      if (kc < KC1) {
+        const uint32_t v = prow[i] < valid_rows ? voff[i] + (uint32_t)t * (CBM * K1 * 2) : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r1, (lds_void_t*)(dst + q * 1024), 16, v, 0, 0, 0);
+      } else {
+        const uint32_t v = prow[i] < valid_rows ? voff[i] + (uint32_t)t * (CBM * K2 * 2) : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r2, (lds_void_t*)(dst + q * 1024), 16, v, 0, 0, 0);
+      }
+    }
+  };
+  auto ring_wait = [&](int p, bool ending) {  // as pw_stream_kernel's
+    if (ending) wait_vm<0>();
+    else if (p == 0) wait_vm<(NS - 2) * P>();
+    else if (NS >= 3 && p == 1) wait_vm<S + (NS - 2) * P>();
+    else wait_vm<VM>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  float s[8], ss[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
+  const int rgb = blockIdx.x;
+  const int nt = rgb < tiles ? (tiles - 1 - rgb) / RG + 1 : 0;
+  __syncthreads();  // bnin
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < nt) issue(rgb + j * RG, j);
+  for (int j = 0; j < nt; ++j) {
+    ring_wait(j, j + NS - 2 >= nt);
+    const int slot = j % NS, m0 = (rgb + j * RG) * CBM;
+    if (j + NS - 1 < nt) issue(rgb + (j + NS - 1) * RG, (j + NS - 1) % NS);
+    const char* img = smem + slot * TILE;
+    // raw h2 images -> a2 image (same physical positions), once per tile
+#pragma unroll
+    for (int c = tid; c < KC2 * CBM * 4; c += NT) {
+      const int kc2 = c / (CBM * 4), rem = c % (CBM * 4), row = rem >> 2, pc = rem & 3;
+      const int lc = pc ^ swz(row);
+      const int off = kc2 * IMG + row * 64 + pc * 16;
+      const f32x4* cs = (const f32x4*)(bnin + 32 * kc2 + 8 * lc);
+      const f32x4* ch = (const f32x4*)(bnin + K2 + 32 * kc2 + 8 * lc);
+      const f32x4 s0 = cs[0], s1 = cs[1], h0 = ch[0], h1 = ch[1];
+      const float sc8[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+      const float sh8[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+      float f[8];
+      unpack8(*(const u32x4*)(img + KC1 * IMG + off), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], sc8[e], sh8[e]), 0.f);
+      *(u32x4*)(a2img + off) = pack8(f);
+    }
+    __syncthreads();
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const char* im = kc < KC1 ? img + kc * IMG : a2img + (kc - KC1) * IMG;
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) acc[mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kc], kfrag(im, 16 * mi), acc[mi], 0, 0, 0);
+    }
+    // stage (lane: channels n0w + 4 g + e of pixel row 16 mi + li), + e, rounded
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      u32x2 pk;
+      pk[0] = pack_bf2(acc[mi][0] + eb[0], acc[mi][1] + eb[1]);
+      pk[1] = pack_bf2(acc[mi][2] + eb[2], acc[mi][3] + eb[3]);
+      *(u32x2*)(stg + (16 * mi + li) * ROWB + (4 * g) * 2) = pk;
+    }
+    const u32x4 v = *(const u32x4*)(stg + erow * ROWB + (lane & 1) * 16);
+    const int m = m0 + erow;
+    if (m < M) {
+      float f[8], x8[8];
+      unpack8(v, f);
+      const int kc2 = nch >> 5, lc = (nch & 31) >> 3;
+      unpack8(*(const u32x4*)(img + (KC1 + kc2) * IMG + erow * 64 + ((lc ^ swz(erow)) << 4)), x8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dz = fmaf(x8[e], bsc[e], bsh[e]) > 0.f ? f[e] : 0.f;
+        s[e] += dz;
+        ss[e] = fmaf(dz, x8[e] - bmu[e], ss[e]);
+      }
+      *(u32x4*)(a.y + (int64_t)m * N + nch) = v;
+    }
+  }
+  // one partial column per block: reduce over the lanes holding the same chunk (lane & 1)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+#pragma unroll
+    for (int o = 2; o < 64; o <<= 1) {
+      s[e] += __shfl_xor(s[e], o, 64);
+      ss[e] += __shfl_xor(ss[e], o, 64);
+    }
+  }
+  if (lane < 2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a.stats[(int64_t)(nch + e) * RG + rgb] = s[e];
+      a.stats[(int64_t)(N + nch + e) * RG + rgb] = ss[e];
+    }
+  }
+}
+
 }  // namespace pw
 }  // namespace dpe
 
 using namespace dpe;
+
+extern "C" int dpe_cu_reserve();  // comm.cpp
+
+// blocks of the concatenated-K data grad: the resident capacity (2 x 4-wave blocks per CU at K2 = 64,
+// 1 x 8-wave at 128), twice that while a CU budget is in force (two dispatch rounds: the CUs that share
+// with RCCL's blocks get fewer); 0 outside (K1, K2) in {(256, 64), (512, 128)} or a row count whose
+// 32-bit byte offsets would overflow.
+extern "C" int dpe_pw_cat_blocks(int64_t M, int64_t K1, int64_t K2) {
+  static const bool on = [] { const char* e = getenv("DPE_PW_CAT"); return !(e && e[0] == '0'); }();
+  if (!on || !((K1 == 256 && K2 == 64) || (K1 == 512 && K2 == 128))) return 0;
+  if (M <= 0 || M * K1 * 2 >= (1ll << 31) - 4096) return 0;
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int per = K2 == 64 ? 2 : 1;
+  const int64_t tiles = (M + pw::CBM - 1) / pw::CBM;
+  const int64_t nb = (int64_t)std::max(1, cus) * per * (dpe_cu_reserve() > 0 ? 2 : 1);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(nb, tiles));
+}
+
+extern "C" int dpe_pw_cat_launch(const PwCatArgs* args, int64_t K1, int64_t K2, hipStream_t st) {
+  const PwCatArgs& a = *args;
+  if (a.rg <= 0 || a.rg != dpe_pw_cat_blocks(a.M, K1, K2)) return -1;
+  if (K1 == 256 && K2 == 64) hipLaunchKernelGGL((pw::pw_cat_kernel<256, 64, 3>), dim3(a.rg), dim3(256), 0, st, a);
+  else if (K1 == 512 && K2 == 128) hipLaunchKernelGGL((pw::pw_cat_kernel<512, 128, 3>), dim3(a.rg), dim3(512), 0, st, a);
+  else return -1;
+  return 0;
+}
 
 extern "C" int dpe_cu_reserve();  // comm.cpp
 
