@@ -6,7 +6,8 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out/hog
 NB=${1:-16}; TH=${2:-256}; LDS=${3:-20480}; VG=${4:-64}; MODE=${5:-0}
-H="--threads $TH --lds $LDS --vgprs $VG --sleepy $MODE"
+# WINDOWED=<GB/s>: hogs only in the modelled W = 8 bucket all-reduce windows (scripts/hog_probe.py --windowed)
+H="--threads $TH --lds $LDS --vgprs $VG --sleepy $MODE --windowed ${WINDOWED:-0}"
 cd $R
 timeout -k 10 300 python3 scripts/hog_probe.py --model resnet50 $H --modes 0:0 $NB:0 $NB:$NB 0:$NB > gpurun_out/hog/rn.jsonl 2>&1 || { tail -20 gpurun_out/hog/rn.jsonl; exit 1; }
 cat gpurun_out/hog/rn.jsonl

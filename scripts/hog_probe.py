@@ -34,6 +34,11 @@ ap.add_argument("--steps", type=int, default=6, help="timed steps per mode per r
 ap.add_argument("--sleepy", type=int, default=0,
                 help="0: VALU-saturating hogs (worst case), 1: resident but idle (s_sleep), "
                      "2: RCCL-like reduce-copy streaming (two reads + one write per element, little VALU)")
+ap.add_argument("--windowed", type=float, default=0.0,
+                help="> 0: hogs resident only in the bucket all-reduce windows the W = 8 bucket policy predicts "
+                     "(parallel/buckets.py): one hog launch per bucket when its gradients are ready, alive for "
+                     "alpha + 2 (7/8) bytes / (this many GB/s of bus bandwidth) -- a model of RCCL's channel "
+                     "blocks at 8 ranks instead of the whole-backward worst case")
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--modes", nargs="+", default=["0:0", "16:0", "16:16", "0:16"])
 args = ap.parse_args()
@@ -45,7 +50,7 @@ if args.model == "resnet50":
     bs = args.batch_size or 512
     model = get_model("resnet50").to(dev)
     opt = build_optimizer("sgd", model.parameters(), lr=0.1, weight_decay=5e-5)
-    x = Fx.to_s2d_input(torch.randn(bs, 3, 224, 224, device=dev))
+    x = torch.randn(bs, 3, 224, 224, device=dev)
     y = torch.randint(0, 1000, (bs,), device=dev)
 
     def fwd():
@@ -64,10 +69,43 @@ side = torch.cuda.Stream()
 stop = torch.zeros(1, dtype=torch.int32, device=dev)
 modes = [tuple(int(v) for v in m.split(":")) for m in args.modes]
 
+# windowed: the W = 8 buckets (same policy and ready order as DDP: reverse registration order)
+params = [p for p in model.parameters() if p.requires_grad]
+win = {"on": False, "hogs": 0, "pending": [], "left": []}
+if args.windowed > 0:
+    from distributed_pytorch_example_amd.parallel.buckets import assign_buckets, xgmi_bucket_policy
+
+    sizes = [p.numel() * 4 for p in params]
+    f_mb, cap_mb, last_mb = xgmi_bucket_policy(8, sum(sizes))
+    buckets = assign_buckets(sizes, list(range(len(params)))[::-1], int(cap_mb * 2**20), int(f_mb * 2**20),
+                             None, int(last_mb * 2**20) if last_mb else None)
+    bucket_of = {id(params[i]): b for b, idx in enumerate(buckets) for i in idx}
+    bucket_us = [15.0 + 2 * 7 / 8 * sum(sizes[i] for i in idx) / (args.windowed * 1e3) for idx in buckets]
+    print(json.dumps({"windowed_gbps": args.windowed, "buckets_mb": [round(sum(sizes[i] for i in idx) / 2**20, 2) for idx in buckets],
+                      "window_us": [round(t, 1) for t in bucket_us]}), flush=True)
+
+    def on_grad(p):
+        if not win["on"]:
+            return
+        b = bucket_of.get(id(p))
+        if b is None:
+            return
+        win["left"][b] -= 1
+        if win["left"][b] == 0:  # the bucket's all-reduce would start now: hogs for its modelled duration
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                C.cu_hog(win["hogs"], args.threads, args.lds, bucket_us[b], args.vgprs, stop, mode=args.sleepy)
+
+    for p in params:
+        p.register_post_accumulate_grad_hook(on_grad)
+
 
 def step(hogs, reserve):
     loss = fwd()
-    if hogs:
+    if hogs and args.windowed > 0:
+        C.hog_stop(stop, 0)
+        win.update(on=True, hogs=hogs, left=[len(idx) for idx in buckets])
+    elif hogs:
         C.hog_stop(stop, 0)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -76,8 +114,10 @@ def step(hogs, reserve):
     C.set_comm_active(reserve > 0)
     loss.backward()
     C.set_comm_active(False)
+    win["on"] = False
     if hogs:
         C.hog_stop(stop, 1)
+        torch.cuda.current_stream().wait_stream(side)
     opt.step()
     for p in model.parameters():
         p.grad = None
@@ -102,6 +142,6 @@ for m in modes:
     ts = sorted(res[m])
     med = ts[len(ts) // 2]
     base = med if base is None else base
-    print(json.dumps({"model": args.model, "batch": bs, "hogs": m[0], "reserve": m[1], "threads": args.threads,
+    print(json.dumps({"model": args.model, "batch": bs, "hogs": m[0], "reserve": m[1], "windowed": args.windowed, "threads": args.threads,
                       "lds": args.lds, "vgprs": args.vgprs, "sleepy": args.sleepy, "ms_step_median": round(med, 3),
                       "ms_step_min": round(ts[0], 3), "vs_first_mode": round(med / base, 4)}), flush=True)
