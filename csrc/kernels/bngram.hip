@@ -340,81 +340,6 @@ __global__ __launch_bounds__(256) void gram_coef_kernel(const float* __restrict_
   }
 }
 
-// Forward, fused: u = W G for KR output channels per block AND their coefficients (gram_mm + gram_coef in
-// one launch).  Thread j owns column j of the block's u rows (Cin <= 256 = the block's threads): u[k][j] =
-// sum_i w[k][i] G[i][j] with w's KR rows broadcast from LDS and G's rows read coalesced; then e2, w.s, w.mu
-// are reduced per k in double (fixed order: lanes, then waves) and thread k < KR writes coef / running stats
-// exactly as gram_coef_kernel.
-constexpr int KR = 8;
-__global__ __launch_bounds__(256) void gram_coef_fused_kernel(const float* __restrict__ G, const float* __restrict__ s,
-                                                              const uint16_t* __restrict__ w, int Cin, int Cout, int64_t M,
-                                                              const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                              float* __restrict__ rmean, float* __restrict__ rvar,
-                                                              float momentum, float eps, float* __restrict__ coef,
-                                                              float* __restrict__ u) {
-  __shared__ float ws_[KR][256];
-  __shared__ double red[3][KR][4];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, k0 = blockIdx.x * KR;
-  for (int e = tid; e < KR * Cin; e += 256) {
-    const int kk = e / Cin, j = e - kk * Cin;
-    ws_[kk][j] = k0 + kk < Cout ? bf2f(w[(int64_t)(k0 + kk) * Cin + j]) : 0.f;
-  }
-  __syncthreads();
-  double e2[KR], wsv[KR], wmv[KR];
-#pragma unroll
-  for (int kk = 0; kk < KR; ++kk) { e2[kk] = 0.0; wsv[kk] = 0.0; wmv[kk] = 0.0; }
-  const int j = tid;
-  if (j < Cin) {
-    float acc[KR];
-#pragma unroll
-    for (int kk = 0; kk < KR; ++kk) acc[kk] = 0.f;
-    for (int i = 0; i < Cin; ++i) {
-      const float gij = G[(int64_t)i * Cin + j];
-#pragma unroll
-      for (int kk = 0; kk < KR; ++kk) acc[kk] = fmaf(ws_[kk][i], gij, acc[kk]);
-    }
-    const float sj = s[j], mj = s[Cin + j];
-#pragma unroll
-    for (int kk = 0; kk < KR; ++kk) {
-      if (k0 + kk < Cout) u[(int64_t)(k0 + kk) * Cin + j] = acc[kk];
-      const double wv = ws_[kk][j];
-      e2[kk] = wv * acc[kk];
-      wsv[kk] = wv * sj;
-      wmv[kk] = wv * mj;
-    }
-  }
-#pragma unroll
-  for (int kk = 0; kk < KR; ++kk) {
-    for (int o = 32; o > 0; o >>= 1) {
-      e2[kk] += __shfl_xor(e2[kk], o, 64);
-      wsv[kk] += __shfl_xor(wsv[kk], o, 64);
-      wmv[kk] += __shfl_xor(wmv[kk], o, 64);
-    }
-    if (lane == 0) { red[0][kk][wid] = e2[kk]; red[1][kk][wid] = wsv[kk]; red[2][kk][wid] = wmv[kk]; }
-  }
-  __syncthreads();
-  if (tid >= KR || k0 + tid >= Cout) return;
-  const int k = k0 + tid;
-  double E2 = 0.0, WS = 0.0, WM = 0.0;
-  for (int q = 0; q < 4; ++q) { E2 += red[0][tid][q]; WS += red[1][tid][q]; WM += red[2][tid][q]; }
-  const double ms = WS / (double)M;
-  const double mean = WM + ms;
-  double var = E2 / (double)M - ms * ms;
-  if (var < 0) var = 0;
-  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  const float gm = gamma ? gamma[k] : 1.f, bt = beta ? beta[k] : 0.f;
-  const float sc = gm * invstd;
-  coef[k] = sc;
-  coef[Cout + k] = bt - (float)mean * sc;
-  coef[2 * Cout + k] = (float)mean;
-  coef[3 * Cout + k] = invstd;
-  if (rmean) {
-    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    rmean[k] = (1.f - momentum) * rmean[k] + momentum * (float)mean;
-    rvar[k] = (1.f - momentum) * rvar[k] + momentum * (float)unbiased;
-  }
-}
-
 constexpr int KPB = 8;  // output channels per block of the backward coefficient kernel
 
 // Backward, per output channel k.  part [2][Cout][RG]: row 0 = partial sums of dz3 (row 1 unused);
@@ -600,11 +525,6 @@ extern "C" int dpe_gram_coef(const float* G, const float* s, const uint16_t* w, 
                              const float* gamma, const float* beta, float* rmean, float* rvar, float momentum, float eps,
                              float* coef, float* u, hipStream_t st) {
   if (Cin % 32 || Cout % 32) return -1;
-  if (Cin <= 256) {  // u = W G and the coefficients in one launch
-    hipLaunchKernelGGL(gram::gram_coef_fused_kernel, dim3((Cout + gram::KR - 1) / gram::KR), dim3(256), 0, st, G, s, w,
-                       Cin, Cout, M, gamma, beta, rmean, rvar, momentum, eps, coef, u);
-    return 0;
-  }
   // u = W G  (M = Cout, N = Cin, K = Cin)
   hipLaunchKernelGGL((gram::gram_mm_kernel<false, float>), dim3(Cin / 32, Cout / 32, 1), dim3(256), 0, st, w,
                      (int64_t)Cin, (const float*)nullptr, G, (int64_t)Cin, Cin, Cin, u, (int64_t)Cin, (int64_t)0);
