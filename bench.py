@@ -148,7 +148,6 @@ def main():
         from distributed_pytorch_example_amd.ops import ext as _ext
 
         cfg["rccl_max_channels"] = pdist.comm_max_channels()
-        cfg["cu_reserve_slots"] = _ext().cu_reserve_config() if dev.type == "cuda" else 0
     opt = build_optimizer(opt_name, model.parameters(), lr=lr, weight_decay=wd)
     if args.overlap_optimizer and dev.type == "cuda" and not args.graph:
         ddp.overlap_optimizer(opt)
@@ -174,6 +173,10 @@ def main():
 
     for i in range(args.warmup):
         step(i)
+    if world > 1:  # after warm-up: DDP may have dropped the CU budget (parallel/ddp.py, adaptive CU budget)
+        cfg["cu_reserve_slots"] = _ext().cu_reserve_config() if dev.type == "cuda" else 0
+        if ddp.cu_budget_decision is not None:
+            cfg["cu_budget"] = ddp.cu_budget_decision
     if args.graph and dev.type == "cuda":
         step = _graph_step(args, world, ddp, opt, model, xs, ys, fused_loss, num_classes, Fx)
     _sync(dev)

@@ -314,36 +314,52 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const uint16_t* __re
   }
   auto putd = [&](int oh, const u32x4 (&v)[4]) {
     char* sl = dbuf + (oh & 1) * DSLOT;
+    // FUSED: this thread's 8 channels are cg = tid % 8 for every chunk (c = tid + 256 u); the pooled rows
+    // i0 .. i1 of dY row oh
+    const int cg = tid & 7, i0 = oh >> 1, i1 = (oh + 1) >> 1, ni = i1 == i0 ? 1 : 2;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int c = tid + 256 * u;
       if (c >= dch) continue;
       if constexpr (FUSED) {
         // dY chunk (pixel ow = c / 8, channels 8 (c % 8) ..): the windows (i, j) covering (oh, ow), in the
-        // apply kernel's order (row-major), tap 3 (oh - 2i + 1) + (ow - 2j + 1)
-        const int ow = c >> 3, cg = c & 7;
-        const int i0 = oh >> 1, i1 = (oh + 1) >> 1, j0 = ow >> 1, j1 = (ow + 1) >> 1;
+        // apply kernel's order (row-major), tap 3 (oh - 2i + 1) + (ow - 2j + 1).  Branch-free over the
+        // column windows (a duplicate or out-of-range one gets tap 0x100, which no argmax byte equals, and
+        // adds +0): every window's LDS reads are issued before the first compare.
+        const int ow = c >> 3;
+        const int j0 = ow >> 1, j1 = (ow + 1) >> 1;
+        u32x4 gv[2][2];
+        u32x2 bv[2][2];
+        uint32_t tp[2][2];
+#pragma unroll
+        for (int wi = 0; wi < 2; ++wi) {
+          if (wi >= ni) break;  // wave-uniform (oh is)
+          const int i = wi ? i1 : i0;
+          const char* sl2 = pring + (i & 1) * PSLOT;
+#pragma unroll
+          for (int wj = 0; wj < 2; ++wj) {
+            const int j = wj ? j1 : j0;
+            const bool valid = (wj == 0 || j1 != j0) && j < OW;
+            const int jj = min(j, OW - 1);
+            gv[wi][wj] = *(const u32x4*)(sl2 + (jj * 8 + cg) * 16);
+            bv[wi][wj] = *(const u32x2*)(sl2 + PDY + (jj * 64 + cg * 8));
+            tp[wi][wj] = valid ? (uint32_t)(3 * (oh - 2 * i + 1) + (ow - 2 * j + 1)) : 0x100u;
+          }
+        }
         float dz[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) dz[e] = 0.f;
 #pragma unroll
         for (int wi = 0; wi < 2; ++wi) {
-          const int i = wi ? i1 : i0;
-          if (wi && i1 == i0) break;
+          if (wi >= ni) break;
 #pragma unroll
           for (int wj = 0; wj < 2; ++wj) {
-            const int j = wj ? j1 : j0;
-            if (wj && j1 == j0) break;
-            if (j >= OW) continue;
-            const char* sl2 = pring + (i & 1) * PSLOT;
             float g[8];
-            unpack8(*(const u32x4*)(sl2 + (j * 8 + cg) * 16), g);
-            const u32x2 b = *(const u32x2*)(sl2 + PDY + (j * 64 + cg * 8));
-            const uint32_t tap = (uint32_t)(3 * (oh - 2 * i + 1) + (ow - 2 * j + 1));
+            unpack8(gv[wi][wj], g);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const uint32_t t = (b[e >> 2] >> ((e & 3) * 8)) & 0xffu;
-              dz[e] += t == tap ? g[e] : 0.f;
+              const uint32_t t = (bv[wi][wj][e >> 2] >> ((e & 3) * 8)) & 0xffu;
+              dz[e] += t == tp[wi][wj] ? g[e] : 0.f;
             }
           }
         }

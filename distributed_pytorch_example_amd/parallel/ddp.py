@@ -258,6 +258,7 @@ class DistributedDataParallel(nn.Module):
         if broadcast_buffers and self.world_size > 1:
             self._flatten_buffers()
         self._ov_opt = None  # overlap_optimizer()
+        self._budget_probe = self._budget_probe_init()
         self._build_buckets(None)
         self._queued = False
         self._hooks = []
@@ -511,8 +512,75 @@ class DistributedDataParallel(nn.Module):
         if self._ov_opt is not None:
             self._ov_mark(p, 1)
 
+    # ------------------------------------------------------- adaptive CU budget
+    def _budget_probe_init(self):
+        """The CU budget (parallel/dist.py cu_reserve_for: persistent kernels leave slots to RCCL's channel
+        blocks while a bucket all-reduce is in flight) pays off only when collectives occupy a good part of
+        backward.  It is in force from the first bucket launch to the end of backward, while RCCL's blocks
+        are resident only during the all-reduces.  So after warm-up the step's forward + backward time is
+        measured (events, no sync) and the budget is dropped when the modelled all-reduce time,
+        2 (W-1)/W x gradient bytes / DPE_XGMI_BUS_GBPS (default 300), is below DPE_CU_BUDGET_MIN_DUTY
+        (default 0.10) of the backward (taken as 2/3 of forward + backward).  Probe on one GPU
+        (profiles/cu_hog_probe_r5.txt, 16 RCCL-sized workgroups resident only in the modelled W = 8
+        windows): ResNet-50 +1.9 % without the budget vs +4.8 % with it (duty ~3 %: the budget is dropped),
+        GPT-2 +5.4 % vs +4.1 % (duty ~35 %: kept).  An explicit DPE_CU_RESERVE is never changed."""
+        if (self.world_size <= 1 or os.environ.get("DPE_CU_RESERVE") or os.environ.get("DPE_CU_BUDGET_ADAPT", "1") == "0"
+                or not self._params or not self._params[0].is_cuda or not _has_ext()):
+            return None
+        from ..ops._ext import ext
+
+        if ext().cu_reserve_config() <= 0:
+            return None
+        gbps = float(os.environ.get("DPE_XGMI_BUS_GBPS", "300"))
+        nbytes = 4 * sum(p.numel() for p in self._params)
+        comm_ms = 2.0 * (self.world_size - 1) / self.world_size * nbytes / (gbps * 1e6)
+        return {"step": 0, "ev": [], "samples": [], "comm_ms": comm_ms,
+                "min_duty": float(os.environ.get("DPE_CU_BUDGET_MIN_DUTY", "0.10")), "decision": None}
+
+    def _budget_probe_forward(self):
+        pr = self._budget_probe
+        if pr is None or pr["decision"] is not None:
+            return
+        pr["step"] += 1
+        # completed (forward start, backward end) pairs -> samples; the host may run a step ahead of the GPU
+        keep = []
+        for a, b in pr["ev"]:
+            if b is not None and b.query():
+                pr["samples"].append(a.elapsed_time(b))
+            elif b is not None:
+                keep.append([a, b])
+        pr["ev"] = keep
+        if len(pr["samples"]) >= 2:
+            fb_ms = min(pr["samples"])
+            duty = pr["comm_ms"] / max(1e-3, fb_ms * 2.0 / 3.0)
+            pr["decision"] = {"fwd_bwd_ms": round(fb_ms, 3), "comm_ms_model": round(pr["comm_ms"], 3),
+                              "duty": round(duty, 4), "budget": duty >= pr["min_duty"]}
+            pr["ev"] = []
+            if duty < pr["min_duty"]:
+                from .dist import set_cu_budget
+
+                set_cu_budget(0)
+            return
+        if pr["step"] >= 2 and len(pr["ev"]) < 4:  # step 1: warm-up (allocator, bucket rebuild)
+            a = torch.cuda.Event(enable_timing=True)
+            a.record()
+            pr["ev"].append([a, None])
+
+    def _budget_probe_backward_end(self):
+        pr = self._budget_probe
+        if pr is not None and pr["decision"] is None and pr["ev"] and pr["ev"][-1][1] is None:
+            b = torch.cuda.Event(enable_timing=True)
+            b.record()
+            pr["ev"][-1][1] = b
+
+    @property
+    def cu_budget_decision(self):
+        """None until decided (or when not adaptive); else the measured inputs and whether the budget stays."""
+        return None if self._budget_probe is None else self._budget_probe["decision"]
+
     def _finalize(self):
         self._queued = False
+        self._budget_probe_backward_end()
         for i, p in enumerate(self._params):  # fresh but never written this step: zero, as stock
             if getattr(p, "_dpe_fresh", False):
                 p._dpe_fresh = False
@@ -555,6 +623,7 @@ class DistributedDataParallel(nn.Module):
             for p in self._params:
                 p._dpe_uses = 0
             if self.require_backward_grad_sync:
+                self._budget_probe_forward()
                 self.reducer.prepare()
                 if self._ov_opt is not None:
                     self._ov_reset()

@@ -297,3 +297,50 @@ def test_channel_cap_is_opt_in_and_follows_env(monkeypatch):
         assert "NCCL_MAX_NCHANNELS" not in __import__("os").environ
     finally:
         pdist.destroy_process_group()
+
+
+def test_adaptive_cu_budget_decision(monkeypatch):
+    """DDP drops the CU budget when the modelled all-reduce time is a small part of backward
+    (parallel/ddp.py, adaptive CU budget), from event timings the host may see a step late."""
+    import torch
+
+    from distributed_pytorch_example_amd.parallel import ddp as D
+    from distributed_pytorch_example_amd.parallel import dist as pd
+
+    class Ev:
+        t = 0.0
+
+        def __init__(self, enable_timing=False):
+            self.ts, self.done = None, False
+
+        def record(self):
+            Ev.t += 10.0
+            self.ts = Ev.t
+
+        def query(self):
+            return self.done
+
+        def elapsed_time(self, other):
+            return other.ts - self.ts
+
+    monkeypatch.setattr(torch.cuda, "Event", Ev)
+    calls = []
+    monkeypatch.setattr(pd, "set_cu_budget", lambda n: calls.append(n))
+
+    def run(comm_ms):
+        m = D.DistributedDataParallel.__new__(D.DistributedDataParallel)
+        m._budget_probe = {"step": 0, "ev": [], "samples": [], "comm_ms": comm_ms, "min_duty": 0.10, "decision": None}
+        for _ in range(8):
+            m._budget_probe_forward()
+            m._budget_probe_backward_end()  # fwd+bwd = 10 "ms" per step in the fake clock
+            for pair in m._budget_probe["ev"][:-1]:  # the GPU finishes a step one forward late
+                pair[1].done = True
+            if m.cu_budget_decision is not None:
+                break
+        return m.cu_budget_decision
+
+    d = run(0.2)  # duty 0.2 / (10 * 2/3) = 3 %: dropped
+    assert d is not None and d["budget"] is False and calls == [0]
+    calls.clear()
+    d = run(3.0)  # 45 %: kept
+    assert d is not None and d["budget"] is True and calls == []
