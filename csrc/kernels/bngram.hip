@@ -19,6 +19,10 @@
 // coefficient kernel (BN3 scale / shift / mean / invstd + running stats, and u = W3 G for the
 // backward), and the two backward coefficient kernels (BN3 parameter grads, the dW3 correction, the
 // data grad's concatenated B operand and bias).
+#include <cstdlib>
+#include <type_traits>
+#include <utility>
+
 #include "common.h"
 
 namespace dpe {
@@ -225,6 +229,252 @@ __global__ __launch_bounds__(NT) void gram_partial_kernel(const uint16_t* __rest
         for (int e = 0; e < 8; ++e) v[e] += rs[((2 * (c8 / 4) + h) * 64 + l) * 8 + e];
 #pragma unroll
     for (int e = 0; e < 8; ++e) sp[(int64_t)blockIdx.x * C + 8 * c8 + e] = v[e];
+  }
+}
+
+// The same partials, streamed by LDS-DMA (gram_partial_kernel above is register-staged: one tile ahead at
+// C = 256 for lack of registers, ~14-35 % of HBM speed).  A 32-row tile [32][C] bf16 lands in an NS-deep
+// LDS ring by buffer_load ... lds (rows past M read as zeros), row-major with 16-B chunk c of row r at
+// c ^ 2 h(r) (h below: the MFMA operand's transposed reads are bank-conflict-free); the 256 threads then
+// transform it IN PLACE -- thread (chunk c = tid % CPR) applies relu(x scale + shift), rounds, subtracts
+// the pilot shift mu, rounds again (exactly the register-staged kernel's operand) and keeps the column
+// sums of its 8 channels -- and every wave multiplies its fragments (I <= J) of G straight from the tile
+// with ds_read_b64_tr_b16 (8 rows of 16 channels per operand).  Two barriers per tile.  Output layout and
+// reduction order of the partials as gram_partial_kernel (fixed: deterministic).
+DPE_DEVICE int gram_h(int row, int C) {
+  return C >= 128 ? ((row & 3) | (((row >> 3) & 1) << 2)) : (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
+}
+DPE_DEVICE void gram_dma16(__amdgpu_buffer_rsrc_t r, char* wave_dst, uint32_t voff, uint32_t soff) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)wave_dst);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               ::"s"(m0), "v"(voff), "s"(r), "s"(soff) : "memory");
+}
+template <int N>
+DPE_DEVICE void gram_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+  asm volatile("" ::: "memory");
+}
+typedef __attribute__((address_space(3))) s16x4 gram_lds4;
+
+// fragment f of the upper triangle (I <= J, row-major) -> (I << 8) | J; f >= NF: the last one (padding)
+constexpr int gram_frag(int f, int NB, int NF) {
+  if (f >= NF) f = NF - 1;
+  int I = 0;
+  while (f >= NB - I) { f -= NB - I; ++I; }
+  return (I << 8) | (I + f);
+}
+
+// does wave W (fragments W + NW i, i < FPW) read operand block I
+constexpr bool gram_uses(int W, int I, int NB, int NF, int NW, int FPW) {
+  for (int i = 0; i < FPW; ++i) {
+    const int f = gram_frag(W + NW * i, NB, NF);
+    if ((f >> 8) == I || (f & 255) == I) return true;
+  }
+  return false;
+}
+// compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>)
+template <class F, int... Is>
+DPE_DEVICE void gram_sfor_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+DPE_DEVICE void gram_sfor(F&& f) {
+  gram_sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int C>
+__global__ __launch_bounds__(512, 1) void gram_dma_kernel(const uint16_t* __restrict__ x, const float* __restrict__ coef,
+                                                          const float* __restrict__ scoef, int64_t M, int rpb,
+                                                          float* __restrict__ gp, float* __restrict__ sp,
+                                                          float* __restrict__ mu_out) {
+  constexpr int NT = 512, NW = 8;
+  constexpr int CPR = C / 8, RB = 2 * C, SB = TR * RB;  // chunks per row, bytes per row / tile
+  constexpr int NS = C == 256 ? 8 : (C == 128 ? 12 : 16); // ring depth (tiles)
+  constexpr int GT = C == 64 ? 4 : 2, NG = NS / GT;        // tiles per step (one barrier pair), ring groups
+  constexpr int DPG = GT * SB / 1024 / NW;                // DMA pieces (1 KiB) per wave per group
+  constexpr int RPT = NT / CPR, TPG = GT * TR / RPT;      // transform: row stride, rows per thread per group
+  constexpr int NB = C / 16, NF = NB * (NB + 1) / 2, FPW = (NF + NW - 1) / NW;
+  static_assert(NG * GT == NS && NG >= 3 && DPG >= 1 && DPG * NW * 1024 == GT * SB && TPG * RPT == GT * TR, "split");
+  __shared__ __attribute__((aligned(16))) char ring[NS * SB];
+  __shared__ __attribute__((aligned(16))) float cf[3 * C];  // scale | shift | mu
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = min<int64_t>(M, r0 + rpb);
+  const int ntile = r0 < r1 ? (int)((r1 - r0 + TR - 1) / TR) : 0;
+  for (int c = tid; c < C; c += NT) {
+    cf[c] = coef ? coef[c] : 1.f;
+    cf[C + c] = coef ? coef[C + c] : 0.f;
+    const float m = scoef ? relu_gauss_mean(scoef, C, c) : 0.f;
+    cf[2 * C + c] = m;
+    if (blockIdx.x == 0) mu_out[c] = m;
+  }
+  // DMA: lane l of the group's piece q (= wid + NW v) fills byte 1024 q + 16 l of the group's GT tiles
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(x), (short)0, (int)(M * C * 2), 0x00020000);
+  uint32_t voff[DPG];
+#pragma unroll
+  for (int v = 0; v < DPG; ++v) {
+    const int o = ((wid + NW * v) * 1024 + lane * 16) % SB, tk = ((wid + NW * v) * 1024) / SB;
+    const int row = o / RB, chs = (o % RB) / 16;
+    const int ch = chs ^ (2 * gram_h(row, C));
+    voff[v] = (uint32_t)(((tk * TR + row) * C + ch * 8) * 2);
+  }
+  const int ngrp = (ntile + GT - 1) / GT;
+  // group q = tiles [q GT, q GT + GT) in ring slots (q % NG) GT + [0, GT); rows past the block's range (the
+  // next block's, or zeros past M) are masked in the transform
+  auto dma_group = [&](int q) {
+    const uint32_t so = (uint32_t)((r0 + (int64_t)q * GT * TR) * C * 2);
+    char* slot = ring + (q % NG) * GT * SB;
+#pragma unroll
+    for (int v = 0; v < DPG; ++v) gram_dma16(rs, slot + (wid + NW * v) * 1024, voff[v], so);
+  };
+  __syncthreads();
+  // transform: this thread's chunk and its coefficients
+  const int tc = tid % CPR, trow = tid / CPR;
+  float sc8[8], sh8[8], mu8[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc8[e] = cf[8 * tc + e];
+    sh8[e] = cf[C + 8 * tc + e];
+    mu8[e] = cf[2 * C + 8 * tc + e];
+  }
+  f32x4 acc[FPW];  // fragments (I <= J) f = wid + NW i of G (gram_frag)
+#pragma unroll
+  for (int i = 0; i < FPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 csa[FPW];  // column sums of block J for the wave's diagonal fragments (J, J): ones^T X'
+#pragma unroll
+  for (int i = 0; i < FPW; ++i) csa[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
+  // operand read: lane (g, i = 4 q + p) takes rows 8 g + q (+ 4), channels 16 I + 4 p .. + 3
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  const int rw1 = 8 * g + qq, rw2 = rw1 + 4;
+  const int ro1 = rw1 * RB, ro2 = rw2 * RB;
+  const int h1 = 2 * gram_h(rw1, C), h2 = 2 * gram_h(rw2, C);
+
+#pragma unroll 1
+  for (int q = 0; q < NG - 1; ++q)
+    if (q < ngrp) dma_group(q);
+#pragma unroll 1
+  for (int q = 0; q < ngrp; ++q) {
+    // every DMA of groups <= q retired (younger: groups q + 1 .. q + NG - 2, all issued when they exist)
+    if (q + NG - 2 < ngrp) gram_wait_vm<(NG - 2) * DPG>();
+    else gram_wait_vm<0>();
+    __syncthreads();  // group q landed for every wave; every wave is past group q - 1's operand reads
+    if (q + NG - 1 < ngrp) dma_group(q + NG - 1);  // into group q - 1's slots
+    char* const S = ring + (q % NG) * GT * SB;
+    const bool full = r0 + (int64_t)(q + 1) * GT * TR <= r1;  // block-uniform
+#pragma unroll
+    for (int k = 0; k < TPG; ++k) {
+      const int rg = trow + RPT * k, row = rg % TR;
+      char* a = S + (rg / TR) * SB + row * RB + ((tc ^ (2 * gram_h(row, C))) << 4);
+      float f[8];
+      unpack8(*(const u32x4*)a, f);
+      if (coef) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], sc8[e], sh8[e]), 0.f);
+        unpack8(pack8(f), f);  // the rounded operand
+      }
+      if (full) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] -= mu8[e];
+      } else {
+        const bool valid = r0 + (int64_t)q * GT * TR + rg < r1;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = valid ? f[e] - mu8[e] : 0.f;  // (pad rows stay 0, not -mu)
+      }
+      *(u32x4*)a = pack8(f);  // the centred MFMA operand
+    }
+    __syncthreads();
+    // the wave's fragments are compile-time per wave index: operands read once, only those it uses
+    auto mm = [&](auto wc) {
+      constexpr int W = decltype(wc)::value;
+#pragma unroll
+      for (int tk = 0; tk < GT; ++tk) {
+        const char* T = S + tk * SB;
+        bf16x8 op[NB];
+        gram_sfor<NB>([&](auto Ic) {
+          constexpr int I = decltype(Ic)::value;
+          if constexpr (!gram_uses(W, I, NB, NF, NW, FPW)) return;
+          const int ch = 2 * I + (pp >> 1), sub = (pp & 1) * 8;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((gram_lds4*)(T + ro1 + ((ch ^ h1) << 4) + sub));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((gram_lds4*)(T + ro2 + ((ch ^ h2) << 4) + sub));
+          s16x8 r;
+          r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+          r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+          op[I] = __builtin_bit_cast(bf16x8, r);
+        });
+        gram_sfor<FPW>([&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+          constexpr int f = gram_frag(W + NW * i, NB, NF);
+          if constexpr (W + NW * i < NF) {
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(op[f >> 8], op[f & 255], acc[i], 0, 0, 0);
+            if constexpr ((f >> 8) == (f & 255))
+              csa[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, op[f & 255], csa[i], 0, 0, 0);
+          }
+        });
+      }
+    };
+    switch (wid) {
+      case 0: mm(std::integral_constant<int, 0>{}); break;
+      case 1: mm(std::integral_constant<int, 1>{}); break;
+      case 2: mm(std::integral_constant<int, 2>{}); break;
+      case 3: mm(std::integral_constant<int, 3>{}); break;
+      case 4: mm(std::integral_constant<int, 4>{}); break;
+      case 5: mm(std::integral_constant<int, 5>{}); break;
+      case 6: mm(std::integral_constant<int, 6>{}); break;
+      default: mm(std::integral_constant<int, 7>{}); break;
+    }
+  }
+  // partial G, upper-triangle fragments only, fragment-native: fragment f's element e of lane l at
+  // [block][f][e][l] (whole 256-B rows per store; gram_reduce_tri_kernel mirrors); the column sums (every row
+  // of ones^T X' is the same): row 0 = lanes 0..15, element 0
+  float* Gt = gp + (int64_t)blockIdx.x * NF * 256;
+  const int li = lane & 15;
+#pragma unroll
+  for (int i = 0; i < FPW; ++i) {
+    const int fl = wid + NW * i;
+    if (fl >= NF) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) Gt[(int64_t)fl * 256 + e * 64 + lane] = acc[i][e];
+    const int f = gram_frag(fl, NB, NF);
+    if ((f >> 8) == (f & 255) && g == 0) sp[(int64_t)blockIdx.x * C + 16 * (f & 255) + li] = csa[i][0];
+  }
+}
+
+// gram_reduce_kernel for the triangle layout of gram_dma_kernel: output j < NF * 256 is element e of lane l of
+// fragment f (contiguous partial reads across the block), written to G at (r, c) and mirrored at (c, r); then
+// the C column sums.  Same fixed order (8 slab groups, then group order, in double).
+__global__ __launch_bounds__(256) void gram_reduce_tri_kernel(const float* __restrict__ gp, const float* __restrict__ sp,
+                                                              int nb, int C, float* __restrict__ G, float* __restrict__ s) {
+  __shared__ double part[8][32];
+  const int o = threadIdx.x & 31, q = threadIdx.x >> 5;
+  const int NB = C / 16, NF = NB * (NB + 1) / 2;
+  const int64_t nt = (int64_t)NF * 256;
+  const int64_t j = (int64_t)blockIdx.x * 32 + o;
+  double a = 0.0;
+  if (j < nt) {
+    for (int b = q; b < nb; b += 8) a += gp[(int64_t)b * nt + j];
+  } else if (j < nt + C) {
+    for (int b = q; b < nb; b += 8) a += sp[(int64_t)b * C + (j - nt)];
+  }
+  part[q][o] = a;
+  __syncthreads();
+  if (q == 0) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += part[k][o];
+    if (j < nt) {
+      const int fr = gram_frag((int)(j >> 8), NB, NF), I = fr >> 8, J = fr & 255;
+      const int e = (int)((j >> 6) & 3), l = (int)(j & 63);
+      const int r = 16 * I + 4 * (l >> 4) + e, c = 16 * J + (l & 15);
+      G[(int64_t)r * C + c] = (float)t;
+      if (I != J) G[(int64_t)c * C + r] = (float)t;
+    } else if (j < nt + C) {
+      s[j - nt] = (float)t;
+    }
   }
 }
 
@@ -495,8 +745,13 @@ using namespace dpe;
 // Gram pass: x [M][C] bf16 (C in {64, 128, 256}), coef = BN [scale | shift] applied with ReLU on load (or
 // nullptr), scoef = the [4][C] BN coefficients the pilot shift comes from (nullptr: no shift);
 // ws >= dpe_gram_ws_floats(M, C) floats.  Writes G [C][C] and s [2][C] = (colsum, mu), centred on mu.
+static bool gram_dma_on() {
+  const char* ev = getenv("DPE_GRAM_DMA");  // (read per call: tests compare both kernels in one process)
+  return !(ev && ev[0] == '0');
+}
 extern "C" int dpe_gram_blocks(int64_t M, int C) {
-  const int nb = C <= 128 ? 256 : 128;
+  // (the LDS-DMA pass keeps 256 blocks at C = 256 too: its triangle partials are half the full matrices)
+  const int nb = (C <= 128 || gram_dma_on()) ? 256 : 128;
   return (int)std::min<int64_t>(nb, std::max<int64_t>(1, (M + gram::TR - 1) / gram::TR));
 }
 extern "C" int64_t dpe_gram_ws_floats(int64_t M, int C) { return (int64_t)dpe_gram_blocks(M, C) * ((int64_t)C * C + C); }
@@ -510,14 +765,29 @@ extern "C" int dpe_gram(const uint16_t* x, const float* coef, const float* scoef
   float* gp = ws;
   float* sp = ws + (int64_t)nb * C * C;
   float* mu = s + C;
-  if (C == 64)
+  // DPE_GRAM_DMA=0: the register-staged kernel (A/B)
+  const bool dma = gram_dma_on();
+  const bool dma_used = dma && M * C * 2 < (1ll << 31) - 4096;
+  if (dma_used) {
+    if (C == 64)
+      hipLaunchKernelGGL(gram::gram_dma_kernel<64>, dim3(nb), dim3(512), 0, st, x, coef, scoef, M, rpb, gp, sp, mu);
+    else if (C == 128)
+      hipLaunchKernelGGL(gram::gram_dma_kernel<128>, dim3(nb), dim3(512), 0, st, x, coef, scoef, M, rpb, gp, sp, mu);
+    else
+      hipLaunchKernelGGL(gram::gram_dma_kernel<256>, dim3(nb), dim3(512), 0, st, x, coef, scoef, M, rpb, gp, sp, mu);
+  } else if (C == 64)
     hipLaunchKernelGGL(gram::gram_partial_kernel<64>, dim3(nb), dim3(256), 0, st, x, coef, scoef, M, rpb, gp, sp, mu);
   else if (C == 128)
     hipLaunchKernelGGL(gram::gram_partial_kernel<128>, dim3(nb), dim3(256), 0, st, x, coef, scoef, M, rpb, gp, sp, mu);
   else
     hipLaunchKernelGGL(gram::gram_partial_kernel<256>, dim3(nb), dim3(512), 0, st, x, coef, scoef, M, rpb, gp, sp, mu);
   const int64_t n = (int64_t)C * C + C;
-  hipLaunchKernelGGL(gram::gram_reduce_kernel, dim3((unsigned)((n + 31) / 32)), dim3(256), 0, st, gp, sp, nb, C, G, s);
+  if (dma_used) {
+    const int64_t nf = (int64_t)(C / 16) * (C / 16 + 1) / 2, nt = nf * 256 + C;
+    hipLaunchKernelGGL(gram::gram_reduce_tri_kernel, dim3((unsigned)((nt + 31) / 32)), dim3(256), 0, st, gp, sp, nb, C, G, s);
+  }
+  else
+    hipLaunchKernelGGL(gram::gram_reduce_kernel, dim3((unsigned)((n + 31) / 32)), dim3(256), 0, st, gp, sp, nb, C, G, s);
   return 0;
 }
 

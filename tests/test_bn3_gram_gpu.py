@@ -8,6 +8,8 @@ concatenated-K data grad itself, and finally a whole ResNet-50 step with the pat
 """
 import copy
 
+import os
+
 import pytest
 import torch
 
@@ -82,6 +84,40 @@ def test_gram_and_coef(C, with_coef):
     assert _rel(coef3, ref) < 1e-4, _rel(coef3, ref)
     assert _rel(u, w.reshape(Cout, C).double() @ Gc) < 2e-5  # (u = W G of the centred G)
     assert _rel(rm, 0.1 * mean) < 1e-4 and _rel(rv, 0.9 + 0.1 * h.var(0, unbiased=True)) < 1e-4
+
+
+@pytest.mark.parametrize("C", [64, 128, 256])
+def test_gram_many_tiles_per_block(C):
+    """Layer-scale row counts: every block of the Gram pass walks many 32-row tiles (the LDS-DMA ring wraps
+    several times) and the last block ends mid-tile."""
+    X = ext()
+    g = torch.Generator(device=DEV).manual_seed(5 + C)
+    M = 100_000 + 7
+    x = torch.randn(M, C, device=DEV, generator=g).bfloat16()
+    coef = torch.stack([1 + 0.2 * torch.randn(C, device=DEV, generator=g), 0.5 * torch.randn(C, device=DEV, generator=g),
+                        torch.zeros(C, device=DEV), torch.ones(C, device=DEV)]).float()
+    G, s = X.bn_gram(x, coef, coef)
+    # the kernels' operand: relu(fma(x, scale, shift)) rounded once to fp32 (double then float: exact product)
+    a = torch.relu((x.double() * coef[0].double() + coef[1].double()).float()).bfloat16().double()
+    ac = (a - s[1].double()).float().bfloat16().double()
+    Gc, sc = ac.t() @ ac, ac.sum(0)
+    assert _rel(G, Gc) < 2e-5 and _rel(s[0], sc) < 2e-5, (_rel(G, Gc), _rel(s[0], sc))
+    G2, s2 = X.bn_gram(x, coef, coef)
+    assert torch.equal(G, G2) and torch.equal(s, s2)  # fixed-order partials: run-to-run identical
+    # the LDS-DMA pass and the register-staged one (DPE_GRAM_DMA=0): G summed in the same order (bitwise
+    # equal at C <= 128); the column sums by an MFMA against ones vs per-thread adds (fp32 rounding apart)
+    old = os.environ.get("DPE_GRAM_DMA")
+    os.environ["DPE_GRAM_DMA"] = "0"
+    try:
+        G3, s3 = X.bn_gram(x, coef, coef)
+    finally:
+        if old is None:
+            os.environ.pop("DPE_GRAM_DMA")
+        else:
+            os.environ["DPE_GRAM_DMA"] = old
+    # (at C = 256 the DMA pass runs 256 blocks, the register-staged one 128: G's block partials differ too)
+    assert (torch.equal(G, G3) if C <= 128 else _rel(G, G3) < 1e-6) and torch.equal(s[1], s3[1])
+    assert _rel(s[0], s3[0]) < 1e-6, _rel(s[0], s3[0])
 
 
 @pytest.mark.parametrize("K", [64, 128, 256])
