@@ -1,6 +1,6 @@
 #!/bin/bash
 # Stall breakdown (one --pmc pass, kernel trace only) of the kernels a script launches:
-#   bash scripts/gpu_pmc_kernels.sh <script.py> [args...]   -> gpurun_out/pmck/summary.txt
+#   [FILTER=substring] bash scripts/gpu_pmc_kernels.sh <script.py> [args...]   -> gpurun_out/pmck/summary.txt
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out/pmck
@@ -20,7 +20,9 @@ for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
     for row in csv.DictReader(open(f)):
         k = row.get("Kernel_Name", "?").split("(")[0]
         per[k][row["Counter_Name"]] += float(row["Counter_Value"])
-rows = sorted(per.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0))[:12]
+import os
+flt = os.environ.get("FILTER", "")
+rows = sorted([kv for kv in per.items() if flt in kv[0]], key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0))[:14]
 for k, c in rows:
     wc = c.get("SQ_WAVE_CYCLES", 1) or 1
     print(k[:100])
