@@ -6,7 +6,7 @@ mkdir -p gpurun_out/pub
 run() {  # name, args...
   local n=$1; shift
   timeout -k 10 300 python bench.py "$@" > gpurun_out/pub/$n.log 2>&1 || { echo "$n FAILED"; tail -20 gpurun_out/pub/$n.log; exit 1; }
-  echo "$n $(tail -1 gpurun_out/pub/$n.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], "ms/step", round(d["value"]), d["unit"])')"
+  echo "$n $(grep "\"metric\"" gpurun_out/pub/$n.log | tail -1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], "ms/step", round(d["value"]), d["unit"])')"
 }
 run gpt2_a --model gpt2 --steps 20 --warmup 5
 run resnet512 --steps 20 --warmup 5
