@@ -333,6 +333,16 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
       CV ? (int)((((int64_t)cg.N * cg.H * cg.W * cg.C) + apre) * 2) : 0, 0x00020000);
   const int cshift = CV ? 31 - __builtin_clz(cg.C) : 0;
   const float inv_ow = BC ? 1.f / (float)cg.OW : 0.f, inv_hw = BC ? 1.f / (float)(cg.OH * cg.OW) : 0.f;
+  // BC: each B half stages the unit's K-tiles in order (half 0: 0, 1, 2, ..; half 1: 0, 1, 2, ..), so the
+  // output pixel of a lane's piece is a cursor advanced by TK pixels per staging instead of decoded from
+  // scratch (two float-reciprocal divisions with corrections): bq = the pixel's input offset
+  // (img H + oh sh) W + ow sw, bohw = oh << 16 | ow.  Per-TK-step increments (wave-uniform):
+  const int bc_dow = BC ? TK % cg.OW : 0, bc_doh = BC ? (TK / cg.OW) % cg.OH : 0,
+            bc_dimg = BC ? (TK / cg.OW) / cg.OH : 0;
+  const int bc_dq = BC ? bc_dow * cg.sw + bc_doh * cg.sh * cg.W + bc_dimg * cg.H * cg.W : 0;
+  const int bc_cw = BC ? cg.sh * cg.W - cg.OW * cg.sw : 0;        // ow wrapped: oh + 1
+  const int bc_ch = BC ? cg.H * cg.W - cg.OH * cg.sh * cg.W : 0;  // oh wrapped: img + 1
+  uint32_t bq[2][BC ? GB : 1], bohw[2][BC ? GB : 1];
   int m0, n0, kb, nt, split;
   // Grouped tile order: consecutive unit ids (which run together on one XCD -- xcd_remap) walk
   // GROUP_M tile rows before moving one tile column, so an XCD's concurrent tiles form a
@@ -414,6 +424,23 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
           gb[h][i] = off;
           gbt[h][i] = disp;
         }
+      // the pixel cursors at K-tile 0 of this unit (same for both halves: the pixel depends on the lane's
+      // row of the piece, not on the column half)
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        const int px = kb + 4 * (wid * GB + i) + (lane >> 4);
+        int img = (int)((float)px * inv_hw);
+        img -= img * cg.OH * cg.OW > px;
+        img += (img + 1) * cg.OH * cg.OW <= px;
+        const int rem = px - img * cg.OH * cg.OW;
+        int oh = (int)((float)rem * inv_ow);
+        oh -= oh * cg.OW > rem;
+        oh += (oh + 1) * cg.OW <= rem;
+        const int ow = rem - oh * cg.OW;
+        const uint32_t q = (uint32_t)((img * cg.H + oh * cg.sh) * cg.W + ow * cg.sw);
+        bq[0][i] = bq[1][i] = q;
+        bohw[0][i] = bohw[1][i] = ((uint32_t)oh << 16) | (uint32_t)ow;
+      }
     } else {
       stage_setup<BN, WC, CH, GB, BK>(qldb, p.b_dim > 0 ? p.b_dim : qN, n0, BK ? kb : 0, gb);
     }
@@ -455,21 +482,21 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
   do {                                                                                       \
     if constexpr (BC) {                                                                      \
       _Pragma("unroll") for (int i_ = 0; i_ < GB; ++i_) {                                    \
-        /* this lane's pixel row of the K-tile: (image, oh, ow) by float reciprocals, corrected */ \
-        const int px_ = kb + (t) * TK + 4 * (wid * GB + i_) + (lane >> 4);                   \
-        int img_ = (int)((float)px_ * inv_hw);                                               \
-        img_ -= img_ * cg.OH * cg.OW > px_;                                                  \
-        img_ += (img_ + 1) * cg.OH * cg.OW <= px_;                                           \
-        const int rem_ = px_ - img_ * cg.OH * cg.OW;                                         \
-        int oh_ = (int)((float)rem_ * inv_ow);                                               \
-        oh_ -= oh_ * cg.OW > rem_;                                                           \
-        oh_ += (oh_ + 1) * cg.OW <= rem_;                                                    \
-        const int ow_ = rem_ - oh_ * cg.OW;                                                  \
+        /* this lane's pixel of K-tile t: half h's cursor (tile t exactly: stagings are in order) */ \
+        const int ow_ = (int)(bohw[h][i_] & 0xffffu), oh_ = (int)(bohw[h][i_] >> 16);       \
         const int ih_ = oh_ * cg.sh + ((int)gbt[h][i_] >> 16);                               \
         const int iw_ = ow_ * cg.sw + (int)(int16_t)(gbt[h][i_] & 0xffffu);                  \
-        const bool v_ = px_ < p.K && (unsigned)ih_ < (unsigned)cg.H && (unsigned)iw_ < (unsigned)cg.W; \
-        const uint32_t po_ = (uint32_t)((((int64_t)img_ * cg.H + oh_ * cg.sh) * cg.W + ow_ * cg.sw) << cshift) * 2u; \
+        const bool v_ = 4 * (wid * GB + i_) + (lane >> 4) < p.K - kb - (t) * TK &&           \
+                        (unsigned)ih_ < (unsigned)cg.H && (unsigned)iw_ < (unsigned)cg.W;    \
+        const uint32_t po_ = (bq[h][i_] << cshift) * 2u;                                     \
         bdma16(arsrc, wdB + ((buf) * 2 + (h)) * BHB + i_ * 1024, v_ ? po_ + gb[h][i_] : 0x80000000u, 0u); \
+        /* advance the cursor one K-tile (TK pixels) */                                      \
+        int ow2_ = ow_ + bc_dow, oh2_ = oh_ + bc_doh;                                        \
+        uint32_t q2_ = bq[h][i_] + (uint32_t)bc_dq;                                          \
+        if (ow2_ >= cg.OW) { ow2_ -= cg.OW; oh2_ += 1; q2_ += (uint32_t)bc_cw; }             \
+        if (oh2_ >= cg.OH) { oh2_ -= cg.OH; q2_ += (uint32_t)bc_ch; }                         \
+        bq[h][i_] = q2_;                                                                     \
+        bohw[h][i_] = ((uint32_t)oh2_ << 16) | (uint32_t)ow2_;                               \
       }                                                                                      \
     } else {                                                                                 \
       const char* b_ = Bb + (int64_t)(t) * bstep;                                            \
