@@ -916,35 +916,54 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
 #undef BG_SUM
 }
 
-// sum of K-split partial slabs -> the real epilogue; one thread per 4 output columns
-template <int EPI, int ACT>
+// sum of K-split partial slabs -> the real epilogue.  A block is FQ = 256 / FG output quads (4 columns
+// each) x FG split groups (FG = 8 from 32 splits on): thread (quad, group g) sums slabs g, g + 8, g + 16, ... (loads issued 4 at a time),
+// the 8 group sums are added in group order in LDS (fixed: run-to-run identical), and the group-0 threads
+// run the epilogue.  (One thread per quad over every split left the many-split weight grads -- 100-200
+// slabs of a 512 x 128 output in 64 blocks -- latency-bound at ~17 us.)
+// FG = 1 (few splits: the per-thread loop is short, and the quads of 256 threads keep the grid small) is the
+// plain per-quad sum.
+template <int EPI, int ACT, int FG>
 __global__ __launch_bounds__(256) void hgemm_finalize_kernel(HgemmArgs p) {
-  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  constexpr int FQ = 256 / FG;
+  __shared__ f32x4 part[FG][FQ];
+  __shared__ float bpart[FG][FQ];
+  const int qi = threadIdx.x % FQ, grp = threadIdx.x / FQ;
+  const int64_t q = (int64_t)blockIdx.x * FQ + qi;
   const int nq = p.N >> 2;
-  if (q >= (int64_t)p.M * nq) return;
-  const int r = (int)(q / nq), c = (int)(q % nq) * 4;
+  const bool ok = q < (int64_t)p.M * nq;
+  const int r = ok ? (int)(q / nq) : 0, c = ok ? (int)(q % nq) * 4 : 0;
   const float alpha = p.alpha * (p.alpha_ptr ? *p.alpha_ptr : 1.f);
   const int64_t plane = (int64_t)p.M * p.N;
-  // the slabs' loads are issued 4 at a time (independent), then summed in split order: a load per
-  // loop trip left the pass at ~3.9 TB/s (latency-bound at 4-16 slabs)
-  const float* src = p.ws + (int64_t)r * p.N + c;
-  f32x4 s = *(const f32x4*)src;
-  int k = 1;
-  for (; k + 3 < p.splits; k += 4) {
-    const f32x4 a0 = *(const f32x4*)(src + k * plane), a1 = *(const f32x4*)(src + (k + 1) * plane);
-    const f32x4 a2 = *(const f32x4*)(src + (k + 2) * plane), a3 = *(const f32x4*)(src + (k + 3) * plane);
-    s += a0;
-    s += a1;
-    s += a2;
-    s += a3;
+  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bs = 0.f;
+  if (ok) {
+    const float* src = p.ws + (int64_t)r * p.N + c;
+    int k = grp;
+    for (; k + 3 * FG < p.splits; k += 4 * FG) {
+      const f32x4 a0 = *(const f32x4*)(src + k * plane), a1 = *(const f32x4*)(src + (k + FG) * plane);
+      const f32x4 a2 = *(const f32x4*)(src + (k + 2 * FG) * plane), a3 = *(const f32x4*)(src + (k + 3 * FG) * plane);
+      s += a0;
+      s += a1;
+      s += a2;
+      s += a3;
+    }
+    for (; k < p.splits; k += FG) s += *(const f32x4*)(src + k * plane);
+    if (p.dbias && c == 0)  // fused bias gradient: the units' partial row sums, same grouping
+      for (int kk = grp; kk < p.splits; kk += FG) bs += p.ws_bias[(int64_t)kk * p.M + r];
   }
-  for (; k < p.splits; ++k) s += *(const f32x4*)(src + k * plane);
+  part[grp][qi] = s;
+  bpart[grp][qi] = bs;
+  __syncthreads();
+  if (grp != 0 || !ok) return;
+#pragma unroll
+  for (int g = 1; g < FG; ++g) s += part[g][qi];
   s *= alpha;
   if (p.bias) s += *(const f32x4*)(p.bias + c);
-  if (p.dbias && c == 0) {  // fused bias gradient: the units' partial row sums, in split order
-    float b = 0.f;
-    for (int k = 0; k < p.splits; ++k) b += p.ws_bias[(int64_t)k * p.M + r];
-    p.dbias[r] += alpha * b;
+  if (p.dbias && c == 0) {
+#pragma unroll
+    for (int g = 1; g < FG; ++g) bs += bpart[g][qi];
+    p.dbias[r] += alpha * bs;
   }
   const int64_t o = (int64_t)r * p.ldc + c;
   if constexpr (EPI == HE_BF16) {
@@ -1148,8 +1167,13 @@ extern "C" int dpe_hgemm_finalize(const HgemmArgs* a, int epi, hipStream_t st) {
   const HgemmArgs& p = *a;
   if (p.N % 4) return -1;
   const int64_t n = (int64_t)p.M * (p.N / 4);
-  const dim3 g((unsigned)((n + 255) / 256)), b(256);
-#define FL(E, A) hipLaunchKernelGGL((hg::hgemm_finalize_kernel<E, A>), g, b, 0, st, p)
+  const bool grouped = p.splits >= 32;
+  const dim3 g((unsigned)(grouped ? (n + 31) / 32 : (n + 255) / 256)), b(256);
+#define FL(E, A)                                                                   \
+  do {                                                                             \
+    if (grouped) hipLaunchKernelGGL((hg::hgemm_finalize_kernel<E, A, 8>), g, b, 0, st, p); \
+    else hipLaunchKernelGGL((hg::hgemm_finalize_kernel<E, A, 1>), g, b, 0, st, p);        \
+  } while (0)
   if (epi == HE_BF16) {
     if (p.act == ACT_NONE) FL(HE_BF16, ACT_NONE);
     else if (p.act == ACT_GELU) FL(HE_BF16, ACT_GELU);
