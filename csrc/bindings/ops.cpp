@@ -26,6 +26,7 @@ int dpe_gram(const uint16_t* x, const float* coef, const float* scoef, int64_t M
 int dpe_gram_coef(const float* G, const float* s, const uint16_t* w, int Cin, int Cout, int64_t M, const float* gamma,
                   const float* beta, float* rmean, float* rvar, float momentum, float eps, float* coef, float* u,
                   hipStream_t st);
+int64_t dpe_gram_bwd_ws_floats(int Cin, int Cout);
 int dpe_gram_bwd(const float* part, int rg, const float* P, const uint16_t* w, const float* u, const float* s,
                  const float* coef3, const float* gamma, int Cin, int Cout, int64_t M, float* dgamma, float* dbeta,
                  float* dw, uint16_t* bcat, float* abc, float* ebias, float* qws, hipStream_t st);
@@ -1310,7 +1311,7 @@ std::vector<Tensor> bn_gram_bwd(const Tensor& part, const Tensor& P, const Tenso
               "bn_gram_bwd: shapes");
   auto fo = P.options();
   Tensor bcat = at::empty({Cout + Cin, Cin}, w.options()), abc = at::empty({3, Cout}, fo), e = at::empty({Cin}, fo);
-  Tensor qws = at::empty({(Cout + 127) / 128, Cin, Cin}, fo);
+  Tensor qws = at::empty({dpe_gram_bwd_ws_floats((int)Cin, (int)Cout)}, fo);
   CHECK_RC(dpe_gram_bwd(fp(part), (int)part.size(2), fp(P), bp(w), fp(u), fp(sv), fp(coef), fpo(gamma), (int)Cin,
                         (int)Cout, M, fpom(dgamma), fpom(dbeta), fp(dw), bpm(bcat), fp(abc), fp(e), fp(qws), cur_stream()),
            "bn_gram_bwd");

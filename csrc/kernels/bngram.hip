@@ -444,6 +444,28 @@ __global__ __launch_bounds__(512, 1) void gram_dma_kernel(const uint16_t* __rest
   }
 }
 
+// sum_b p[b * stride] over b = q, q + 8, ... < nb in that order (double): 32 (then 8) loads in flight per batch
+__device__ __forceinline__ double gram_slab_sum(const float* __restrict__ p, int64_t stride, int q, int nb) {
+  double a = 0.0;
+  int b = q;
+  for (; b + 248 < nb; b += 256) {
+    float v[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = p[(int64_t)(b + 8 * i) * stride];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) a += v[i];
+  }
+  for (; b + 56 < nb; b += 64) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = p[(int64_t)(b + 8 * i) * stride];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a += v[i];
+  }
+  for (; b < nb; b += 8) a += p[(int64_t)b * stride];
+  return a;
+}
+
 // gram_reduce_kernel for the triangle layout of gram_dma_kernel: output j < NF * 256 is element e of lane l of
 // fragment f (contiguous partial reads across the block), written to G at (r, c) and mirrored at (c, r); then
 // the C column sums.  Same fixed order (8 slab groups, then group order, in double).
@@ -455,11 +477,8 @@ __global__ __launch_bounds__(256) void gram_reduce_tri_kernel(const float* __res
   const int64_t nt = (int64_t)NF * 256;
   const int64_t j = (int64_t)blockIdx.x * 32 + o;
   double a = 0.0;
-  if (j < nt) {
-    for (int b = q; b < nb; b += 8) a += gp[(int64_t)b * nt + j];
-  } else if (j < nt + C) {
-    for (int b = q; b < nb; b += 8) a += sp[(int64_t)b * C + (j - nt)];
-  }
+  if (j < nt) a = gram_slab_sum(gp + j, nt, q, nb);
+  else if (j < nt + C) a = gram_slab_sum(sp + (j - nt), C, q, nb);
   part[q][o] = a;
   __syncthreads();
   if (q == 0) {
@@ -488,11 +507,8 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restric
   const int64_t i = (int64_t)blockIdx.x * 32 + o;
   const int64_t cc = (int64_t)C * C;
   double a = 0.0;
-  if (i < cc) {
-    for (int b = q; b < nb; b += 8) a += gp[(int64_t)b * cc + i];
-  } else if (i < cc + C) {
-    for (int b = q; b < nb; b += 8) a += sp[(int64_t)b * C + (i - cc)];
-  }
+  if (i < cc) a = gram_slab_sum(gp + i, cc, q, nb);
+  else if (i < cc + C) a = gram_slab_sum(sp + (i - cc), C, q, nb);
   part[q][o] = a;
   __syncthreads();
   if (q == 0) {
@@ -507,44 +523,93 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restric
 // Small fp32 GEMM on 32x32 output tiles: out[m][n] = sum_k A(m, k) B[k][n].
 //   AT = false: A(m, k) = a[m * lda + k]        (row-major, u = W G: A = W3 [Cout][Cin] bf16)
 //   AT = true:  A(m, k) = a[k * lda + m] scale[k] (Q = W^T diag(b) W: A = W3 read down its columns)
-// K chunks of 64 staged in LDS as fp32; 256 threads, each 1 row x 4 columns of the tile.
-template <bool AT, typename TB>
+// K chunks of KC staged in LDS as fp32 (KC = the whole K slice at the shapes used: one memory round trip),
+// any next chunk's loads in flight (registers) during the current chunk's FMAs; 256 threads, each 1 row x 4
+// columns of the tile.  A row-major A is read along k (coalesced).
+// AT with ecoef: the blocks of tile row 0 also form eout[z][n] = sum_{k in slice z} ecoef[k] B[k][n] (the data
+// grad's bias c^T W from the staged B rows: 8 k groups per column, then the groups in order).
+template <bool AT, typename TB, int KC>
 __global__ __launch_bounds__(256) void gram_mm_kernel(const uint16_t* __restrict__ a, int64_t lda,
                                                       const float* __restrict__ scale, const TB* __restrict__ b,
                                                       int64_t ldb, int K, int kslice, float* __restrict__ out,
-                                                      int64_t ldo, int64_t slab) {
+                                                      int64_t ldo, int64_t slab, const float* __restrict__ ecoef,
+                                                      float* __restrict__ eout) {
   // blockIdx.z: K slice [z * kslice, +kslice) -> out + z * slab (partials summed by the caller, in order)
-  __shared__ float As[64][33], Bs[64][32];
+  constexpr int NE = KC / 8, GK = KC / 8;  // elements per thread per operand; k per e group
+  __shared__ float As[KC][33], Bs[KC][32], Es[KC];
+  __shared__ float ep[8][32];
   const int tid = threadIdx.x, m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
   const int tm = tid >> 3, tn = (tid & 7) * 4;
   const int kb = blockIdx.z * kslice, ke = min(K, kb + kslice);
+  const bool doe = AT && ecoef != nullptr && blockIdx.y == 0;
   out += (int64_t)blockIdx.z * slab;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int k0 = kb; k0 < ke; k0 += 64) {
-    for (int e = tid; e < 64 * 32; e += 256) {
-      const int kk = e >> 5, c = e & 31, k = k0 + kk;
-      float av = 0.f, bv = 0.f;
-      if (k < ke) {
-        if constexpr (AT) av = bf2f(a[(int64_t)k * lda + m0 + c]) * (scale ? scale[k] : 1.f);
-        else av = bf2f(a[(int64_t)(m0 + c) * lda + k]);
-        if constexpr (sizeof(TB) == 2) bv = bf2f((uint16_t)b[(int64_t)k * ldb + n0 + c]);
-        else bv = (float)b[(int64_t)k * ldb + n0 + c];
+  // raw operands in flight: loads are unconditional (k clamped into the slice) so a chunk's are all
+  // outstanding together; conversion, scaling and the k < ke mask happen at the LDS store
+  uint16_t ra[NE];
+  TB rb[NE];
+  float rs[NE], rc = 0.f, re = 0.f;
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = tid + 256 * i;
+      const int kB = min(k0 + (e >> 5), ke - 1), c = e & 31;
+      rb[i] = b[(int64_t)kB * ldb + n0 + c];
+      if constexpr (AT) {
+        ra[i] = a[(int64_t)kB * lda + m0 + c];
+        rs[i] = scale ? scale[kB] : 1.f;
+      } else {
+        ra[i] = a[(int64_t)(m0 + e / KC) * lda + min(k0 + e % KC, ke - 1)];
       }
-      As[kk][c] = av;
-      Bs[kk][c] = bv;
     }
+    if (doe) rc = ecoef[min(k0 + (tid % KC), ke - 1)];
+  };
+  auto tof = [](TB v) -> float {
+    if constexpr (sizeof(TB) == 2) return bf2f((uint16_t)v);
+    else return (float)v;
+  };
+  load(kb);
+  for (int k0 = kb; k0 < ke; k0 += KC) {
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = tid + 256 * i;
+      const bool kv = k0 + (e >> 5) < ke;
+      Bs[e >> 5][e & 31] = kv ? tof(rb[i]) : 0.f;
+      if constexpr (AT) As[e >> 5][e & 31] = kv ? bf2f(ra[i]) * rs[i] : 0.f;
+      else As[e % KC][e / KC] = k0 + e % KC < ke ? bf2f(ra[i]) : 0.f;
+    }
+    if (doe && tid < KC) Es[tid] = k0 + tid < ke ? rc : 0.f;
     __syncthreads();
+    if (k0 + KC < ke) load(k0 + KC);
+    const int kn = min(KC, ke - k0);  // (a multiple of 8: K % 32 == 0)
 #pragma unroll 8
-    for (int kk = 0; kk < 64; ++kk) {
+    for (int kk = 0; kk < kn; ++kk) {
       const float av = As[kk][tm];
       const f32x4 bv = *(const f32x4*)&Bs[kk][tn];
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[e] = fmaf(av, bv[e], acc[e]);
     }
+    if (doe) {
+      const int o = tid & 31, q = tid >> 5;
+#pragma unroll
+      for (int u = 0; u < GK; ++u)
+        if (GK * q + u < kn) re = fmaf(Es[GK * q + u], Bs[GK * q + u][o], re);
+    }
     __syncthreads();
   }
 #pragma unroll
   for (int e = 0; e < 4; ++e) out[(int64_t)(m0 + tm) * ldo + n0 + tn + e] = acc[e];
+  if (doe) {
+    const int o = tid & 31, q = tid >> 5;
+    ep[q][o] = re;
+    __syncthreads();
+    if (q == 0) {
+      float t = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) t += ep[g][o];
+      eout[(int64_t)blockIdx.z * ldo + n0 + o] = t;
+    }
+  }
 }
 
 // Forward: per output channel k of conv3 (weights w [Cout][Cin] bf16, u = W G from gram_mm_kernel, G and
@@ -595,13 +660,16 @@ constexpr int KPB = 8;  // output channels per block of the backward coefficient
 // Backward, per output channel k.  part [2][Cout][RG]: row 0 = partial sums of dz3 (row 1 unused);
 // P [Cout][Cin] = dz3^T a2 (uncentred: the weight-grad GEMM); G, u = W3 G and s centred on mu (gram_partial);
 // coef3 = BN3's (scale, shift, mean, invstd).  With a' = a2 - mu, h = h' + w_k . mu (h' = w_k . a'):
-//   Sdz = sum dz,  P'[k] = P[k] - Sdz mu = dz^T a',  ms = w_k . s / M  (the centred mean, ~0)
+//   Sdz = sum dz,  w_k . P'[k] = w_k . P[k] - Sdz (w_k . mu)  (P' = dz^T a'),  ms = w_k . s / M  (centred mean, ~0)
 //   Sdzx = invstd sum dz (h - mean) = invstd (w_k . P'[k] - Sdz ms)
 //   dgamma += Sdzx, dbeta += Sdz;  a = gamma invstd, b = -a invstd Sdzx / M, c = -a Sdz / M - b mean
 //   dW3[k] += sum dh a2 = sum dh a' (sum dh = 0) = a P'[k] + b u[k] + (-a Sdz / M - b ms) s
 //   bcat[k][:] = bf16(a w_k)                              (the data grad's B rows 0 .. Cout-1)
-//   abc [3][Cout] = (a, b, c) for gram_q_kernel
-// Every term is formed from centred quantities in double: no E[h^2] - mean^2 style cancellation.
+//   abc [3][Cout] = (a, b, c) for the Q GEMM and the bias
+// Every term is formed in double from exact products: no E[h^2] - mean^2 style cancellation (w_k . P and
+// Sdz w_k . mu cancel only down to P' itself, at double's 1e-16).  Cin <= 256: thread j owns column j of the
+// block's KPB channels.  Every operand is loaded up front (one memory round trip), the 4 KPB dot products
+// and sums reduce in one LDS pass (thread (value, group) sums 32 partials in order, then 8 groups by xor).
 __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__ part, int rg, const float* __restrict__ P,
                                                        const uint16_t* __restrict__ w, const float* __restrict__ u,
                                                        const float* __restrict__ s, const float* __restrict__ coef3,
@@ -609,131 +677,124 @@ __global__ __launch_bounds__(256) void gram_bwd_kernel(const float* __restrict__
                                                        float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                        float* __restrict__ dw, uint16_t* __restrict__ bcat,
                                                        float* __restrict__ abc) {
-  __shared__ double red[3][KPB][4];
-  __shared__ double sdz_s[KPB];
-  __shared__ double kc[KPB][4];  // A, B, the s coefficient, Sdz
-  const int k0 = blockIdx.x * KPB, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const float* mu = s + Cin;
-  // pass 1: Sdz
-  double sdz[KPB];
+  constexpr int NV = 4 * KPB;  // Sdz, w.P, w.mu, w.s per channel
+  __shared__ double red[NV][8][33];
+  __shared__ double tot[NV];
+  __shared__ float kc[KPB][4];  // A, B, the s coefficient, Sdz
+  const int k0 = blockIdx.x * KPB, tid = threadIdx.x, j = tid;
+  const bool jv = j < Cin;
+  // every load unconditional (indices clamped in range, masked after): all in flight at once
+  const int jc = min(j, Cin - 1);
+  float wv[KPB], pv[KPB], uv[KPB], dwv[KPB], sp[KPB];
+  uint16_t wr[KPB];
+  const float muj0 = s[Cin + jc], sj0 = s[jc];
+  const int qc = min(tid, rg - 1);
 #pragma unroll
   for (int kk = 0; kk < KPB; ++kk) {
-    sdz[kk] = 0.0;
-    const int k = k0 + kk;
-    if (k < Cout)
-      for (int q = tid; q < rg; q += 256) sdz[kk] += part[(int64_t)k * rg + q];
+    const int64_t o = (int64_t)min(k0 + kk, Cout - 1) * Cin + jc;
+    wr[kk] = w[o];
+    pv[kk] = P[o];
+    uv[kk] = u[o];
+    dwv[kk] = dw[o];
+    sp[kk] = part[(int64_t)min(k0 + kk, Cout - 1) * rg + qc];
+  }
+  const int kt = k0 + tid, ktc = min(k0 + (tid & (KPB - 1)), Cout - 1);
+  const float cmean = coef3[2 * Cout + ktc], cinv = coef3[3 * Cout + ktc];
+  const float cgm = gamma ? gamma[ktc] : 1.f, cdg = dgamma ? dgamma[ktc] : 0.f, cdb = dbeta ? dbeta[ktc] : 0.f;
+  const float muj = jv ? muj0 : 0.f, sj = jv ? sj0 : 0.f;
+#pragma unroll
+  for (int kk = 0; kk < KPB; ++kk) {
+    const bool ok = jv && k0 + kk < Cout;
+    wv[kk] = ok ? bf2f(wr[kk]) : 0.f;
+    pv[kk] = ok ? pv[kk] : 0.f;
+    if (k0 + kk >= Cout || tid >= rg) sp[kk] = 0.f;
   }
 #pragma unroll
   for (int kk = 0; kk < KPB; ++kk) {
-    for (int o = 32; o > 0; o >>= 1) sdz[kk] += __shfl_xor(sdz[kk], o, 64);
-    if (lane == 0) red[0][kk][wid] = sdz[kk];
+    double sd = sp[kk];
+    if (k0 + kk < Cout)
+      for (int q = tid + 256; q < rg; q += 256) sd += part[(int64_t)(k0 + kk) * rg + q];
+    const double wd = wv[kk];
+    red[kk][tid >> 5][tid & 31] = sd;
+    red[KPB + kk][tid >> 5][tid & 31] = wd * pv[kk];
+    red[2 * KPB + kk][tid >> 5][tid & 31] = wd * muj;
+    red[3 * KPB + kk][tid >> 5][tid & 31] = wd * sj;
   }
   __syncthreads();
-  if (tid < KPB) {
+  {
+    const int v = tid >> 3, g = tid & 7;
     double t = 0.0;
-    for (int q = 0; q < 4; ++q) t += red[0][tid][q];
-    sdz_s[tid] = t;
-  }
-  __syncthreads();
-  // pass 2: w_k . P'[k] and w_k . s (centred)
-  double sdzh[KPB], wsv[KPB];
 #pragma unroll
-  for (int kk = 0; kk < KPB; ++kk) {
-    sdzh[kk] = 0.0;
-    wsv[kk] = 0.0;
-    const int k = k0 + kk;
-    if (k >= Cout) continue;
-    const float Sdzf = (float)sdz_s[kk];
-    for (int j = tid; j < Cin; j += 256) {
-      const float wv = bf2f(w[(int64_t)k * Cin + j]);
-      // P' = P - Sdz mu in one fp32 fma: exact product, one rounding -- an error of P's own size
-      sdzh[kk] += (double)(wv * fmaf(-Sdzf, mu[j], P[(int64_t)k * Cin + j]));
-      wsv[kk] += (double)(wv * s[j]);
-    }
-  }
+    for (int i = 0; i < 32; ++i) t += red[v][g][i];
 #pragma unroll
-  for (int kk = 0; kk < KPB; ++kk) {
-    for (int o = 32; o > 0; o >>= 1) {
-      sdzh[kk] += __shfl_xor(sdzh[kk], o, 64);
-      wsv[kk] += __shfl_xor(wsv[kk], o, 64);
-    }
-    if (lane == 0) { red[1][kk][wid] = sdzh[kk]; red[2][kk][wid] = wsv[kk]; }
+    for (int o = 1; o < 8; o <<= 1) t += __shfl_xor(t, o, 64);
+    if (g == 0) tot[v] = t;
   }
   __syncthreads();
   if (tid < KPB) {
-    const int k = k0 + tid;
-    double A = 0.0, B = 0.0, Cs = 0.0;
-    if (k < Cout) {
-      const double Sdz = sdz_s[tid];
-      double Sdzh = 0.0, Ws = 0.0;
-      for (int q = 0; q < 4; ++q) { Sdzh += red[1][tid][q]; Ws += red[2][tid][q]; }
-      const double ms = Ws / (double)M;
-      const double mean = coef3[2 * Cout + k], invstd = coef3[3 * Cout + k];
+    double A = 0.0, B = 0.0, Cs = 0.0, Sdz = 0.0;
+    if (kt < Cout) {
+      Sdz = tot[tid];
+      const double Sdzh = tot[KPB + tid] - Sdz * tot[2 * KPB + tid];
+      const double ms = tot[3 * KPB + tid] / (double)M;
+      const double mean = cmean, invstd = cinv;
       const double Sdzx = invstd * (Sdzh - Sdz * ms);
-      const double gm = gamma ? gamma[k] : 1.0;
-      if (dgamma) dgamma[k] += (float)Sdzx;
-      if (dbeta) dbeta[k] += (float)Sdz;
-      A = gm * invstd;
+      if (dgamma) dgamma[kt] = cdg + (float)Sdzx;
+      if (dbeta) dbeta[kt] = cdb + (float)Sdz;
+      A = (double)cgm * invstd;
       B = -A * invstd * Sdzx / (double)M;
       const double Cc = -A * Sdz / (double)M - B * mean;
       Cs = -A * Sdz / (double)M - B * ms;
-      abc[k] = (float)A;
-      abc[Cout + k] = (float)B;
-      abc[2 * Cout + k] = (float)Cc;
+      abc[kt] = (float)A;
+      abc[Cout + kt] = (float)B;
+      abc[2 * Cout + kt] = (float)Cc;
     }
-    kc[tid][0] = A; kc[tid][1] = B; kc[tid][2] = Cs; kc[tid][3] = k < Cout ? sdz_s[tid] : 0.0;
+    kc[tid][0] = (float)A; kc[tid][1] = (float)B; kc[tid][2] = (float)Cs; kc[tid][3] = (float)Sdz;
   }
   __syncthreads();
 #pragma unroll
   for (int kk = 0; kk < KPB; ++kk) {
     const int k = k0 + kk;
-    if (k >= Cout) continue;
-    const float A = (float)kc[kk][0], B = (float)kc[kk][1], Cs = (float)kc[kk][2], Sdz = (float)kc[kk][3];
-    for (int j = tid; j < Cin; j += 256) {
-      const int64_t o = (int64_t)k * Cin + j;
-      const float wv = bf2f(w[o]);
-      const float pc = fmaf(-Sdz, mu[j], P[o]);  // P' = dz^T (a2 - mu)
-      dw[o] += fmaf(A, pc, fmaf(B, u[o], Cs * s[j]));
-      bcat[o] = f2bf(A * wv);
-    }
+    if (!jv || k >= Cout) continue;
+    const float A = kc[kk][0], B = kc[kk][1], Cs = kc[kk][2], Sdz = kc[kk][3];
+    const int64_t o = (int64_t)k * Cin + j;
+    const float pc = fmaf(-Sdz, muj, pv[kk]);  // P' = dz^T (a2 - mu)
+    dw[o] = dwv[kk] + fmaf(A, pc, fmaf(B, uv[kk], Cs * sj));
+    bcat[o] = f2bf(A * wv[kk]);
   }
 }
 
-// Backward: the data grad's bias e[j] = sum_k c_k W3[k][j] (fp32) -- block = 32 columns x 8 k groups,
-// fixed-order combine -- and the bf16 cast of Q (gram_mm_kernel, fp32) into the B rows Cout + j'.
-__global__ __launch_bounds__(256) void gram_e_kernel(const uint16_t* __restrict__ w, const float* __restrict__ abc,
-                                                     int Cin, int Cout, const float* __restrict__ Q, int qslices,
-                                                     uint16_t* __restrict__ bcat, float* __restrict__ ebias) {
-  const int ne = (Cin + 31) / 32;
-  if ((int)blockIdx.x >= ne) {
-    // Q cast: blocks [ne, grid) own 1024-element spans of the [Cin][Cin] fp32 Q; the K-slice partials
-    // are summed in slice order (fixed, run-to-run identical)
-    const int64_t n = (int64_t)Cin * Cin, slab = n;
-    const int64_t i = ((int64_t)(blockIdx.x - ne) * 256 + threadIdx.x) * 4;
-    if (i < n) {
-      float4 acc = *(const float4*)(Q + i);
-      for (int z = 1; z < qslices; ++z) {
-        const float4 v = *(const float4*)(Q + z * slab + i);
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-      }
-      uint16_t* dst = bcat + (int64_t)Cout * Cin + i;
-      *(uint2*)dst = make_uint2(pack_bf2(acc.x, acc.y), pack_bf2(acc.z, acc.w));
-    }
-    return;
-  }
-  __shared__ float part[8][32];
-  const int o = threadIdx.x & 31, q = threadIdx.x >> 5, j = blockIdx.x * 32 + o;
-  const float* c = abc + 2 * Cout;
-  float e = 0.f;
-  if (j < Cin)
-    for (int k = q; k < Cout; k += 8) e = fmaf(c[k], bf2f(w[(int64_t)k * Cin + j]), e);
-  part[q][o] = e;
-  __syncthreads();
-  if (q == 0 && j < Cin) {
-    float t = 0.f;
+// Backward: the bf16 cast of Q (gram_mm_kernel's K-slice partials, fp32, summed in slice order) into the B
+// rows Cout + j', and (the last block) the data grad's bias e[j] = sum_k c_k W3[k][j] from gram_mm_kernel's
+// per-slice partials, in slice order.
+__global__ __launch_bounds__(256) void gram_e_kernel(int Cin, int Cout, const float* __restrict__ Q, int qslices,
+                                                     const float* __restrict__ ep, uint16_t* __restrict__ bcat,
+                                                     float* __restrict__ ebias) {
+  const int64_t n = (int64_t)Cin * Cin, slab = n;
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i < n) {
+    float4 v[8];
+    const int z0 = min(qslices, 8);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) t += part[k][o];
-    ebias[j] = t;
+    for (int z = 0; z < 8; ++z)
+      if (z < z0) v[z] = *(const float4*)(Q + z * slab + i);
+    float4 acc = v[0];
+#pragma unroll
+    for (int z = 1; z < 8; ++z)
+      if (z < z0) { acc.x += v[z].x; acc.y += v[z].y; acc.z += v[z].z; acc.w += v[z].w; }
+    for (int z = 8; z < qslices; ++z) {
+      const float4 t = *(const float4*)(Q + z * slab + i);
+      acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+    }
+    uint16_t* dst = bcat + (int64_t)Cout * Cin + i;
+    *(uint2*)dst = make_uint2(pack_bf2(acc.x, acc.y), pack_bf2(acc.z, acc.w));
+  }
+  if (blockIdx.x == gridDim.x - 1) {
+    for (int jj = threadIdx.x; jj < Cin; jj += 256) {
+      float t = 0.f;
+      for (int z = 0; z < qslices; ++z) t += ep[(int64_t)z * Cin + jj];
+      ebias[jj] = t;
+    }
   }
 }
 
@@ -796,28 +857,35 @@ extern "C" int dpe_gram_coef(const float* G, const float* s, const uint16_t* w, 
                              float* coef, float* u, hipStream_t st) {
   if (Cin % 32 || Cout % 32) return -1;
   // u = W G  (M = Cout, N = Cin, K = Cin)
-  hipLaunchKernelGGL((gram::gram_mm_kernel<false, float>), dim3(Cin / 32, Cout / 32, 1), dim3(256), 0, st, w,
-                     (int64_t)Cin, (const float*)nullptr, G, (int64_t)Cin, Cin, Cin, u, (int64_t)Cin, (int64_t)0);
+  hipLaunchKernelGGL((gram::gram_mm_kernel<false, float, 256>), dim3(Cin / 32, Cout / 32, 1), dim3(256), 0, st, w,
+                     (int64_t)Cin, (const float*)nullptr, G, (int64_t)Cin, Cin, Cin, u, (int64_t)Cin, (int64_t)0,
+                     (const float*)nullptr, (float*)nullptr);
   hipLaunchKernelGGL(gram::gram_coef_kernel, dim3((Cout + 3) / 4), dim3(256), 0, st, u, s, w, Cin, Cout, M, gamma, beta,
                      rmean, rvar, momentum, eps, coef);
   return 0;
 }
 
-// qws (the caller's scratch) >= ceil(Cout / 128) * Cin * Cin floats: Q's K-slice partials before the bf16 cast
+// qws (the caller's scratch) >= dpe_gram_bwd_ws_floats(Cin, Cout): Q's K-slice partials before the bf16 cast,
+// then the bias's per-slice partials
+extern "C" int64_t dpe_gram_bwd_ws_floats(int Cin, int Cout) {
+  return (int64_t)((Cout + 127) / 128) * ((int64_t)Cin * Cin + Cin);
+}
 extern "C" int dpe_gram_bwd(const float* part, int rg, const float* P, const uint16_t* w, const float* u, const float* s,
                             const float* coef3, const float* gamma, int Cin, int Cout, int64_t M, float* dgamma,
                             float* dbeta, float* dw, uint16_t* bcat, float* abc, float* ebias, float* qws, hipStream_t st) {
-  if (Cin % 32 || Cout % 32) return -1;
+  if (Cin % 32 || Cout % 32 || Cin > 256) return -1;
   const unsigned nb = (unsigned)((Cout + gram::KPB - 1) / gram::KPB);
   hipLaunchKernelGGL(gram::gram_bwd_kernel, dim3(nb), dim3(256), 0, st, part, rg, P, w, u, s, coef3, gamma, Cin, Cout, M,
                      dgamma, dbeta, dw, bcat, abc);
-  // Q = W^T diag(b) W  (M = N = Cin, K = Cout; A = W read down its columns, scaled by b = abc row 1)
+  // Q = W^T diag(b) W  (M = N = Cin, K = Cout; A = W read down its columns, scaled by b = abc row 1), and the
+  // bias partials c^T W from tile row 0 (c = abc row 2)
   // (split over K = Cout in 128-deep slices: the 32x32-tile grid alone is 4-64 blocks)
   const int qs = (Cout + 127) / 128;
-  hipLaunchKernelGGL((gram::gram_mm_kernel<true, uint16_t>), dim3(Cin / 32, Cin / 32, qs), dim3(256), 0, st, w,
-                     (int64_t)Cin, abc + Cout, w, (int64_t)Cin, Cout, 128, qws, (int64_t)Cin, (int64_t)Cin * Cin);
+  float* ep = qws + (int64_t)qs * Cin * Cin;
+  hipLaunchKernelGGL((gram::gram_mm_kernel<true, uint16_t, 128>), dim3(Cin / 32, Cin / 32, qs), dim3(256), 0, st, w,
+                     (int64_t)Cin, abc + Cout, w, (int64_t)Cin, Cout, 128, qws, (int64_t)Cin, (int64_t)Cin * Cin,
+                     abc + 2 * Cout, ep);
   const int ncast = (int)(((int64_t)Cin * Cin + 1023) / 1024);
-  hipLaunchKernelGGL(gram::gram_e_kernel, dim3((Cin + 31) / 32 + ncast), dim3(256), 0, st, w, abc, Cin, Cout, qws, qs,
-                     bcat, ebias);
+  hipLaunchKernelGGL(gram::gram_e_kernel, dim3(ncast), dim3(256), 0, st, Cin, Cout, qws, qs, ep, bcat, ebias);
   return 0;
 }
