@@ -624,12 +624,29 @@ __global__ __launch_bounds__(256) void gram_coef_kernel(const float* __restrict_
                                                         float eps, float* __restrict__ coef) {
   const int lane = threadIdx.x & 63, k = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (k >= Cout) return;
+  // Cin <= 256 (the Gram pass's C): every lane's <= 4 columns and the channel's scalars loaded up front,
+  // unconditionally (clamped, masked after), so they are all in flight at once
+  const int jl = min(lane, Cin - 1);
+  const float gm = gamma ? gamma[k] : 1.f, bt = beta ? beta[k] : 0.f;
+  const float rm0 = rmean ? rmean[k] : 0.f, rv0 = rmean ? rvar[k] : 0.f;
+  uint16_t wr[4];
+  float ur[4], sr[4], mr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = min(jl + 64 * i, Cin - 1);
+    wr[i] = w[(int64_t)k * Cin + j];
+    ur[i] = u[(int64_t)k * Cin + j];
+    sr[i] = s[j];
+    mr[i] = s[Cin + j];
+  }
   double e2 = 0.0, ws = 0.0, wm = 0.0;
-  for (int j = lane; j < Cin; j += 64) {
-    const double wv = bf2f(w[(int64_t)k * Cin + j]);
-    e2 += wv * u[(int64_t)k * Cin + j];
-    ws += wv * s[j];
-    wm += wv * s[Cin + j];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (lane + 64 * i >= Cin) continue;
+    const double wv = bf2f(wr[i]);
+    e2 += wv * ur[i];
+    ws += wv * sr[i];
+    wm += wv * mr[i];
   }
   for (int o = 32; o > 0; o >>= 1) {
     e2 += __shfl_xor(e2, o, 64);
@@ -642,7 +659,6 @@ __global__ __launch_bounds__(256) void gram_coef_kernel(const float* __restrict_
   double var = e2 / (double)M - ms * ms;
   if (var < 0) var = 0;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  const float gm = gamma ? gamma[k] : 1.f, bt = beta ? beta[k] : 0.f;
   const float sc = gm * invstd;
   coef[k] = sc;
   coef[Cout + k] = bt - (float)mean * sc;
@@ -650,8 +666,8 @@ __global__ __launch_bounds__(256) void gram_coef_kernel(const float* __restrict_
   coef[3 * Cout + k] = invstd;
   if (rmean) {
     const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    rmean[k] = (1.f - momentum) * rmean[k] + momentum * (float)mean;
-    rvar[k] = (1.f - momentum) * rvar[k] + momentum * (float)unbiased;
+    rmean[k] = (1.f - momentum) * rm0 + momentum * (float)mean;
+    rvar[k] = (1.f - momentum) * rv0 + momentum * (float)unbiased;
   }
 }
 
@@ -855,7 +871,7 @@ extern "C" int dpe_gram(const uint16_t* x, const float* coef, const float* scoef
 extern "C" int dpe_gram_coef(const float* G, const float* s, const uint16_t* w, int Cin, int Cout, int64_t M,
                              const float* gamma, const float* beta, float* rmean, float* rvar, float momentum, float eps,
                              float* coef, float* u, hipStream_t st) {
-  if (Cin % 32 || Cout % 32) return -1;
+  if (Cin % 32 || Cout % 32 || Cin > 256) return -1;
   // u = W G  (M = Cout, N = Cin, K = Cin)
   hipLaunchKernelGGL((gram::gram_mm_kernel<false, float, 256>), dim3(Cin / 32, Cout / 32, 1), dim3(256), 0, st, w,
                      (int64_t)Cin, (const float*)nullptr, G, (int64_t)Cin, Cin, Cin, u, (int64_t)Cin, (int64_t)0,
