@@ -56,6 +56,15 @@ DPE_DEVICE void wait_vm() {  // s_waitcnt vmcnt(N): loads, LDS-DMA and stores co
   asm volatile("" ::: "memory");
 }
 
+// Barrier for LDS data only: this wave's LDS writes complete, then s_barrier.  (__syncthreads() is a
+// workgroup-scope release + acquire, which on this target also drains vmcnt(0): inside a tile loop that
+// waits for the ring's in-flight DMAs and the previous tiles' stores.)
+DPE_DEVICE void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // K: reduction depth; WN: output columns per wave (4 waves -> 4*WN per block); NS: ring depth
 // DYN: the dynamic row-group schedule (a compile-time variant: the static kernels keep their registers)
 template <int K, int WN, int NS, int EPI, bool DYN = false>
@@ -71,11 +80,15 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
   constexpr int STG = 32 * ROWB;
   // stores outstanding per wave per tile, for the counted vmcnt below (the epilogue's operand
   // loads are consumed -- waited for -- inside the tile, so they are not outstanding here)
-  constexpr int S = 2 * NPS;
+  constexpr int S = (EPI == PW_APPLY ? 4 : 2) * NPS;  // (PW_APPLY: the y chunk and its ReLU-mask byte)
   constexpr int VM = (NS - 1) * S + (NS - 2) * P;
   static_assert(VM < 64, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) char smem[NS * TILE + 4 * STG];
-  __shared__ __attribute__((aligned(16))) float bnin[2 * K];  // in_coef: [scale | shift] of the K input channels
+  // ONE LDS object: ring, staging, in_coef's [scale | shift] of the K input channels, the claim slot.  (With a
+  // second __shared__ object the compiler cannot tell the ring DMA's LDS writes from the other accesses and
+  // drains vmcnt(0) -- the next tile's DMA -- before each tile's fragment reads.)
+  __shared__ __attribute__((aligned(16))) char smem[NS * TILE + 4 * STG + 2 * K * 4 + 16];
+  float* const bnin = (float*)(smem + NS * TILE + 4 * STG);
+  int* const claim_slot = (int*)(smem + NS * TILE + 4 * STG + 2 * K * 4);
 
   // PW_DSUM: the data grad's BN-backward partials are the sums of dz only (no pre-BN input)
   constexpr bool DG = EPI == PW_DGRAD || EPI == PW_DSUM;
@@ -91,7 +104,6 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
   // (RCCL channel blocks) takes fewer of them.  A row group's tiles, their summation order and its
   // partial column do not depend on which block runs it: results are schedule-independent, bitwise.
   const int SRG = (int)gridDim.x / nbN;  // row groups started statically (DYN: the rest are claimed)
-  __shared__ int claim_slot;
   const int n0w = nb * 4 * WN + wid * WN;  // the wave's first output channel
   const int tiles = (M + BM - 1) / BM;
   const int ch = lane % CPRW;              // the lane's 16-B chunk of each staged row
@@ -137,8 +149,8 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
   }
   auto issue = [&](int t, int slot) {
     char* dst = smem + slot * TILE;
-    const int64_t base = (int64_t)t * BM * K * 2;
-    const int valid_rows = M - t * BM;  // rows past M read as zeros (offset out of range)
+    const int64_t base = t >= 0 ? (int64_t)t * BM * K * 2 : 0;
+    const int valid_rows = t >= 0 ? M - t * BM : 0;  // rows past M (or t < 0: no tile) read as zeros
 #pragma unroll
     for (int i = 0; i < P; ++i) {
       const int q = wid * P + i, row = (q & 3) * 16 + (lane >> 2);
@@ -171,6 +183,22 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
     return ((int64_t)(n * (rh >> 1) + (h >> 1)) * (rw >> 1) + (w >> 1)) * N + nch;
   };
 
+  // Epilogue operands and outputs through buffer resources (a null operand: a 0-byte resource): every
+  // load and store of a tile is issued unconditionally -- out-of-range offsets read 0 / drop the store --
+  // so the number of memory ops between a hoisted load and its use is the same on every path and the
+  // compiler's wait for it is a counted vmcnt.  (A load or store under a branch, or the DMA issue skipped
+  // for the last tiles, made those waits vmcnt(0): each tile's epilogue then also waited for the NEXT
+  // tile's ring DMA -- the layer-2/3 data grads and applies ran at 55-77 % of their HBM roofline.)
+  constexpr uint32_t OOB = 0xfffffff0u;  // past every resource here (M N < 2^31 - 256: pw_plan)
+  const uint32_t ybytes = (uint32_t)((int64_t)M * N * 2), mbytes = (uint32_t)((int64_t)M * N / 8);
+  const uint32_t rbytes = rh > 0 ? (uint32_t)((int64_t)(M / (rh * rw)) * (rh >> 1) * (rw >> 1) * N * 2) : ybytes;
+  const __amdgpu_buffer_rsrc_t yrs = rsrc(a.y, ybytes);
+  const __amdgpu_buffer_rsrc_t rrs = rsrc(a.residual, a.residual ? rbytes : 0u);
+  const __amdgpu_buffer_rsrc_t rmrs = rsrc(a.res_mask, a.res_mask ? mbytes : 0u);
+  const __amdgpu_buffer_rsrc_t xsrs = rsrc(a.st_x, bnx ? ybytes : 0u);
+  const __amdgpu_buffer_rsrc_t smrs = rsrc(a.st_mask, (bnb && a.st_mask) ? mbytes : 0u);
+  const __amdgpu_buffer_rsrc_t obrs = rsrc(a.out_bits, (EPI == PW_APPLY && a.out_bits) ? mbytes : 0u);
+
   if (!DG && a.in_coef) {  // before the ring's first DMA (its counted waits start after this)
     for (int i = tid; i < 2 * K; i += 256) bnin[i] = a.in_coef[i];
     __syncthreads();
@@ -195,18 +223,17 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
         for (int ps = 0; ps < HN; ++ps) {
           const int m = min(m0 + 32 * hf + ps * RPP + lane / CPRW, M - 1);
           const int64_t off = (int64_t)m * N + nch;
-          if (a.residual) {
-            const int64_t ro = EPI == PW_APPLY ? off : res_off(m);
-            hrv[hf][ps] = ro >= 0 ? *(const u32x4*)(a.residual + ro) : u32x4{0u, 0u, 0u, 0u};
-          }
+          const int64_t ro = EPI == PW_APPLY ? off : res_off(m);
+          // (absent operands skipped -- uniform branches; the explicit wait before the epilogue covers every
+          // path.  A null mask's 0xff is selected at the use.)
+          if (a.residual) hrv[hf][ps] = __builtin_amdgcn_raw_buffer_load_b128(rrs, ro >= 0 ? (uint32_t)(ro * 2) : OOB, 0, 0);
           if constexpr (DG) {
-            hrmb[hf][ps] = a.res_mask ? (uint32_t)a.res_mask[off >> 3] : 0xffu;
-            if (bnx) hxv[hf][ps] = *(const u32x4*)(a.st_x + off);
-            hsmb[hf][ps] = (bnb && a.st_mask) ? (uint32_t)a.st_mask[off >> 3] : 0xffu;
+            if (a.res_mask) hrmb[hf][ps] = __builtin_amdgcn_raw_buffer_load_b8(rmrs, (uint32_t)(off >> 3), 0, 0);
+            if (bnx) hxv[hf][ps] = __builtin_amdgcn_raw_buffer_load_b128(xsrs, (uint32_t)(off * 2), 0, 0);
+            if (bnb && a.st_mask) hsmb[hf][ps] = __builtin_amdgcn_raw_buffer_load_b8(smrs, (uint32_t)(off >> 3), 0, 0);
           }
         }
     }
-    if (nxt_tile >= 0) issue(nxt_tile, nxt_slot);
     if (!DG && a.in_coef) {
       // BN + ReLU of the producer applied to the landed tile ONCE, cooperatively in LDS (every wave reads
       // the whole tile as its MFMA operand: transformed in each wave's registers it was done four times
@@ -230,8 +257,10 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
         for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], sc8[e], sh8[e]), 0.f);
         *pch = pack8(f);
       }
-      __syncthreads();
+      lds_barrier();
     }
+    // (unconditional: past the stream's end a zero-filled DMA into the free slot -- see the resources above)
+    issue(nxt_tile, nxt_slot);
     const char* img = smem + cur_slot * TILE;
     f32x4 acc[MI][NI];
 #pragma unroll
@@ -263,8 +292,8 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
         for (int ps = 0; ps < HN; ++ps) {
           rv[ps] = hrv[hf][ps];
           xv[ps] = hxv[hf][ps];
-          rmb[ps] = hrmb[hf][ps];
-          smb[ps] = hsmb[hf][ps];
+          rmb[ps] = a.res_mask ? hrmb[hf][ps] : 0xffu;
+          smb[ps] = (bnb && a.st_mask) ? hsmb[hf][ps] : 0xffu;
         }
       } else if constexpr (DG) {
 #pragma unroll
@@ -291,6 +320,10 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
           *(u32x2*)(stg + (16 * mh + li) * ROWB + (16 * ni + 4 * g) * 2) = pk;
         }
       }
+      // the hoisted epilogue operands (both halves): everything but the P ring DMAs issued after them has
+      // landed.  (The DMA issue is unconditional, so P younger ops exist on every path; with this counted
+      // wait the compiler needs no wait of its own for the conditionally loaded operands.)
+      if (HOIST && hf == 0) wait_vm<P>();
 #pragma unroll
       for (int ps = 0; ps < NPS; ++ps) {
         const int row = ps * RPP + lane / CPRW;
@@ -311,7 +344,10 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
             f[e] = fmaxf(t, 0.f);
           }
           v = pack8(f);
-          if (valid && a.out_bits) a.out_bits[((int64_t)m * N + nch) >> 3] = relu_mask_byte(v);
+          if constexpr (HOIST)
+            __builtin_amdgcn_raw_buffer_store_b8(relu_mask_byte(v), obrs, valid ? (uint32_t)(((int64_t)m * N + nch) >> 3) : OOB, 0, 0);
+          else if (valid && a.out_bits)
+            a.out_bits[((int64_t)m * N + nch) >> 3] = relu_mask_byte(v);
         } else if constexpr (EPI == PW_FWD) {
           // statistics of the stored (rounded) values (rows past M: zeros, or relu(shift) terms
           // with in_coef -- masked)
@@ -352,7 +388,8 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
             }
           }
         }
-        if (valid) *(u32x4*)(a.y + (int64_t)m * N + nch) = v;
+        if constexpr (HOIST) __builtin_amdgcn_raw_buffer_store_b128(v, yrs, valid ? (uint32_t)(((int64_t)m * N + nch) * 2) : OOB, 0, 0);
+        else if (valid) *(u32x4*)(a.y + (int64_t)m * N + nch) = v;
       }
     }
   };
@@ -395,6 +432,10 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
     asm volatile("" ::: "memory");
   };
 
+  // the preamble's loads (weights, coefficients -- some under uniform branches) retired here, before the
+  // ring starts: left pending, the compiler's first-use waits for them sat inside the tile loop as vmcnt(0),
+  // which also waits for the ring's in-flight DMAs every tile
+  wait_vm<0>();
   if constexpr (!DYN) {
     // static: this row group's tiles rg, rg + RG, ...
     const int nt = rg < tiles ? (tiles - 1 - rg) / RG + 1 : 0;
@@ -443,9 +484,9 @@ __global__ __launch_bounds__(256, (K == 64 && EPI == PW_FWD) ? 3 : 2) void pw_st
       const int jpub = ntc - (NS + 1), jcl = max(0, jpub - 7);
       if (jc == jcl && tid == 0)
         claimv = SRG + (int)__hip_atomic_fetch_add(a.sched + nb * 256, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (jc == jpub && tid == 0) claim_slot = claimv;  // published by the next barrier
+      if (jc == jpub && tid == 0) *claim_slot = claimv;  // published by the next barrier
       if (jc == jpub + 1) {
-        const int c = __builtin_amdgcn_readfirstlane(claim_slot);
+        const int c = __builtin_amdgcn_readfirstlane(*claim_slot);
         nu = c < RG ? c : -1;
       }
       const int t = next_issue();
@@ -495,8 +536,9 @@ __global__ __launch_bounds__(64 * (K2 / 16), K2 == 64 ? 2 : 1) void pw_cat_kerne
   constexpr int S = 1;                        // stores per lane per tile (32 rows x 2 chunks / 64 lanes)
   constexpr int VM = (NS - 1) * S + (NS - 2) * P;
   static_assert(VM < 64, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) char smem[NS * TILE + KC2 * IMG + NW * STG];
-  __shared__ __attribute__((aligned(16))) float bnin[2 * K2];
+  // one LDS object (see pw_stream_kernel): ring, a2 image, staging, BN2's [scale | shift]
+  __shared__ __attribute__((aligned(16))) char smem[NS * TILE + KC2 * IMG + NW * STG + 2 * K2 * 4];
+  float* const bnin = (float*)(smem + NS * TILE + KC2 * IMG + NW * STG);
   char* const a2img = smem + NS * TILE;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -570,6 +612,7 @@ __global__ __launch_bounds__(64 * (K2 / 16), K2 == 64 ? 2 : 1) void pw_cat_kerne
   for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
   const int rgb = blockIdx.x;
   const int nt = rgb < tiles ? (tiles - 1 - rgb) / RG + 1 : 0;
+  wait_vm<0>();  // the preamble's loads retired before the ring starts (see pw_stream_kernel)
   __syncthreads();  // bnin
 #pragma unroll
   for (int j = 0; j < NS - 1; ++j)
@@ -596,7 +639,7 @@ __global__ __launch_bounds__(64 * (K2 / 16), K2 == 64 ? 2 : 1) void pw_cat_kerne
       for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], sc8[e], sh8[e]), 0.f);
       *(u32x4*)(a2img + off) = pack8(f);
     }
-    __syncthreads();
+    lds_barrier();
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
@@ -757,7 +800,7 @@ static PwPlan pw_plan(int64_t M, int64_t N, int64_t K, int epi) {
   if (epi != PW_FWD && epi != PW_DGRAD && epi != PW_APPLY && epi != PW_DSUM) return {0, 0};
   const int bnb = 4 * pw_wn((int)K, epi);
   if (N % bnb || N < 2 * K) return {0, 0};  // write-heavy shapes only (N >= 2K)
-  if (M * K * 2 >= (1ll << 31) - 4096 || M * N >= (1ll << 31)) return {0, 0};
+  if (M * K * 2 >= (1ll << 31) - 4096 || M * N >= (1ll << 31) - 256) return {0, 0};
   const int64_t tiles = (M + pw::BM - 1) / pw::BM;
   const int64_t nbN = N / bnb;
   const int reserve = dpe_cu_reserve();
