@@ -61,6 +61,23 @@ DPE_DEVICE uint8_t relu_mask_byte(const u32x4& pk) {
   return (uint8_t)b;
 }
 
+// Barrier for LDS data only: this wave's LDS ops complete, then s_barrier.  __syncthreads() is a
+// workgroup-scope release + acquire, which on this target also drains vmcnt(0) -- inside a streaming
+// loop that waits for every load / DMA prefetched for later rows or tiles and for the earlier stores.
+DPE_DEVICE void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Raw buffer resource over [base, base + bytes): an offset past `bytes` reads zeros / drops the store, so
+// a streaming kernel's loads and stores can be issued unconditionally (a load or store under a
+// lane-divergent branch makes the compiler's later waits vmcnt(0): the op count differs between paths).
+constexpr uint32_t BUF_OOB = 0xfffffff0u;  // past any resource of < 0xffffff00 bytes
+DPE_DEVICE __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
 DPE_DEVICE float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -56,15 +56,6 @@ DPE_DEVICE void wait_vm() {  // s_waitcnt vmcnt(N): loads, LDS-DMA and stores co
   asm volatile("" ::: "memory");
 }
 
-// Barrier for LDS data only: this wave's LDS writes complete, then s_barrier.  (__syncthreads() is a
-// workgroup-scope release + acquire, which on this target also drains vmcnt(0): inside a tile loop that
-// waits for the ring's in-flight DMAs and the previous tiles' stores.)
-DPE_DEVICE void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
 // K: reduction depth; WN: output columns per wave (4 waves -> 4*WN per block); NS: ring depth
 // DYN: the dynamic row-group schedule (a compile-time variant: the static kernels keep their registers)
 template <int K, int WN, int NS, int EPI, bool DYN = false>

@@ -84,11 +84,18 @@ __global__ __launch_bounds__(256, 2) void conv3x3_rows_kernel(RowArgs p) {
   int n = 0;
   int64_t img = 0;
   const int nch = W * 8;
+  // every global load / store through a buffer resource, issued unconditionally (out-of-range rows and
+  // chunks: an offset past the resource -> zeros / dropped), so the compiler's waits stay counted and the
+  // row prefetch stays in flight (the host checks N H W 64 2 < 0xffffff00)
+  const uint32_t xbytes = (uint32_t)((int64_t)p.N * H * W * CO * 2);
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(p.x, xbytes), yr = buf_rsrc(p.y, xbytes);
+  const __amdgpu_buffer_rsrc_t sxr = buf_rsrc(p.st_x, BNB ? xbytes : 0u);
   auto load_row = [&](int ih, u32x4 (&v)[2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int c = tid + 256 * u;
-      v[u] = (c < nch && (unsigned)ih < (unsigned)H) ? *(const u32x4*)(p.x + img + (int64_t)ih * W * 64 + c * 8) : zero16();
+      const bool ok = c < nch && (unsigned)ih < (unsigned)H;
+      v[u] = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (uint32_t)((img + (int64_t)ih * W * 64 + c * 8) * 2) : BUF_OOB, 0, 0);
     }
   };
   // INBN: this thread's input channels are 8 (tid & 7) .. +7 for every row (256 % 8 == 0)
@@ -117,17 +124,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_rows_kernel(RowArgs p) {
   };
   // store-phase channel chunk of this thread and its BN coefficients
   const int sc = tid & 7;
-  float s[8], ss[8], bsc[8], bsh[8], bmu[8];
+  float s[8], ss[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     s[e] = 0.f;
     ss[e] = 0.f;
-    if constexpr (BNB) {
-      bsc[e] = p.st_coef[sc * 8 + e];
-      bsh[e] = p.st_coef[CO + sc * 8 + e];
-      bmu[e] = p.st_coef[2 * CO + sc * 8 + e];
-    }
   }
+  // BNB: [scale | shift | mean] x 64 channels in LDS, read per stored chunk (24 registers held across
+  // the row loop spilled beside the filter fragments and the two prefetch sets)
+  __shared__ __attribute__((aligned(16))) float bcs[BNB ? 3 * CO : 4];
+  if constexpr (BNB)
+    if (tid < 3 * CO) bcs[tid] = p.st_coef[tid];
   // this wave's pixel fragments: 32 mh + 16 i + lm (rows >= W compute on zero pixels, never stored)
   const int nfr = min(2, max(0, (W - 32 * mh + 15) / 16));
 
@@ -152,12 +159,23 @@ __global__ __launch_bounds__(256, 2) void conv3x3_rows_kernel(RowArgs p) {
     write_row(oh_beg, t1);
     write_row(oh_beg + 1, t2);
   }
-  u32x4 pf0[2], pf1[2];
+  u32x4 pf0[2], pf1[2];  // input rows oh + 2, oh + 3 (two sets: a prefetch is first used two rows later)
   load_row(oh_beg + 2, pf0);
   load_row(oh_beg + 3, pf1);
   __syncthreads();
 
-  for (int oh = oh_beg; oh < oh_end; ++oh) {
+  auto row = [&](const int oh, u32x4 (&pfA)[2]) {
+    // the store phase's pre-BN input (BNB) first: its latency overlaps the MFMAs, and it is older than
+    // this row's prefetch, so waiting for it leaves the prefetch in flight
+    const int64_t rowoff = ((int64_t)n * H + oh) * W * CO;
+    u32x4 xv[2];
+    uint32_t bo[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int px = (tid >> 3) + 32 * k;
+      bo[k] = px < W ? (uint32_t)((rowoff + px * CO + sc * 8) * 2) : BUF_OOB;
+      if constexpr (BNB) xv[k] = __builtin_amdgcn_raw_buffer_load_b128(sxr, bo[k], 0, 0);
+    }
     f32x4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -179,11 +197,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_rows_kernel(RowArgs p) {
         }
       }
     }
-    // input row oh + 2 into the slot of row oh - 2 (free); prefetch row oh + 4
-    write_row(oh + 2, pf0);
-    pf0[0] = pf1[0];
-    pf0[1] = pf1[1];
-    load_row(oh + 4, pf1);
+    // input row oh + 2 into the slot of row oh - 2 (free); prefetch row oh + 4 into the same registers
+    write_row(oh + 2, pfA);
+    load_row(oh + 4, pfA);
     // stage: acc[i][j][e] = pixel 32 mh + 16 i + lm, channel 32 nh + 16 j + 4 kc + e
     char* ob = obuf + (oh & 1) * OBUF;
 #pragma unroll
@@ -199,37 +215,45 @@ __global__ __launch_bounds__(256, 2) void conv3x3_rows_kernel(RowArgs p) {
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     // store: thread t -> chunk t & 7 of pixels t / 8 and t / 8 + 32
-    const int64_t rowoff = ((int64_t)n * H + oh) * W * CO;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int px = (tid >> 3) + 32 * k;
-      if (px < W) {
-        const int64_t off = rowoff + px * CO + sc * 8;
-        const u32x4 v = *(const u32x4*)(ob + px * OROW + sc * 16);
-        u32x4 xv;
-        if constexpr (BNB) xv = *(const u32x4*)(p.st_x + off);
-        *(u32x4*)(p.y + off) = v;
-        if (p.stats) {
-          float f[8];
-          unpack8(v, f);
-          if constexpr (BNB) {  // (sum dz, sum dz * (x - mean)), dz = f * relu'(x * scale + shift)
-            float xf[8];
-            unpack8(xv, xf);
+      const u32x4 v = *(const u32x4*)(ob + px * OROW + sc * 16);
+      __builtin_amdgcn_raw_buffer_store_b128(v, yr, bo[k], 0, 0);
+      if (p.stats && px < W) {
+        float f[8];
+        unpack8(v, f);
+        if constexpr (BNB) {  // (sum dz, sum dz * (x - mean)), dz = f * relu'(x * scale + shift)
+          float xf[8];
+          unpack8(xv[k], xf);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float dz = fmaf(xf[e], bsc[e], bsh[e]) > 0.f ? f[e] : 0.f;
+          for (int h4 = 0; h4 < 2; ++h4) {
+            const f32x4 k0 = *(const f32x4*)(bcs + sc * 8 + 4 * h4), k1 = *(const f32x4*)(bcs + CO + sc * 8 + 4 * h4);
+            const f32x4 k2 = *(const f32x4*)(bcs + 2 * CO + sc * 8 + 4 * h4);
+#pragma unroll
+            for (int e4 = 0; e4 < 4; ++e4) {
+              const int e = 4 * h4 + e4;
+              const float dz = fmaf(xf[e], k0[e4], k1[e4]) > 0.f ? f[e] : 0.f;
               s[e] += dz;
-              ss[e] += dz * (xf[e] - bmu[e]);
+              ss[e] += dz * (xf[e] - k2[e4]);
             }
-          } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) { s[e] += f[e]; ss[e] = fmaf(f[e], f[e], ss[e]); }
           }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { s[e] += f[e]; ss[e] = fmaf(f[e], f[e], ss[e]); }
         }
       }
     }
+  };
+  // the loop's only backedge follows the second row (a conditional second row before a shared latch
+  // merged two paths with different load counts: the compiler's waits became vmcnt(0)); oh_beg < oh_end
+  for (int oh = oh_beg;; oh += 2) {
+    row(oh, pf0);
+    if (oh + 1 >= oh_end) break;
+    row(oh + 1, pf1);
+    if (oh + 2 >= oh_end) break;
   }
   }  // segments
   if (p.stats) {
@@ -316,12 +340,16 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_rows_kernel(const uint16_t* _
 
   for (int i = tid; i < LDS / 16; i += 256) *(u32x4*)(smem + i * 16) = zero16();
 
+  // buffer loads issued unconditionally (see conv3x3_rows_kernel)
+  const uint32_t tbytes = (uint32_t)((int64_t)N * H * W * 64 * 2);
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(x, tbytes), dr = buf_rsrc(dy, tbytes);
   auto load = [&](const uint16_t* src, int row, u32x4 (&v)[2]) {
+    const __amdgpu_buffer_rsrc_t r = src == x ? xr : dr;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int c = tid + 256 * u;
-      v[u] = (c < nch && (unsigned)row < (unsigned)H) ? *(const u32x4*)(src + img + (int64_t)row * W * 64 + c * 8)
-                                                      : zero16();
+      const bool ok = c < nch && (unsigned)row < (unsigned)H;
+      v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, ok ? (uint32_t)((img + (int64_t)row * W * 64 + c * 8) * 2) : BUF_OOB, 0, 0);
     }
   };
   auto put = [&](char* sl, int px0, const u32x4 (&v)[2]) {  // chunk c -> pixel row px0 + c / 8
@@ -381,7 +409,7 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_rows_kernel(const uint16_t* _
     put(dbuf + ((oh + 1) & 1) * DSLOT, 0, pdA);
     load(x, oh + 4, pxA);
     load(dy, oh + 3, pdA);
-    __syncthreads();
+    lds_barrier();  // (LDS only: __syncthreads would drain the prefetch just issued)
   };
   // The block owns output rows [r0, r1) of the N*H rows (image-major), one segment per image it
   // touches (dy rows outside the segment are never stepped on, so no row is counted twice).
@@ -411,9 +439,11 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_rows_kernel(const uint16_t* _
     load(dy, oh_beg + 1, pd0);
     load(dy, oh_beg + 2, pd1);
     __syncthreads();
-    for (int oh = oh_beg; oh < oh_end; oh += 2) {
+    for (int oh = oh_beg;; oh += 2) {  // (one backedge, after the second step: see conv3x3_rows_kernel)
       step(oh, px0, pd0);
-      if (oh + 1 < oh_end) step(oh + 1, px1, pd1);
+      if (oh + 1 >= oh_end) break;
+      step(oh + 1, px1, pd1);
+      if (oh + 2 >= oh_end) break;
     }
   }
   // acc[m][t][e]: co = 16 m + (lane & 15), ci = 16 w + 4 (lane >> 4) + e, tap t
@@ -495,7 +525,7 @@ int rows_grid(int N, int H) {
 // Blocks of the launch for an [N, H, W, 64] input (0: outside the kernel's envelope).  Depends on the
 // CU budget in force: compute it once per launch and pass it to dpe_conv3x3_rows_launch.
 extern "C" int dpe_conv3x3_rows_blocks(int N, int H, int W) {
-  if (N <= 0 || H < 2 || W < 1 || W > 64) return 0;
+  if (N <= 0 || H < 2 || W < 1 || W > 64 || (int64_t)N * H * W * 128 >= 0xffffff00ll) return 0;
   return rows_grid(N, H);
 }
 
@@ -506,7 +536,9 @@ extern "C" int dpe_conv3x3_rows_blocks(int N, int H, int W) {
 extern "C" int dpe_conv3x3_rows_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const uint16_t* st_x,
                                        const float* st_coef, int N, int H, int W, int nb, int bnb, const float* in_coef,
                                        hipStream_t st) {
-  if (nb <= 0 || N <= 0 || H < 2 || W < 1 || W > 64 || (bnb && (!stats || !st_x || !st_coef)) || (bnb && in_coef)) return -1;
+  if (nb <= 0 || N <= 0 || H < 2 || W < 1 || W > 64 || (bnb && (!stats || !st_x || !st_coef)) || (bnb && in_coef) ||
+      (int64_t)N * H * W * 128 >= 0xffffff00ll)
+    return -1;
   dpe::rowconv::RowArgs a{x, w, y, stats, st_x, st_coef, N, H, W, in_coef};
   if (bnb) hipLaunchKernelGGL(dpe::rowconv::conv3x3_rows_kernel<true>, dim3(nb), dim3(256), 0, st, a);
   else if (in_coef) hipLaunchKernelGGL((dpe::rowconv::conv3x3_rows_kernel<false, true>), dim3(nb), dim3(256), 0, st, a);
@@ -516,7 +548,7 @@ extern "C" int dpe_conv3x3_rows_launch(const uint16_t* x, const uint16_t* w, uin
 
 // Blocks of the weight-grad launch (0: outside the envelope); as dpe_conv3x3_rows_blocks.
 extern "C" int dpe_wgrad3x3_rows_blocks(int N, int H, int W) {
-  if (N <= 0 || H < 1 || W < 1 || W > 64) return 0;
+  if (N <= 0 || H < 1 || W < 1 || W > 64 || (int64_t)N * H * W * 128 >= 0xffffff00ll) return 0;
   return rows_grid(N, H);
 }
 namespace {
@@ -535,7 +567,7 @@ extern "C" int64_t dpe_wgrad3x3_rows_scratch(int nb) {
 // shift] of 64 channels), applied on load.
 extern "C" int dpe_wgrad3x3_rows_launch(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H,
                                         int W, int nb, float alpha, const float* in_coef, hipStream_t st) {
-  if (nb <= 0 || N <= 0 || H < 1 || W < 1 || W > 64 || !scratch) return -1;
+  if (nb <= 0 || N <= 0 || H < 1 || W < 1 || W > 64 || !scratch || (int64_t)N * H * W * 128 >= 0xffffff00ll) return -1;
   using namespace dpe::rowconv::wg;
   if (in_coef) hipLaunchKernelGGL(wgrad3x3_rows_kernel<true>, dim3(nb), dim3(256), 0, st, x, dy, scratch, N, H, W, in_coef);
   else hipLaunchKernelGGL(wgrad3x3_rows_kernel<false>, dim3(nb), dim3(256), 0, st, x, dy, scratch, N, H, W, in_coef);

@@ -18,6 +18,7 @@
 // One barrier per output row.  Same K order as the implicit GEMM (two taps per K-step), so the
 // output is bitwise identical to it.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -63,9 +64,15 @@ __global__ __launch_bounds__(256, 3) void stem_conv_kernel(const uint16_t* __res
 
   // one input row = W pixels x 32 B = up to 224 16-B chunks: thread t < 2W owns chunk t
   const int64_t img = (int64_t)n * H * W * 16;
+  // global loads / stores through buffer resources, issued unconditionally (out-of-range: an offset past
+  // the resource), so the compiler's waits stay counted and the row prefetch stays in flight (host:
+  // N H W 128 < 0xffffff00)
+  const int NI = gridDim.x / parts;
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(x, (uint32_t)((int64_t)NI * H * W * 32));
+  const __amdgpu_buffer_rsrc_t yr = buf_rsrc(y, (uint32_t)((int64_t)NI * H * W * CO * 2));
   auto load_row = [&](int ih) -> u32x4 {
-    if (tid < 2 * W && (unsigned)ih < (unsigned)H) return *(const u32x4*)(x + img + ((int64_t)ih * W) * 16 + tid * 8);
-    return zero16();
+    const bool ok = tid < 2 * W && (unsigned)ih < (unsigned)H;
+    return __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (uint32_t)((img + (int64_t)ih * W * 16 + tid * 8) * 2) : BUF_OOB, 0, 0);
   };
   auto write_row = [&](int ih, const u32x4& v) {  // input row ih -> slot (ih + 2) % 5, pixel iw + 2
     if (tid < 2 * W) *(u32x4*)(ring + ((ih + 2 + 5 * 4) % NSLOT) * SLOT + 64 + tid * 16) = v;
@@ -81,7 +88,9 @@ __global__ __launch_bounds__(256, 3) void stem_conv_kernel(const uint16_t* __res
   for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
   const int sc = tid & 7;  // this thread's 8-channel chunk in the store phase
 
-  for (int oh = oh_beg; oh < oh_end; ++oh) {
+  // one output row; pfA holds input row oh + 2 and is refilled with row oh + 4 (two register sets, rows
+  // alternate: a prefetch is first used two rows after it was issued)
+  auto row = [&](const int oh, u32x4& pfA) {
     f32x4 acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -103,9 +112,8 @@ __global__ __launch_bounds__(256, 3) void stem_conv_kernel(const uint16_t* __res
       }
     }
     // input row oh + 2 into the slot of row oh - 3 (no longer read); prefetch row oh + 4
-    write_row(oh + 2, pf0);
-    pf0 = pf1;
-    pf1 = load_row(oh + 4);
+    write_row(oh + 2, pfA);
+    pfA = load_row(oh + 4);
     // stage the output row: acc[i][j][e] = pixel (mh*4+i)*16 + lm, channel 32 nh + 16 j + 4 kc + e
     char* ob = obuf + (oh & 1) * OBUF;
 #pragma unroll
@@ -121,21 +129,27 @@ __global__ __launch_bounds__(256, 3) void stem_conv_kernel(const uint16_t* __res
         }
       }
     }
-    __syncthreads();
+    lds_barrier();  // (LDS only: __syncthreads would drain the prefetch just issued)
     // store: thread t -> chunk t & 7 of pixels t / 8 + 32 k (whole 128-B pixel rows per 8 lanes)
-    uint16_t* yrow = y + ((int64_t)n * H + oh) * W * CO;
+    const int64_t yrow = ((int64_t)n * H + oh) * W * CO;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int px = (tid >> 3) + 32 * k;
+      const u32x4 v = *(const u32x4*)(ob + min(px, 111) * OROW + sc * 16);
+      __builtin_amdgcn_raw_buffer_store_b128(v, yr, px < W ? (uint32_t)((yrow + px * CO + sc * 8) * 2) : BUF_OOB, 0, 0);
       if (px < W) {
-        const u32x4 v = *(const u32x4*)(ob + px * OROW + sc * 16);
-        *(u32x4*)(yrow + px * CO + sc * 8) = v;
         float f[8];
         unpack8(v, f);
 #pragma unroll
         for (int e = 0; e < 8; ++e) { s[e] += f[e]; ss[e] = fmaf(f[e], f[e], ss[e]); }
       }
     }
+  };
+  for (int oh = oh_beg;; oh += 2) {  // (one backedge, after the second row: see stem_wgrad_kernel)
+    row(oh, pf0);
+    if (oh + 1 >= oh_end) break;
+    row(oh + 1, pf1);
+    if (oh + 2 >= oh_end) break;
   }
   if (stats) {
     // reduce over the 32 threads of each chunk: lanes sc + 8 t (xor 8, 16, 32), then 4 waves via LDS
@@ -261,9 +275,13 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const uint16_t* __re
 
   for (int i = tid; i < LDS / 16; i += 256) *(u32x4*)(smem + i * 16) = zero16();
 
+  // global loads through buffer resources, issued unconditionally (see stem_conv_kernel)
+  const int NI = gridDim.x / halves;
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(x, (uint32_t)((int64_t)NI * H * W * 32));
+  const __amdgpu_buffer_rsrc_t dr = buf_rsrc(FUSED ? (const void*)fb.h : (const void*)dy, (uint32_t)((int64_t)NI * H * W * 128));
   auto loadx = [&](int ih) -> u32x4 {
-    if (tid < xch && (unsigned)ih < (unsigned)H) return *(const u32x4*)(x + ximg + (int64_t)ih * W * 16 + tid * 8);
-    return zero16();
+    const bool ok = tid < xch && (unsigned)ih < (unsigned)H;
+    return __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (uint32_t)((ximg + (int64_t)ih * W * 16 + tid * 8) * 2) : BUF_OOB, 0, 0);
   };
   auto putx = [&](int ih, const u32x4& v) {  // chunk t -> pixel t / 2 (slot row + 2), half t & 1
     if (tid < xch) *(u32x4*)(ring + ((ih + 2 + 5 * 4) % NSLOT) * XSLOT + x_off((tid >> 1) + 2) + (tid & 1) * 16) = v;
@@ -274,24 +292,28 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const uint16_t* __re
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int c = tid + 256 * u;
-      v[u] = (c < dch && oh < H) ? *(const u32x4*)(dsrc + dimg + (int64_t)oh * W * 64 + c * 8) : zero16();
+      const bool ok = c < dch && oh < H;
+      v[u] = __builtin_amdgcn_raw_buffer_load_b128(dr, ok ? (uint32_t)((dimg + (int64_t)oh * W * 64 + c * 8) * 2) : BUF_OOB, 0, 0);
     }
   };
   // FUSED: pooled row i (dy and argmax bytes) -> registers -> LDS slot i & 1
   const int OH = H >> 1, OW = W >> 1;
   const int64_t pimg = (int64_t)n * OH * OW * 64;
   const int pdch = OW * 8, pich = OW * 4;  // 16-B chunks of a pooled dy / idx row
+  const __amdgpu_buffer_rsrc_t pr = buf_rsrc(FUSED ? (const void*)fb.dyp : (const void*)x, FUSED ? (uint32_t)((int64_t)NI * OH * OW * 128) : 0u);
+  const __amdgpu_buffer_rsrc_t ir = buf_rsrc(FUSED ? (const void*)fb.idx : (const void*)x, FUSED ? (uint32_t)((int64_t)NI * OH * OW * 64) : 0u);
   auto loadp = [&](int i, u32x4 (&v)[3]) {
     if constexpr (FUSED) {
-      const bool ok = i < OH;
+      const bool ok = i < OH;  // (block-uniform)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int c = tid + 256 * u;
-        v[u] = (ok && c < pdch) ? *(const u32x4*)(fb.dyp + pimg + (int64_t)i * OW * 64 + c * 8) : zero16();
+        v[u] = __builtin_amdgcn_raw_buffer_load_b128(pr, (ok && c < pdch) ? (uint32_t)((pimg + (int64_t)i * OW * 64 + c * 8) * 2) : BUF_OOB, 0, 0);
       }
-      // an out-of-range pooled row: argmax 0xff never matches a tap
-      v[2] = (ok && tid < pich) ? *(const u32x4*)(fb.idx + pimg + (int64_t)i * OW * 64 + tid * 16)
-                                : u32x4{~0u, ~0u, ~0u, ~0u};
+      // an out-of-range pooled row: argmax 0xff never matches a tap (selected after the load: the load
+      // itself stays unconditional)
+      const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(ir, (ok && tid < pich) ? (uint32_t)(pimg + (int64_t)i * OW * 64 + tid * 16) : BUF_OOB, 0, 0);
+      v[2] = ok ? t : u32x4{~0u, ~0u, ~0u, ~0u};
     }
   };
   auto putp = [&](int i, const u32x4 (&v)[3]) {
@@ -424,7 +446,11 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const uint16_t* __re
   // rows oh + 4 / oh + 3 (the loop runs two rows per trip with two buffer sets, so a prefetch is
   // first waited on two rows after it was issued -- a register copy between the sets would wait
   // after one)
-  auto step = [&](int oh, u32x4& pxA, u32x4 (&pdA)[4]) {
+  // ODD: oh is odd (the block's first row is even: host check), a compile-time tag so the pooled-row
+  // refill below is unconditional code in the odd step (a load under a run-time branch made the
+  // compiler's later waits vmcnt(0), draining the row prefetch)
+  auto step = [&](int oh, u32x4& pxA, u32x4 (&pdA)[4], auto odd_tag) {
+    constexpr bool ODD = decltype(odd_tag)::value;
     const char* ds = dbuf + (oh & 1) * DSLOT;
     // input row oh - 2 + w sits in slot (oh + w) % 5; output pixel ow reads slot row ow + dx
     const char* xs = ring + ((oh + w) % NSLOT) * XSLOT;
@@ -447,21 +473,19 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const uint16_t* __re
       // was last read by dY row 2q - 1 (previous step, behind its barrier) and no dY row computed later needs
       // it: pooled row q + 1 (prefetched in pp) goes into its slot now, read first by dY row 2q + 1 (next
       // step, behind this step's barrier).
-      if (((oh + 1) & 1) == 0) {
+      if constexpr (ODD) {  // q + 1 > p0 + 1 always holds here: rows p0, p0 + 1 were placed before the loop
         const int q = (oh + 1) >> 1;
-        if (q + 1 > p0 + 1) {  // (rows p0, p0 + 1 were placed before the loop)
-          putp(q + 1, pp);
-          loadp(q + 2, pp);
-        }
+        putp(q + 1, pp);
+        loadp(q + 2, pp);
       }
     }
     pxA = loadx(oh + 4);
     loadd(oh + 3, pdA);
-    __syncthreads();
+    lds_barrier();  // (LDS only: __syncthreads would drain the prefetch just issued)
   };
   for (int oh = oh0; oh < oh1; oh += 2) {
-    step(oh, px0, pd0);
-    if (oh + 1 < oh1) step(oh + 1, px1, pd1);
+    step(oh, px0, pd0, std::false_type{});
+    if (oh + 1 < oh1) step(oh + 1, px1, pd1, std::true_type{});
   }
   // acc[m][t][e]: o = 16 m + (lane & 15), c = 4 (lane >> 4) + e, tap (dy = w, dx = t)
   float* pb = part + (int64_t)blockIdx.x * PART;
@@ -496,7 +520,7 @@ __global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __r
 
 // Blocks of the launch for an [N, H, W, 16] s2d input (0: outside the kernel's envelope).
 extern "C" int dpe_stem_blocks(int N, int H, int W) {
-  if (N <= 0 || H < 3 || W < 97 || W > 112) return 0;  // 7 pixel fragments, 4 + 3 per wave pair
+  if (N <= 0 || H < 3 || W < 97 || W > 112 || (int64_t)N * H * W * 128 >= 0xffffff00ll) return 0;  // 7 pixel fragments, 4 + 3 per wave pair
   return N * 3;
 }
 
@@ -520,7 +544,7 @@ static int stem_wgrad_halves(int H) {
 
 // Scratch floats of the stem weight-grad launch (per-block partials), 0: outside the envelope.
 extern "C" int64_t dpe_stem_wgrad_scratch(int N, int H, int W) {
-  if (N <= 0 || H < 2 || W < 1 || W > 112) return 0;
+  if (N <= 0 || H < 2 || W < 1 || W > 112 || (int64_t)N * H * W * 128 >= 0xffffff00ll) return 0;
   return (int64_t)N * stem_wgrad_halves(H) * dpe::stem::wg::PART;
 }
 
