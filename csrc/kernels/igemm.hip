@@ -1222,6 +1222,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, (BN / WGN > 64) ? 2 : 1) void igemm
   epilogue_atomic_f32<BM, BN, LDS, WGM, WGN>(p, acc, smem, m0, n0, wn, split);
 }
 
+#ifndef DPE_WG_NS
+#define DPE_WG_NS 2  // ring stages of the 4-wave weight-grad DMA tiles (compile-time A/B arm)
+#endif
+
 template <int BM, int BN, int AL, int BL, int EPI>
 static void launch_t(const IgemmArgs& a, int splits, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
@@ -1393,7 +1397,7 @@ extern "C" int dpe_igemm_wgrad_dma_launch(const IgemmArgs* args, int bm, int bn,
   const int tiles = ((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
 #define DPE_WG(BM_, BN_, BL_)                                                                                \
   if (bm == BM_ && bn == BN_ && bload == BL_) {                                                               \
-    hipLaunchKernelGGL((igemm_wgrad_dma_kernel<BM_, BN_, BL_, 2, 2, 2>), dim3(tiles * splits), dim3(NT), 0, st, a); \
+    hipLaunchKernelGGL((igemm_wgrad_dma_kernel<BM_, BN_, BL_, 2, 2, DPE_WG_NS>), dim3(tiles * splits), dim3(NT), 0, st, a); \
     return 0;                                                                                                 \
   }
 #define DPE_WG_T(BL_) DPE_WG(128, 128, BL_) DPE_WG(128, 64, BL_) DPE_WG(64, 128, BL_) DPE_WG(64, 64, BL_)
