@@ -316,11 +316,14 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
   Cfg c = pick_cfg(a.M, a.N, a.K, allow_split && epi == dpe::EPI_ATOMIC_F32);
   a.k_split = c.k_split;
   // weight grads over an im2col B (3x3 / strided; split-K fp32 atomics): LDS-DMA kernel, measured 1.3-1.5x
-  // faster (scripts/bench_convs.py); on the dense 1x1 ones it measured 10-15 % slower, so those stay
-  // register-staged (DPE_WGRAD_DMA=0: all register-staged)
+  // faster (scripts/bench_convs.py) (DPE_WGRAD_DMA=0: the im2col ones register-staged)
+  // the dense 1x1 ones (< 256 channels) too: on the LDS-DMA kernel since its round-5 changes, same-box
+  // ResNet-50 31.42-31.47 vs 31.48-31.60 ms/step (3 alternating pairs; the register-staged tile measured
+  // 10-15 % faster in round 1).  DPE_WGRAD_DMA_1X1=0: register-staged (A/B)
+  static const bool dma_1x1 = [] { const char* e = getenv("DPE_WGRAD_DMA_1X1"); return !(e && e[0] == '0'); }();
   if (conv && epi == dpe::EPI_ATOMIC_F32 && aload == dpe::A_DENSE_M &&
       ((igemm_dma_on() && wgrad_dma_on() && bload == dpe::B_CONV_WGRAD) ||
-       (bload == dpe::B_DENSE_N && a.b_coef))) {
+       (bload == dpe::B_DENSE_N && (a.b_coef || (dma_1x1 && igemm_dma_on()))))) {
     int bm = c.bm, bn = c.bn, splits = c.splits;
     {
       // ~3 resident 128x128 blocks per CU (4 fit): ResNet-50 step, alternating
