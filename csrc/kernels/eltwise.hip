@@ -204,12 +204,16 @@ __global__ __launch_bounds__(ET) void nchw_to_s2d_kernel(const float* __restrict
     const int64_t t = i / Wo;
     const int q = (int)(t % Ho);
     const int n = (int)(t / Ho);
+    // the two horizontal neighbours (ax = 0, 1) of a channel row in one 8-B load (W even)
     float v[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int c = j & 3, ax = (j >> 2) & 1, ay = j >> 3;
-      v[j] = c < C ? x[(((int64_t)n * C + c) * H + 2 * q + ay) * W + 2 * p + ax] : 0.f;
-    }
+    for (int ay = 0; ay < 2; ++ay)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float2 t2 = c < C ? *(const float2*)(x + (((int64_t)n * C + c) * H + 2 * q + ay) * W + 2 * p) : float2{0.f, 0.f};
+        v[ay * 8 + c] = t2.x;      // j = c + 4 ax + 8 ay
+        v[ay * 8 + 4 + c] = t2.y;
+      }
     u32x4* o = (u32x4*)(y + i * 16);
     o[0] = pack8(v);
     o[1] = pack8(v + 8);

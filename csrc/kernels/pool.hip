@@ -20,7 +20,9 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
   const int k = KK > 0 ? KK : k_rt;
   const int CPR = C >> 3;
   const int total = N * OH * OW * CPR;
-  const int i = blockIdx.x * 256 + threadIdx.x;
+  // XCD-contiguous block order: an XCD's concurrent blocks cover neighbouring output rows, whose 3x3 / s2
+  // windows share input rows in that XCD's L2 (round-robin dispatch spread them over all 8 L2s)
+  const int i = xcd_remap(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
   if (i >= total) return;
   const int c8 = (i % CPR) * 8;
   int t = i / CPR;
@@ -272,7 +274,8 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_reduce_quad_kernel(const u
   const int c = tid % CPR, r = tid / CPR;
   const int OH = H >> 1, OW = W >> 1;
   const int Q = N * OH * OW;
-  const int qb = blockIdx.x * quads_per_block;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);  // (XCD-contiguous: neighbouring quads share pooled rows in one L2)
+  const int qb = lb * quads_per_block;
   const int qe = min(Q, qb + quads_per_block);
   float sm[8], sq[8], mean[8], sc[8], sh[8];
 #pragma unroll
@@ -320,8 +323,8 @@ __global__ __launch_bounds__(256) void maxpool_bn_bwd_reduce_quad_kernel(const u
     const int cc = ch >> 3, e = ch & 7;
     float a = 0.f, b2 = 0.f;
     for (int rr = 0; rr < QPI; ++rr) { a += red[0][rr * CPR + cc][e]; b2 += red[1][rr * CPR + cc][e]; }
-    part[(int64_t)ch * gridDim.x + blockIdx.x] = a;
-    part[(int64_t)(C + ch) * gridDim.x + blockIdx.x] = b2;
+    part[(int64_t)ch * gridDim.x + lb] = a;
+    part[(int64_t)(C + ch) * gridDim.x + lb] = b2;
   }
 }
 
