@@ -243,6 +243,9 @@ void launch_planned(dpe::HgemmArgs a, const Plan& pl, int ak, int bk, int epi, h
                                                   c10::hip::getStreamFromExternal(fin_stream, (c10::DeviceIndex)dev));
       fs = fin_stream;
     }
+    // DPE_AB_SKIP_FINALIZE=1: timing diagnostic only (what the slab reductions cost the step; gradients WRONG)
+    static const bool skip = [] { const char* e = getenv("DPE_AB_SKIP_FINALIZE"); return e && e[0] == '1'; }();
+    if (skip) return;
     const int rf = dpe_hgemm_finalize(&a, epi, fs);
     e = hipGetLastError();
     TORCH_CHECK(rf == 0 && e == hipSuccess, "hgemm finalize failed rc=", rf, " ", hipGetErrorString(e));

@@ -371,7 +371,8 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
     a.slab = nullptr;
     TORCH_CHECK(rc == 0 || (!a.b_coef && !deterministic),
                 "weight grad with BN on load / deterministic: outside the LDS-DMA kernel's envelope (rc=", rc, ")");
-    if (rc == 0 && slab.defined()) {
+    static const bool skip_fin = [] { const char* e = getenv("DPE_AB_SKIP_FINALIZE"); return e && e[0] == '1'; }();
+    if (rc == 0 && slab.defined() && !skip_fin) {
       dpe::HgemmArgs f;
       memset(&f, 0, sizeof(f));
       f.C = a.C; f.ws = fp(slab); f.M = a.M; f.N = a.N; f.ldc = a.ldc; f.splits = splits; f.alpha = 1.f;

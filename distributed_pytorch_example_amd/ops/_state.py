@@ -148,7 +148,7 @@ def note_use(p: torch.Tensor) -> None:
 # Off: measured 2 % SLOWER on ResNet-50 / MI355X at batch 512 (46.6 vs 47.6 ms/step): the
 # concurrent kernels contend more than they overlap.  set_wgrad_stream(True) keeps the path
 # testable (tests/test_comm_gpu.py: the reducer waits on this stream too).
-_WGRAD_STREAM_ON = False
+_WGRAD_STREAM_ON = __import__("os").environ.get("DPE_WGRAD_STREAM", "0") == "1"  # (A/B)
 
 
 def set_wgrad_stream(on: bool) -> bool:

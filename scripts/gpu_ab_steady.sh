@@ -1,6 +1,7 @@
 #!/bin/bash
 # Same-box per-kernel A/B: steady kernel traces of bench.py for the default build (A) and an alternative
 # extension (B: DPE_EXT_SO=<path>), alternating.  bash scripts/gpu_ab_steady.sh <path-to-alt.so> [rounds]
+# (path "-": the default build in both arms; BENV="VAR=val ..." adds an environment to the B arm)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/abs
@@ -12,7 +13,8 @@ for r in $(seq 1 $N); do
     if [ $arm = A ]; then
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/abs/tr -o run -- python3 $R/bench.py --steps 8 --warmup 3 ${BENCH_ARGS} > $R/gpurun_out/abs/$arm.log 2>&1 || { echo "$arm FAILED"; tail -20 $R/gpurun_out/abs/$arm.log; exit 1; }
     else
-      DPE_EXT_SO=$ALT timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/abs/tr -o run -- python3 $R/bench.py --steps 8 --warmup 3 ${BENCH_ARGS} > $R/gpurun_out/abs/$arm.log 2>&1 || { echo "$arm FAILED"; tail -20 $R/gpurun_out/abs/$arm.log; exit 1; }
+      if [ "$ALT" = "-" ]; then XS=""; else XS="DPE_EXT_SO=$ALT"; fi
+      env $XS ${BENV} timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/abs/tr -o run -- python3 $R/bench.py --steps 8 --warmup 3 ${BENCH_ARGS} > $R/gpurun_out/abs/$arm.log 2>&1 || { echo "$arm FAILED"; tail -20 $R/gpurun_out/abs/$arm.log; exit 1; }
     fi
     f=$(find $R/gpurun_out/abs/tr -name "*kernel_trace.csv" | head -1)
     python3 $R/scripts/prof_steady.py $f 4 ${MARK:-sgd_kernel} ${TOP:-80} > $R/gpurun_out/abs/steady_${arm}$r.txt
