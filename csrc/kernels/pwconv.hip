@@ -783,7 +783,7 @@ static int pw_cap(int64_t K, int epi) {
 // Row groups of a launch: rg (= partial columns) and srg, the row groups started statically (the grid is
 // srg x nbN blocks).  srg == rg: static schedule, one resident wave of blocks over the whole launch,
 // sized to the resident capacity minus the slots left to in-flight RCCL channel blocks (comm.cpp CU
-// budget).  srg < rg (CU budget in force): the dynamic variant, rg = 3 srg row groups of >= 7 tiles each
+// budget).  srg < rg (CU budget in force): the dynamic variant, rg = 8 srg row groups of >= 7 tiles each
 // (>= NS + 3: the stream claims the next row group NS + 2 tiles before the current one ends).
 struct PwPlan { int rg, srg; };
 static PwPlan pw_plan(int64_t M, int64_t N, int64_t K, int epi) {
@@ -797,9 +797,13 @@ static PwPlan pw_plan(int64_t M, int64_t N, int64_t K, int epi) {
   const int reserve = dpe_cu_reserve();
   if (reserve > 0 && pw_dynamic()) {
     const int64_t srg = std::max<int64_t>(1, (pw_cap<true>(K, epi) - reserve) / nbN);
-    // (a third static, two thirds claimed: a block two or three times slower than its peers -- a
-    // VALU-bound foreign wave on its SIMD -- still ends its static row group by the launch's end)
-    const int64_t rg = std::min<int64_t>(3 * srg, tiles / 7);
+    // (an eighth static, the rest claimed: a block two or three times slower than its peers -- a
+    // VALU-bound foreign wave on its SIMD -- ends its static row group well before the launch's end, and
+    // the launch's tail is one short row group at its speed.  Worst-case hog probe, same box: 8 vs 3 row
+    // groups per resident block 36.41 / 36.56 vs 36.92 / 37.10 ms/step, 16 twice 36.49 / 36.92 -- the
+    // >= 7-tile floor binds at layers 3-4; DPE_PW_DYN_FACTOR: A/B)
+    static const int64_t fac = [] { const char* e = getenv("DPE_PW_DYN_FACTOR"); return (int64_t)(e ? std::max(2, atoi(e)) : 8); }();
+    const int64_t rg = std::min<int64_t>(fac * srg, tiles / 7);
     if (rg > srg) return {(int)rg, (int)srg};
   }
   int64_t rg = (pw_cap<false>(K, epi) - reserve) / nbN;
