@@ -51,7 +51,8 @@ constexpr TileCfg kTiles[] = {
 double layout_rate(int ak, int bk) { return ak && bk ? 5.2e12 : (ak ? 5.0e12 : 4.7e12); }
 constexpr double kEpi = 5.0e-11;  // s per output byte per CU: the store tail is issue-bound (~20 GB/s per CU)
 constexpr double kFix = 2.0e-6;   // first prologue + launch
-constexpr double kBw = 4.0e12;    // slab write + finalize read bandwidth
+// slab write + finalize read bandwidth (DPE_HGEMM_SLAB_GBPS: A/B)
+const double kBw = [] { const char* e = getenv("DPE_HGEMM_SLAB_GBPS"); return e ? atof(e) * 1e9 : 4.0e12; }();
 constexpr double kLaunch = 3.0e-6;
 
 int g_force_cfg = -1, g_force_splits = -1;
