@@ -245,7 +245,12 @@ void launch_planned(dpe::HgemmArgs a, const Plan& pl, int ak, int bk, int epi, h
       fs = fin_stream;
     }
     // DPE_AB_SKIP_FINALIZE=1: timing diagnostic only (what the slab reductions cost the step; gradients WRONG)
-    static const bool skip = [] { const char* e = getenv("DPE_AB_SKIP_FINALIZE"); return e && e[0] == '1'; }();
+    static const bool skip = [] {
+      const char* e = getenv("DPE_AB_SKIP_FINALIZE");
+      const bool on = e && e[0] == '1';
+      if (on) fprintf(stderr, "[dpe] DPE_AB_SKIP_FINALIZE=1: K-split weight gradients are NOT reduced (timing only)\n");
+      return on;
+    }();
     if (skip) return;
     const int rf = dpe_hgemm_finalize(&a, epi, fs);
     e = hipGetLastError();

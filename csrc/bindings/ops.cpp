@@ -371,7 +371,12 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
     a.slab = nullptr;
     TORCH_CHECK(rc == 0 || (!a.b_coef && !deterministic),
                 "weight grad with BN on load / deterministic: outside the LDS-DMA kernel's envelope (rc=", rc, ")");
-    static const bool skip_fin = [] { const char* e = getenv("DPE_AB_SKIP_FINALIZE"); return e && e[0] == '1'; }();
+    static const bool skip_fin = [] {  // (timing diagnostic: gemm.cpp launch_planned)
+      const char* e = getenv("DPE_AB_SKIP_FINALIZE");
+      const bool on = e && e[0] == '1';
+      if (on) fprintf(stderr, "[dpe] DPE_AB_SKIP_FINALIZE=1: deterministic weight-grad splits are NOT reduced (timing only)\n");
+      return on;
+    }();
     if (rc == 0 && slab.defined() && !skip_fin) {
       dpe::HgemmArgs f;
       memset(&f, 0, sizeof(f));
