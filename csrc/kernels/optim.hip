@@ -97,27 +97,45 @@ DPE_DEVICE void optim_chunk(const TensorDesc& d, const Rule& rule, int chunk) {
   const bool vec = (align & 15) == 0 && ((uintptr_t)d.shadow & 7) == 0;
   int64_t i = beg;
   if (vec) {
+    // Software-pipelined one 1024-element step ahead: the next step's loads are issued before this step's
+    // stores, so the wait for them counts past those stores (loads and stores share vmcnt: loaded after the
+    // stores, every step waited for its predecessor's stores to complete).  Every load and store goes through
+    // a buffer resource and is issued unconditionally -- an absent state or shadow is a 0-byte resource
+    // (loads read 0, stores are dropped) and the last step's look-ahead re-reads its own elements -- so the
+    // compiler's waits stay counted instead of vmcnt(0) (common.h buf_rsrc).
     const int64_t vend = beg + ((end - beg) & ~(int64_t)1023);
-    for (int64_t j = beg + threadIdx.x * 4; j < vend; j += 1024) {
-      f32x4 p = *(const f32x4*)(d.p + j);
-      const f32x4 g = *(const f32x4*)(d.g + j);
-      f32x4 m = has_s1 ? *(const f32x4*)(d.s1 + j) : f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 v = TWO_STATES ? *(const f32x4*)(d.s2 + j) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nsteps = (int)((vend - beg) >> 10);
+    const uint32_t bytes = (uint32_t)((vend - beg) * 4);  // <= 64 KiB (CHUNK)
+    const __amdgpu_buffer_rsrc_t prs = buf_rsrc(d.p + beg, bytes), grs = buf_rsrc(d.g + beg, bytes);
+    const __amdgpu_buffer_rsrc_t mrs = buf_rsrc(has_s1 ? d.s1 + beg : nullptr, has_s1 ? bytes : 0u);
+    const __amdgpu_buffer_rsrc_t vrs = buf_rsrc(TWO_STATES ? d.s2 + beg : nullptr, TWO_STATES ? bytes : 0u);
+    const __amdgpu_buffer_rsrc_t srs = buf_rsrc(d.shadow ? d.shadow + beg : nullptr, d.shadow ? bytes / 2 : 0u);
+    auto ld = [](__amdgpu_buffer_rsrc_t r, uint32_t o) {
+      return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
+    };
+    const uint32_t lo = threadIdx.x * 16u;  // the lane's 16 B of a 4-KiB step
+    f32x4 pn = ld(prs, lo), gn = ld(grs, lo), mn = ld(mrs, lo), vn = ld(vrs, lo);
+    for (int k = 0; k < nsteps; ++k) {
+      f32x4 p = pn, m = mn, v = vn;
+      const f32x4 g = gn;
+      const uint32_t o = lo + (uint32_t)k * 4096u, on = k + 1 < nsteps ? o + 4096u : o;
+      pn = ld(prs, on);
+      gn = ld(grs, on);
+      mn = ld(mrs, on);
+      vn = ld(vrs, on);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float pe = p[e], me = m[e], ve = v[e];
         rule(pe, g[e], me, ve);
         p[e] = pe; m[e] = me; v[e] = ve;
       }
-      *(f32x4*)(d.p + j) = p;
-      if (has_s1) *(f32x4*)(d.s1 + j) = m;
-      if (TWO_STATES) *(f32x4*)(d.s2 + j) = v;
-      if (d.shadow) {
-        u32x2 sh;
-        sh[0] = pack_bf2(p[0], p[1]);
-        sh[1] = pack_bf2(p[2], p[3]);
-        *(u32x2*)(d.shadow + j) = sh;
-      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, p), prs, o, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, m), mrs, o, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), vrs, o, 0, 0);
+      u32x2 sh;
+      sh[0] = pack_bf2(p[0], p[1]);
+      sh[1] = pack_bf2(p[2], p[3]);
+      __builtin_amdgcn_raw_buffer_store_b64(sh, srs, o >> 1, 0, 0);
     }
     i = vend;
   }
