@@ -29,7 +29,7 @@ struct HgemmProblem {
   int tile_end;       // cumulative 256x256 tile count through this problem
   int overwrite;      // 1: C = alpha*acc (the gradient's first writer of the step), 0: C += alpha*acc
 };
-constexpr int HGEMM_MAX_GROUP = 8;
+constexpr int HGEMM_MAX_GROUP = 12;
 // act values beyond igemm.h's Act: gelu backward, C = (alpha*acc) * gelu'(aux_in)
 constexpr int HACT_GELU_BWD = 3;
 // HE_BF16 + the BatchNorm-backward partials of the stored values (a conv data grad dL/dy of a BN + ReLU

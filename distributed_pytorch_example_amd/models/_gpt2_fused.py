@@ -53,6 +53,14 @@ _carry: list = [None]
 # that live in DDP bucket views are deferred (the reducer is told when the group has been written; a
 # gradient autograd would receive from this node must be complete when backward returns).  0 = off.
 _WG_GROUP = int(os.environ.get("DPE_GPT2_WGRAD_GROUP", "2"))
+# Launches are cut by output tiles, not by layers: a grouped launch takes the longest queue prefix of at most
+# _WG_TILES 256x256 tiles (one round of the persistent grid) and _WG_MAXP problems; what does not fill a round
+# waits for the next layer, and at the end of backward a remainder under half a round runs as ordinary
+# (K-split) weight-grad GEMMs instead of a mostly idle round.  GPT-2-small: 1296 tiles -> 5 launches of
+# 252 + 36 tiles alone (was 6 launches of 216).  DPE_GPT2_WGRAD_POLICY=layers: the _WG_GROUP-layer groups (A/B).
+_WG_TILES = int(os.environ.get("DPE_GPT2_WGRAD_TILES", "256"))
+_WG_MAXP = 12  # hgemm.h HGEMM_MAX_GROUP
+_WG_BY_TILES = os.environ.get("DPE_GPT2_WGRAD_POLICY", "tiles") != "layers"
 _wq: list = []  # (dy, x, dw, db | None, overwrite, weight param, bias param | None)
 # The LayerNorm weight / bias gradients of the same layers: their [blocks][2][D] partial sums are kept and
 # reduced by one grouped launch at the same flush (a standalone finalize is a ~5 us latency-bound launch,
@@ -96,18 +104,46 @@ def flush_ln_queue() -> None:
             grad_done(q[5], True)
 
 
-def flush_wgrad_queue() -> None:
-    """Launch the queued weight gradients (groups of at most 8 problems) and announce them."""
+def _wg_tiles(q) -> int:
+    M, N = q[2].shape[0], q[2].shape[1]
+    return ((M + 255) // 256) * ((N + 255) // 256)
+
+
+def _wg_launch_group(C, chunk) -> None:
+    C.linear_wgrad_group([q[0] for q in chunk], [q[1] for q in chunk], [q[2] for q in chunk],
+                         [q[3] if q[3] is not None else _EMPTY(q[2]) for q in chunk], [q[4] for q in chunk])
+
+
+def flush_wgrad_queue(final: bool = True) -> None:
+    """Launch queued weight gradients and announce them.  ``final`` (end of backward, a token-count change, or
+    grouping off): everything; else (tile policy) only the whole-round prefixes, the rest stays queued."""
     flush_ln_queue()
     if not _wq:
         return
     C = ext()
-    items = list(_wq)
-    _wq.clear()
-    for i in range(0, len(items), 8):
-        chunk = items[i:i + 8]
-        C.linear_wgrad_group([q[0] for q in chunk], [q[1] for q in chunk], [q[2] for q in chunk],
-                             [q[3] if q[3] is not None else _EMPTY(q[2]) for q in chunk], [q[4] for q in chunk])
+    items = []
+    if not _WG_BY_TILES:
+        items = list(_wq)
+        _wq.clear()
+        for i in range(0, len(items), 8):
+            _wg_launch_group(C, items[i:i + 8])
+    else:
+        while _wq:
+            n, t = 0, 0
+            while n < len(_wq) and n < _WG_MAXP and t + _wg_tiles(_wq[n]) <= _WG_TILES:
+                t += _wg_tiles(_wq[n])
+                n += 1
+            n = max(n, 1)  # (a problem of more than one round alone)
+            if n == len(_wq) and not final:
+                break  # the queue fits in one round: wait for the next layer's problems
+            chunk = _wq[:n]
+            del _wq[:n]
+            if n == len(chunk) and not _wq and final and t < _WG_TILES // 2:
+                for q in chunk:  # a small remainder: ordinary K-split GEMMs (planner) instead of an idle round
+                    C.linear_wgrad(q[0], q[1], q[2], 1.0, None, q[3], 0, q[4])
+            else:
+                _wg_launch_group(C, chunk)
+            items += chunk
     for q in items:
         q[5]._dpe_deferred = False
         if q[6] is not None:
@@ -242,7 +278,11 @@ class BlockFn(Function):
         dqkv = dqkv.view(a.shape[0], a.shape[1], -1)
         dh1 = linear_bwd(blk.c_attn, dqkv, h1)
         g1, g1b = ln_bwd(blk.ln_1, dh1, x, m1, r1, g2)
-        if (_wq or _lnq) and (len(_wq) >= 4 * _WG_GROUP or getattr(blk, "_dpe_layer", 0) == 0 or not group):
+        last = getattr(blk, "_dpe_layer", 0) == 0 or not group
+        if _WG_BY_TILES:
+            if (_wq or _lnq) and (last or sum(_wg_tiles(q) for q in _wq) > _WG_TILES):
+                flush_wgrad_queue(final=last)  # whole rounds as they fill, everything at the first block
+        elif (_wq or _lnq) and (len(_wq) >= 4 * _WG_GROUP or last):
             flush_wgrad_queue()  # every _WG_GROUP layers, and always at the first block (end of backward)
         _carry[0] = (g1, g1b, g1._version)
         pgrads = [grads.get(id(p)) for p in block_params(blk)]
