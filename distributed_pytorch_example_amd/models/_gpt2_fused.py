@@ -48,8 +48,8 @@ _carry: list = [None]
 # Grouped weight gradients.  Alone, a layer's four weight-grad GEMMs (dW = dy^T x over K = B*T tokens;
 # 27 / 9 / 36 / 36 output tiles of 256x256 at d = 768) need an 8-9-way K split each to fill 256 CUs,
 # and the split's fp32 partial slabs plus their finalize launch cost about as much as the GEMM itself.
-# Deferred here and launched together (C.linear_wgrad_group, hgemm HE_GROUP), DPE_GPT2_WGRAD_GROUP layers
-# at a time (default 2: 216 whole-K tiles, one round of the persistent grid, no slabs).  Only gradients
+# Deferred here and launched together (C.linear_wgrad_group, hgemm HE_GROUP: whole-K tiles, no slabs) in
+# whole rounds of the persistent grid (below; DPE_GPT2_WGRAD_GROUP=0: no grouping).  Only gradients
 # that live in DDP bucket views are deferred (the reducer is told when the group has been written; a
 # gradient autograd would receive from this node must be complete when backward returns).  0 = off.
 _WG_GROUP = int(os.environ.get("DPE_GPT2_WGRAD_GROUP", "2"))
