@@ -56,9 +56,10 @@ def parse():
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--optimizer", default=None)
     ap.add_argument("--lr", type=float, default=None)
-    ap.add_argument("--bucket-timing", action="store_true",
-                    help="after the timed steps, one instrumented step: per-bucket all-reduce time and its overlap "
-                         "with backward (HIP events on the RCCL stream), reported under 'buckets'")
+    ap.add_argument("--bucket-timing", type=int, default=None,
+                    help="1: after the timed steps, one instrumented (untimed) step: per-bucket all-reduce time and "
+                         "its overlap with backward (HIP events on the RCCL stream), reported under 'buckets' "
+                         "(default: on at world size > 1, so a multi-GPU run documents its communication)")
     ap.add_argument("--force-comm", action="store_true",
                     help="run the RCCL bucket all-reduces even at world size 1 (reducer/overlap mechanics check)")
     ap.add_argument("--nbatches", type=int, default=4, help="distinct synthetic batches cycled")
@@ -84,10 +85,14 @@ def main():
     from distributed_pytorch_example_amd.optim import build_optimizer
     from distributed_pytorch_example_amd.ops import functional as Fx
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # a bare `python bench.py --gpus N` would silently measure one GPU: refuse instead
+        raise SystemExit(f"[bench] --gpus {args.gpus} needs one process per GPU: launch with "
+                         f"`python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus} ...`")
     ensure_single_process_env()
     rank, world, local_rank = pdist.init_process_group("auto", comm_max_channels=args.comm_max_channels)
-    if world != args.gpus and rank == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"[bench] --gpus {args.gpus} but the launcher started WORLD_SIZE={world} processes")
     dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
     torch.manual_seed(1234 + rank)
 
@@ -173,10 +178,9 @@ def main():
 
     for i in range(args.warmup):
         step(i)
-    if world > 1:  # after warm-up: DDP may have dropped the CU budget (parallel/ddp.py, adaptive CU budget)
+    if world > 1:  # after warm-up: the adaptive CU budget decided from measured comm (parallel/ddp.py)
+        cfg["cu_budget"] = ddp.settle_cu_budget()
         cfg["cu_reserve_slots"] = _ext().cu_reserve_config() if dev.type == "cuda" else 0
-        if ddp.cu_budget_decision is not None:
-            cfg["cu_budget"] = ddp.cu_budget_decision
     if args.graph and dev.type == "cuda":
         step = _graph_step(args, world, ddp, opt, model, xs, ys, fused_loss, num_classes, Fx)
     _sync(dev)
@@ -198,7 +202,7 @@ def main():
     ms = 1000.0 * dt / args.steps
     value = samples_per_step * world * args.steps / dt
     extra = {}
-    if args.bucket_timing:
+    if args.bucket_timing if args.bucket_timing is not None else world > 1:
         # one extra (untimed) step with per-bucket HIP events on the comm stream
         ddp.enable_timing(True)
         step(args.warmup + args.steps)

@@ -512,6 +512,8 @@ void linear_wgrad_group(const std::vector<Tensor>& dys, const std::vector<Tensor
 }  // namespace
 
 void register_gemm(pybind11::module& m) {
+  m.attr("HGEMM_MAX_GROUP") = dpe::HGEMM_MAX_GROUP;
+  m.def("num_cus", &num_cus, "compute units of the current device (256 on MI355X; 256 without a device)");
   m.def("linear_wgrad_group", &linear_wgrad_group, pybind11::arg("dys"), pybind11::arg("xs"), pybind11::arg("dws"),
         pybind11::arg("dbs"), pybind11::arg("overwrite"),
         "grouped TN weight grads in one launch: dws[g] (+)= dys[g]^T xs[g], dbs[g] += colsum(dys[g]) "

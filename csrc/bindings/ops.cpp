@@ -264,6 +264,13 @@ Tensor flipped(const Tensor& w, int K, int R, int S, int C, int r0, int rs, int 
     CHECK_RC(dpe_conv_w_flipT(bp(w), bpm(wt), K, R, S, C, r0, rs, Rp, s0, ss, Sp, cur_stream()), "conv_w_flipT");
     return wt;
   }
+  if (!g_flips.empty() && g_flips.front().w.device() != w.device()) {
+    // one device per table: the batched refresh launches on the current device's stream
+    g_flips.clear();
+    g_flip_desc = Tensor();
+    g_flip_start = Tensor();
+    g_flip_table_dirty = true;
+  }
   FlipEntry* hit = nullptr;
   for (auto& e : g_flips)
     if (e.d.w == bp(w) && e.w.is_same(w) && e.d.K == K && e.d.R == R && e.d.S == S && e.d.C == C && e.d.r0 == r0 &&
@@ -273,8 +280,10 @@ Tensor flipped(const Tensor& w, int K, int R, int S, int C, int r0, int rs, int 
     }
   if (hit && hit->epoch == g_weight_epoch) return hit->wt;
   if (hit) {
-    // a new epoch: refresh every cached copy at once (their filters are all current now: no optimizer step
-    // runs inside a backward pass before the node that needs them -- DDP.overlap_optimizer included)
+    // a new epoch: refresh every cached copy at once.  This first stale request comes from the first
+    // flipped-filter user of the backward pass; every other cached filter's layer back-propagates after it,
+    // so none of them can have been stepped yet -- with DDP.overlap_optimizer a bucket is stepped only after
+    // every reader of its parameters returned -- and all cached weights are current (one device: below)
     if (g_flip_table_dirty) {
       std::vector<int> start(g_flips.size() + 1, 0);
       std::vector<FlipDescHost> desc(g_flips.size());

@@ -282,7 +282,8 @@ Reducer::Reducer(std::vector<at::Tensor> buckets, std::vector<std::vector<int64_
       force_(force), comm_bf16_(comm_bf16), sync_debug_(sync_debug) {
   for (auto& b : buckets_) TORCH_CHECK(b.is_cuda(), "bucket buffers must be GPU tensors (host transport: Reducer.host)");
   init_tracking(nparams);
-  const unsigned flags = timing_ ? hipEventDefault : hipEventDisableTiming;
+  // timing-capable events whether or not timing is on now: set_timing() may switch it per step
+  const unsigned flags = hipEventDefault;
   ev_ready_.resize(buckets_.size());
   ev_aux_.resize(buckets_.size());
   ev_start_.resize(buckets_.size());
@@ -378,7 +379,9 @@ void Reducer::prepare() {
   next_ = 0;
   launch_order_.clear();
   step_open_ = true;
-  if (timing_) HIP_CHECK(hipEventRecord(ev_step_begin_, c10::hip::getCurrentHIPStream().stream()));
+  timed_ = timing_ && !host_launch_;
+  timed_done_ = false;
+  if (timed_) HIP_CHECK(hipEventRecord(ev_step_begin_, c10::hip::getCurrentHIPStream().stream()));
 }
 
 void Reducer::launch(int64_t b) {
@@ -400,7 +403,7 @@ void Reducer::launch(int64_t b) {
     HIP_CHECK(hipEventRecord(ev_aux_[b], aux));
     HIP_CHECK(hipStreamWaitEvent(cs, ev_aux_[b], 0));
   }
-  if (timing_) HIP_CHECK(hipEventRecord(ev_start_[b], cs));
+  if (timed_) HIP_CHECK(hipEventRecord(ev_start_[b], cs));
   auto& t = buckets_[b];
   if (comm_bf16_) {
     auto& h = staging_[b];
@@ -410,7 +413,7 @@ void Reducer::launch(int64_t b) {
   } else {
     comm_->all_reduce_raw(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), ncclAvg, cs);
   }
-  if (timing_) HIP_CHECK(hipEventRecord(ev_end_[b], cs));
+  if (timed_) HIP_CHECK(hipEventRecord(ev_end_[b], cs));
   if (sync_debug_) {
     HIP_CHECK(hipStreamSynchronize(cs));
     const std::string err = comm_->async_error();
@@ -438,7 +441,7 @@ void Reducer::finalize() {
     return;
   }
   hipStream_t cur = c10::hip::getCurrentHIPStream().stream();
-  if (timing_) HIP_CHECK(hipEventRecord(ev_bwd_end_, cur));
+  if (timed_) HIP_CHECK(hipEventRecord(ev_bwd_end_, cur));
   // Unused parameters: their (zero / stale-accumulated) slices are reduced
   // anyway so every rank issues the same collective sequence.
   while (next_ < (int64_t)buckets_.size()) launch(next_++);
@@ -448,11 +451,20 @@ void Reducer::finalize() {
   }
   set_comm_active(false);  // later compute kernels are ordered after the last collective
   step_open_ = false;
+  timed_done_ = timed_;
+}
+
+bool Reducer::timings_ready() {
+  if (host_launch_ || !timed_done_ || !comm_ || (comm_->world() == 1 && !force_)) return false;
+  const hipError_t e = hipEventQuery(ev_done_);
+  if (e == hipErrorNotReady) return false;
+  HIP_CHECK(e);
+  return true;
 }
 
 std::vector<std::tuple<int64_t, double, double>> Reducer::last_timings() {
   std::vector<std::tuple<int64_t, double, double>> out;
-  if (host_launch_ || !timing_ || !comm_ || (comm_->world() == 1 && !force_)) return out;
+  if (host_launch_ || !timed_done_ || !comm_ || (comm_->world() == 1 && !force_)) return out;
   HIP_CHECK(hipEventSynchronize(ev_done_));
   for (size_t b = 0; b < buckets_.size(); ++b) {
     float ms = 0.f, rel = 0.f;
@@ -530,6 +542,10 @@ void register_comm(pybind11::module& m) {
       .def("mark_ready", &Reducer::mark_ready)
       .def("finalize", &Reducer::finalize)
       .def("last_timings", &Reducer::last_timings)
+      .def("set_timing", &Reducer::set_timing, py::arg("on"), "per-bucket timing events from the next prepare()")
+      .def_property_readonly("timing", &Reducer::timing)
+      .def("timings_ready", &Reducer::timings_ready,
+           "the last finalized step was timed and its collectives completed (non-blocking)")
       .def_property_readonly("num_buckets", &Reducer::num_buckets)
       .def_property_readonly("buckets_launched", &Reducer::buckets_launched)
       .def("stream_wait_comm", &Reducer::stream_wait_comm, py::arg("stream"),

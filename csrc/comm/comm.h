@@ -97,6 +97,11 @@ class Reducer {
   void finalize();
   // (bucket, comm_ms, issued_before_backward_end) for the last finalized step
   std::vector<std::tuple<int64_t, double, double>> last_timings();
+  // per-bucket timing on / off from the next prepare() (the adaptive CU budget times a few warm-up steps)
+  void set_timing(bool on) { timing_ = on; }
+  bool timing() const { return timing_; }
+  // the last finalized step was timed and its collectives have completed (non-blocking)
+  bool timings_ready();
   int64_t num_buckets() const { return (int64_t)buckets_.size(); }
   int64_t registered_buffers() const;
   int world() const { return host_launch_ ? host_world_ : (comm_ ? comm_->world() : 1); }
@@ -117,6 +122,8 @@ class Reducer {
   int64_t next_ = 0;
   std::shared_ptr<Communicator> comm_;
   bool timing_;
+  bool timed_ = false;       // the step in flight (or last finalized) records timing events
+  bool timed_done_ = false;  // ... and it reached finalize()
   bool force_;  // issue collectives even at world size 1 (exercises the comm path on a 1-GPU box)
   bool comm_bf16_, sync_debug_;
   std::vector<at::Tensor> staging_;  // bf16 copies of the buckets (comm_bf16)

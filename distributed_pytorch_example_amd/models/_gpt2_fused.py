@@ -54,12 +54,21 @@ _carry: list = [None]
 # gradient autograd would receive from this node must be complete when backward returns).  0 = off.
 _WG_GROUP = int(os.environ.get("DPE_GPT2_WGRAD_GROUP", "2"))
 # Launches are cut by output tiles, not by layers: a grouped launch takes the longest queue prefix of at most
-# _WG_TILES 256x256 tiles (one round of the persistent grid) and _WG_MAXP problems; what does not fill a round
+# one round of 256x256 tiles (the persistent grid: CUs minus the RCCL-reserved slots, _wg_round) and
+# HGEMM_MAX_GROUP problems; what does not fill a round
 # waits for the next layer, and at the end of backward a remainder under half a round runs as ordinary
 # (K-split) weight-grad GEMMs instead of a mostly idle round.  GPT-2-small: 1296 tiles -> 5 launches of
 # 252 + 36 tiles alone (was 6 launches of 216).  DPE_GPT2_WGRAD_POLICY=layers: the _WG_GROUP-layer groups (A/B).
-_WG_TILES = int(os.environ.get("DPE_GPT2_WGRAD_TILES", "256"))
-_WG_MAXP = 12  # hgemm.h HGEMM_MAX_GROUP
+_WG_TILES_ENV = os.environ.get("DPE_GPT2_WGRAD_TILES")
+
+
+def _wg_round(C) -> int:
+    """Tiles of one round of the grouped launch's persistent grid right now: the device's CUs minus the
+    slots left to resident RCCL blocks (the CU budget, while a bucket all-reduce is in flight) -- the grid
+    linear_wgrad_group launches, so a round-sized group never spills into a second round."""
+    if _WG_TILES_ENV:
+        return int(_WG_TILES_ENV)
+    return max(64, C.num_cus() - C.cu_reserve())
 _WG_BY_TILES = os.environ.get("DPE_GPT2_WGRAD_POLICY", "tiles") != "layers"
 _wq: list = []  # (dy, x, dw, db | None, overwrite, weight param, bias param | None)
 # The LayerNorm weight / bias gradients of the same layers: their [blocks][2][D] partial sums are kept and
@@ -128,9 +137,10 @@ def flush_wgrad_queue(final: bool = True) -> None:
         for i in range(0, len(items), 8):
             _wg_launch_group(C, items[i:i + 8])
     else:
+        rnd, maxp = _wg_round(C), C.HGEMM_MAX_GROUP
         while _wq:
             n, t = 0, 0
-            while n < len(_wq) and n < _WG_MAXP and t + _wg_tiles(_wq[n]) <= _WG_TILES:
+            while n < len(_wq) and n < maxp and t + _wg_tiles(_wq[n]) <= rnd:
                 t += _wg_tiles(_wq[n])
                 n += 1
             n = max(n, 1)  # (a problem of more than one round alone)
@@ -138,7 +148,7 @@ def flush_wgrad_queue(final: bool = True) -> None:
                 break  # the queue fits in one round: wait for the next layer's problems
             chunk = _wq[:n]
             del _wq[:n]
-            if n == len(chunk) and not _wq and final and t < _WG_TILES // 2:
+            if n == len(chunk) and not _wq and final and t < rnd // 2:
                 for q in chunk:  # a small remainder: ordinary K-split GEMMs (planner) instead of an idle round
                     C.linear_wgrad(q[0], q[1], q[2], 1.0, None, q[3], 0, q[4])
             else:
@@ -280,7 +290,7 @@ class BlockFn(Function):
         g1, g1b = ln_bwd(blk.ln_1, dh1, x, m1, r1, g2)
         last = getattr(blk, "_dpe_layer", 0) == 0 or not group
         if _WG_BY_TILES:
-            if (_wq or _lnq) and (last or sum(_wg_tiles(q) for q in _wq) > _WG_TILES):
+            if (_wq or _lnq) and (last or sum(_wg_tiles(q) for q in _wq) > _wg_round(ext())):
                 flush_wgrad_queue(final=last)  # whole rounds as they fill, everything at the first block
         elif (_wq or _lnq) and (len(_wq) >= 4 * _WG_GROUP or last):
             flush_wgrad_queue()  # every _WG_GROUP layers, and always at the first block (end of backward)

@@ -163,7 +163,10 @@ class _FusedMixin:
 
     def _ov_detach(self):
         if self._ov_open:
-            torch.cuda.current_stream().wait_stream(self._ov_stream)
+            # buckets of this iteration were already stepped during backward: detaching now would leave
+            # the rest for a normal step() that re-steps everything (a silent double update)
+            raise RuntimeError("overlap_optimizer(enable=False) between backward and optimizer.step(): "
+                               "call optimizer.step() first to finish the iteration's overlapped update")
         self._ov_stream, self._ov_open = None, False
 
     def _ov_launch(self, tis, stream):

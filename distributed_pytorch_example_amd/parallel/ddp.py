@@ -56,6 +56,7 @@ from __future__ import annotations
 import contextlib
 import hashlib
 import os
+import time
 from typing import Callable, List, Optional
 
 import torch
@@ -183,13 +184,19 @@ class _GlooTransport:
     waits for all of them and averages.  The readiness tracking, index-order issue and finalize
     sequencing stay in C++ (``_C.Reducer.host``), the same code the RCCL path runs."""
 
-    def __init__(self, buckets: List[torch.Tensor], world: int, compression: Optional[str]):
+    def __init__(self, buckets: List[torch.Tensor], world: int, compression: Optional[str], timing: bool = False):
         self.buckets, self.world, self.compression = buckets, world, compression
         self.works = []
+        # timing: host-clock per-bucket (issue -> wait returned) times of the last step, like the RCCL
+        # reducer's event timings: [(bucket, allreduce_ms, start relative to the end of backward, ms)]
+        self.timing, self.timings, self._t0 = timing, [], {}
+        self.t_bwd_end = None  # set by DDP._finalize (end of backward)
 
     def on_launch(self, b: int):
         if self.world == 1:
             return
+        if self.timing:
+            self._t0[b] = time.perf_counter()
         t = self.buckets[b]
         if t.is_cuda:
             _aux_wait(t.device)  # weight grads written on the side stream
@@ -200,14 +207,22 @@ class _GlooTransport:
             self.works.append((b, None, dist.all_reduce(t, async_op=True)))
 
     def on_finalize(self):
+        t_end = self.t_bwd_end if self.t_bwd_end is not None else time.perf_counter()
+        self.t_bwd_end = None
+        timings = []
         for b, c, w in self.works:
             w.wait()
+            if self.timing and b in self._t0:
+                now = time.perf_counter()
+                timings.append((b, 1e3 * (now - self._t0[b]), 1e3 * (self._t0[b] - t_end)))
             t = self.buckets[b]
             if c is not None:
                 t.copy_(c.float().div_(self.world))
             else:
                 t.div_(self.world)
         self.works = []
+        if self.timing:
+            self.timings, self._t0 = timings, {}
 
 
 class DistributedDataParallel(nn.Module):
@@ -334,7 +349,7 @@ class DistributedDataParallel(nn.Module):
             # gloo / CPU: the C++ reducer in host-transport mode (same sequencing as the RCCL path)
             from ..ops._ext import ext
 
-            self._transport = _GlooTransport(self.buckets, self.world_size, self._compression)
+            self._transport = _GlooTransport(self.buckets, self.world_size, self._compression, self._timing)
             self.reducer = ext().Reducer.host(self.buckets, self.bucket_indices, len(self._params), self.world_size,
                                               self._transport.on_launch, self._transport.on_finalize)
             self._native = False
@@ -373,9 +388,14 @@ class DistributedDataParallel(nn.Module):
         """Per-bucket comm timing (HIP events) for the overlap / bucket-size sweep."""
         self._timing = on
         if self._native:
-            self._make_reducer()
+            self.reducer.set_timing(on)  # from the next step's prepare()
+        elif getattr(self, "_transport", None) is not None:
+            self._transport.timing = on
 
     def bucket_timings(self):
+        """[(bucket, allreduce_ms, start relative to the end of backward in ms)] of the last timed step."""
+        if not self._native and getattr(self, "_transport", None) is not None:
+            return list(self._transport.timings)
         return self.reducer.last_timings()
 
     def _attach_grads(self, zero: bool):
@@ -517,13 +537,18 @@ class DistributedDataParallel(nn.Module):
         """The CU budget (parallel/dist.py cu_reserve_for: persistent kernels leave slots to RCCL's channel
         blocks while a bucket all-reduce is in flight) pays off only when collectives occupy a good part of
         backward.  It is in force from the first bucket launch to the end of backward, while RCCL's blocks
-        are resident only during the all-reduces.  So after warm-up the step's forward + backward time is
-        measured (events, no sync) and the budget is dropped when the modelled all-reduce time,
-        2 (W-1)/W x gradient bytes / DPE_XGMI_BUS_GBPS (default 300), is below DPE_CU_BUDGET_MIN_DUTY
-        (default 0.10) of the backward (taken as 2/3 of forward + backward).  Probe on one GPU
-        (profiles/cu_hog_probe_r5.txt, 16 RCCL-sized workgroups resident only in the modelled W = 8
-        windows): ResNet-50 +1.9 % without the budget vs +4.8 % with it (duty ~3 %: the budget is dropped),
-        GPT-2 +5.4 % vs +4.1 % (duty ~35 %: kept).  An explicit DPE_CU_RESERVE is never changed."""
+        are resident only during the all-reduces.  So a few steps after warm-up (steps 2 .. 1 + N,
+        N = DPE_CU_BUDGET_SAMPLES, default 3) are timed with events -- forward + backward on the compute
+        stream, and every bucket all-reduce on the comm stream (the reducer's own per-bucket events) -- and
+        the budget is dropped when the MEASURED all-reduce time is below DPE_CU_BUDGET_MIN_DUTY (default
+        0.10) of the backward (taken as 2/3 of forward + backward).  Each quantity is the minimum over the
+        samples (the first timed step can still carry first-call costs), then the MAX over ranks through
+        the control plane, so every rank applies the same decision (same persistent-kernel slot counts and
+        split plans everywhere).  The modelled time, 2 (W-1)/W x gradient bytes / DPE_XGMI_BUS_GBPS
+        (default 300), decides only if no step could be timed (``settle_cu_budget`` before any sample).
+        Probe on one GPU (profiles/cu_hog_probe_r5.txt, 16 RCCL-sized workgroups resident only in the
+        modelled W = 8 windows): ResNet-50 +1.9 % without the budget vs +4.8 % with it, GPT-2 +5.4 % vs
+        +4.1 %.  An explicit DPE_CU_RESERVE is never changed."""
         if (self.world_size <= 1 or os.environ.get("DPE_CU_RESERVE") or os.environ.get("DPE_CU_BUDGET_ADAPT", "1") == "0"
                 or not self._params or not self._params[0].is_cuda or not _has_ext()):
             return None
@@ -534,53 +559,115 @@ class DistributedDataParallel(nn.Module):
         gbps = float(os.environ.get("DPE_XGMI_BUS_GBPS", "300"))
         nbytes = 4 * sum(p.numel() for p in self._params)
         comm_ms = 2.0 * (self.world_size - 1) / self.world_size * nbytes / (gbps * 1e6)
-        return {"step": 0, "ev": [], "samples": [], "comm_ms": comm_ms,
-                "min_duty": float(os.environ.get("DPE_CU_BUDGET_MIN_DUTY", "0.10")), "decision": None}
+        return {"step": 0, "pending": None, "samples": [], "comm_ms_model": comm_ms,
+                "nsamples": max(1, int(os.environ.get("DPE_CU_BUDGET_SAMPLES", "3"))),
+                "min_duty": float(os.environ.get("DPE_CU_BUDGET_MIN_DUTY", "0.10")), "decision": None,
+                "reserve": ext().cu_reserve_config()}
+
+    def _budget_collect(self):
+        """Read the timed step in flight (blocks until its collectives completed; warm-up steps only)."""
+        pr = self._budget_probe
+        pend, pr["pending"] = pr["pending"], None
+        if pend is None:
+            return
+        a, b = pend
+        if self._native and not self._timing:
+            self.reducer.set_timing(False)
+        if b is None:
+            return
+        b.synchronize()
+        tim = self.reducer.last_timings() if self._native else []
+        if tim:
+            pr["samples"].append((a.elapsed_time(b), sum(t[1] for t in tim)))
+
+    def _budget_decide(self):
+        pr = self._budget_probe
+        if pr["samples"]:
+            fb = min(s[0] for s in pr["samples"])
+            cm = min(s[1] for s in pr["samples"])
+            source = "measured"
+        else:
+            fb, cm, source = 0.0, pr["comm_ms_model"], "model"
+        v = torch.tensor([fb, cm, float(len(pr["samples"]))], dtype=torch.float64)
+        if self.world_size > 1 and dist.is_initialized():
+            dist.all_reduce(v, op=dist.ReduceOp.MAX)  # control plane: one decision for every rank
+            m = torch.tensor([float(len(pr["samples"]))], dtype=torch.float64)
+            dist.all_reduce(m, op=dist.ReduceOp.MIN)
+            if m.item() == 0:  # some rank has no sample: everyone falls back to the model
+                source = "model"
+        fb, cm = v[0].item(), v[1].item()
+        if source == "model":
+            cm = pr["comm_ms_model"]
+        duty = cm / max(1e-3, fb * 2.0 / 3.0) if fb > 0 else float("inf")
+        keep = duty >= pr["min_duty"]
+        pr["decision"] = {"source": source, "fwd_bwd_ms": round(fb, 3), "comm_ms": round(cm, 3),
+                          "comm_ms_model": round(pr["comm_ms_model"], 3), "samples": len(pr["samples"]),
+                          "duty": round(duty, 4) if fb > 0 else None, "min_duty": pr["min_duty"],
+                          "reserve_slots": pr["reserve"], "budget": keep}
+        if not keep:
+            from .dist import set_cu_budget
+
+            set_cu_budget(0)
 
     def _budget_probe_forward(self):
         pr = self._budget_probe
         if pr is None or pr["decision"] is not None:
             return
         pr["step"] += 1
-        # completed (forward start, backward end) pairs -> samples; the host may run a step ahead of the GPU
-        keep = []
-        for a, b in pr["ev"]:
-            if b is not None and b.query():
-                pr["samples"].append(a.elapsed_time(b))
-            elif b is not None:
-                keep.append([a, b])
-        pr["ev"] = keep
-        if pr["samples"]:  # (one step's time decides: the duties compared differ by ~10x)
-            fb_ms = min(pr["samples"])
-            duty = pr["comm_ms"] / max(1e-3, fb_ms * 2.0 / 3.0)
-            pr["decision"] = {"fwd_bwd_ms": round(fb_ms, 3), "comm_ms_model": round(pr["comm_ms"], 3),
-                              "duty": round(duty, 4), "budget": duty >= pr["min_duty"]}
-            pr["ev"] = []
-            if duty < pr["min_duty"]:
-                from .dist import set_cu_budget
-
-                set_cu_budget(0)
+        self._budget_collect()
+        if len(pr["samples"]) >= pr["nsamples"] or pr["step"] > pr["nsamples"] + 4:
+            self._budget_decide()
             return
-        if pr["step"] >= 2 and len(pr["ev"]) < 4:  # step 1: warm-up (allocator, bucket rebuild)
+        if pr["step"] >= 2:  # step 1: warm-up (allocator, bucket rebuild, first-call costs)
+            if self._native:
+                self.reducer.set_timing(True)
             a = torch.cuda.Event(enable_timing=True)
             a.record()
-            pr["ev"].append([a, None])
+            pr["pending"] = [a, None]
 
     def _budget_probe_backward_end(self):
         pr = self._budget_probe
-        if pr is not None and pr["decision"] is None and pr["ev"] and pr["ev"][-1][1] is None:
+        if pr is not None and pr["decision"] is None and pr["pending"] is not None and pr["pending"][1] is None:
             b = torch.cuda.Event(enable_timing=True)
             b.record()
-            pr["ev"][-1][1] = b
+            pr["pending"][1] = b
+
+    def settle_cu_budget(self):
+        """Decide the adaptive CU budget now (collective: every rank calls it at the same point, e.g. after
+        the warm-up loop) from the steps timed so far; the model decides if none was.  Returns the decision
+        record (``cu_budget_info``)."""
+        pr = self._budget_probe
+        if pr is not None and pr["decision"] is None:
+            self._budget_collect()
+            self._budget_decide()
+        return self.cu_budget_info()
 
     @property
     def cu_budget_decision(self):
         """None until decided (or when not adaptive); else the measured inputs and whether the budget stays."""
         return None if self._budget_probe is None else self._budget_probe["decision"]
 
+    def cu_budget_info(self) -> dict:
+        """The CU-budget state for reports: the adaptive decision, or why there is none."""
+        if self._budget_probe is not None:
+            return self._budget_probe["decision"] or {"source": "pending"}
+        if self.world_size <= 1:
+            return {"source": "off", "reason": "world size 1 (no collectives)", "budget": False}
+        if not (self._params and self._params[0].is_cuda and _has_ext()):
+            return {"source": "off", "reason": "host transport (no GPU compute kernels)", "budget": False}
+        if os.environ.get("DPE_CU_RESERVE"):
+            return {"source": "env", "reserve_slots": int(os.environ["DPE_CU_RESERVE"]),
+                    "budget": int(os.environ["DPE_CU_RESERVE"]) > 0}
+        from ..ops._ext import ext
+
+        r = ext().cu_reserve_config()
+        return {"source": "fixed", "reserve_slots": r, "budget": r > 0}
+
     def _finalize(self):
         self._queued = False
         self._budget_probe_backward_end()
+        if getattr(self, "_transport", None) is not None and not self._native:
+            self._transport.t_bwd_end = time.perf_counter()
         for i, p in enumerate(self._params):  # fresh but never written this step: zero, as stock
             if getattr(p, "_dpe_fresh", False):
                 p._dpe_fresh = False

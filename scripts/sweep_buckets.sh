@@ -9,10 +9,10 @@ OUT=gpurun_out/sweep_buckets_N${N}.jsonl
 mkdir -p gpurun_out && : > $OUT
 for MB in 5 10 25 50 100; do
   if [ "$N" = "1" ]; then
-    timeout -k 10 300 python bench.py --steps 10 --warmup 3 --bucket-mb $MB --bucket-timing --force-comm >> $OUT || exit $?
+    timeout -k 10 300 python bench.py --steps 10 --warmup 3 --bucket-mb $MB --bucket-timing 1 --force-comm >> $OUT || exit $?
   else
     timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 \
-      --master-port $((29700 + MB)) bench.py --gpus $N --steps 10 --warmup 3 --bucket-mb $MB --bucket-timing >> $OUT || exit $?
+      --master-port $((29700 + MB)) bench.py --gpus $N --steps 10 --warmup 3 --bucket-mb $MB --bucket-timing 1 >> $OUT || exit $?
   fi
   tail -1 $OUT | python -c "import json,sys; d=json.loads(sys.stdin.read()); b=d.get('buckets',{}); print(f\"bucket {d['config']['bucket_mb']} MB: {d['value']:.0f} {d['unit']}, {b.get('count')} buckets, comm {b.get('comm_ms')} ms, overlap {b.get('overlap_pct')}%\")"
 done

@@ -11,7 +11,7 @@ OUT=$R/gpurun_out/w${N}_$MODEL
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 PORT=$((29500 + RANDOM % 1000))
-args="--gpus $N --model $MODEL --batch-size $BS --steps 6 --warmup 3 --bucket-timing"
+args="--gpus $N --model $MODEL --batch-size $BS --steps 6 --warmup 3"
 pids=()
 for r in $(seq 1 $((N - 1))); do
   RANK=$r WORLD_SIZE=$N LOCAL_RANK=0 LOCAL_WORLD_SIZE=$N MASTER_ADDR=127.0.0.1 MASTER_PORT=$PORT \

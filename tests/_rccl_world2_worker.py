@@ -188,5 +188,68 @@ def main_gpt2():
     pdist.destroy_process_group()
 
 
+def main_ovopt():
+    """DDP.overlap_optimizer at world N: the optimizer stream must wait for each bucket's
+    RCCL all-reduce (Reducer.stream_wait_comm) -- and, on the bf16 hook path, for the cast-back on the
+    comm stream -- before stepping it.  Against the same model stepped after backward: the parameters
+    after 4 steps (one bucket rebuild included) agree to the model's own run-to-run noise, and every
+    rank holds bitwise the same parameters (a too-early wait would step un-reduced, rank-local grads)."""
+    from distributed_pytorch_example_amd.models import get_model
+    from distributed_pytorch_example_amd.optim import build_optimizer
+    from distributed_pytorch_example_amd.parallel.hooks import bf16_compress_hook
+
+    rank, world, _ = pdist.init_process_group("rccl")
+    dev = torch.device("cuda", 0)
+    out = []
+    for model, opt_name in (("resnet_tiny", "sgd"), ("gpt2_tiny", "adamw")):
+        for comp in (None, "bf16"):
+            torch.manual_seed(300)  # same init on every rank (the init broadcast also aligns them)
+            kw = {"num_classes": 10} if model == "resnet_tiny" else {}
+            base = get_model(model, **kw).to(dev)
+            runs = {}
+            for overlap in (False, "again", True):
+                m = copy.deepcopy(base)
+                ddp = DDP(m, bucket_cap_mb=0.25, first_bucket_mb=0.05)
+                if comp == "bf16":
+                    ddp.register_comm_hook(None, bf16_compress_hook)
+                assert ddp._native and ddp.reducer.world == world
+                opt = build_optimizer(opt_name, m.parameters(), lr=1e-2, weight_decay=1e-2)
+                if overlap is True:
+                    ddp.overlap_optimizer(opt)
+                g = torch.Generator(device=dev).manual_seed(11 + rank)  # rank-local data: grads differ
+                for step in range(4):
+                    if model == "resnet_tiny":
+                        x = torch.randn(8, 3, 32, 32, device=dev, generator=g)
+                        y = torch.randint(0, 10, (8,), device=dev, generator=g)
+                        loss = Fx.cross_entropy(ddp(x), y, 10)
+                    else:
+                        x = torch.randint(0, 512, (2, 64), device=dev, generator=g)
+                        y = torch.randint(0, 512, (2, 64), device=dev, generator=g)
+                        loss = ddp(x, y)
+                    loss.backward()
+                    opt.step()
+                    for p in m.parameters():
+                        p.grad = None
+                torch.cuda.synchronize()
+                assert ddp.num_buckets() > 2
+                runs[overlap] = [p.detach().float().clone() for p in m.parameters()]
+                # identical on every rank: the all-reduced gradients are the same bits everywhere
+                flat = torch.cat([p.reshape(-1) for p in runs[overlap]]).cpu()
+                allf = [torch.empty_like(flat) for _ in range(world)]
+                dist.all_gather(allf, flat)
+                assert all(torch.equal(allf[0], f) for f in allf), (model, comp, overlap, "ranks diverged")
+
+            def dev_(x, y):
+                return max(((a - b).abs().max() / (b.abs().max() + 1e-30)).item() for a, b in zip(x, y))
+
+            noise = dev_(runs["again"], runs[False])
+            d = dev_(runs[True], runs[False])
+            assert d <= 10 * noise + 1e-6, (model, comp, d, noise)
+            out.append(f"{model}/{comp or 'fp32'} {d:.1e} (noise {noise:.1e})")
+    print(f"rank {rank} ok: world-{world} overlap_optimizer " + ", ".join(out), flush=True)
+    pdist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    main_gpt2() if len(sys.argv) > 1 and sys.argv[1] == "gpt2" else main()
+    mode = sys.argv[1] if len(sys.argv) > 1 else ""
+    {"gpt2": main_gpt2, "ovopt": main_ovopt}.get(mode, main)()

@@ -40,6 +40,24 @@ def test_bench_json_line_torchrun_world2():
     assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 128
     # whole-job aggregate: samples/s = per-GPU batch * world * steps / time
     assert abs(d["value"] - 64 * 2 * 1000.0 / d["ms_per_step"]) / d["value"] < 0.01
+    # a multi-rank run documents its communication by default (one untimed
+    # instrumented step after the timed loop) and records where the CU-budget decision came from
+    b = d["buckets"]
+    assert b["count"] >= 1 and len(b["per_bucket"]) == b["count"] and b["comm_ms"] > 0
+    assert all(r["allreduce_ms"] >= 0 and r["bytes"] > 0 for r in b["per_bucket"])
+    assert "overlap_pct" in b
+    assert "source" in d["config"]["cu_budget"]
+
+
+def test_bench_bare_multi_gpu_refused():
+    """`python bench.py --gpus 2` without a launcher must fail, not report a one-GPU number."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "simplenet",
+                        "--steps", "1", "--warmup", "0"], cwd="/tmp", env=env, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=300)
+    assert p.returncode != 0
+    assert not _json_lines(p.stdout), p.stdout
+    assert "torch.distributed.run" in p.stderr, p.stderr[-1000:]
 
 
 def test_bench_defaults_single_process():

@@ -300,8 +300,10 @@ def test_channel_cap_is_opt_in_and_follows_env(monkeypatch):
 
 
 def test_adaptive_cu_budget_decision(monkeypatch):
-    """DDP drops the CU budget when the modelled all-reduce time is a small part of backward
-    (parallel/ddp.py, adaptive CU budget), from event timings the host may see a step late."""
+    """DDP drops the CU budget when the MEASURED all-reduce time (the reducer's per-bucket events of a
+    few timed warm-up steps) is a small part of backward (parallel/ddp.py, adaptive CU budget); the
+    minimum over the samples decides (a first-call-inflated step does not), and with no timed step the
+    bandwidth model decides (``settle_cu_budget``)."""
     import torch
 
     from distributed_pytorch_example_amd.parallel import ddp as D
@@ -311,36 +313,60 @@ def test_adaptive_cu_budget_decision(monkeypatch):
         t = 0.0
 
         def __init__(self, enable_timing=False):
-            self.ts, self.done = None, False
+            self.ts = None
 
         def record(self):
             Ev.t += 10.0
             self.ts = Ev.t
 
-        def query(self):
-            return self.done
+        def synchronize(self):
+            pass
 
         def elapsed_time(self, other):
             return other.ts - self.ts
+
+    class Red:
+        def __init__(self, comm):
+            self.comm, self.timing, self.step = comm, False, 0
+
+        def set_timing(self, on):
+            self.timing = on
+
+        def last_timings(self):  # two buckets; the first timed step pays a first-call cost
+            self.step += 1
+            c = self.comm * (4.0 if self.step == 1 else 1.0)
+            return [(0, c / 2, -1.0), (1, c / 2, 0.0)]
 
     monkeypatch.setattr(torch.cuda, "Event", Ev)
     calls = []
     monkeypatch.setattr(pd, "set_cu_budget", lambda n: calls.append(n))
 
-    def run(comm_ms):
+    def make(comm_ms, model_ms=0.2):
         m = D.DistributedDataParallel.__new__(D.DistributedDataParallel)
-        m._budget_probe = {"step": 0, "ev": [], "samples": [], "comm_ms": comm_ms, "min_duty": 0.10, "decision": None}
+        object.__setattr__(m, "_native", True)
+        object.__setattr__(m, "_timing", False)
+        object.__setattr__(m, "world_size", 1)
+        object.__setattr__(m, "reducer", Red(comm_ms))
+        m._budget_probe = {"step": 0, "pending": None, "samples": [], "comm_ms_model": model_ms, "nsamples": 3,
+                           "min_duty": 0.10, "decision": None, "reserve": 32}
+        return m
+
+    def run(comm_ms):
+        m = make(comm_ms)
         for _ in range(8):
             m._budget_probe_forward()
             m._budget_probe_backward_end()  # fwd+bwd = 10 "ms" per step in the fake clock
-            for pair in m._budget_probe["ev"][:-1]:  # the GPU finishes a step one forward late
-                pair[1].done = True
             if m.cu_budget_decision is not None:
                 break
+        assert m.reducer.timing is False  # timing switched off again after the probe
         return m.cu_budget_decision
 
-    d = run(0.2)  # duty 0.2 / (10 * 2/3) = 3 %: dropped
-    assert d is not None and d["budget"] is False and calls == [0]
+    d = run(0.2)  # measured duty 0.2 / (10 * 2/3) = 3 % (the 4x first sample ignored): dropped
+    assert d is not None and d["source"] == "measured" and d["samples"] == 3 and d["budget"] is False
+    assert d["comm_ms"] == 0.2 and calls == [0]
     calls.clear()
     d = run(3.0)  # 45 %: kept
     assert d is not None and d["budget"] is True and calls == []
+    m = make(3.0, model_ms=0.2)  # settled before any timed step: the model decides (no fwd/bwd time: keep)
+    d = m.settle_cu_budget()
+    assert d["source"] == "model" and d["comm_ms"] == 0.2 and d["budget"] is True

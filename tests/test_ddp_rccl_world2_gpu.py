@@ -86,6 +86,17 @@ def test_native_reducer_world2_rccl_gpt2():
 
 
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_overlap_optimizer_world2_rccl():
+    """the optimizer-in-backward stream waits for each bucket's real RCCL
+    all-reduce (fp32, and bf16 with the cast-back on the comm stream); parameters match the
+    step-after run and are bitwise identical across ranks (tests/_rccl_world2_worker.py main_ovopt)."""
+    codes, outs = _run_world2([os.path.join(ROOT, "tests", "_rccl_world2_worker.py"), "ovopt"], timeout=150)
+    assert codes == [0, 0], "\n".join(o[-3000:] for o in outs)
+    for o in outs:
+        print([ln for ln in o.splitlines() if "ok: world-2" in ln][0])
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
 def test_rank_death_mid_allreduce_aborts_survivor(tmp_path):
     """Failure detection on the real RCCL path: rank 1 SIGKILLs itself at batch 3 of
     epoch 0 (DPE_FAULT_INJECT) while rank 0 keeps issuing bucket all-reduces that can never complete.
