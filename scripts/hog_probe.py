@@ -10,7 +10,13 @@ around `reserve` slots during that window (the CU budget the reducer applies at 
 csrc/comm/comm.cpp); `set_comm_active` brackets the backward as Reducer::launch / finalize do.
 
     python scripts/hog_probe.py --model resnet50 --modes 0:0 16:0 16:16 0:16     (hogs:reserve pairs)
-prints one JSON line per mode (median / min ms per step over alternating rounds)."""
+prints one JSON line per mode (median / min ms per step over alternating rounds).
+
+Production path (default, --ddp 1): the model runs under DDP at world 1 with the W = 8 bucket layout
+(parallel/buckets.py xgmi_bucket_policy(8)), so the gradients are bucket views, the overwrite-mode
+first writes and GPT-2's grouped whole-round weight-grad launches are live exactly as in bench.py;
+the windowed hogs start when the reducer issues a bucket (its transport's on_launch, index order), and
+each round of --steps steps is timed as one window with no synchronisation inside it."""
 import argparse
 import json
 import os
@@ -41,6 +47,7 @@ ap.add_argument("--windowed", type=float, default=0.0,
                      "blocks at 8 ranks instead of the whole-backward worst case")
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--modes", nargs="+", default=["0:0", "16:0", "16:16", "0:16"])
+ap.add_argument("--ddp", type=int, default=1, help="1: through DDP (production path); 0: the bare model (round-5 probe)")
 args = ap.parse_args()
 
 C = ext()
@@ -54,7 +61,7 @@ if args.model == "resnet50":
     y = torch.randint(0, 1000, (bs,), device=dev)
 
     def fwd():
-        return Fx.cross_entropy(model(x), y, 1000)
+        return Fx.cross_entropy(net(x), y, 1000)
 else:
     bs = args.batch_size or 8
     model = get_model("gpt2").to(dev)
@@ -63,15 +70,25 @@ else:
     y = torch.randint(0, 50257, (bs, 1024), device=dev)
 
     def fwd():
-        return model(x, y)
+        return net(x, y)
 
+net = model
+ddp = None
+if args.ddp:
+    from distributed_pytorch_example_amd.parallel import DDP
+    from distributed_pytorch_example_amd.parallel.buckets import xgmi_bucket_policy
+
+    # world 1: no collectives, but the W = 8 bucket layout and every gradient-as-bucket-view path
+    f8, c8, l8 = xgmi_bucket_policy(8, 4 * sum(p.numel() for p in model.parameters()))
+    ddp = DDP(model, bucket_cap_mb=c8, first_bucket_mb=f8, last_bucket_mb=l8 or 0, rebuild_buckets=False)
+    net = ddp
 side = torch.cuda.Stream()
 stop = torch.zeros(1, dtype=torch.int32, device=dev)
 modes = [tuple(int(v) for v in m.split(":")) for m in args.modes]
 
 # windowed: the W = 8 buckets (same policy and ready order as DDP: reverse registration order)
 params = [p for p in model.parameters() if p.requires_grad]
-win = {"on": False, "hogs": 0, "pending": [], "left": []}
+win = {"on": False, "hogs": 0, "pending": [], "left": [], "reserve": 0}
 if args.windowed > 0:
     from distributed_pytorch_example_amd.parallel.buckets import assign_buckets, xgmi_bucket_policy
 
@@ -96,8 +113,29 @@ if args.windowed > 0:
             with torch.cuda.stream(side):
                 C.cu_hog(win["hogs"], args.threads, args.lds, bucket_us[b], args.vgprs, stop, mode=args.sleepy)
 
-    for p in params:
-        p.register_post_accumulate_grad_hook(on_grad)
+    def launch_window(b):
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            C.cu_hog(win["hogs"], args.threads, args.lds, bucket_us[b], args.vgprs, stop, mode=args.sleepy)
+
+    if ddp is not None:
+        # the reducer issues bucket b (index order, as the RCCL reducer would start its all-reduce)
+        assert [list(i) for i in ddp.bucket_indices] == [list(i) for i in buckets], "bucket layout differs from the W=8 policy"
+        tr = ddp._transport
+        orig = tr.on_launch
+
+        def on_launch(b, _orig=orig):
+            if win["on"]:
+                launch_window(b)
+            if win["reserve"] > 0:
+                C.set_comm_active(True)  # as Reducer::launch: the budget from the first bucket issue on
+            return _orig(b)
+
+        tr.on_launch = on_launch
+        ddp.reducer = C.Reducer.host(ddp.buckets, ddp.bucket_indices, len(ddp._params), 1, tr.on_launch, tr.on_finalize)
+    else:
+        for p in params:
+            p.register_post_accumulate_grad_hook(on_grad)
 
 
 def step(hogs, reserve):
@@ -111,7 +149,9 @@ def step(hogs, reserve):
         with torch.cuda.stream(side):
             C.cu_hog(hogs, args.threads, args.lds, 200000.0, args.vgprs, stop, mode=args.sleepy)  # bounded: 200 ms
     C.set_cu_reserve(reserve)
-    C.set_comm_active(reserve > 0)
+    win["reserve"] = reserve
+    if ddp is None or args.windowed <= 0:
+        C.set_comm_active(reserve > 0)  # whole backward (DDP windowed: from the first bucket issue)
     loss.backward()
     C.set_comm_active(False)
     win["on"] = False
@@ -131,6 +171,13 @@ for _ in range(args.rounds):
     for m in modes:
         step(*m)  # untimed: settles the allocator for this mode
         torch.cuda.synchronize()
+        if args.ddp:  # one window of --steps steps, no synchronisation inside (as bench.py times)
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step(*m)
+            torch.cuda.synchronize()
+            res[m].append((time.perf_counter() - t0) * 1e3 / args.steps)
+            continue
         for _ in range(args.steps):
             t0 = time.perf_counter()
             step(*m)
@@ -142,6 +189,6 @@ for m in modes:
     ts = sorted(res[m])
     med = ts[len(ts) // 2]
     base = med if base is None else base
-    print(json.dumps({"model": args.model, "batch": bs, "hogs": m[0], "reserve": m[1], "windowed": args.windowed, "threads": args.threads,
+    print(json.dumps({"model": args.model, "ddp": args.ddp, "batch": bs, "hogs": m[0], "reserve": m[1], "windowed": args.windowed, "threads": args.threads,
                       "lds": args.lds, "vgprs": args.vgprs, "sleepy": args.sleepy, "ms_step_median": round(med, 3),
                       "ms_step_min": round(ts[0], 3), "vs_first_mode": round(med / base, 4)}), flush=True)
