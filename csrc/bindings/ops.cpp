@@ -66,6 +66,10 @@ int dpe_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N,
                     int s, int p, hipStream_t st);
 int dpe_gavgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st);
 int dpe_gavgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st);
+int dpe_cross_entropy_mean(const void* logits, int in_bf16, const int64_t* labels, int B, int V, int64_t ld,
+                           float grad_scale, void* dlogits, int out_bf16, float* loss_rows, float* out4, int ignore_index,
+                           hipStream_t st);
+int dpe_ce_grad_scale(const void* d, void* o, int64_t n, int bf16, const float* g, const float* inv_n, hipStream_t st);
 int dpe_cross_entropy(const void* logits, int in_bf16, const int64_t* labels, int B, int V, int64_t ld, float grad_scale,
                       void* dlogits, int out_bf16, float* loss_rows, float* loss_sum, float* correct, int ignore_index,
                       hipStream_t st);
@@ -1727,6 +1731,46 @@ std::vector<Tensor> cross_entropy(const Tensor& logits, const Tensor& labels, in
   return {rows, sums.slice(0, 0, 1), sums.slice(0, 1, 2), d};
 }
 
+// Training form: (out4 = [loss_sum, correct, mean over non-ignored rows, 1 / their count], dlogits).  The
+// mean and the backward scale come out of the reduction kernel itself (no torch count / clamp / divide
+// launches at the forward -> backward seam).
+std::vector<Tensor> cross_entropy_mean(const Tensor& logits, const Tensor& labels, int64_t V, bool grad_bf16,
+                                       int64_t ignore_index, bool inplace) {
+  CHECK_GPU(logits); CHECK_CONTIG(logits); CHECK_CONTIG(labels);
+  TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
+  const bool in_bf16 = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(in_bf16 || logits.scalar_type() == at::kFloat, "logits must be f32 or bf16");
+  const int64_t ld = logits.size(-1), B = logits.numel() / ld;
+  TORCH_CHECK(labels.numel() == B, "labels size mismatch");
+  auto fo = logits.options().dtype(at::kFloat);
+  Tensor rows = at::empty({B}, fo);
+  Tensor out4 = at::zeros({4}, fo);
+  Tensor d;
+  if (inplace) {
+    TORCH_CHECK(grad_bf16 == in_bf16, "cross_entropy: in-place gradient needs the logits dtype");
+    d = logits;
+  } else {
+    d = at::empty(logits.sizes(), logits.options().dtype(grad_bf16 ? at::kBFloat16 : at::kFloat));
+  }
+  CHECK_RC(dpe_cross_entropy_mean(logits.data_ptr(), in_bf16, (const int64_t*)labels.data_ptr(), (int)B, (int)V, ld, 1.f,
+                                  d.data_ptr(), grad_bf16, fp(rows), fp(out4), (int)ignore_index, cur_stream()),
+           "cross_entropy_mean");
+  return {out4, d};
+}
+
+// d * g * inv_n (g, inv_n: one-element fp32 device tensors) in the dtype of d
+Tensor ce_grad_scale(const Tensor& d, const Tensor& g, const Tensor& inv_n) {
+  CHECK_GPU(d); CHECK_CONTIG(d); CHECK_F32(g); CHECK_F32(inv_n);
+  const bool bf = d.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || d.scalar_type() == at::kFloat, "ce_grad_scale: f32 or bf16");
+  TORCH_CHECK(g.numel() == 1 && inv_n.numel() == 1 && g.is_cuda() && inv_n.is_cuda(), "ce_grad_scale: device scalars");
+  Tensor o = at::empty_like(d);
+  CHECK_RC(dpe_ce_grad_scale(d.data_ptr(), o.data_ptr(), d.numel(), bf ? 1 : 0, fp(g.contiguous()), fp(inv_n.contiguous()),
+                             cur_stream()),
+           "ce_grad_scale");
+  return o;
+}
+
 // ---------------------------------------------------------------- eltwise
 Tensor cast_bf16(const Tensor& x, const c10::optional<Tensor>& out) {
   CHECK_GPU(x); CHECK_F32(x); CHECK_CONTIG(x);
@@ -2067,6 +2111,10 @@ void register_ops(pybind11::module& m) {
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("gavgpool_fwd", &gavgpool_fwd);
   m.def("gavgpool_bwd", &gavgpool_bwd);
+  m.def("cross_entropy_mean", &cross_entropy_mean, py::arg("logits"), py::arg("labels"), py::arg("V"),
+        py::arg("grad_bf16"), py::arg("ignore_index") = -100, py::arg("inplace") = false,
+        "training CE: (out4 = [sum, correct, mean, 1/n_valid], softmax - onehot)");
+  m.def("ce_grad_scale", &ce_grad_scale, py::arg("d"), py::arg("g"), py::arg("inv_n"), "d * g * inv_n (device scalars)");
   m.def("cross_entropy", &cross_entropy, py::arg("logits"), py::arg("labels"), py::arg("V"), py::arg("grad_scale"),
         py::arg("want_grad"), py::arg("grad_bf16"), py::arg("ignore_index") = -100, py::arg("inplace") = false);
   m.def("cast_bf16", &cast_bf16, py::arg("x"), py::arg("out") = py::none());

@@ -7,6 +7,9 @@
 // (GPT-2 pads its vocab to a multiple of 64).  Per row: loss_i = lse - z_y.
 // dlogits (optional) = (softmax - onehot) * grad_scale, written in the
 // dtype requested (bf16 feeds the dgrad/wgrad GEMMs directly).
+#include <algorithm>
+#include <type_traits>
+
 #include "common.h"
 
 namespace dpe {
@@ -233,18 +236,50 @@ __global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 1) void ce_vec_kernel(const TI
 
 // loss_sum[0] += sum of the B per-row losses in a fixed order (thread t takes rows t, t + 256, ...,
 // then a fixed-shape tree): the reported loss is bitwise reproducible, unlike a float atomicAdd per
-// row whose order follows the block schedule.
-__global__ __launch_bounds__(256) void ce_sum_kernel(const float* __restrict__ rows, int B, float* __restrict__ out) {
+// row whose order follows the block schedule.  With labels: out[2] = the mean over the rows whose
+// label is not ignore_index (torch's reduction="mean"; 0 valid rows -> divided by 1) and out[3] = 1 / that
+// count -- the mean loss and its backward scale without the count / clamp / divide kernels of a
+// torch-level reduction (the forward -> backward seam is launch-bound: ~10 tiny kernels there).
+__global__ __launch_bounds__(256) void ce_sum_kernel(const float* __restrict__ rows, int B, float* __restrict__ out,
+                                                     const int64_t* __restrict__ labels, int ignore_index) {
   __shared__ float sh[256];
+  __shared__ int shn[256];
   float s = 0.f;
-  for (int i = threadIdx.x; i < B; i += 256) s += rows[i];
+  int n = 0;
+  for (int i = threadIdx.x; i < B; i += 256) {
+    s += rows[i];
+    if (labels) n += labels[i] != (int64_t)ignore_index;
+  }
   sh[threadIdx.x] = s;
+  shn[threadIdx.x] = n;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    if ((int)threadIdx.x < o) {
+      sh[threadIdx.x] += sh[threadIdx.x + o];
+      shn[threadIdx.x] += shn[threadIdx.x + o];
+    }
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[0] += sh[0];
+  if (threadIdx.x == 0) {
+    const float tot = out[0] + sh[0];
+    out[0] = tot;
+    if (labels) {
+      const float cnt = (float)max(shn[0], 1);
+      out[2] = tot / cnt;
+      out[3] = 1.f / cnt;
+    }
+  }
+}
+
+// d_out = d * (*g) * (*inv_n): the mean cross-entropy's backward scale (device scalars) in one pass
+template <typename T>
+__global__ __launch_bounds__(256) void ce_grad_scale_kernel(const T* __restrict__ d, T* __restrict__ o, int64_t n,
+                                                            const float* __restrict__ g, const float* __restrict__ inv_n) {
+  const float sc = g[0] * inv_n[0];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    if constexpr (std::is_same<T, float>::value) o[i] = d[i] * sc;
+    else o[i] = f2bf(bf2f(d[i]) * sc);
+  }
 }
 
 template <typename TIn, typename TOut>
@@ -286,8 +321,32 @@ extern "C" int dpe_cross_entropy(const void* logits, int in_bf16, const int64_t*
   if (dlogits == logits && in_bf16 != out_bf16) return -2;  // in-place needs equal dtypes
   const int rc = dpe_cross_entropy_rows(logits, in_bf16, labels, B, V, ld, grad_scale, dlogits, out_bf16, loss_rows, loss_sum,
                                         correct, ignore_index, st);
-  if (rc == 0 && loss_rows && loss_sum) hipLaunchKernelGGL(ce_sum_kernel, dim3(1), dim3(256), 0, st, loss_rows, B, loss_sum);
+  if (rc == 0 && loss_rows && loss_sum)
+    hipLaunchKernelGGL(ce_sum_kernel, dim3(1), dim3(256), 0, st, loss_rows, B, loss_sum, (const int64_t*)nullptr, 0);
   return rc;
+}
+
+// as dpe_cross_entropy, and out4[2] = mean over the non-ignored rows, out4[3] = 1 / their count (out4 = loss_sum)
+extern "C" int dpe_cross_entropy_mean(const void* logits, int in_bf16, const int64_t* labels, int B, int V, int64_t ld,
+                                      float grad_scale, void* dlogits, int out_bf16, float* loss_rows, float* out4,
+                                      int ignore_index, hipStream_t st) {
+  if (dlogits == logits && in_bf16 != out_bf16) return -2;
+  const int rc = dpe_cross_entropy_rows(logits, in_bf16, labels, B, V, ld, grad_scale, dlogits, out_bf16, loss_rows, out4,
+                                        out4 + 1, ignore_index, st);
+  if (rc == 0) hipLaunchKernelGGL(ce_sum_kernel, dim3(1), dim3(256), 0, st, loss_rows, B, out4, labels, ignore_index);
+  return rc;
+}
+
+extern "C" int dpe_ce_grad_scale(const void* d, void* o, int64_t n, int bf16, const float* g, const float* inv_n,
+                                 hipStream_t st) {
+  const int grid = (int)std::min<int64_t>(2048, (n + 255) / 256);
+  if (grid <= 0) return 0;
+  if (bf16)
+    hipLaunchKernelGGL(ce_grad_scale_kernel<uint16_t>, dim3(grid), dim3(256), 0, st, (const uint16_t*)d, (uint16_t*)o, n, g,
+                       inv_n);
+  else
+    hipLaunchKernelGGL(ce_grad_scale_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)d, (float*)o, n, g, inv_n);
+  return 0;
 }
 
 static int dpe_cross_entropy_rows(const void* logits, int in_bf16, const int64_t* labels, int B, int V, int64_t ld,

@@ -525,21 +525,21 @@ def global_avg_pool_nhwc(x):
 
 # ===================================================================== loss
 class _CEFn(Function):
+    """Mean CE: the kernel pair (per-row pass + fixed-order reduction) also yields the mean over the
+    non-ignored rows and 1 / their count, and backward is one scaling pass -- no torch-level count /
+    clamp / divide / cast kernels at the launch-bound forward -> backward seam."""
+
     @staticmethod
     def forward(ctx, logits, labels, num_classes: int, ignore_index: int):
-        rows, s, correct, d = ext().cross_entropy(logits.contiguous(), labels.contiguous(), num_classes, 1.0, True,
-                                                  logits.dtype == torch.bfloat16, ignore_index)
-        n = (labels != ignore_index).sum().clamp_min(1).to(torch.float32)
-        ctx.save_for_backward(d)
-        ctx.n = n
-        ctx.correct = correct
-        return s.reshape(()) / n
+        out4, d = ext().cross_entropy_mean(logits.contiguous(), labels.contiguous(), num_classes,
+                                           logits.dtype == torch.bfloat16, ignore_index)
+        ctx.save_for_backward(d, out4)
+        return out4[2:3].reshape(())
 
     @staticmethod
     def backward(ctx, g):
-        (d,) = ctx.saved_tensors
-        scale = g / ctx.n
-        return (d * scale.to(d.dtype)), None, None, None
+        d, out4 = ctx.saved_tensors
+        return ext().ce_grad_scale(d, g.float().reshape(1), out4[3:4]), None, None, None
 
 
 def cross_entropy(logits, labels, num_classes: Optional[int] = None, ignore_index: int = -100):
@@ -780,18 +780,17 @@ class _LMHeadCEFn(Function):
         xb = xb.reshape(-1, xb.shape[-1])
         logits = C.linear_fwd(xb, w16, None, 0, False, None, None)
         lab = labels.reshape(-1).contiguous()
-        _, s, _, d = C.cross_entropy(logits, lab, wte.shape[0], 1.0, True, True, ignore_index, True)
-        n = (lab != ignore_index).sum().clamp_min(1).to(torch.float32)
-        ctx.save_for_backward(xb, d, n)
+        out4, d = C.cross_entropy_mean(logits, lab, wte.shape[0], True, ignore_index, True)
+        ctx.save_for_backward(xb, d, out4)
         ctx.wte, ctx.pad, ctx.xshape = wte, pad_rows, x.shape
         note_use(wte)
-        return s.reshape(()) / n
+        return out4[2:3].reshape(())  # mean over the non-ignored tokens (kernel-side count)
 
     @staticmethod
     def backward(ctx, g):
         C = ext()
-        xb, d, n = ctx.saved_tensors
-        scale = (g.float() / n).reshape(1).contiguous()
+        xb, d, out4 = ctx.saved_tensors
+        scale = g.float().reshape(1) * out4[3:4]  # dL/dlogits = (softmax - onehot) * g / n, applied by the GEMMs
         dx = C.linear_dgrad(d, shadow(ctx.wte, ctx.pad), None, scale)
         buf, direct = grad_sink(ctx.wte)
         C.linear_wgrad(d, xb, buf, 1.0, scale, None, 0, direct and grad_fresh(ctx.wte))
