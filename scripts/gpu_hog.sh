@@ -9,10 +9,12 @@ NB=${1:-16}; TH=${2:-256}; LDS=${3:-20480}; VG=${4:-64}; MODE=${5:-0}
 # WINDOWED=<GB/s>: hogs only in the modelled W = 8 bucket all-reduce windows (scripts/hog_probe.py --windowed)
 H="--threads $TH --lds $LDS --vgprs $VG --sleepy $MODE --windowed ${WINDOWED:-0}"
 cd $R
+if [ "${TRACE_ONLY:-0}" != "1" ]; then
 timeout -k 10 300 python3 scripts/hog_probe.py --model resnet50 $H --modes 0:0 $NB:0 $NB:$NB 0:$NB > gpurun_out/hog/rn.jsonl 2>&1 || { tail -20 gpurun_out/hog/rn.jsonl; exit 1; }
 cat gpurun_out/hog/rn.jsonl
 timeout -k 10 300 python3 scripts/hog_probe.py --model gpt2 $H --modes 0:0 $NB:0 $NB:$NB 0:$NB > gpurun_out/hog/gpt2.jsonl 2>&1 || { tail -20 gpurun_out/hog/gpt2.jsonl; exit 1; }
 cat gpurun_out/hog/gpt2.jsonl
+fi
 cd /tmp && export TMPDIR=/tmp
 for model in resnet50 gpt2; do
   mark=sgd_kernel; [ $model = gpt2 ] && mark=adam_kernel
