@@ -745,7 +745,9 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = gelu_fwd(v[e]);
           } else if constexpr (ACT == HACT_GELU_BWD) {
-            const u32x2 a = c < qN ? *(const u32x2*)(p.aux_in + (int64_t)r * qldc + c) : u32x2{0u, 0u};
+            // unconditional load (clamped column): a load under the lane-divergent c < qN test got a full
+            // vmcnt wait of its own; a column past N is never stored, so its value does not matter
+            const u32x2 a = *(const u32x2*)(p.aux_in + (int64_t)r * qldc + (c < qN ? c : 0));
             v[0] *= gelu_grad(__uint_as_float(a[0] << 16));
             v[1] *= gelu_grad(__uint_as_float(a[0] & 0xffff0000u));
             v[2] *= gelu_grad(__uint_as_float(a[1] << 16));
@@ -775,23 +777,34 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
             mu = *(const f32x4*)(p.st_coef + 2 * qN + cc);
           }
           f32x4 s1 = f32x4{0.f, 0.f, 0.f, 0.f}, s2 = f32x4{0.f, 0.f, 0.f, 0.f};
+          // the pre-BN inputs of this column fragment's rows, all loads issued before the first use and
+          // unconditionally (clamped row / column; invalid rows masked below): under the lane-divergent
+          // row test each load was followed by its own full vmcnt wait -- 2*FMH round trips per fragment
+          u32x2 xr[ACT == HACT_BNB ? 2 * FMH : 1];
+          if constexpr (ACT == HACT_BNB) {
+#pragma unroll
+            for (int i = 0; i < 2 * FMH; ++i) {
+              const int r = min(rbase + (i / FMH) * RH + (i % FMH) * 16, qM - 1);
+              xr[i] = *(const u32x2*)(p.st_x + (int64_t)r * qldc + cc);
+            }
+          }
 #pragma unroll
           for (int i = 0; i < 2 * FMH; ++i) {
             const int r = rbase + (i / FMH) * RH + (i % FMH) * 16;
-            if (r < qM && cv) {
-              const float v4[4] = {__uint_as_float(pk[i][j][0] << 16), __uint_as_float(pk[i][j][0] & 0xffff0000u),
-                                   __uint_as_float(pk[i][j][1] << 16), __uint_as_float(pk[i][j][1] & 0xffff0000u)};
+            const bool rv = r < qM && cv;
+            const float v4[4] = {__uint_as_float(pk[i][j][0] << 16), __uint_as_float(pk[i][j][0] & 0xffff0000u),
+                                 __uint_as_float(pk[i][j][1] << 16), __uint_as_float(pk[i][j][1] & 0xffff0000u)};
+            {
               if constexpr (ACT == HACT_BNB) {
-                const u32x2 xr = *(const u32x2*)(p.st_x + (int64_t)r * qldc + c);
-                const float x4[4] = {__uint_as_float(xr[0] << 16), __uint_as_float(xr[0] & 0xffff0000u),
-                                     __uint_as_float(xr[1] << 16), __uint_as_float(xr[1] & 0xffff0000u)};
+                const float x4[4] = {__uint_as_float(xr[i][0] << 16), __uint_as_float(xr[i][0] & 0xffff0000u),
+                                     __uint_as_float(xr[i][1] << 16), __uint_as_float(xr[i][1] & 0xffff0000u)};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                  const float dz = fmaf(x4[e], sc[e], sh[e]) > 0.f ? v4[e] : 0.f;
+                  const float dz = (rv && fmaf(x4[e], sc[e], sh[e]) > 0.f) ? v4[e] : 0.f;
                   s1[e] += dz;
                   s2[e] = fmaf(dz, x4[e] - mu[e], s2[e]);
                 }
-              } else {  // forward statistics of the stored values
+              } else if (rv) {  // forward statistics of the stored values
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                   s1[e] += v4[e];

@@ -302,8 +302,8 @@ DPE_DEVICE float act_fn(float x, int act) {
 // partials are always per 128-row (64 for BM = 64) sub-tile, so the partial layout does not
 // depend on which kernel / tile ran: column (tm * NSUB + sub) of [2][N][stats_ld].
 template <int BM, int BN, int RM, int RN, int NTH, int EPI>
-DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* smem, int m0, int n0, int tm, int wm,
-                              int wn) {
+DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, float alpha, f32x4 (&acc)[RM][RN], char* smem, int m0, int n0, int tm,
+                              int wm, int wn) {
   constexpr int CROW = BN * 2 + 16;
   constexpr int NW = NTH / 64;
   constexpr int SUBM = BM < 128 ? BM : 128, NSUB = BM / SUBM;
@@ -323,7 +323,7 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* sm
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float b = (p.bias && n + e < p.N) ? p.bias[n + e] : 0.f;
-        v[e] = act_fn(p.alpha * acc[i][j][e] + b, p.act);
+        v[e] = act_fn(alpha * acc[i][j][e] + b, p.act);
       }
       u32x2 pk;
       pk[0] = pack_bf2(v[0], v[1]);
@@ -405,23 +405,35 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* sm
   constexpr int RPS = SUBM / RPP;               // rows per thread per stats sub-tile
   constexpr int G = RPS < 4 ? RPS : 4;          // rows whose operand loads are issued together
   const u32x4 z4 = zero16();
-  const bool fast = vec && !p.g.remap && m0 + BM <= p.M;
+  // output row of tile row m: itself, or (phase data grads of strided convs) the real dX pixel of the
+  // virtual row (n, hh, ww) -- remap 1: dgrad-form geometry (virtual output = H x W); 2: forward-form
+  // (OH x OW).  The remapped rows take the batched path too: one row at a time, each waiting for its own
+  // pre-BN / residual load, put the strided 3x3 data grads' epilogues at ~3x their streaming time
+  // (4 phase launches of 52-157 us where the output bytes alone take ~17-50 us).
+  auto orow_of = [&](int m) -> int64_t {
+    if (!p.g.remap) return m;
+    const int VW = p.g.remap == 2 ? p.g.OW : p.g.W, VH = p.g.remap == 2 ? p.g.OH : p.g.H;
+    const int ww = m % VW, t = m / VW, hh = t % VH, nn = t / VH;
+    return ((int64_t)nn * p.g.Hr + p.g.oa + p.g.psh * hh) * p.g.Wr + p.g.ob + p.g.psw * ww;
+  };
+  const bool fast = vec && m0 + BM <= p.M;
 #pragma unroll
   for (int sub = 0; sub < NSUB; ++sub) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
     const int rb = sub * SUBM;
     if (fast) {
-      // full tile, contiguous rows: G rows' residual / pre-BN / mask loads in flight at once
+      // full tile: G rows' residual / pre-BN / mask loads in flight at once
 #pragma unroll
       for (int u0 = 0; u0 < RPS; u0 += G) {
-        u32x4 tv[G], rv[G], xv[G];
+        u32x4 rv[G], xv[G];  // (the staged tile is read from LDS at the row's finish: fewer live registers)
         uint32_t mb[G], rmb[G];
+        int64_t offs[G];
 #pragma unroll
         for (int q = 0; q < G; ++q) {
           const int rr = rb + r0 + (u0 + q) * RPP;
-          const int64_t off = (int64_t)(m0 + rr) * p.ldc + n;
-          tv[q] = *(const u32x4*)(smem + rr * CROW + c * 16);
+          const int64_t off = orow_of(m0 + rr) * p.ldc + n;
+          offs[q] = off;
           rv[q] = p.residual ? (p.res_nt ? __builtin_nontemporal_load((const u32x4*)(p.residual + off))
                                          : ld16(p.residual + off))
                              : z4;
@@ -432,7 +444,7 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* sm
 #pragma unroll
         for (int q = 0; q < G; ++q) {
           const int rr = rb + r0 + (u0 + q) * RPP;
-          finish_row(tv[q], rv[q], xv[q], mb[q], rmb[q], C + (int64_t)(m0 + rr) * p.ldc + n, true);
+          finish_row(*(const u32x4*)(smem + rr * CROW + c * 16), rv[q], xv[q], mb[q], rmb[q], C + offs[q], true);
         }
       }
     } else {
@@ -440,14 +452,7 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, f32x4 (&acc)[RM][RN], char* sm
         const int m = m0 + rr;
         if (m >= p.M) break;
         const u32x4 v = *(const u32x4*)(smem + rr * CROW + c * 16);
-        int64_t orow = m;
-        if (p.g.remap) {  // phase dgrad: virtual row (n, hh, ww) -> real dX pixel
-          // remap 1: dgrad-form geometry (virtual output = H x W); 2: forward-form (OH x OW)
-          const int VW = p.g.remap == 2 ? p.g.OW : p.g.W, VH = p.g.remap == 2 ? p.g.OH : p.g.H;
-          const int ww = m % VW, t = m / VW, hh = t % VH, nn = t / VH;
-          orow = ((int64_t)nn * p.g.Hr + p.g.oa + p.g.psh * hh) * p.g.Wr + p.g.ob + p.g.psw * ww;
-        }
-        const int64_t off = orow * p.ldc + n;
+        const int64_t off = orow_of(m) * p.ldc + n;
         u32x4 rv = z4, xv = z4;
         uint32_t mb = 0;
         if (vec) {
@@ -642,6 +647,7 @@ __global__ __launch_bounds__(NT, DPE_IGEMM_OCC4 ? 4 : 1) void igemm_kernel(Igemm
   // ---------------------------------------------------------------- epilogue
   // acc[i][j][e]: m = m0 + wm + 16i + (lane&15), n = n0 + wn + 16j + (lane>>4)*4 + e
   if (p.alpha_ptr) p.alpha *= *p.alpha_ptr;
+  const float alpha = p.alpha;
   const int lm = lane & 15, ln4 = (lane >> 4) * 4;
   if constexpr (EPI == EPI_ATOMIC_F32) {
     epilogue_atomic_f32<BM, BN, LDS>(p, acc, smem, m0, n0, wn);
@@ -659,7 +665,7 @@ __global__ __launch_bounds__(NT, DPE_IGEMM_OCC4 ? 4 : 1) void igemm_kernel(Igemm
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float b = (p.bias && n + e < p.N) ? p.bias[n + e] : 0.f;
-          v[e] = act_fn(p.alpha * acc[i][j][e] + b, p.act);
+          v[e] = act_fn(alpha * acc[i][j][e] + b, p.act);
           if (p.residual_f32 && n + e < p.N) v[e] += p.residual_f32[(int64_t)m * p.ldc + n + e];
         }
         float* dst = C + (int64_t)m * p.ldc + n;
@@ -673,7 +679,7 @@ __global__ __launch_bounds__(NT, DPE_IGEMM_OCC4 ? 4 : 1) void igemm_kernel(Igemm
     }
     return;
   } else {
-    epilogue_bf16<BM, BN, RM, RN, NT, EPI>(p, acc, smem, m0, n0, tm, wm, wn);
+    epilogue_bf16<BM, BN, RM, RN, NT, EPI>(p, alpha, acc, smem, m0, n0, tm, wm, wn);
   }
 }
 
@@ -1042,8 +1048,8 @@ void igemm_dma_kernel(IgemmArgs p, int a_dense) {
     }
   }
   __syncthreads();
-  if (p.alpha_ptr) p.alpha *= *p.alpha_ptr;
-  epilogue_bf16<BM, BN, RM, RN, NTH, EPI>(p, acc, smem, m0, n0, tm, wm, wn);
+  const float alpha = p.alpha_ptr ? p.alpha * *p.alpha_ptr : p.alpha;  // (a local: no scratch copy of p)
+  epilogue_bf16<BM, BN, RM, RN, NTH, EPI>(p, alpha, acc, smem, m0, n0, tm, wm, wn);
 }
 
 // ------------------------------------------- LDS-DMA weight-grad (split-K) kernel
@@ -1067,6 +1073,8 @@ DPE_DEVICE int mn_swz(int k) {
 // runs 4, and the one-barrier-per-32-K ring does not hide the DMA latency at that occupancy.
 // Not instantiated; the waves-per-EU bound below is what such a tile needs.
 template <int BM, int BN, int BL, int WGM = 2, int WGN = 2, int NS = DSTAGES>
+// (the 4-wave tiles need <= 128 VGPRs for 4 waves per SIMD: a build of the 128x128 3x3 tile at 133 ran 1.3x
+// slower; check scripts/isa_stats.py after edits -- a launch bound forcing it spilled the 1x1 tile instead)
 __global__ __launch_bounds__(64 * WGM * WGN, (BN / WGN > 64) ? 2 : 1) void igemm_wgrad_dma_kernel(IgemmArgs p) {
   constexpr int NW = WGM * WGN;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");

@@ -127,53 +127,21 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int e = 0; e < 8; ++e) { pw[j][e] = 0.f; pb[j][e] = 0.f; }
-  // A wave's rows are software-pipelined: every operand of row r + stride (dy, x, the fp32 residual-stream
-  // gradient it accumulates into, mean / rstd) is loaded before row r is reduced and stored, and all of a
-  // row's loads are issued together -- the row-serial form waited one memory round trip for dy / x and a
-  // second for the residual operand, twice per wave (~4.4 TB/s at the GPT-2 shape).
-  struct RowIn {
-    u32x4 d[NJ];
-    float x[NJ][8];
-    f32x4 q0[NJ], q1[NJ];
-    float mean, rstd;
-  };
-  const int64_t stride = (int64_t)gridDim.x * 4;
-  auto load_row = [&](int64_t row, RowIn& in) {
+  for (int64_t row = blockIdx.x * 4ll + wid; row < rows; row += (int64_t)gridDim.x * 4) {
     const int64_t base = row * Dtot + col0;
-    in.mean = mean_in[row];
-    in.rstd = rstd_in[row];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int c = lane + 64 * j;
-      if (c < CH) {
-        in.d[j] = *(const u32x4*)(dy + base + c * 8);
-        load8<XBF>(x, base + c * 8, in.x[j]);
-        if (dx_acc) {
-          const float* q = res_in ? res_in + base + c * 8 : (const float*)dx + base + c * 8;
-          in.q0[j] = *(const f32x4*)q;
-          in.q1[j] = *(const f32x4*)(q + 4);
-        }
-      }
-    }
-  };
-  int64_t row = blockIdx.x * 4ll + wid;
-  RowIn cur;
-  if (row < rows) load_row(row, cur);
-  for (; row < rows; row += stride) {
-    RowIn nxt;
-    if (row + stride < rows) load_row(row + stride, nxt);
-    const int64_t base = row * Dtot + col0;
-    const float mean = cur.mean, rstd = cur.rstd;
+    const float mean = mean_in[row], rstd = rstd_in[row];
     float sg = 0.f, sgx = 0.f;
     float dd[NJ][8], xh[NJ][8];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int c = lane + 64 * j;
       if (c < CH) {
-        unpack8(cur.d[j], dd[j]);
+        float f[8];
+        unpack8(*(const u32x4*)(dy + base + c * 8), dd[j]);
+        load8<XBF>(x, base + c * 8, f);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          xh[j][e] = (cur.x[j][e] - mean) * rstd;
+          xh[j][e] = (f[e] - mean) * rstd;
           const float g = dd[j][e] * w[c * 8 + e];
           sg += g;
           sgx += g * xh[j][e];
@@ -198,7 +166,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
         for (int e = 0; e < 8; ++e) o[e] = rstd * (dd[j][e] * w[c * 8 + e] - sg - xh[j][e] * sgx);
         if (dx_acc) {  // fp32 residual-stream grad: dx = (res_in or dx) + dLN, optional bf16 copy
           float* p = (float*)dx + base + c * 8;
-          f32x4 a = cur.q0[j], bb = cur.q1[j];
+          const float* q = res_in ? res_in + base + c * 8 : p;
+          f32x4 a = *(const f32x4*)q, bb = *(const f32x4*)(q + 4);
           a[0] += o[0]; a[1] += o[1]; a[2] += o[2]; a[3] += o[3];
           bb[0] += o[4]; bb[1] += o[5]; bb[2] += o[6]; bb[3] += o[7];
           *(f32x4*)p = a;
@@ -216,7 +185,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
         }
       }
     }
-    cur = nxt;
   }
   // block-reduce partials over 4 waves
   // (dynamic LDS sized [2][4][D]: 24 KiB at D = 768 instead of a fixed 64 KiB -> 6 blocks per CU)

@@ -28,20 +28,24 @@ def timeit(fn, reps=20):
 
 C = ext()
 B = int(os.environ.get("B", "512"))
-for (ci, co, h) in [(128, 128, 28), (256, 256, 14), (64, 64, 56)]:
+for (ci, co, h, st) in [(128, 128, 28, 1), (256, 256, 14, 1), (64, 64, 56, 1), (128, 128, 56, 2), (256, 256, 28, 2),
+                        (512, 512, 14, 2)]:
+    if len(sys.argv) > 1 and sys.argv[1] == "strided" and st == 1:
+        continue
+    ho = h // st
     x = torch.randn(B, h, h, ci, device="cuda").to(torch.bfloat16)
     w = (torch.randn(co, 3, 3, ci, device="cuda") / (9 * ci) ** 0.5).to(torch.bfloat16)
-    dy = torch.randn(B, h, h, co, device="cuda").to(torch.bfloat16)
+    dy = torch.randn(B, ho, ho, co, device="cuda").to(torch.bfloat16)
     hh = torch.randn(B, h, h, ci, device="cuda").to(torch.bfloat16)
     coef = torch.stack([torch.rand(ci, device="cuda") + 0.5, torch.randn(ci, device="cuda") * 0.1,
                         torch.randn(ci, device="cuda") * 0.1, torch.rand(ci, device="cuda") + 0.5]).contiguous()
     arms = {
-        "fwd+stats": lambda: C.conv_fwd(x, w, [1, 1], [1, 1], [1, 1], True, None),
-        "dgrad": lambda: C.conv_dgrad(dy, w, list(x.shape), [1, 1], [1, 1], [1, 1], None),
-        "dgrad+bnb": lambda: C.conv_dgrad_bn(dy, w, list(x.shape), [1, 1], [1, 1], [1, 1], None, hh, coef),
+        "fwd+stats": lambda: C.conv_fwd(x, w, [st, st], [1, 1], [1, 1], True, None),
+        "dgrad": lambda: C.conv_dgrad(dy, w, list(x.shape), [st, st], [1, 1], [1, 1], None),
+        "dgrad+bnb": lambda: C.conv_dgrad_bn(dy, w, list(x.shape), [st, st], [1, 1], [1, 1], None, hh, coef),
     }
     res = {k: [] for k in arms}
     for _ in range(3):
         for k, f in arms.items():
             res[k].append(timeit(f))
-    print(f"{ci}->{co} 3x3 @{h}: " + "  ".join(f"{k} {min(v):.1f} us" for k, v in res.items()), flush=True)
+    print(f"{ci}->{co} 3x3/s{st} @{h}: " + "  ".join(f"{k} {min(v):.1f} us" for k, v in res.items()), flush=True)
