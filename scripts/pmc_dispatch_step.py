@@ -53,4 +53,4 @@ for n, d in enumerate(sa):
     wr = cb[sb[n]].get("WRITE_SIZE", 0.0) * 1024 / 1e6 if n < len(sb) else 0.0
     mf = 100.0 * ca[d].get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (us * 1e-6 * 2.4e9 * 1024) if us > 0 else 0.0
     name = re.sub(r"\(.*", "", ma[d][0])[:80]
-    print(f"{n:4d} {us:8.1f} {mf:6.1f} {rd:8.1f} {wr:8.1f} {(rd + wr) / us / 1e6 * 1e0:6.2f}  {ma[d][1]:>8}  {name}")
+    print(f"{n:4d} {us:8.1f} {mf:6.1f} {rd:8.1f} {wr:8.1f} {(rd + wr) / us:6.2f}  {ma[d][1]:>8}  {name}")
