@@ -53,6 +53,7 @@ int dpe_bn_apply2(const uint16_t* x, const float* coef, const uint16_t* x2, cons
                   int relu, uint8_t* mbits, hipStream_t st);
 int dpe_bn_apply_m(const uint16_t* x, const uint16_t* res, uint16_t* y, int64_t M, int C, const float* coef, int relu,
                    uint8_t* mbits, hipStream_t st);
+void dpe_set_pool_legacy(int on);
 int dpe_bnrelu_maxpool_fwd(const uint16_t* h, const float* coef, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH,
                            int OW, int k, int s, int p, hipStream_t st);
 int dpe_stem_wgrad_launch2(const uint16_t* x, const uint16_t* dy, float* dw, float* scratch, int N, int H, int W,
@@ -2080,6 +2081,8 @@ void register_ops(pybind11::module& m) {
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("coef"), py::arg("residual") = py::none(),
         py::arg("residual_coef") = py::none(), py::arg("relu") = true, py::arg("want_mask") = false);
   m.def("bnrelu_maxpool_fwd", &bnrelu_maxpool_fwd, py::arg("h"), py::arg("coef"), py::arg("k"), py::arg("s"), py::arg("p"));
+  m.def("set_pool_legacy", [](bool on) { dpe_set_pool_legacy(on ? 1 : 0); },
+        "test hook: the stem max-pool on the reference (per-tap compare) kernel instead of the key-max one");
   m.def("stem_bwd_fused", &stem_bwd_fused, py::arg("dy"), py::arg("idx"), py::arg("h"), py::arg("xs"), py::arg("gamma"),
         py::arg("coef"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dw"),
         "stem backward without dY: BN-backward coefficients of the pooled gradient, then the stem weight grad "

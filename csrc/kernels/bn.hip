@@ -248,7 +248,13 @@ __global__ __launch_bounds__(BN_T) void bn_apply2_kernel(const uint16_t* __restr
 // With adx: the same pass also applies ANOTHER BatchNorm's backward to the same dz,
 // adx = a*dz + b*ax + c (abcoef [3][C]) -- a bottleneck's BN3 apply fused with its
 // downsample BN's reduce (both are functions of dz3): dz3 is read once.
-template <int U>
+// RELU (compile-time: 0 none, 1 y > 0, 2 ybits) and ADX select the operands, so no load sits under a
+// run-time branch, and the row tail is clamped (loads always issued, the rows past the end masked out of
+// the sums and their adx stores dropped by the buffer unit): a load or store under a lane-divergent test
+// made the compiler drain every load in flight, 7 full vmcnt(0) per trip (the layer-3/4 reduces ran at
+// 2.6-4.1 TB/s, 182 VGPRs for the union of the variants' operands).
+constexpr uint32_t BN_OOB = 0x80000000u;
+template <int U, int RELU, bool ADX>
 __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
                                                              const uint8_t* __restrict__ ybits,
                                                              const uint16_t* __restrict__ x, const float* __restrict__ coef,
@@ -265,53 +271,54 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const uint16_t* __r
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s[e] = 0.f; q[e] = 0.f; mean[e] = coef[2 * C + c * 8 + e]; }
   Coef8<3> ac;
-  if (adx) ac.load(abcoef, C, c * 8);
-  if (r < RPI) {
+  if constexpr (ADX) ac.load(abcoef, C, c * 8);
+  // adx stores through a buffer resource: a tail row's offset is out of range and the store is dropped
+  const __amdgpu_buffer_rsrc_t adr = __builtin_amdgcn_make_buffer_rsrc(
+      ADX ? (void*)adx : (void*)part, (short)0, ADX ? (int)min<int64_t>(M * C * 2, 0x7fffffffll) : 0, 0x00020000);
+  if (r < RPI && rb < re) {
     // U rows per thread per iteration, all of their loads issued before the first use
-    // (1024 blocks x 256 threads leave 4 blocks per CU: one row in flight per thread
-    // was latency-bound)
     for (int64_t row0 = rb + r; row0 < re; row0 += (int64_t)U * RPI) {
-      u32x4 rd[U], rx[U], ra[U], ry[U];
-      uint32_t mbits[U];
+      u32x4 rd[U], rx[U], ra[ADX ? U : 1], ry[RELU == 1 ? U : 1];
+      uint32_t mbits[RELU == 2 ? U : 1];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t row = row0 + (int64_t)u * RPI;
-        if (U == 1 || row < re) {
-          const int64_t off = row * C + c * 8;
-          rd[u] = *(const u32x4*)(dy + off);
-          rx[u] = *(const u32x4*)(x + off);
-          if (adx) ra[u] = *(const u32x4*)(ax + off);
-          if (ybits) mbits[u] = ybits[off >> 3];
-          else if (y) ry[u] = *(const u32x4*)(y + off);
-        }
+        const int64_t row = min(row0 + (int64_t)u * RPI, re - 1);
+        const int64_t off = row * C + c * 8;
+        rd[u] = *(const u32x4*)(dy + off);
+        rx[u] = *(const u32x4*)(x + off);
+        if constexpr (ADX) ra[u] = *(const u32x4*)(ax + off);
+        if constexpr (RELU == 2) mbits[u] = ybits[off >> 3];
+        if constexpr (RELU == 1) ry[u] = *(const u32x4*)(y + off);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t row = row0 + (int64_t)u * RPI;
-        if (U > 1 && row >= re) break;
+        const bool ok = row < re;
         const int64_t off = row * C + c * 8;
         float d[8], xv[8];
         unpack8(rd[u], d);
         unpack8(rx[u], xv);
-        if (adx) {
+        if constexpr (ADX) {
           float av[8], o[8];
           unpack8(ra[u], av);
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = fmaf(ac.v[0][e], d[e], fmaf(ac.v[1][e], av[e], ac.v[2][e]));
-          *(u32x4*)(adx + off) = pack8(o);
+          __builtin_amdgcn_raw_buffer_store_b128(pack8(o), adr, ok ? (uint32_t)(off * 2) : BN_OOB, 0, 0);
         }
-        if (ybits) {
-          const uint32_t mb = mbits[u];
+        if constexpr (RELU == 2) {
+          const uint32_t mb = ok ? mbits[u] : 0u;
 #pragma unroll
           for (int e = 0; e < 8; ++e) d[e] = ((mb >> e) & 1u) ? d[e] : 0.f;
-        } else if (y) {
+        } else {
           float yv[8];
-          unpack8(ry[u], yv);
+          if constexpr (RELU == 1) unpack8(ry[u], yv);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+          for (int e = 0; e < 8; ++e) d[e] = (ok && (RELU == 0 || yv[e] > 0.f)) ? d[e] : 0.f;
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { s[e] += d[e]; q[e] += d[e] * (xv[e] - mean[e]); }
+        // (explicit fma: every RELU / ADX instantiation rounds the same way -- the compiler's own contraction
+        // choice differed between them, and the y / ybits paths must agree bit for bit)
+        for (int e = 0; e < 8; ++e) { s[e] += d[e]; q[e] = fmaf(d[e], xv[e] - mean[e], q[e]); }
       }
     }
   }
@@ -491,8 +498,13 @@ extern "C" int dpe_bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, const ui
                                  const float* coef, int64_t M, int C, int nb, float* part, hipStream_t st) {
   if (C % 8 || C / 8 > BN_T) return -1;
   const int64_t rpb = (M + nb - 1) / nb;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel<4>, dim3(nb), dim3(BN_T), 0, st, dy, y, ybits, x, coef, M, C, rpb, part,
-                     (const uint16_t*)nullptr, (const float*)nullptr, (uint16_t*)nullptr);
+#define DPE_BNR(RELU_)                                                                                          \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<4, RELU_, false>), dim3(nb), dim3(BN_T), 0, st, dy, y, ybits, x, coef, M, C, \
+                     rpb, part, (const uint16_t*)nullptr, (const float*)nullptr, (uint16_t*)nullptr)
+  if (ybits) DPE_BNR(2);
+  else if (y) DPE_BNR(1);
+  else DPE_BNR(0);
+#undef DPE_BNR
   return 0;
 }
 
@@ -502,7 +514,8 @@ extern "C" int dpe_bn_bwd_reduce_apply(const uint16_t* dz, const uint16_t* x, co
                                        hipStream_t st) {
   if (C % 8 || C / 8 > BN_T) return -1;
   const int64_t rpb = (M + nb - 1) / nb;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel<4>, dim3(nb), dim3(BN_T), 0, st, dz, (const uint16_t*)nullptr,
+  if ((int64_t)M * C * 2 >= 0x7fffffffll) return -1;  // 32-bit buffer offsets of the adx stores
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<4, 0, true>), dim3(nb), dim3(BN_T), 0, st, dz, (const uint16_t*)nullptr,
                      (const uint8_t*)nullptr, x, coef, M, C, rpb, part, ax, abcoef, adx);
   return 0;
 }

@@ -83,6 +83,84 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
   *(u32x2*)(idx + (int64_t)i * 8) = pk;
 }
 
+// The stem's 3x3 / s2 / p1 max-pool over relu(BN(h)) (C = 8 CPR), VALU-lean: maxpool_fwd_kernel<true, 3>
+// spent ~850 VALU instructions per 8-channel output (unpack, fma, max, bf16 round trip, compare, two selects
+// per tap and element plus 32-bit index division) -- at 12.8 M outputs that is the whole 276 us it took
+// at batch 512 (profiles/resnet50_dispatch_r6.txt: VALU-bound, 4.1 TB/s).  Here each (tap, element) is one
+// sortable key: after the bf16 round (RNE, as a materialised BN output) a value's bits shifted to the top
+// half compare as a signed int exactly as the float does for every non-negative value, and a negative one
+// (ReLU -> 0) compares below 0; the low bits carry 15 - tap, so the running max = max3(best, key, code)
+// does the ReLU, the max and the first-tap-wins tie break (the strict '>' scan of the reference kernel) in
+// one v_max3_i32.  Same values and argmax bytes as maxpool_fwd_kernel<true, 3> (a -0 maximum is stored as
+// +0; a NaN input propagates instead of being clamped to 0 by fmaxf).  Rows: one block covers part of one
+// output row (n, oh): the row-tap validity is block-uniform, only the q = 0 / 2 column taps are per lane.
+template <int CPR>
+__global__ __launch_bounds__(256) void bnrelu_maxpool3_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                              uint8_t* __restrict__ idx, int H, int W, int OH, int OW,
+                                                              int nx, const float* __restrict__ coef) {
+  constexpr int C = CPR * 8;
+  const int rb = xcd_remap(blockIdx.x, gridDim.x);  // XCD-contiguous rows (shared input rows in one L2)
+  const int row = rb / nx, xb = rb - row * nx;
+  const int n = row / OH, oh = row - n * OH;
+  const int j = xb * 256 + (int)threadIdx.x;
+  if (j >= OW * CPR) return;
+  const int c8 = (j % CPR) * 8, ow = j / CPR;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { sc[e] = coef[c8 + e]; sh[e] = coef[C + c8 + e]; }
+  const uint16_t* xn = x + (int64_t)n * H * W * C + c8;
+  const int ih0 = 2 * oh - 1, iw0 = 2 * ow - 1;
+  u32x4 raw[9];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int ihc = min(max(ih0 + r, 0), H - 1), iwc = min(max(iw0 + q, 0), W - 1);
+      raw[r * 3 + q] = *(const u32x4*)(xn + ((int64_t)ihc * W + iwc) * C);
+    }
+  int best[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) best[e] = 0;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    if ((unsigned)(ih0 + r) >= (unsigned)H) continue;  // block-uniform
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      // q = 1 (iw = 2 ow) is always inside the image; q = 0 / 2 per lane
+      const bool cok = q == 1 || (unsigned)(iw0 + q) < (unsigned)W;
+      const int code = cok ? 15 - (r * 3 + q) : 0;
+      const u32x4& v = raw[r * 3 + q];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float lo = fmaf(__uint_as_float(v[k] << 16), sc[2 * k], sh[2 * k]);
+        const float hi = fmaf(__uint_as_float(v[k] & 0xffff0000u), sc[2 * k + 1], sh[2 * k + 1]);
+        const uint32_t pk = pack_bf2(lo, hi);
+        int klo = (int)((pk << 16) | (uint32_t)code), khi = (int)((pk & 0xffff0000u) | (uint32_t)code);
+        if (q != 1) {
+          klo = cok ? klo : 0;
+          khi = cok ? khi : 0;
+        }
+        best[2 * k] = max(max(best[2 * k], klo), code);
+        best[2 * k + 1] = max(max(best[2 * k + 1], khi), code);
+      }
+    }
+  }
+  const int64_t o = ((int64_t)row * OW + ow) * C + c8;
+  u32x4 out;
+  u32x2 ib;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) out[k] = ((uint32_t)best[2 * k] >> 16) | ((uint32_t)best[2 * k + 1] & 0xffff0000u);
+#pragma unroll
+  for (int h2 = 0; h2 < 2; ++h2) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w |= (((uint32_t)best[4 * h2 + e] & 15u) ^ 15u) << (8 * e);
+    ib[h2] = w;
+  }
+  *(u32x4*)(y + o) = out;
+  *(u32x2*)(idx + o) = ib;
+}
+
 // d(pool input)[n,h,w,c8..c8+7]: sum of dy over the windows containing (h, w) whose argmax it is
 DPE_DEVICE void pool_grad8(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ idx, int n, int h, int w, int c8,
                            int C, int OH, int OW, int k, int s, int p, float* acc) {
@@ -408,6 +486,11 @@ using namespace dpe;
 
 static unsigned exact_grid(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + 255) / 256); }
 
+// 1: the stem max-pool on maxpool_fwd_kernel<true, 3> instead of bnrelu_maxpool3_kernel (test hook: the two
+// must agree bit for bit on values and argmax bytes)
+static int g_pool_legacy = 0;
+extern "C" void dpe_set_pool_legacy(int on) { g_pool_legacy = on; }
+
 static int gs(int64_t n) {
   int64_t g = (n + 255) / 256;
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
@@ -427,6 +510,12 @@ extern "C" int dpe_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int
 extern "C" int dpe_bnrelu_maxpool_fwd(const uint16_t* h, const float* coef, uint16_t* y, uint8_t* idx, int N, int H, int W,
                                       int C, int OH, int OW, int k, int s, int p, hipStream_t st) {
   if (C % 8 || k * k > 255 || (int64_t)N * OH * OW * C / 8 >= (1ll << 31)) return -1;
+  if (k == 3 && s == 2 && p == 1 && C == 64 && OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 && !g_pool_legacy) {
+    const int nx = (OW * 8 + 255) / 256;
+    hipLaunchKernelGGL((bnrelu_maxpool3_kernel<8>), dim3((unsigned)((int64_t)N * OH * nx)), dim3(256), 0, st, h, y, idx, H, W,
+                       OH, OW, nx, coef);
+    return 0;
+  }
   const dim3 g(exact_grid((int64_t)N * OH * OW * C / 8));
   if (k == 3)
     hipLaunchKernelGGL((maxpool_fwd_kernel<true, 3>), g, dim3(256), 0, st, h, y, idx, N, H, W, C, OH, OW, k, s, p, coef);

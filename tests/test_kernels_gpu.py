@@ -1324,6 +1324,34 @@ def test_flipped_filter_cache_refresh(C, cin, cout, stride, hw):
     assert rel_err(d1, ref) > 0.5  # (the first call used the old filter)
 
 
+@pytest.mark.parametrize("H,W", [(112, 112), (29, 30), (30, 29), (7, 9)])
+def test_bnrelu_maxpool_key_kernel_matches_reference(C, H, W):
+    """The stem max-pool's key-max kernel (bnrelu_maxpool3_kernel: ReLU, max and first-tap tie break in one
+    integer max per tap) equals the per-tap compare kernel bit for bit: values (a -0 max reads as +0) and
+    argmax bytes, including the ties that the bf16 round creates, odd borders and negative BN scales."""
+    g = torch.Generator(device=dev).manual_seed(H * 100 + W)
+    N = 3
+    h = (torch.randn(N, H, W, 64, device=dev, generator=g) * 3).bfloat16()
+    h[0, :4] = h[0, :4].round()  # many exact ties
+    sc = 1 + 0.5 * torch.randn(64, device=dev, generator=g)
+    sc[:8] = -sc[:8].abs()  # negative scales: the max comes from the smallest h
+    sc[8] = 0.0  # constant channel: every tap ties
+    coef = torch.stack([sc, 0.5 * torch.randn(64, device=dev, generator=g), torch.zeros(64, device=dev),
+                        torch.ones(64, device=dev)]).float().contiguous()
+    y1, i1 = C.bnrelu_maxpool_fwd(h, coef, 3, 2, 1)
+    C.set_pool_legacy(True)
+    try:
+        y0, i0 = C.bnrelu_maxpool_fwd(h, coef, 3, 2, 1)
+    finally:
+        C.set_pool_legacy(False)
+    assert torch.equal(i1, i0)
+    assert torch.equal(y1.float(), y0.float())
+    # and against torch: max_pool2d of the bf16-rounded relu(fma) activation
+    a = torch.relu(torch.addcmul(coef[1].view(1, 1, 1, -1), h.float(), coef[0].view(1, 1, 1, -1))).bfloat16().float()
+    ref = torch.nn.functional.max_pool2d(a.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    assert rel_err(y1, ref) < 1e-2
+
+
 @pytest.mark.parametrize("N", [2, 5])
 def test_stem_bwd_fused_matches_apply_path(C, N):
     """The stem backward without dL/dh (stem_bwd_fused: dY computed inside the weight grad from the pooled
