@@ -31,6 +31,7 @@ int dpe_gram_bwd(const float* part, int rg, const float* P, const uint16_t* w, c
                  const float* coef3, const float* gamma, int Cin, int Cout, int64_t M, float* dgamma, float* dbeta,
                  float* dw, uint16_t* bcat, float* abc, float* ebias, float* qws, hipStream_t st);
 int dpe_bn_stats_nblocks(int64_t M, int C);
+int dpe_bn_bwd_nblocks(int64_t M, int C);
 
 int dpe_bn_stats(const uint16_t* x, int64_t M, int C, int nb, float* part, hipStream_t st);
 int dpe_bn_finalize(const float* part, int nb, int C, int64_t M, const float* gamma, const float* beta, float* rmean,
@@ -1234,7 +1235,7 @@ std::vector<Tensor> bn_bwd(const Tensor& dy, const c10::optional<Tensor>& y, con
   }
   hipStream_t st = cur_stream();
   auto fo = x.options().dtype(at::kFloat);
-  const int nb = dpe_bn_stats_nblocks(M, (int)C);
+  const int nb = dpe_bn_bwd_nblocks(M, (int)C);
   Tensor part = at::empty({nb, 2, C}, fo);
   CHECK_RC(dpe_bn_bwd_reduce(bp(dy), yp, yb, bp(x), fp(coef), M, (int)C, nb, fp(part), st), "bn_bwd_reduce");
   Tensor bcoef = at::empty({3, C}, fo);
@@ -1549,7 +1550,7 @@ std::vector<Tensor> bn_bwd_dual(const Tensor& dz, const Tensor& x, const c10::op
   Tensor bcoef = at::empty({3, C}, fo);
   CHECK_RC(dpe_bn_bwd_finalize(fp(partials), (int)partials.size(2), (int)C, M, fpo(gamma), fp(coef), fpom(dgamma),
                                fpom(dbeta), fp(bcoef), st), "bn_bwd_finalize");
-  const int nb = dpe_bn_stats_nblocks(M, (int)C);
+  const int nb = dpe_bn_bwd_nblocks(M, (int)C);
   Tensor part2 = at::empty({2, C, nb}, fo);
   Tensor dx = at::empty_like(x);
   CHECK_RC(dpe_bn_bwd_reduce_apply(bp(dz), bp(x2), fp(coef2), bp(x), fp(bcoef), bpm(dx), M, (int)C, nb, fp(part2), st),

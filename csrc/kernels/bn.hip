@@ -439,6 +439,17 @@ extern "C" int dpe_bn_stats_nblocks(int64_t M, int C) {
   return (int)nb;
 }
 
+// Blocks of the BN-backward reduce: as dpe_bn_stats_nblocks, but at >= 1024 channels (layers 3-4: a block row
+// is one or two pixels) at least DPE_BNR_ROWS (default 64) rows per block, up to 2048 blocks
+extern "C" int dpe_bn_bwd_nblocks(int64_t M, int C) {
+  static const int rows = [] { const char* e = getenv("DPE_BNR_ROWS"); return e ? std::max(4, atoi(e)) : 64; }();
+  if (C < 1024) return dpe_bn_stats_nblocks(M, C);
+  int64_t nb = M / rows;
+  if (nb > 2048) nb = 2048;
+  if (nb < 1) nb = 1;
+  return (int)nb;
+}
+
 extern "C" int dpe_bn_stats(const uint16_t* x, int64_t M, int C, int nb, float* part, hipStream_t st) {
   if (C % 8 || C / 8 > BN_T) return -1;
   const int64_t rpb = (M + nb - 1) / nb;
