@@ -241,6 +241,12 @@ void dma_tile(const dpe::IgemmArgs& a, int aload, int bload, int& bm, int& bn) {
   else if (mode >= 2 && a.N > 64) { bm = 256; bn = 128; }
 }
 
+// Strided data grads: the per-parity sub-GEMMs in one grid (igemm_dma_group_kernel) with DPE_PHASE_GROUP=1 or
+// set_phase_group(true); default one launch per parity.  Measured neutral (ResNet-50 31.07-31.13 vs
+// 31.10-31.16 ms/step; per shape 492 / 334 / 251 vs 487 / 329 / 232 us with the BN epilogue, layers 2 / 3 / 4:
+// the shared dy rows and the single launch are not what the parity sub-GEMMs lose their time to)
+bool g_phase_group = [] { const char* e = getenv("DPE_PHASE_GROUP"); return e && e[0] == '1'; }();
+
 // ---------------------------------------------------------- flipped filters
 // The stride-1 / per-parity data grads run as forward convs of dy with flipped, transposed filters
 // (conv_w_flipT).  A filter only changes when the optimizer (or a torch-side edit) rewrites the bf16 shadow,
@@ -1068,10 +1074,28 @@ std::vector<Tensor> conv_dgrad_impl(const Tensor& dy, const Tensor& w, std::vect
       }
     }
     if (want_bn) part = at::empty({2, g.C, total_tiles}, dy.options().dtype(at::kFloat));
-    for (size_t i = 0; i < subs.size(); ++i) {
-      auto& b = subs[i];
+    const int epi = want_bn ? dpe::EPI_BF16_BNB : dpe::EPI_BF16;
+    for (auto& b : subs)
       if (want_bn) { b.col_stats = fp(part); b.stats_ld = (int)total_tiles; }
-      const int epi = want_bn ? dpe::EPI_BF16_BNB : dpe::EPI_BF16;
+    // g_phase_group: all parities in one grid (igemm_dma_group_kernel), on the first (shortest-K) parity's
+    // tile -- one launch instead of four, an XCD's neighbouring blocks holding the four parities of the same
+    // dy rows (measured neutral: off by default)
+    bool grouped = false;
+    if (g_phase_group && igemm_dma_on() && subs.size() > 1 && subs.size() <= (size_t)dpe::IGEMM_GROUP_MAX &&
+        std::all_of(sub_fwd.begin(), sub_fwd.end(), [](bool f) { return f; })) {
+      const Cfg c0 = pick_cfg(subs[0].M, subs[0].N, subs[0].K, false);
+      int bm = c0.bm, bn = c0.bn;
+      dma_tile(subs[0], dpe::A_CONV_FWD, dpe::B_DENSE_K, bm, bn);
+      for (auto& b : subs) b.k_split = (int)((b.K + 31) / 32 * 32);
+      grouped = dpe_igemm_dma_group_launch(subs.data(), (int)subs.size(), bm, bn, dpe::A_CONV_FWD, dpe::B_DENSE_K, epi,
+                                           cur_stream()) == 0;
+      if (grouped) {
+        const hipError_t e = hipGetLastError();
+        TORCH_CHECK(e == hipSuccess, "igemm_dma group launch failed: ", hipGetErrorString(e));
+      }
+    }
+    for (size_t i = 0; i < subs.size() && !grouped; ++i) {
+      auto& b = subs[i];
       if (sub_fwd[i]) run_igemm(b, dpe::A_CONV_FWD, dpe::B_DENSE_K, epi, false, true);
       else run_igemm(b, dpe::A_CONV_DGRAD, dpe::B_CONV_DGRAD, epi, false, true);
     }
@@ -2179,6 +2203,8 @@ void register_ops(pybind11::module& m) {
         }, "kept for API compatibility: 1 = native kernels (the only backend)");
   m.def("set_wgrad_wide", [](int64_t v) { g_wgrad_wide = (int)v; },
         "64x256 tile for Cout = 64 weight grads: 0 off, 1 when C <= 16 (default), 2 always");
+  m.def("set_phase_group", [](bool on) { g_phase_group = on; },
+        "strided data grads: all parity sub-GEMMs in one grid, or one launch per parity (default)");
   m.def("set_conv_tile", [](int64_t mode) { g_dma_tile = (int)mode; },
         "LDS-DMA conv tile: 0 auto, 1 128-tile, 2 256x128, 3 256x256 (8 waves)");
   m.def("pick_gemm_cfg", [](int64_t M, int64_t N, int64_t K, bool split) {

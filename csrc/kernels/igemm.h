@@ -97,7 +97,20 @@ struct IgemmArgs {
                             //   (summed in split order by a finalize pass: deterministic) instead of atomics
 };
 
+// Up to 4 problems of one LDS-DMA tile class and tile count in one grid (igemm_dma_group_kernel): the
+// per-parity sub-GEMMs of a strided data grad.
+constexpr int IGEMM_GROUP_MAX = 4;
+struct IgemmGroup {
+  IgemmArgs a[IGEMM_GROUP_MAX];
+  int n;
+};
+
 }  // namespace dpe
+
+// n problems (<= IGEMM_GROUP_MAX) with equal M and N, forward-form (A_CONV_FWD or A_DENSE_K) on the LDS-DMA
+// kernel, one grid; -1 when any is outside the kernel's envelope (the caller then launches them one by one).
+extern "C" int dpe_igemm_dma_group_launch(const dpe::IgemmArgs* args, int n, int bm, int bn, int aload, int bload, int epi,
+                                          hipStream_t stream);
 
 extern "C" int dpe_igemm_launch(const dpe::IgemmArgs* args, int bm, int bn, int aload, int bload, int epi,
                                 int splits, hipStream_t stream);

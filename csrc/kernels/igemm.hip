@@ -23,6 +23,7 @@
 //     per-column sum / sum-of-squares for a following BatchNorm.
 //   * Workgroup ids are remapped XCD-aware (bijective) with N-tiles fastest
 //     so the blocks that share an A row-panel share an L2.
+#include <cstring>
 #include "common.h"
 #include "igemm.h"
 
@@ -742,11 +743,11 @@ DPE_DEVICE void wait_vm() {
 // feed the MFMAs.  The waves of the first N tile whose columns start at 0 (exactly one wave per A row)
 // also store the transformed A (and its ReLU-mask bits): the standalone pass that wrote it before
 // read the same two tensors, so the consumer's own read of it is what disappears.
+// The body is a device function of the block's (XCD-remapped) tile index `bid`: igemm_dma_kernel runs one
+// problem, igemm_dma_group_kernel several of one shape class in one grid (the per-parity data grads of a
+// strided conv).
 template <int BM, int BN, int WGM, int WGN, int BL, int EPI, int NS = DSTAGES, int AX = AX_NONE>
-// (AX_CAT 128x128: 3 blocks per CU -- at 128 VGPRs its two-segment loader spilled 27 registers)
-__global__ __launch_bounds__(64 * WGM * WGN, ((BM == 256 && BN == 128) || (DPE_DMA_OCC4 && WGM * WGN == 4))
-                                                 ? ((AX == AX_CAT && BN == 128) ? 3 : 4) : 1)
-void igemm_dma_kernel(IgemmArgs p, int a_dense) {
+DPE_DEVICE void igemm_dma_body(const IgemmArgs& p, int a_dense, const int bid) {
   constexpr int NTH = 64 * WGM * WGN, NW = WGM * WGN;
   constexpr bool BKc = (BL == B_DENSE_K);
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
@@ -767,7 +768,6 @@ void igemm_dma_kernel(IgemmArgs p, int a_dense) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tilesN = (p.N + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = bid / tilesN, tn = bid % tilesN;
   const int m0 = tm * BM, n0 = tn * BN;
   const int wm = (wid / WGN) * (BM / WGM), wn = (wid % WGN) * (BN / WGN);
@@ -1050,6 +1050,26 @@ void igemm_dma_kernel(IgemmArgs p, int a_dense) {
   __syncthreads();
   const float alpha = p.alpha_ptr ? p.alpha * *p.alpha_ptr : p.alpha;  // (a local: no scratch copy of p)
   epilogue_bf16<BM, BN, RM, RN, NTH, EPI>(p, alpha, acc, smem, m0, n0, tm, wm, wn);
+}
+
+#define DPE_DMA_BOUNDS(BM, BN, WGM, WGN, AX)                                                                   \
+  __launch_bounds__(64 * WGM * WGN, ((BM == 256 && BN == 128) || (DPE_DMA_OCC4 && WGM * WGN == 4))              \
+                                        ? ((AX == AX_CAT && BN == 128) ? 3 : 4) : 1)
+// (AX_CAT 128x128: 3 blocks per CU -- at 128 VGPRs its two-segment loader spilled 27 registers)
+template <int BM, int BN, int WGM, int WGN, int BL, int EPI, int NS = DSTAGES, int AX = AX_NONE>
+__global__ DPE_DMA_BOUNDS(BM, BN, WGM, WGN, AX) void igemm_dma_kernel(IgemmArgs p, int a_dense) {
+  igemm_dma_body<BM, BN, WGM, WGN, BL, EPI, NS, AX>(p, a_dense, xcd_remap(blockIdx.x, gridDim.x));
+}
+
+// Several problems with the same tile count in one grid, interleaved: remapped block r runs tile r / n of
+// problem r % n, so an XCD's consecutive blocks hold the n problems of neighbouring tiles -- the four parity
+// sub-GEMMs of a strided data grad read the same dy rows (once from HBM, the rest from that XCD's L2) and
+// store the interleaved pixels of the same dx rows at about the same time; one launch instead of n.
+template <int BM, int BN, int WGM, int WGN, int BL, int EPI, int NS = DSTAGES>
+__global__ DPE_DMA_BOUNDS(BM, BN, WGM, WGN, AX_NONE) void igemm_dma_group_kernel(IgemmGroup gp, int a_dense) {
+  const int r = xcd_remap(blockIdx.x, gridDim.x);
+  const int n = gp.n;
+  igemm_dma_body<BM, BN, WGM, WGN, BL, EPI, NS, AX_NONE>(gp.a[r % n], a_dense, r / n);
 }
 
 // ------------------------------------------- LDS-DMA weight-grad (split-K) kernel
@@ -1380,6 +1400,44 @@ extern "C" int dpe_igemm_dma_launch(const IgemmArgs* args, int bm, int bn, int a
   DPE_DMA(256, 64, 4, 1, B_DENSE_K, EPI_BF16_BNB)
 #undef DPE_DMA_T
 #undef DPE_DMA
+  return -1;
+}
+
+extern "C" int dpe_igemm_dma_group_launch(const IgemmArgs* args, int n, int bm, int bn, int aload, int bload, int epi,
+                                          hipStream_t st) {
+  if (n < 1 || n > IGEMM_GROUP_MAX) return -1;
+  if (aload != A_DENSE_K && aload != A_CONV_FWD) return -1;
+  if (bload != B_DENSE_K || (epi != EPI_BF16 && epi != EPI_BF16_BNB)) return -1;
+  const bool dense = aload == A_DENSE_K;
+  const int64_t lim = (1ll << 31) - 4096;
+  IgemmGroup gp;
+  memset(&gp, 0, sizeof(gp));
+  gp.n = n;
+  for (int i = 0; i < n; ++i) {
+    const IgemmArgs& a = args[i];
+    // the single-problem launcher's envelope (dpe_igemm_dma_launch), no A transform, one tile count
+    if (a.M <= 0 || a.N <= 0 || a.M != args[0].M || a.N != args[0].N || a.a_mode != AX_NONE) return -1;
+    if (a.K <= 0 || a.K % 32 || a.k_split < a.K || a.ldb % 8 || (dense && a.lda % 8)) return -1;
+    const ConvGeom& g = a.g;
+    if (!dense && (g.C % 32 || g.R * g.S > 32 || g.R * g.S * g.C != a.K)) return -1;
+    const int64_t abytes = dense ? (int64_t)a.M * a.lda * 2
+                                 : ((int64_t)g.N * g.H * g.W * g.C + ((int64_t)g.ph * g.W + g.pw) * g.C) * 2;
+    if (abytes >= lim || (int64_t)a.N * a.ldb * 2 >= lim) return -1;
+    gp.a[i] = a;
+  }
+  const int tiles = ((args[0].M + bm - 1) / bm) * ((args[0].N + bn - 1) / bn);
+  const int dn = dense ? 1 : 0;
+#define DPE_DMA_G(BM_, BN_, WGM_, WGN_, NS_, EP_)                                                            \
+  if (bm == BM_ && bn == BN_ && epi == EP_) {                                                                 \
+    hipLaunchKernelGGL((igemm_dma_group_kernel<BM_, BN_, WGM_, WGN_, B_DENSE_K, EP_, NS_>), dim3(tiles * n),   \
+                       dim3(64 * WGM_ * WGN_), 0, st, gp, dn);                                                \
+    return 0;                                                                                                 \
+  }
+  DPE_DMA_G(128, 128, 2, 2, 2, EPI_BF16_BNB)
+  DPE_DMA_G(128, 128, 2, 2, 2, EPI_BF16)
+  DPE_DMA_G(256, 128, 4, 2, 3, EPI_BF16_BNB)
+  DPE_DMA_G(256, 128, 4, 2, 3, EPI_BF16)
+#undef DPE_DMA_G
   return -1;
 }
 

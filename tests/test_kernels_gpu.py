@@ -1324,6 +1324,35 @@ def test_flipped_filter_cache_refresh(C, cin, cout, stride, hw):
     assert rel_err(d1, ref) > 0.5  # (the first call used the old filter)
 
 
+@pytest.mark.parametrize("ci,co,h", [(128, 128, 28), (256, 256, 14), (64, 128, 16)])
+def test_strided_dgrad_phase_group_matches_per_parity(C, ci, co, h):
+    """Strided 3x3 data grad: the four parity sub-GEMMs in one grid (igemm_dma_group_kernel) == one launch
+    per parity, dx bit for bit (same K order per element; the grouped launch may use a smaller tile) and the
+    BN-backward partials to rounding; plain and BN-partials epilogues; and against fp32 torch."""
+    g = torch.Generator(device=dev).manual_seed(ci + h)
+    N = 4
+    w = (torch.randn(co, 3, 3, ci, device=dev, generator=g) / math.sqrt(9 * ci)).bfloat16()
+    dy = torch.randn(N, h // 2, h // 2, co, device=dev, generator=g).bfloat16()
+    hh = torch.randn(N, h, h, ci, device=dev, generator=g).bfloat16()
+    coef = _bn_coef(C, ci)
+    xs = [N, h, h, ci]
+    outs = {}
+    for grp in (True, False):
+        C.set_phase_group(grp)
+        try:
+            d_plain = C.conv_dgrad(dy, w, xs, [2, 2], [1, 1], [1, 1], None)
+            d_bn, part = C.conv_dgrad_bn(dy, w, xs, [2, 2], [1, 1], [1, 1], None, hh, coef)
+        finally:
+            C.set_phase_group(False)
+        outs[grp] = (d_plain, d_bn, part.sum(-1))
+    assert torch.equal(outs[True][0], outs[False][0])
+    assert torch.equal(outs[True][1], outs[False][1])
+    assert rel_err(outs[True][2], outs[False][2]) < 1e-5
+    ref = torch.nn.grad.conv2d_input([N, ci, h, h], w.float().permute(0, 3, 1, 2), dy.float().permute(0, 3, 1, 2),
+                                     stride=2, padding=1).permute(0, 2, 3, 1)
+    assert rel_err(outs[True][0], ref) < 2e-2
+
+
 @pytest.mark.parametrize("H,W", [(112, 112), (29, 30), (30, 29), (7, 9)])
 def test_bnrelu_maxpool_key_kernel_matches_reference(C, H, W):
     """The stem max-pool's key-max kernel (bnrelu_maxpool3_kernel: ReLU, max and first-tap tie break in one
