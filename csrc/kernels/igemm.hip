@@ -312,24 +312,43 @@ DPE_DEVICE void epilogue_bf16(const IgemmArgs& p, float alpha, f32x4 (&acc)[RM][
   const int lm = lane & 15, ln4 = (lane >> 4) * 4;
   const int tilesSub = (p.M + SUBM - 1) / SUBM;
   constexpr bool BNB = (EPI == EPI_BF16_BNB);
-  // Stage bf16 tile in LDS (row stride CROW), then coalesced 16-B stores.
+  // Stage bf16 tile in LDS (row stride CROW), then coalesced 16-B stores.  Without bias and activation
+  // (every conv epilogue) the staging is alpha * acc and the pack: the general path's per-element bias
+  // test (a masked load, then a full vmcnt wait) and activation switch (the GELU branch is inlined per
+  // element) were most of the epilogue's VALU / SALU instructions -- the short-K parity data grads of
+  // strided convs, which store 4x the rows per MFMA of a stride-1 conv, ran epilogue-bound.
+  if (!p.bias && p.act == ACT_NONE) {  // (uniform)
 #pragma unroll
-  for (int i = 0; i < RM; ++i) {
-    const int ml = wm + 16 * i + lm;
+    for (int i = 0; i < RM; ++i) {
+      const int ml = wm + 16 * i + lm;
 #pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int nl = wn + 16 * j + ln4;
-      const int n = n0 + nl;
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float b = (p.bias && n + e < p.N) ? p.bias[n + e] : 0.f;
-        v[e] = act_fn(alpha * acc[i][j][e] + b, p.act);
+      for (int j = 0; j < RN; ++j) {
+        const int nl = wn + 16 * j + ln4;
+        u32x2 pk;
+        pk[0] = pack_bf2(alpha * acc[i][j][0], alpha * acc[i][j][1]);
+        pk[1] = pack_bf2(alpha * acc[i][j][2], alpha * acc[i][j][3]);
+        *(u32x2*)(smem + ml * CROW + nl * 2) = pk;
       }
-      u32x2 pk;
-      pk[0] = pack_bf2(v[0], v[1]);
-      pk[1] = pack_bf2(v[2], v[3]);
-      *(u32x2*)(smem + ml * CROW + nl * 2) = pk;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const int ml = wm + 16 * i + lm;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int nl = wn + 16 * j + ln4;
+        const int n = n0 + nl;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float b = (p.bias && n + e < p.N) ? p.bias[n + e] : 0.f;
+          v[e] = act_fn(alpha * acc[i][j][e] + b, p.act);
+        }
+        u32x2 pk;
+        pk[0] = pack_bf2(v[0], v[1]);
+        pk[1] = pack_bf2(v[2], v[3]);
+        *(u32x2*)(smem + ml * CROW + nl * 2) = pk;
+      }
     }
   }
   __syncthreads();
