@@ -824,8 +824,10 @@ std::vector<Tensor> conv_fwd(const Tensor& x, const Tensor& w, std::vector<int64
   // 1x1 stride-1 forward at depth >= 1024 (layers 3-4 conv1) with BN statistics: the persistent GEMM's
   // BN-forward-partials epilogue (hgemm.hip HACT_BNF; its GEMM alone 60-71 vs 79-89 us,
   // profiles/pw_vs_hgemm_r3.jsonl)
-  if (want_stats && is_pointwise(g) && !a.bias && !icoef && hgemm_dgrad_on() && a.K >= 1024 && a.K % 64 == 0 &&
-      a.N % 8 == 0) {
+  // DPE_HG_BNF_MINK (default 1024): the smallest depth routed there (with >= 256 output channels below 1024)
+  static const int bnf_min_k = [] { const char* e = getenv("DPE_HG_BNF_MINK"); return e ? atoi(e) : 1024; }();
+  if (want_stats && is_pointwise(g) && !a.bias && !icoef && hgemm_dgrad_on() && a.K >= bnf_min_k &&
+      (a.K >= 1024 || a.N >= 256) && a.K % 64 == 0 && a.N % 8 == 0) {
     int pcols = 0;
     const auto pl = dpe_gemm::plan_bnb(a.M, a.N, a.K, 1, 1, &pcols);
     if (pl.cfg >= 0 && pcols > 0) {
