@@ -213,7 +213,7 @@ int g_wgrad_wide = 1;
 // Tile of the LDS-DMA conv kernel: 0 auto, 1 128-tile (pick_cfg), 2 256x128, 3 256x256
 // (8 waves; only where pick_cfg chose a 128-row tile, so BN partial layouts never change).
 // Forced tiles are a test hook (set_conv_tile): every one is numerics-tested, only "auto" is timed.
-int g_dma_tile = 0;
+int g_dma_tile = [] { const char* e = getenv("DPE_CONV_TILE"); return e ? atoi(e) : 0; }();  // (env: A/B runs)
 int dma_tile_mode() { return g_dma_tile; }
 
 void dma_tile(const dpe::IgemmArgs& a, int aload, int bload, int& bm, int& bn) {
