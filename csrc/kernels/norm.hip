@@ -205,6 +205,128 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
   }
 }
 
+// ln_bwd_kernel for whole rows (D <= 2048) with the output form compile-time (ACC: dx = res_in-or-dx + dLN
+// in fp32; RES: res_in given; DXB: bf16 copy) and every load / store unconditional: a lane past the row's
+// last chunk (D / 8 not a multiple of 64: 96 chunks at D = 768) works on the last chunk instead -- it loads
+// the same operands and stores the same bytes as the lane that owns it -- and only its contribution to the
+// row sums and the dw / db partials is masked.  The generic kernel's per-lane `c < CH` tests and run-time
+// output forms put 7 full vmcnt waits in the row loop.
+template <bool XBF, int NJ, bool ACC, bool RES, bool DXB>
+__global__ __launch_bounds__(256) void ln_bwd_lean_kernel(const uint16_t* __restrict__ dy, const void* __restrict__ x,
+                                                          const float* __restrict__ w, const float* __restrict__ mean_in,
+                                                          const float* __restrict__ rstd_in, void* __restrict__ dx,
+                                                          const float* __restrict__ res_in, uint16_t* __restrict__ dx_bf16,
+                                                          float* __restrict__ part, int64_t rows, int D) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int CH = D >> 3;
+  int cc[NJ];
+  bool ok[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = lane + 64 * j;
+    ok[j] = c < CH;
+    cc[j] = min(c, CH - 1);
+  }
+  float pw[NJ][8], pb[NJ][8], wv[NJ][8];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const f32x4 a = *(const f32x4*)(w + cc[j] * 8), b = *(const f32x4*)(w + cc[j] * 8 + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { wv[j][e] = a[e]; wv[j][e + 4] = b[e]; }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { pw[j][e] = 0.f; pb[j][e] = 0.f; }
+  }
+  float* __restrict__ dxf = (float*)dx;
+  for (int64_t row = blockIdx.x * 4ll + wid; row < rows; row += (int64_t)gridDim.x * 4) {
+    const int64_t base = row * D;
+    // every operand of the row slice first (dy, x and -- independent of the row sums -- the residual-stream
+    // input), then the arithmetic: one load round trip per row
+    u32x4 dr[NJ], xb[NJ];
+    f32x4 xr[NJ][2], rr[NJ][2];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      dr[j] = *(const u32x4*)(dy + base + cc[j] * 8);
+      if constexpr (XBF) {
+        xb[j] = *(const u32x4*)((const uint16_t*)x + base + cc[j] * 8);
+      } else {
+        xr[j][0] = *(const f32x4*)((const float*)x + base + cc[j] * 8);
+        xr[j][1] = *(const f32x4*)((const float*)x + base + cc[j] * 8 + 4);
+      }
+      if constexpr (ACC) {
+        const float* q = RES ? res_in + base + cc[j] * 8 : dxf + base + cc[j] * 8;
+        rr[j][0] = *(const f32x4*)q;
+        rr[j][1] = *(const f32x4*)(q + 4);
+      }
+    }
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    __builtin_amdgcn_sched_barrier(0);  // (keeps the scheduler from sinking the loads to their uses)
+    float sg = 0.f, sgx = 0.f;
+    float dd[NJ][8], xh[NJ][8];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float f[8];
+      unpack8(dr[j], dd[j]);
+      if constexpr (XBF) {
+        unpack8(xb[j], f);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { f[e] = xr[j][0][e]; f[e + 4] = xr[j][1][e]; }
+      }
+      const float m = ok[j] ? 1.f : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        xh[j][e] = (f[e] - mean) * rstd;
+        const float dm = dd[j][e] * m;
+        const float g = dm * wv[j][e];
+        sg += g;
+        sgx += g * xh[j][e];
+        pw[j][e] += dm * xh[j][e];
+        pb[j][e] += dm;
+      }
+    }
+    sg = warp_sum(sg) / (float)D;
+    sgx = warp_sum(sgx) / (float)D;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = rstd * (dd[j][e] * wv[j][e] - sg - xh[j][e] * sgx);
+      if constexpr (ACC) {
+        float* pp = dxf + base + cc[j] * 8;
+        f32x4 a = rr[j][0], bb = rr[j][1];
+        a[0] += o[0]; a[1] += o[1]; a[2] += o[2]; a[3] += o[3];
+        bb[0] += o[4]; bb[1] += o[5]; bb[2] += o[6]; bb[3] += o[7];
+        *(f32x4*)pp = a;
+        *(f32x4*)(pp + 4) = bb;
+        if constexpr (DXB) {
+          const float t[8] = {a[0], a[1], a[2], a[3], bb[0], bb[1], bb[2], bb[3]};
+          *(u32x4*)(dx_bf16 + base + cc[j] * 8) = pack8(t);
+        }
+      } else if constexpr (XBF) {
+        *(u32x4*)((uint16_t*)dx + base + cc[j] * 8) = pack8(o);
+      } else {
+        float* pp = dxf + base + cc[j] * 8;
+        *(f32x4*)pp = f32x4{o[0], o[1], o[2], o[3]};
+        *(f32x4*)(pp + 4) = f32x4{o[4], o[5], o[6], o[7]};
+      }
+    }
+  }
+  extern __shared__ float red_dyn[];
+  float* red0 = red_dyn;          // [4][D]
+  float* red1 = red_dyn + 4 * D;  // [4][D]
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    if (ok[j])
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { red0[wid * D + cc[j] * 8 + e] = pw[j][e]; red1[wid * D + cc[j] * 8 + e] = pb[j][e]; }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < D; i += 256) {
+    part[(int64_t)blockIdx.x * 2 * D + i] = red0[i] + red0[D + i] + red0[2 * D + i] + red0[3 * D + i];
+    part[(int64_t)blockIdx.x * 2 * D + D + i] = red1[i] + red1[D + i] + red1[2 * D + i] + red1[3 * D + i];
+  }
+}
+
 // Column-parallel reduction of the [nb][2][D] partials: block = 16 columns x 64 row stripes
 // (16 waves, each lane one (column, stripe); 64-B row segments), 4 independent accumulators per
 // lane, fixed-order tree over the stripes; blockIdx.y picks dw (0) or db (1).  96 blocks at D = 768
@@ -320,7 +442,25 @@ extern "C" int dpe_layernorm_bwd(const uint16_t* dy, const void* x, int x_bf16, 
                      res_in, dx_bf16, part, rows, Dc, D, rs)
 #define DPE_LNB_J(XB) \
   if (nj == 1) DPE_LNB(XB, 1); else if (nj == 2) DPE_LNB(XB, 2); else if (nj == 3) DPE_LNB(XB, 3); else DPE_LNB(XB, 4)
-  if (x_bf16) { DPE_LNB_J(true); } else { DPE_LNB_J(false); }
+  static const bool lean = [] { const char* e = getenv("DPE_LN_BWD_LEAN"); return !(e && e[0] == '0'); }();
+  bool done = false;
+  if (lean && nch == 1 && !rs && nj == 2 && (dx_acc || !dx_bf16)) {
+    // (the GPT-2 widths: 768 = 96 chunks; the fp32 residual-stream form first)
+#define DPE_LNL(XB, A_, R_, B_)                                                                                    \
+  if (!done && (bool)x_bf16 == XB && (dx_acc != 0) == A_ && (res_in != nullptr) == R_ && (dx_bf16 != nullptr) == B_) { \
+    hipLaunchKernelGGL((ln_bwd_lean_kernel<XB, 2, A_, R_, B_>), dim3(nbc), dim3(256), lds, st, dy, x, w, mean, rstd, dx,  \
+                       res_in, dx_bf16, part, rows, D);                                                             \
+    done = true;                                                                                                   \
+  }
+    DPE_LNL(false, true, false, false) DPE_LNL(false, true, true, false) DPE_LNL(false, true, false, true)
+    DPE_LNL(false, true, true, true) DPE_LNL(true, true, false, false) DPE_LNL(true, true, true, false)
+    DPE_LNL(true, true, false, true) DPE_LNL(true, true, true, true)
+    DPE_LNL(false, false, false, false) DPE_LNL(true, false, false, false)
+#undef DPE_LNL
+  }
+  if (!done) {
+    if (x_bf16) { DPE_LNB_J(true); } else { DPE_LNB_J(false); }
+  }
 #undef DPE_LNB_J
 #undef DPE_LNB
   if (!dw && !db) return 0;  // deferred: the caller finalizes `part` later (dpe_layernorm_bwd_finalize_group)
