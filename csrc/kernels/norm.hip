@@ -74,6 +74,67 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
 }
 
+// ln_fwd_kernel with every load issued up front: the weights and bias (independent of the row) with the
+// row itself, a tail lane (D / 8 not a multiple of 64) clamped onto the last chunk -- same loads, same
+// stored bytes as its owner, its share of the sums masked.  One wave per row and every wave resident at
+// once on the GPT-2 shape, so the generic kernel's second, dependent load round trip (w and b after the
+// row reductions) was exposed whole.
+template <bool XBF, int MAXC, bool BIAS>
+__global__ __launch_bounds__(256) void ln_fwd_lean_kernel(const void* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ b, uint16_t* __restrict__ y,
+                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                          int64_t rows, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = blockIdx.x * 4ll + (threadIdx.x >> 6);
+  if (row >= rows) return;  // (wave-uniform)
+  const int CH = D >> 3;
+  const int64_t base = row * D;
+  float f[MAXC][8];
+  f32x4 w0[MAXC], w1[MAXC], b0[MAXC], b1[MAXC];
+  int cc[MAXC];
+  float m[MAXC];
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int c = lane + 64 * j;
+    m[j] = c < CH ? 1.f : 0.f;
+    cc[j] = min(c, CH - 1);
+    load8<XBF>(x, base + cc[j] * 8, f[j]);
+    w0[j] = *(const f32x4*)(w + cc[j] * 8);
+    w1[j] = *(const f32x4*)(w + cc[j] * 8 + 4);
+    if constexpr (BIAS) {
+      b0[j] = *(const f32x4*)(b + cc[j] * 8);
+      b1[j] = *(const f32x4*)(b + cc[j] * 8 + 4);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += f[j][e] * m[j];
+  const float mean = warp_sum(s) / (float)D;
+  float v = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float d = (f[j][e] - mean) * m[j]; v += d * d; }
+  const float rstd = rsqrtf(warp_sum(v) / (float)D + eps);
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    float o[8];
+    o[0] = (f[j][0] - mean) * rstd * w0[j][0]; o[1] = (f[j][1] - mean) * rstd * w0[j][1];
+    o[2] = (f[j][2] - mean) * rstd * w0[j][2]; o[3] = (f[j][3] - mean) * rstd * w0[j][3];
+    o[4] = (f[j][4] - mean) * rstd * w1[j][0]; o[5] = (f[j][5] - mean) * rstd * w1[j][1];
+    o[6] = (f[j][6] - mean) * rstd * w1[j][2]; o[7] = (f[j][7] - mean) * rstd * w1[j][3];
+    if constexpr (BIAS) {
+      o[0] += b0[j][0]; o[1] += b0[j][1]; o[2] += b0[j][2]; o[3] += b0[j][3];
+      o[4] += b1[j][0]; o[5] += b1[j][1]; o[6] += b1[j][2]; o[7] += b1[j][3];
+    }
+    *(u32x4*)(y + base + cc[j] * 8) = pack8(o);
+  }
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
 // Row sums of the LN backward for D > 2048 (one wave per row, the whole row):
 // rs[2 row] = sum(dy*w) / D, rs[2 row + 1] = sum(dy*w*xhat) / D.
 template <bool XBF>
@@ -387,6 +448,16 @@ extern "C" int dpe_layernorm_fwd(const void* x, int x_bf16, const float* w, cons
   if (D % 8) return -1;
   const dim3 grid((unsigned)((rows + 3) / 4));
   const int chunks = (D / 8 + 63) / 64;
+  static const bool lean = [] { const char* e = getenv("DPE_LN_FWD_LEAN"); return !(e && e[0] == '0'); }();
+  if (lean && chunks == 2) {  // (the GPT-2 width, 768)
+#define DPE_LFL(XB, B_)                                                                                                 \
+  if ((bool)x_bf16 == XB && (b != nullptr) == B_) {                                                                     \
+    hipLaunchKernelGGL((ln_fwd_lean_kernel<XB, 2, B_>), grid, dim3(256), 0, st, x, w, b, y, mean, rstd, rows, D, eps);  \
+    return 0;                                                                                                           \
+  }
+    DPE_LFL(false, true) DPE_LFL(false, false) DPE_LFL(true, true) DPE_LFL(true, false)
+#undef DPE_LFL
+  }
 #define LNF(MC)                                                                                                        \
   if (chunks <= MC) {                                                                                                \
     if (x_bf16) hipLaunchKernelGGL((ln_fwd_kernel<true, MC>), grid, dim3(256), 0, st, x, w, b, y, mean, rstd, rows, D, eps); \

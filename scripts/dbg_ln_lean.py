@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""LayerNorm backward, lean vs generic kernel across processes (DPE_LN_BWD_LEAN is read once per process):
+"""LayerNorm forward / backward, lean vs generic kernels across processes (DPE_LN_FWD_LEAN / DPE_LN_BWD_LEAN
+are read once per process):
 `python scripts/dbg_ln_lean.py save <file>` under each setting, then `compare <a> <b>` (bitwise)."""
 import os
 import sys
@@ -27,4 +28,9 @@ for D, rows in ((768, 4100), (1024, 333)):
     wb, bb = torch.zeros(D, device="cuda"), torch.zeros(D, device="cuda")
     dx, dxb = C.layernorm_bwd_residual(dy, x, w, mean, rstd, wb, bb, res)
     out[f"dx{D}"], out[f"dxb{D}"], out[f"dw{D}"], out[f"db{D}"] = dx, dxb, wb, bb
+    bias = torch.randn(D, device="cuda", generator=g)
+    for xx, nm in ((x, "f32"), (x.bfloat16(), "bf16")):
+        yo = C.layernorm_fwd(xx, w, bias)
+        for i, t in enumerate(yo if isinstance(yo, (list, tuple)) else [yo]):
+            out[f"fwd{D}_{nm}_{i}"] = t
 torch.save({k: v.cpu() for k, v in out.items()}, sys.argv[2])
