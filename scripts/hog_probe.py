@@ -3,7 +3,7 @@
 for RCCL channel blocks overlapping the gradient all-reduce at 8 ranks.
 
 Per step: forward on the compute stream; then a side stream launches `hogs` workgroups (threads,
-LDS bytes and ~VGPRs per lane of an RCCL channel block, profiles/rccl_footprint_r3.txt) that stay
+LDS bytes and ~VGPRs per lane of an RCCL channel block, profiles/world8_1gpu_r6.txt) that stay
 resident until the compute stream, after backward, sets their stop flag -- exactly the window in
 which the reducer has bucket all-reduces in flight.  With `reserve` > 0 the persistent kernels plan
 around `reserve` slots during that window (the CU budget the reducer applies at world > 1,
