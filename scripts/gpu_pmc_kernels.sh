@@ -22,7 +22,7 @@ for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
         per[k][row["Counter_Name"]] += float(row["Counter_Value"])
 import os
 flt = os.environ.get("FILTER", "")
-rows = sorted([kv for kv in per.items() if flt in kv[0]], key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0))[:14]
+rows = sorted([kv for kv in per.items() if flt in kv[0]], key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0))[:int(os.environ.get("TOPK", "14"))]
 for k, c in rows:
     wc = c.get("SQ_WAVE_CYCLES", 1) or 1
     print(k[:100])
