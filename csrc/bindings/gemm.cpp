@@ -89,7 +89,39 @@ unsigned* sched_buffer_impl(hipStream_t st) {
   bufs.emplace(key, b);
   return b;
 }
+
+// Stream-K arrival counters (hgemm.h sk_cnt): one zeroed buffer of HGEMM_SK_MAX_TILES words per (device,
+// stream), kept zero by each tile's last arriver; nullptr while the stream is being captured.
+unsigned* sk_counters(hipStream_t st) {
+  static std::mutex mu;
+  static std::unordered_map<uint64_t, unsigned*> bufs;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const uint64_t key = (uint64_t)(uintptr_t)st * 64 + (uint64_t)dev;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = bufs.find(key);
+  if (it != bufs.end()) return it->second;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  unsigned* b = nullptr;
+  const size_t bytes = sizeof(unsigned) * dpe::HGEMM_SK_MAX_TILES;
+  TORCH_CHECK(hipMalloc(&b, bytes) == hipSuccess && hipMemsetAsync(b, 0, bytes, st) == hipSuccess,
+              "hgemm: stream-K counter allocation failed");
+  bufs.emplace(key, b);
+  return b;
+}
 }  // namespace
+
+// Stream-K for the implicit-im2col convolutions (DPE_HGEMM_SK=1 / set_hgemm_sk(true): on; default off): for
+// plans whose whole-K tiles leave a partly empty last round -- ResNet-50's layer-3 3x3 convs at batch 512
+// are 392 tiles of 256x256 on 256 CUs, 1.53 rounds run as 2 (scripts/bench_wave_quant.py).  Measured:
+// that conv 142 -> 134 us alone, the ResNet-50 step within noise (30.82-30.86 vs 30.83-30.89 ms,
+// alternating on one box) -- a partly filled round runs faster per CU, so the idle CUs cost less than
+// their share (docs/perf_notes.md).
+int g_sk = [] { const char* e = getenv("DPE_HGEMM_SK"); return (e && e[0] == '1') ? 1 : 0; }();
 
 unsigned* sched_buffer(hipStream_t st) { return sched_buffer_impl(st); }
 
@@ -212,6 +244,21 @@ Plan2 plan2(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, i
 }
 
 namespace {
+// Stream-K grid for this launch (0: whole-K tiles as planned): conv GEMMs with a 1-block-per-CU tile whose
+// tile count leaves >= 10 % of the last round idle, between one and three rounds of tiles, and enough
+// K-steps per block (>= 8 of 64) that the cut costs little.  (A single partial round is left alone: with
+// fewer CUs busy each runs faster -- layer 4's 196 tiles took the same time whole-K and stream-K.)
+int sk_grid(const dpe::HgemmArgs& a, const Plan& pl, int epi) {
+  if (!g_sk || a.conv != 1 || epi != dpe::HE_BF16 || pl.splits != 1 || pl.cfg < 0 || pl.cfg == dpe::HC_128x128) return 0;
+  const int bm = pl.cfg == dpe::HC_128x256 ? 128 : 256, bn = pl.cfg == dpe::HC_256x128 ? 128 : 256;
+  const int64_t tiles = ((int64_t)(a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+  const int64_t G = std::max(8, num_cus() - dpe_cu_reserve());
+  if (tiles >= dpe::HGEMM_SK_MAX_TILES || tiles <= G || tiles >= 3 * G || tiles * (a.K / 64) < 8 * G) return 0;
+  const double r = (double)tiles / (double)G;
+  if (std::ceil(r) / r < 1.10) return 0;
+  return (int)G;
+}
+
 // one planned launch (+ its slab finalize when K-split)
 void launch_planned(dpe::HgemmArgs a, const Plan& pl, int ak, int bk, int epi, hipStream_t fin_stream) {
   a.splits = pl.splits;
@@ -257,7 +304,20 @@ void launch_planned(dpe::HgemmArgs a, const Plan& pl, int ak, int bk, int epi, h
     TORCH_CHECK(rf == 0 && e == hipSuccess, "hgemm finalize failed rc=", rf, " ", hipGetErrorString(e));
     return;
   }
-  const int rc = dpe_hgemm_launch(&a, pl.cfg, ak, bk, epi, pl.grid, cur_stream());
+  int grid = pl.grid;
+  Tensor skw;
+  if (const int G = sk_grid(a, pl, epi)) {
+    if (unsigned* cnt = sk_counters(cur_stream())) {
+      const int64_t tile_f32 = (pl.cfg == dpe::HC_256x256 ? 256 * 256 : 128 * 256);
+      skw = at::empty({2 * (int64_t)G * tile_f32}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA));
+      a.sk = 1;
+      a.sk_ws = (float*)skw.data_ptr();
+      a.sk_cnt = cnt;
+      a.sched = nullptr;
+      grid = G;
+    }
+  }
+  const int rc = dpe_hgemm_launch(&a, pl.cfg, ak, bk, epi, grid, cur_stream());
   const hipError_t e = hipGetLastError();
   TORCH_CHECK(rc == 0 && e == hipSuccess, "hgemm launch failed rc=", rc, " ", hipGetErrorString(e));
 }
@@ -545,6 +605,8 @@ void register_gemm(pybind11::module& m) {
         "fp32 dw += alpha dy^T x");
   m.def("set_hgemm_force", [](int64_t cfg, int64_t splits) { g_force_cfg = (int)cfg; g_force_splits = (int)splits; },
         py::arg("cfg") = -1, py::arg("splits") = -1, "pin the planner's tile / split (-1: free); A/B testing only");
+  m.def("set_hgemm_sk", [](bool on) { const bool was = g_sk != 0; g_sk = on ? 1 : 0; return was; }, py::arg("on"),
+        "stream-K schedule for the implicit-im2col conv GEMMs (DPE_HGEMM_SK); returns the previous setting");
   m.def("set_hgemm_dynamic", [](bool on) { const bool was = g_dynamic; g_dynamic = on; return was; }, py::arg("on"),
         "persistent GEMM: claim units beyond the grid at run time (default) or round-robin them statically; "
         "returns the previous setting");

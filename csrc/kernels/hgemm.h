@@ -83,7 +83,18 @@ struct HgemmArgs {
   const uint16_t* A2;
   int64_t lda2;
   int k1;
+  // Stream-K schedule (sk != 0; 1-block-per-CU tiles, no K split, static grid <= free CUs): the launch's T
+  // tiles x K/64 K-steps are cut into gridDim.x equal contiguous ranges, one per block, so every block does
+  // the same MFMA work whatever T mod grid is.  A tile cut over P blocks: the segment done last owns it;
+  // the P - 1 others store fp32 partials (sk_ws: two [tile fragments][threads] x 16 B slabs per block,
+  // write-through) and add to the tile's counter (sk_cnt[tile], zero before the launch); the owner waits
+  // for P - 1, resets it, adds the partials in block order (run-to-run identical) and runs the epilogue.
+  // sk_cnt[HGEMM_SK_MAX_TILES - 1] != 0: an owner gave up waiting (a block never ran; output invalid).
+  int sk;
+  float* sk_ws;
+  unsigned* sk_cnt;
 };
+constexpr int HGEMM_SK_MAX_TILES = 8192;  // sk_cnt entries (one per output tile)
 
 // Tile configurations (BMxBN, waves WRxWC).
 enum HCfg : int {

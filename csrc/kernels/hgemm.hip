@@ -181,7 +181,8 @@ DPE_DEVICE float gelu_grad(float x) {
 // CV = 2 (BC): B is the implicit im2col of an NHWC conv input in the TN weight-grad layout (B[k][n], k = output
 // pixel, n = (r, s, ci); N-contiguous): every lane's 16-B chunk is one (tap, 8 channels) column for the whole
 // unit, and its pixel row is decomposed per K-tile (padding and the pixel tail read as zeros).
-template <int BM, int BN, int WR, int WC, bool AK, bool BK, int EPI, int ACT, bool BG = false, int CV = 0>
+template <int BM, int BN, int WR, int WC, bool AK, bool BK, int EPI, int ACT, bool BG = false, int CV = 0,
+          bool SKM = false>
 // (4-wave tiles run 2 blocks per CU: 2 waves per SIMD, so at most 256 VGPRs + AGPRs per wave)
 __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kernel(HgemmArgs p) {
   constexpr bool AC = CV == 1, BC = CV == 2, ACAT = CV == 3;
@@ -211,6 +212,7 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
   int tilesM = (qM + BM - 1) / BM, tilesN = (qN + BN - 1) / BN;
   int ntile = tilesM * tilesN;
   const int nunits = GRP ? p.grp[p.ngroup - 1].tile_end : ntile * p.splits;
+  static_assert(!SKM || (NW == 8 && !GRP && !BG && EPI == HE_BF16), "stream-K: 1-block-per-CU tiles, bf16 epilogues");
   const float alpha = p.alpha * (p.alpha_ptr ? *p.alpha_ptr : 1.f);
 
   // Schedule.  Without p.sched (or with one round of units) block b computes units
@@ -226,7 +228,7 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
   // bitwise independent of the schedule.
   const int G0 = gridDim.x;
 #if HG_SCHED == 1
-  const bool dsched = p.sched != nullptr && nunits > G0;
+  const bool dsched = !SKM && p.sched != nullptr && nunits > G0;
 #else
   // only the HG_SCHED == 1 main loop issues the next-unit claim: any other build runs the static
   // schedule (a dynamic one would re-resolve the same unit forever)
@@ -280,8 +282,58 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
     }
   };
 
+  // Stream-K (SKM, hgemm.h): block lb (XCD-remapped) owns K-steps [lo(lb), lo(lb + 1)) of the tiles'
+  // concatenated K-step sequence (ntk steps per tile, tile order = unit order): the first r blocks q + 1
+  // steps, the rest q (32-bit: tiles x ntk < 2^31).  A segment is a block's part of one tile: unit u = its
+  // tile, kb its first K.  A range that ends inside a tile it did not start in runs that last segment
+  // FIRST (its partial is handed off early, while the other blocks still compute), then the rest in
+  // order.  Nothing of this is kept live across the main loop (the epilogue recomputes it from u, kb and
+  // the grid): the 256x256 tile has no SGPRs or VGPRs to spare.
+  const int ntk = p.K / TK;
+  int sk_kb0 = 0, sk_nt0 = 0;
+  struct SkGrid {
+    unsigned q, r, lb, nk;
+    DPE_DEVICE unsigned lo(unsigned b) const { return b * q + min(b, r); }
+    DPE_DEVICE unsigned blk(unsigned st) const {  // the block whose range holds K-step st
+      const unsigned big = r * (q + 1u);
+      return __builtin_amdgcn_readfirstlane(st < big ? st / (q + 1u) : r + (st - big) / q);
+    }
+    // first step of the tile holding block b's last step, if b runs that tile's segment first; else ~0u
+    DPE_DEVICE unsigned lead(unsigned b) const {
+      const unsigned l = lo(b), h = lo(b + 1u);
+      const unsigned tb = __builtin_amdgcn_readfirstlane((h - 1u) / nk) * nk;
+      return (tb > l && h != tb + nk) ? tb : ~0u;
+    }
+    // block b's segment of the tile starting at step t0: steps from b's start until it is done
+    DPE_DEVICE unsigned done_at(unsigned b, unsigned t0) const {
+      const unsigned l = lo(b), h = lo(b + 1u), tb = lead(b);
+      const unsigned e = min(h, t0 + nk);
+      return tb == ~0u ? e - l : (t0 == tb ? h - tb : (h - tb) + (e - l));
+    }
+  };
+  auto sk_grid = [&]() -> SkGrid {
+    unsigned g = (unsigned)G0;
+    asm volatile("" : "+s"(g));  // recomputed where used, not hoisted out of the unit loop
+    const unsigned total = (unsigned)ntile * (unsigned)ntk;
+    const unsigned q = __builtin_amdgcn_readfirstlane(total / g);
+    return SkGrid{q, total - q * g, (unsigned)xcd_remap(blockIdx.x, (int)g), (unsigned)ntk};
+  };
+  // the segment of K-steps [cur, bound): its tile (returned) and kb / nt
+  auto sk_seg = [&](unsigned cur, unsigned bound) -> int {
+    const int t = __builtin_amdgcn_readfirstlane((int)(cur / (unsigned)ntk));
+    const unsigned t0 = (unsigned)t * (unsigned)ntk;
+    sk_kb0 = (int)(cur - t0) * TK;
+    sk_nt0 = (int)(min(t0 + (unsigned)ntk, bound) - cur);
+    return t;
+  };
+
   int u;
-  if ((int)blockIdx.x < S) {
+  if constexpr (SKM) {
+    const SkGrid sg = sk_grid();
+    const unsigned lo = sg.lo(sg.lb), hi = sg.lo(sg.lb + 1u), tb = sg.lead(sg.lb);
+    if (lo >= hi) return;
+    u = tb != ~0u ? sk_seg(tb, hi) : sk_seg(lo, hi);
+  } else if ((int)blockIdx.x < S) {
     u = xcd_remap(blockIdx.x, S);
     if (u >= nunits) return;  // (the planner's grid never exceeds the unit count)
   } else {
@@ -365,6 +417,9 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
       ntile = tilesM * tilesN;
       tile = uu - (g > 0 ? p.grp[g - 1].tile_end : 0);
       split = 0;
+    } else if constexpr (SKM) {
+      tile = uu;
+      split = 0;
     } else {
       tile = uu % ntile;
       split = uu / ntile;
@@ -375,8 +430,8 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
     const int in = tile % gsz;
     m0 = (g0 + in % grows) * BM;
     n0 = (in / grows) * BN;
-    kb = split * p.kps;
-    nt = (min(p.K, kb + p.kps) - kb) / TK;
+    kb = SKM ? sk_kb0 : split * p.kps;
+    nt = SKM ? sk_nt0 : (min(p.K, kb + p.kps) - kb) / TK;
     if constexpr (AC) {
       // per A piece row: the input pixel of output row m (byte offset from the resource base) and the
       // filter taps that stay inside the image
@@ -699,9 +754,90 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
     //               col n0 + wc*(BN/WC) + (j/FNH)*CH + (j%FNH)*16 + ln4 + e
     const int rbase = m0 + wr * (BM / WR) + lm, cbase = n0 + wc * (BN / WC) + ln4;
     // (readfirstlane: the value is uniform; keeping it scalar keeps the tile indexing in SGPRs)
-    const int next = dyn > 0 ? __builtin_amdgcn_readfirstlane(*slot)
-                             : (u + (int)gridDim.x < nunits ? u + (int)gridDim.x : -1);
+    int next = dyn > 0 ? __builtin_amdgcn_readfirstlane(*slot)
+                       : (u + (int)gridDim.x < nunits ? u + (int)gridDim.x : -1);
     const int cur_split = split;
+
+    // Stream-K: a tile cut over P > 1 blocks.  Its owner is the segment that is done last (SkGrid::done_at;
+    // ties: the lowest block); the others store their fp32 partials write-through (sc1, 16 B per lane per
+    // fragment; two slabs per block: the segment starting the block's range, and the one it runs first),
+    // issue their next segment's prologue, and after the loop-end drain (every wave's vmcnt(0), then the
+    // barrier) one lane adds to the tile's counter.  The owner polls the counter (sc1, one lane) until the
+    // P - 1 others have added, resets it, and after a barrier adds their slabs to its registers in block
+    // order with sc1 loads (MI355X_MICROARCH.md, hand-off table row 1): run-to-run identical.  It only
+    // waits on segments scheduled to be done before it, in blocks that are all resident (one block per CU,
+    // grid <= free CUs); the poll is bounded and flags a timeout in sk_cnt[HGEMM_SK_MAX_TILES - 1]
+    // instead of hanging.
+    bool do_epi = true;
+    int sk_sig = -1;  // tile whose counter this block adds to after the loop-end drain
+    if constexpr (SKM) {
+      constexpr int NF = 4 * FMH * FNH, SLAB = NF * G::NT * 16;  // fragments per lane, bytes per slab
+      const SkGrid sg = sk_grid();
+      const unsigned t0 = (unsigned)u * (unsigned)ntk, lo = sg.lo(sg.lb), hi = sg.lo(sg.lb + 1u), tb = sg.lead(sg.lb);
+      const unsigned cs = t0 + (unsigned)(kb / TK), ce = cs + (unsigned)nt;  // this segment
+      const int bf = (int)sg.blk(t0), P = (int)sg.blk(t0 + (unsigned)ntk - 1u) - bf + 1;
+      if (P > 1) {
+        int own = bf;
+        unsigned best = 0u;
+        for (int b = bf; b < bf + P; ++b) {
+          const unsigned d = sg.done_at((unsigned)b, t0);
+          if (d > best) {
+            best = d;
+            own = b;
+          }
+        }
+        const __amdgpu_buffer_rsrc_t skr = __builtin_amdgcn_make_buffer_rsrc(p.sk_ws, (short)0, 2 * G0 * SLAB, 0x00020000);
+        // block b's slab of this tile: slot 0 if its segment starts b's range, else 1; fragment f of thread x
+        // at + (f * threads + x) * 16 (each store / load instruction moves 1 KB per wave; f in soffset)
+        auto slab_of = [&](int b) -> uint32_t { return (uint32_t)(2 * b + (sg.lo((unsigned)b) >= t0 ? 0 : 1)) * (uint32_t)SLAB; };
+        const uint32_t lofs = (uint32_t)tid * 16u;
+        if ((int)sg.lb != own) {
+          const uint32_t mine = slab_of((int)sg.lb) + lofs;
+#pragma unroll
+          for (int i = 0; i < 2 * FMH; ++i)
+#pragma unroll
+            for (int j = 0; j < 2 * FNH; ++j)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), skr, mine,
+                                                     (i * 2 * FNH + j) * G::NT * 16, 16);
+          sk_sig = u;
+          do_epi = false;
+        } else {
+          if (tid == 0) {
+            unsigned* const cnt = p.sk_cnt + u;
+            for (unsigned n = 0; __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (unsigned)(P - 1); ++n) {
+              if (n == (1u << 22)) {  // ~seconds: a block that never ran; give up rather than hang the GPU
+                __hip_atomic_store(p.sk_cnt + (HGEMM_SK_MAX_TILES - 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+              }
+              __builtin_amdgcn_s_sleep(2);
+            }
+            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          __syncthreads();
+          for (int b = bf; b < bf + P; ++b) {
+            if (b == own) continue;
+            const uint32_t base = slab_of(b) + lofs;
+            constexpr int HI = FMH;  // fragment rows per batch of loads: half the tile
+#pragma unroll
+            for (int i0 = 0; i0 < 2 * FMH; i0 += HI) {
+              u32x4 v[HI][2 * FNH];
+#pragma unroll
+              for (int i = 0; i < HI; ++i)
+#pragma unroll
+                for (int j = 0; j < 2 * FNH; ++j)
+                  v[i][j] = __builtin_amdgcn_raw_buffer_load_b128(skr, base, ((i0 + i) * 2 * FNH + j) * G::NT * 16, 16);
+#pragma unroll
+              for (int i = 0; i < HI; ++i)
+#pragma unroll
+                for (int j = 0; j < 2 * FNH; ++j) acc[i0 + i][j] += __builtin_bit_cast(f32x4, v[i][j]);
+            }
+          }
+        }
+      }
+      // next: after the lead segment the range from its start (up to the lead tile), else onward
+      const unsigned bound = tb != ~0u ? tb : hi;
+      next = (tb != ~0u && ce == hi) ? sk_seg(lo, bound) : (ce < bound ? sk_seg(ce, bound) : -1);
+    }
 
     // 0) bias gradient: the 4 lane groups hold k-slices of the same 16 rows
     if constexpr (BG) {
@@ -717,6 +853,21 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
             else qdbias[row] += alpha * v;                                   // the row's only writer
           }
         }
+      }
+    }
+
+    if constexpr (SKM) {
+      if (!do_epi) {  // a partial for the tile's head: the next segment's prologue, then the drain and the add
+        if (next >= 0) {
+          u = next;
+          decode(u);
+          PROLOGUE();
+        }
+        wait_vm<0>();
+        HG_BARRIER();
+        if (tid == 0) __hip_atomic_fetch_add(p.sk_cnt + sk_sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (next < 0) break;
+        continue;
       }
     }
 
@@ -1056,7 +1207,16 @@ template <int BM, int BN, int WR, int WC>
 int launch_conv(const HgemmArgs& p, int epi, int grid, hipStream_t st) {
   if (epi != HE_BF16 || p.splits != 1 || p.dbias || p.bias) return -3;
   const dim3 g((unsigned)grid), b(WR * WC * 64);
-#define HC(A) hipLaunchKernelGGL((hg::hgemm_kernel<BM, BN, WR, WC, true, true, HE_BF16, A, false, 1>), g, b, 0, st, p)
+#define HC(A)                                                                                                     \
+  do {                                                                                                            \
+    if constexpr (WR * WC == 8) {                                                                                 \
+      if (p.sk) {                                                                                                 \
+        hipLaunchKernelGGL((hg::hgemm_kernel<BM, BN, WR, WC, true, true, HE_BF16, A, false, 1, true>), g, b, 0, st, p); \
+        break;                                                                                                    \
+      }                                                                                                           \
+    }                                                                                                             \
+    hipLaunchKernelGGL((hg::hgemm_kernel<BM, BN, WR, WC, true, true, HE_BF16, A, false, 1>), g, b, 0, st, p);      \
+  } while (0)
   if (p.act == ACT_NONE) HC(ACT_NONE);
   else if (p.act == HACT_BNF && p.col_stats) HC(HACT_BNF);
   else if (p.act == HACT_BNB && p.col_stats && p.st_x && p.st_coef) HC(HACT_BNB);
@@ -1147,6 +1307,14 @@ extern "C" int dpe_hgemm_launch(const HgemmArgs* a, int cfg, int a_k, int b_k, i
     return -4;
   }
   if ((b_k ? (int64_t)bdim * p.ldb : (int64_t)p.K * p.ldb) * 2 >= (1ll << 32)) return -4;
+  if (p.sk) {
+    // stream-K: one block per CU, whole-K units, static grid; two slabs per block, one counter per tile
+    const int bm = cfg == HC_128x256 ? 128 : 256, bn = cfg == HC_256x128 ? 128 : 256;
+    const int64_t tiles = (int64_t)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn);
+    if (cfg == HC_128x128 || p.conv != 1 || epi != HE_BF16 || p.splits != 1 || p.kps != p.K || !p.sk_ws || !p.sk_cnt ||
+        tiles >= HGEMM_SK_MAX_TILES || (int64_t)grid * 2 * (bm * bn * 4) >= (1ll << 31))
+      return -1;
+  }
   switch (cfg) {
     case HC_256x256: return launch_layout<256, 256, 2, 4>(p, a_k, b_k, epi, grid, st);
     case HC_128x256: return launch_layout<128, 256, 2, 4>(p, a_k, b_k, epi, grid, st);

@@ -621,6 +621,38 @@ def test_dgrad_bn_backward_partials(C, N, H, W, Ci, Co, k, s, p):
     assert rel_err(dh, dh_ref) < 2e-2 and rel_err(dg1, dg2) < 1e-3 and rel_err(db1, db2) < 1e-3
 
 
+@pytest.mark.parametrize("Ci,H,B", [(256, 14, 512)])
+def test_stream_k_conv_matches_whole_k(C, Ci, H, B):
+    """Stream-K schedule of the implicit-im2col conv GEMM (hgemm.hip SKM; ResNet-50's layer-3 3x3 shape, 392
+    tiles of 256x256 on 256 CUs, where the whole-K tiles leave most of the second round idle): forward with
+    BN sums and the data grad with BN-backward partials equal the whole-K launch within fp32 reassociation, agree
+    with torch, and are bitwise identical run to run (fixed cut, partials added in block order)."""
+    torch.manual_seed(21)
+    x = bf(torch.randn(B, H, H, Ci, device=dev))
+    w = bf(torch.randn(Ci, 3, 3, Ci, device=dev) / math.sqrt(9 * Ci))
+    h = bf(torch.randn(B, H, H, Ci, device=dev))
+    coef = _bn_coef(C, Ci)
+    z = ([1, 1], [1, 1], [1, 1])
+    prev = C.set_hgemm_sk(False)
+    try:
+        y0, s0 = C.conv_fwd(x, w, *z, True, None)
+        d0, p0 = C.conv_dgrad_bn(x, w, [B, H, H, Ci], *z, None, h, coef)
+        C.set_hgemm_sk(True)
+        runs = [(C.conv_fwd(x, w, *z, True, None), C.conv_dgrad_bn(x, w, [B, H, H, Ci], *z, None, h, coef))
+                for _ in range(2)]
+    finally:
+        C.set_hgemm_sk(prev)
+    (y1, s1), (d1, p1) = runs[0]
+    (y2, s2), (d2, p2) = runs[1]
+    assert torch.equal(y1, y2) and torch.equal(s1, s2) and torch.equal(d1, d2) and torch.equal(p1, p2)
+    # the stream-K cut really ran (a different fp32 summation order moves a few bf16 roundings)
+    assert 0 < (y1 != y0).float().mean().item() < 1e-2
+    assert rel_err(y1, y0) < 1e-2 and rel_err(d1, d0) < 1e-2
+    assert rel_err(s1.sum(-1), s0.sum(-1)) < 1e-4 and rel_err(p1.sum(-1), p0.sum(-1)) < 1e-4
+    ref = F.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), padding=1).permute(0, 2, 3, 1)
+    assert rel_err(y1, ref) < 1e-2
+
+
 def test_bn_apply_mask_bits_and_residual_relu_dgrad(C):
     """bn_apply's ReLU-mask bits, and the dgrad epilogue variant that masks dx with them
     (BN + residual + ReLU backward: dx stored as dz, BN partials of dz)."""
