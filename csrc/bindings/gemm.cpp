@@ -118,9 +118,10 @@ unsigned* sk_counters(hipStream_t st) {
 // Stream-K for the implicit-im2col convolutions (DPE_HGEMM_SK=1 / set_hgemm_sk(true): on; default off): for
 // plans whose whole-K tiles leave a partly empty last round -- ResNet-50's layer-3 3x3 convs at batch 512
 // are 392 tiles of 256x256 on 256 CUs, 1.53 rounds run as 2 (scripts/bench_wave_quant.py).  Measured:
-// that conv 142 -> 134 us alone, the ResNet-50 step within noise (30.82-30.86 vs 30.83-30.89 ms,
-// alternating on one box) -- a partly filled round runs faster per CU, so the idle CUs cost less than
-// their share (docs/perf_notes.md).
+// that conv 142 -> 134 us alone, the ResNet-50 step -0.06 ms on average over 9 alternating pairs -- a partly
+// filled round runs faster per CU, so the idle CUs cost less than their share.  Off by default: its owners
+// wait on blocks of their own grid, which an RCCL kernel holding CUs can delay by a whole all-reduce
+// (docs/perf_notes.md).
 int g_sk = [] { const char* e = getenv("DPE_HGEMM_SK"); return (e && e[0] == '1') ? 1 : 0; }();
 
 unsigned* sched_buffer(hipStream_t st) { return sched_buffer_impl(st); }
