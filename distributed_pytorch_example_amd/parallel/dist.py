@@ -94,13 +94,16 @@ SUGGESTED_MAX_CHANNELS = 16
 
 def cu_reserve_for(world: int, channels: Optional[int]) -> int:
     """Persistent-kernel slots left free while a bucket all-reduce is in flight: one per RCCL channel
-    block (a 256-thread RCCL workgroup displaces at most one block of ours per CU; measured footprint
-    in profiles/rccl_footprint_r3.txt).  ``DPE_CU_RESERVE`` overrides; 0 at world 1."""
+    block (a 256-thread RCCL workgroup displaces at most one block of ours per CU; the kernels' grid =
+    channel blocks, 256 threads, 140 VGPRs, ~20 KB LDS: profiles/world8_1gpu_r6.txt, and round 3's
+    footprint run in git history).  ``DPE_CU_RESERVE`` overrides; 0 at world 1."""
     if os.environ.get("DPE_CU_RESERVE"):
         return max(0, int(os.environ["DPE_CU_RESERVE"]))
     if world <= 1:
         return 0
-    # RCCL's own channel count is not queryable: assume 32 resident channel blocks when uncapped
+    # RCCL's own channel count is not queryable from here: when uncapped assume 32 resident channel blocks
+    # (an upper bound for an 8-GPU xGMI all-reduce; the one-GPU socket rehearsal ran 4).  DDP keeps this
+    # reserve only while the measured all-reduce duty warrants it (DDP.settle_cu_budget).
     return int(channels) if channels else 32
 
 
