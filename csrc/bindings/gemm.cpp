@@ -195,7 +195,7 @@ Plan plan(int64_t M, int64_t N, int64_t K, int ak, int bk, bool allow_split, int
 
 // Tile rows per grouped-order band.  An XCD runs grid/8 consecutive units at a time; with 4-row
 // bands those 32 (1 block/CU) units form a 4 x 8 tile block sharing A rows and B columns in the
-// XCD's L2.  Interleaved A/B (scripts/ab_hgemm.py, profiles/hgemm_group_ab_r2.jsonl), TF/s vs
+// XCD's L2.  Interleaved A/B (scripts/ab_hgemm.py, profiles/hgemm_group_ab_r2.jsonl in git history), TF/s vs
 // row-major: 8192^3 NT 1340 -> 1478, NN 1054 -> 1201, TN 989 -> 1132; GPT-2 LM head fwd 973 ->
 // 1055; 4096^3 and the small GPT-2 GEMMs neutral; 8-row bands equal on squares, worse on the LM
 // head; 16-row bands worse everywhere.

@@ -354,7 +354,7 @@ void run_igemm(dpe::IgemmArgs& a, int aload, int bload, int epi, bool allow_spli
       // 3 per CU (768 on 256 CUs), less the slots an overlapped RCCL collective holds (CU budget,
       // comm.cpp): a split that needs more blocks than fit beside the collective's workgroups runs a
       // second, nearly empty wave (x1.56-1.60 per kernel next to 16 RCCL-sized workgroups,
-      // profiles/cu_hog_probe_r3.txt).  Rounded down, so tiles x splits <= the target.
+      // profiles/cu_hog_probe_r3.txt in git history).  Rounded down, so tiles x splits <= the target.
       // With a CU budget in force the split targets TWO rounds of blocks: foreign workgroups do not take
       // our slots away (they fit beside them) but slow the CUs they share, and with one round the
       // slowest CU set the kernel's time (x1.27 next to 16 VALU-bound hogs, profiles/cu_hog_probe_r4.txt);
@@ -1382,7 +1382,7 @@ std::vector<Tensor> conv1x1_dgrad_cat(const Tensor& dz, const Tensor& a2src, con
   Tensor dx = at::empty_like(bn_x);
   // a2 materialised and >= 256 channels (layer 3): the persistent GEMM's NN layout with the two A segments
   // (hgemm.hip CV = 3) and its BN-backward-partials epilogue; 156-167 us per call on the LDS-DMA kernel
-  // here (416 TF, profiles/resnet50_bs512_sequence_r4.txt)
+  // here (416 TF, profiles/resnet50_bs512_sequence_r4.txt in git history)
   if (g_hgemm_conv && !(a2_coef.has_value() && a2_coef->defined()) && C >= 256 && C % 64 == 0 && K1 % 64 == 0) {
     int pcols = 0;
     const auto pl = dpe_gemm::plan_bnb(M, C, K1 + C, 1, 0, &pcols);

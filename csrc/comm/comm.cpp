@@ -255,7 +255,7 @@ void Communicator::abort() {
 // Every RCCL channel is one workgroup resident on a CU for the duration of a collective.  The
 // persistent compute kernels (hgemm, pw_stream) size their grids to exactly the resident capacity and
 // give every block a static share; a foreign workgroup on a CU whose slots they fill displaces one of
-// their blocks into a second wave (x1.45-1.7 measured, profiles/cu_hog_probe_r2.txt).  While the
+// their blocks into a second wave (x1.45-1.7 measured, profiles/cu_hog_probe_r2.txt in git history).  While the
 // reducer has a bucket all-reduce in flight (first launch of a backward .. finalize) those kernels
 // plan with `reserve` slots fewer (bindings/gemm.cpp plan(), pwconv.hip pw_capacity()).  The
 // reserve is the communicator's channel count (parallel/dist.py).  Host-side state: every rank

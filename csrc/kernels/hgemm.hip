@@ -399,7 +399,7 @@ __global__ __launch_bounds__(WR * WC * 64, WR * WC == 4 ? 2 : 1) void hgemm_kern
   // Grouped tile order: consecutive unit ids (which run together on one XCD -- xcd_remap) walk
   // GROUP_M tile rows before moving one tile column, so an XCD's concurrent tiles form a
   // GROUP_M x (chunk / GROUP_M) block sharing A rows AND B columns in its L2 (row-major order
-  // shares only A: L2 hit rate 50 % on 8192^3, measured -- profiles/hgemm_pmc_r2.txt).
+  // shares only A: L2 hit rate 50 % on 8192^3, measured -- profiles/hgemm_pmc_r2.txt in git history).
   const int gm_rows = p.group_m > 0 ? p.group_m : 1;
   auto decode = [&](int uu) {
     int tile;

@@ -512,7 +512,7 @@ int rows_slots() {  // resident blocks of the row-walking kernels (2 per CU), mi
 }
 // One block per resident slot, each owning a contiguous range of the N*H output rows (>= 16 rows):
 // a single wave of blocks -- a fixed N*2 grid went from exactly 2 waves to 2 + a sliver when RCCL
-// channel blocks held 16 slots (x1.4-1.6, profiles/cu_hog_probe_r3.txt).  While the budget is in force,
+// channel blocks held 16 slots (x1.4-1.6, profiles/cu_hog_probe_r3.txt in git history).  While the budget is in force,
 // two rounds of half-size blocks instead: a foreign workgroup that fits beside a block still slows its
 // CU, and with one round the slowest CU's block set the launch's time (x1.7-1.8 next to 16 VALU-bound
 // RCCL-sized workgroups, profiles/cu_hog_probe_r4.txt); with two, the dispatcher hands it fewer.
